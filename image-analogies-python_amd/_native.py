@@ -1,0 +1,214 @@
+"""ctypes boundary to libia.so (include/ia.h).
+
+This is the only way the package reaches the GPU: there is no CPU fallback.  If libia.so is
+missing, or no gfx950 device is visible, every entry point raises IAError loudly.
+"""
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, 'libia.so')
+
+IA_MEM_HOST, IA_MEM_DEVICE = 0, 1
+_ERRNAMES = {-1: 'IA_EINVAL', -2: 'IA_EHIP', -3: 'IA_ENOMEM', -4: 'IA_ENODEV', -5: 'IA_ECOMM'}
+
+
+class IAError(RuntimeError):
+    pass
+
+
+class LevelArgs(ctypes.Structure):
+    _fields_ = [('ch', ctypes.c_int), ('n_ap', ctypes.c_int), ('a_h', ctypes.c_int), ('a_w', ctypes.c_int),
+                ('b_h', ctypes.c_int), ('b_w', ctypes.c_int),
+                ('A', ctypes.c_void_p), ('Ac', ctypes.c_void_p), ('Ap', ctypes.c_void_p), ('Apc', ctypes.c_void_p),
+                ('B', ctypes.c_void_p), ('Bc', ctypes.c_void_p), ('Bpc', ctypes.c_void_p), ('Bp', ctypes.c_void_p),
+                ('weights', ctypes.c_void_p), ('kappa_factor', ctypes.c_double),
+                ('s_out', ctypes.c_void_p), ('im_out', ctypes.c_void_p), ('mem', ctypes.c_int)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [('pixels', ctypes.c_int64), ('steps', ctypes.c_int64), ('coherence_wins', ctypes.c_int64),
+                ('reranked', ctypes.c_int64), ('fallbacks', ctypes.c_int64), ('db_ms', ctypes.c_double),
+                ('synth_ms', ctypes.c_double), ('dist_ms', ctypes.c_double), ('dist_launches', ctypes.c_int64),
+                ('dist_flops', ctypes.c_double)]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+EXPORTS = {
+    'ia_init': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    'ia_destroy': (None, [ctypes.c_void_p]),
+    'ia_last_error': (ctypes.c_char_p, []),
+    'ia_version': (ctypes.c_int, []),
+    'ia_set_option': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
+    'ia_comm_unique_id': (ctypes.c_int, [ctypes.c_char_p]),
+    'ia_comm_init': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
+    'ia_synthesize_level': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LevelArgs), ctypes.POINTER(Stats)]),
+    'ia_index_build': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_void_p)]),
+    'ia_index_query': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                      ctypes.c_void_p]),
+    'ia_index_destroy': (None, [ctypes.c_void_p]),
+    'ia_merge_winners': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    'ia_wavefront_shape': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                                          ctypes.POINTER(ctypes.c_int64)]),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load libia.so (raises IAError if it was not built: run __graft_entry__.build())."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise IAError('libia.so not found at %s — build it with `make -C image-analogies-python_amd/csrc` '
+                              'or __graft_entry__.build(); there is no CPU fallback' % LIB_PATH)
+            L = ctypes.CDLL(LIB_PATH)
+            for name, (res, args) in EXPORTS.items():
+                fn = getattr(L, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = L
+    return _lib
+
+
+def check(rc, what):
+    if rc != 0:
+        msg = lib().ia_last_error()
+        raise IAError('%s failed (%s): %s' % (what, _ERRNAMES.get(rc, rc), msg.decode() if msg else ''))
+
+
+def _ptr(a):
+    return ctypes.c_void_p(a.ctypes.data)
+
+
+def _c64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+class Context(object):
+    """One GPU (ia_ctx).  device: HIP ordinal (default: LOCAL_RANK or 0)."""
+
+    def __init__(self, device=None):
+        if device is None:
+            device = int(os.environ.get('LOCAL_RANK', 0))
+        self._h = ctypes.c_void_p()
+        check(lib().ia_init(device, ctypes.byref(self._h)), 'ia_init(%d)' % device)
+        self.device = device
+
+    @property
+    def handle(self):
+        return self._h
+
+    def close(self):
+        if self._h:
+            lib().ia_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_option(self, name, value):
+        check(lib().ia_set_option(self._h, name.encode(), int(value)), 'ia_set_option')
+
+    def comm_init(self, rank, world, uid):
+        check(lib().ia_comm_init(self._h, rank, world, bytes(uid)), 'ia_comm_init')
+
+    def synthesize_level(self, A, Ac, Ap_list, Apc_list, B, Bc, Bpc, Bp, weights, kappa_factor, stats=None):
+        """ia_synthesize_level on host numpy arrays.  Bp (fp64, C-contiguous) is updated in place
+        (the reference mutates Bp_pyr[level], image_analogies.py:214).  Returns (s, im):
+        s (N, 2) int32 source pixel in A', im (N,) int32 source A' image, raster order."""
+        A, Ac, B, Bc, Bpc = _c64(A), _c64(Ac), _c64(B), _c64(Bc), _c64(Bpc)
+        Ap = _c64(np.stack(Ap_list))
+        Apc = _c64(np.stack(Apc_list))
+        w = _c64(weights)
+        if not (Bp.dtype == np.float64 and Bp.flags.c_contiguous):
+            raise IAError('Bp must be a C-contiguous float64 array (updated in place)')
+        ch = 1 if A.ndim == 2 else A.shape[2]
+        bh, bw = B.shape[:2]
+        s = np.empty((bh * bw, 2), dtype=np.int32)
+        im = np.empty(bh * bw, dtype=np.int32)
+        args = LevelArgs(ch, Ap.shape[0], A.shape[0], A.shape[1], bh, bw,
+                         _ptr(A), _ptr(Ac), _ptr(Ap), _ptr(Apc), _ptr(B), _ptr(Bc), _ptr(Bpc), _ptr(Bp), _ptr(w),
+                         float(kappa_factor), _ptr(s), _ptr(im), IA_MEM_HOST)
+        st = stats if stats is not None else Stats()
+        check(lib().ia_synthesize_level(self._h, ctypes.byref(args), ctypes.byref(st)), 'ia_synthesize_level')
+        return s, im
+
+    def synthesize_level_device(self, ch, n_ap, a_hw, b_hw, ptrs, kappa_factor, stats=None):
+        """Same on device pointers (IA_MEM_DEVICE): ptrs = dict of int addresses for
+        A, Ac, Ap, Apc, B, Bc, Bpc, Bp, weights, s_out, im_out (e.g. torch tensor data_ptr())."""
+        p = {k: ctypes.c_void_p(int(v)) for k, v in ptrs.items()}
+        args = LevelArgs(ch, n_ap, a_hw[0], a_hw[1], b_hw[0], b_hw[1], p['A'], p['Ac'], p['Ap'], p['Apc'],
+                         p['B'], p['Bc'], p['Bpc'], p['Bp'], p['weights'], float(kappa_factor),
+                         p['s_out'], p['im_out'], IA_MEM_DEVICE)
+        st = stats if stats is not None else Stats()
+        check(lib().ia_synthesize_level(self._h, ctypes.byref(args), ctypes.byref(st)), 'ia_synthesize_level')
+        return st
+
+
+class ExactIndex(object):
+    """ia_index_*: exact 1-NN over fp64 rows (FLANN `linear` semantics, numpy summation order)."""
+
+    def __init__(self, ctx, pts):
+        pts = _c64(pts)
+        if pts.ndim != 2 or pts.shape[0] < 1:
+            raise IAError('ExactIndex: pts must be a non-empty (n, d) array')
+        self.ctx = ctx
+        self.n, self.d = pts.shape
+        self._h = ctypes.c_void_p()
+        check(lib().ia_index_build(ctx.handle, _ptr(pts), self.n, self.d, ctypes.byref(self._h)), 'ia_index_build')
+
+    def query(self, q):
+        q = _c64(np.atleast_2d(q))
+        if q.shape[1] != self.d:
+            raise IAError('ExactIndex.query: query width %d != index width %d' % (q.shape[1], self.d))
+        idx = np.empty(q.shape[0], dtype=np.int64)
+        dist = np.empty(q.shape[0], dtype=np.float64)
+        check(lib().ia_index_query(self._h, _ptr(q), q.shape[0], _ptr(idx), _ptr(dist)), 'ia_index_query')
+        return idx, dist
+
+    def close(self):
+        if self._h:
+            lib().ia_index_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def comm_unique_id():
+    buf = ctypes.create_string_buffer(128)
+    check(lib().ia_comm_unique_id(buf), 'ia_comm_unique_id')
+    return buf.raw
+
+
+def merge_winners(dist, row):
+    """Host restatement-free merge (compiled in libia): dist/row (world, nq) -> (nq,) winners."""
+    dist = _c64(dist)
+    row = np.ascontiguousarray(row, dtype=np.int64)
+    world, nq = dist.shape
+    do = np.empty(nq, dtype=np.float64)
+    ro = np.empty(nq, dtype=np.int64)
+    check(lib().ia_merge_winners(_ptr(dist), _ptr(row), world, nq, _ptr(do), _ptr(ro)), 'ia_merge_winners')
+    return do, ro
+
+
+def wavefront_shape(h, w):
+    s, m = ctypes.c_int64(), ctypes.c_int64()
+    check(lib().ia_wavefront_shape(h, w, ctypes.byref(s), ctypes.byref(m)), 'ia_wavefront_shape')
+    return s.value, m.value

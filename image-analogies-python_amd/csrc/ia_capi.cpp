@@ -1,0 +1,496 @@
+// ia_capi.cpp — host runtime of libia.so: context, device memory, the per-level skewed
+// wavefront scheduler, the FLANN-compatible exact index and the RCCL shard exchange.
+// Entry points are declared (with the reference interfaces they replace) in include/ia.h.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/ia.h"
+#include "ia_internal.h"
+#include "ia_launch.h"
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string &msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                          \
+  do {                                                                                         \
+    hipError_t e_ = (expr);                                                                    \
+    if (e_ != hipSuccess)                                                                      \
+      return fail(IA_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));                 \
+  } while (0)
+#define NCCL_TRY(expr)                                                                         \
+  do {                                                                                         \
+    ncclResult_t r_ = (expr);                                                                  \
+    if (r_ != ncclSuccess) return fail(IA_ECOMM, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+// grow-only device buffer
+struct DevBuf {
+  void *p = nullptr;
+  size_t cap = 0;
+  int ensure(size_t bytes) {
+    if (bytes <= cap) return IA_OK;
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+    size_t want = std::max<size_t>(bytes, 256);
+    if (hipMalloc(&p, want) != hipSuccess) return fail(IA_ENOMEM, "hipMalloc of " + std::to_string(want) + " bytes failed");
+    cap = want;
+    return IA_OK;
+  }
+  void release() {
+    if (p) hipFree(p);
+    p = nullptr;
+    cap = 0;
+  }
+  template <class T>
+  T *as() const {
+    return reinterpret_cast<T *>(p);
+  }
+};
+
+int kh_for(int d_plus_norm) {  // smallest instantiated K3 width that holds d + norm column
+  if (d_plus_norm <= 56) return 28;
+  if (d_plus_norm <= 112) return 56;
+  if (d_plus_norm <= 168) return 84;
+  return -1;
+}
+
+}  // namespace
+
+struct ia_ctx {
+  int dev = 0;
+  hipStream_t st = nullptr;
+  // uploads (IA_MEM_HOST) and per-level scratch
+  DevBuf A, Ac, Ap, Apc, B, Bc, Bpc, Bp, S, IM, W;
+  DevBuf db, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters;
+  // per-step K3 timing (optional)
+  int time_dist = 0;
+  std::vector<hipEvent_t> evs;
+  hipEvent_t lv0 = nullptr, lv1 = nullptr, lv2 = nullptr;
+  // multi-GPU
+  int rank = 0, world = 1;
+  ncclComm_t comm = nullptr;
+};
+
+struct ia_index {
+  ia_ctx *ctx = nullptr;
+  int64_t n = 0;
+  int d = 0, KH = 0, n_tiles = 0, tpw = 0, nwg = 0;
+  DevBuf pts, db, mu, Rbits, q, q64, qn2, qf, rec, recT, idx, dist, counters;
+};
+
+extern "C" {
+
+const char *ia_last_error(void) { return g_last_error.c_str(); }
+int ia_version(void) { return 1; }
+
+int ia_init(int device, ia_ctx **out) {
+  if (!out) return fail(IA_EINVAL, "ia_init: out is NULL");
+  int n = 0;
+  if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(IA_ENODEV, "ia_init: no HIP device visible");
+  if (device < 0 || device >= n) return fail(IA_EINVAL, "ia_init: device index out of range");
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(IA_ENODEV, std::string("ia_init: libia is built for gfx950 only, device is ") + prop.gcnArchName);
+  HIP_TRY(hipSetDevice(device));
+  ia_ctx *c = new ia_ctx();
+  c->dev = device;
+  if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+    delete c;
+    return fail(IA_EHIP, "ia_init: hipStreamCreate failed");
+  }
+  hipEventCreate(&c->lv0);
+  hipEventCreate(&c->lv1);
+  hipEventCreate(&c->lv2);
+  *out = c;
+  return IA_OK;
+}
+
+void ia_destroy(ia_ctx *c) {
+  if (!c) return;
+  hipSetDevice(c->dev);
+  hipStreamSynchronize(c->st);
+  for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->B, &c->Bc, &c->Bpc, &c->Bp, &c->S, &c->IM, &c->W, &c->db,
+                    &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters})
+    b->release();
+  for (hipEvent_t e : c->evs) hipEventDestroy(e);
+  hipEventDestroy(c->lv0);
+  hipEventDestroy(c->lv1);
+  hipEventDestroy(c->lv2);
+  if (c->comm) ncclCommDestroy(c->comm);
+  hipStreamDestroy(c->st);
+  delete c;
+}
+
+int ia_set_option(ia_ctx *c, const char *name, int value) {
+  if (!c || !name) return fail(IA_EINVAL, "ia_set_option: NULL argument");
+  if (!std::strcmp(name, "time_dist")) {
+    c->time_dist = value;
+    return IA_OK;
+  }
+  return fail(IA_EINVAL, std::string("ia_set_option: unknown option ") + name);
+}
+
+int ia_comm_unique_id(unsigned char id_out[128]) {
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  std::memcpy(id_out, &id, 128);
+  return IA_OK;
+}
+
+int ia_comm_init(ia_ctx *c, int rank, int world, const unsigned char id[128]) {
+  if (!c || world < 1 || rank < 0 || rank >= world) return fail(IA_EINVAL, "ia_comm_init: bad rank/world");
+  HIP_TRY(hipSetDevice(c->dev));
+  if (c->comm) ncclCommDestroy(c->comm);
+  c->comm = nullptr;
+  c->rank = rank;
+  c->world = world;
+  if (world == 1) return IA_OK;
+  ncclUniqueId uid;
+  std::memcpy(&uid, id, 128);
+  NCCL_TRY(ncclCommInitRank(&c->comm, world, uid, rank));
+  return IA_OK;
+}
+
+int ia_wavefront_shape(int h, int w, int64_t *steps, int64_t *max_queries) {
+  if (h < 1 || w < 1) return fail(IA_EINVAL, "ia_wavefront_shape: empty level");
+  if (steps) *steps = (int64_t)w + 3 * (int64_t)(h - 1);
+  if (max_queries) *max_queries = std::min<int64_t>(h, (w + 2) / 3);
+  return IA_OK;
+}
+
+int ia_merge_winners(const double *dist, const int64_t *row, int world, int64_t nq, double *dist_out,
+                     int64_t *row_out) {
+  if (!dist || !row || !dist_out || !row_out || world < 1 || nq < 0) return fail(IA_EINVAL, "ia_merge_winners: bad args");
+  for (int64_t m = 0; m < nq; m++) {
+    double bd = dist[m];
+    int64_t bi = row[m];
+    for (int k = 1; k < world; k++) {  // identical order on every rank (k_finish_level)
+      const double d = dist[(int64_t)k * nq + m];
+      const int64_t i = row[(int64_t)k * nq + m];
+      if (d < bd || (d == bd && i < bi)) {
+        bd = d;
+        bi = i;
+      }
+    }
+    dist_out[m] = bd;
+    row_out[m] = bi;
+  }
+  return IA_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// fast path: one pyramid level (image_analogies.py:130-239)
+// ------------------------------------------------------------------------------------------
+static int stage(ia_ctx *c, DevBuf &buf, const void *src, size_t bytes, int mem, const void **dev) {
+  if (mem == IA_MEM_DEVICE) {
+    *dev = src;
+    return IA_OK;
+  }
+  int rc = buf.ensure(bytes);
+  if (rc) return rc;
+  HIP_TRY(hipMemcpyAsync(buf.p, src, bytes, hipMemcpyHostToDevice, c->st));
+  *dev = buf.p;
+  return IA_OK;
+}
+
+int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
+  if (!c || !a) return fail(IA_EINVAL, "ia_synthesize_level: NULL argument");
+  if (a->ch < 1 || a->ch > 3) return fail(IA_EINVAL, "ia_synthesize_level: ch must be 1, 2 or 3");
+  if (a->n_ap < 1 || a->a_h < 1 || a->a_w < 1 || a->b_h < 1 || a->b_w < 1)
+    return fail(IA_EINVAL, "ia_synthesize_level: empty image or no A' image");
+  if (!a->A || !a->Ac || !a->Ap || !a->Apc || !a->B || !a->Bc || !a->Bpc || !a->Bp || !a->weights || !a->s_out ||
+      !a->im_out)
+    return fail(IA_EINVAL, "ia_synthesize_level: NULL image pointer");
+  if (a->mem != IA_MEM_HOST && a->mem != IA_MEM_DEVICE) return fail(IA_EINVAL, "ia_synthesize_level: bad mem kind");
+  if ((int64_t)a->n_ap * a->a_h * a->a_w >= (int64_t)INT32_MAX)
+    return fail(IA_EINVAL, "ia_synthesize_level: DB rows exceed int32 row ids");
+  HIP_TRY(hipSetDevice(c->dev));
+
+  LevelGeo g;
+  g.ch = a->ch;
+  g.D = 55 * a->ch;
+  g.KH = kh_for(g.D + 1);
+  const int DP = 2 * g.KH;
+  g.n_ap = a->n_ap;
+  g.ah = a->a_h;
+  g.aw = a->a_w;
+  g.ahc = (a->a_h + 1) / 2;
+  g.awc = (a->a_w + 1) / 2;
+  g.bh = a->b_h;
+  g.bw = a->b_w;
+  g.bhc = (a->b_h + 1) / 2;
+  g.bwc = (a->b_w + 1) / 2;
+  g.NA = (int64_t)g.n_ap * g.ah * g.aw;
+  g.n_tiles = (int)((g.NA + IA_TILE - 1) / IA_TILE);
+  // shard the DB over ranks unless the level is too small to be worth an exchange per step
+  const bool sharded = c->world > 1 && g.n_tiles >= 64 * c->world;
+  const int world = sharded ? c->world : 1, rank = sharded ? c->rank : 0;
+  g.tile0 = (int)((int64_t)g.n_tiles * rank / world);
+  g.tile1 = (int)((int64_t)g.n_tiles * (rank + 1) / world);
+  const int ns = g.tile1 - g.tile0;
+  g.tiles_per_wg = std::max(4, (ns + IA_WG_TARGET - 1) / IA_WG_TARGET);
+  g.nwg = (ns + g.tiles_per_wg - 1) / g.tiles_per_wg;
+
+  const size_t nA = (size_t)g.ah * g.aw * g.ch, nAc = (size_t)g.ahc * g.awc * g.ch;
+  const size_t nB = (size_t)g.bh * g.bw * g.ch, nBc = (size_t)g.bhc * g.bwc * g.ch;
+  const int64_t NB = (int64_t)g.bh * g.bw;
+  const void *dA, *dAc, *dAp, *dApc, *dB, *dBc, *dBpc, *dW;
+  int rc;
+  if ((rc = stage(c, c->A, a->A, nA * 8, a->mem, &dA)) || (rc = stage(c, c->Ac, a->Ac, nAc * 8, a->mem, &dAc)) ||
+      (rc = stage(c, c->Ap, a->Ap, nA * g.n_ap * 8, a->mem, &dAp)) ||
+      (rc = stage(c, c->Apc, a->Apc, nAc * g.n_ap * 8, a->mem, &dApc)) ||
+      (rc = stage(c, c->B, a->B, nB * 8, a->mem, &dB)) || (rc = stage(c, c->Bc, a->Bc, nBc * 8, a->mem, &dBc)) ||
+      (rc = stage(c, c->Bpc, a->Bpc, nBc * 8, a->mem, &dBpc)) ||
+      (rc = stage(c, c->W, a->weights, (size_t)g.D * 8, a->mem, &dW)))
+    return rc;
+  double *dBp;
+  int32_t *dS, *dIM;
+  if (a->mem == IA_MEM_DEVICE) {
+    dBp = a->Bp;
+    dS = a->s_out;
+    dIM = a->im_out;
+  } else {
+    if ((rc = c->Bp.ensure(nB * 8)) || (rc = c->S.ensure((size_t)NB * 8)) || (rc = c->IM.ensure((size_t)NB * 4)))
+      return rc;
+    dBp = c->Bp.as<double>();
+    dS = c->S.as<int32_t>();
+    dIM = c->IM.as<int32_t>();
+    HIP_TRY(hipMemcpyAsync(dBp, a->Bp, nB * 8, hipMemcpyHostToDevice, c->st));
+  }
+
+  // per-level scratch
+  int64_t T, Mmax;
+  ia_wavefront_shape(g.bh, g.bw, &T, &Mmax);
+  const int64_t Mpad_max = (Mmax + IA_TILE - 1) / IA_TILE * IA_TILE;
+  if ((rc = c->db.ensure((size_t)std::max(ns, 1) * IA_TILE * DP * 4)) || (rc = c->mu.ensure(4 * g.ch * 8)) ||
+      (rc = c->Rbits.ensure(4)) || (rc = c->q64.ensure((size_t)Mpad_max * g.D * 8)) ||
+      (rc = c->qn2.ensure((size_t)Mpad_max * 8)) || (rc = c->qf.ensure((size_t)Mpad_max * DP * 4)) ||
+      (rc = c->rec.ensure((size_t)Mmax * std::max(g.nwg, 1) * 16)) ||
+      (rc = c->recT.ensure((size_t)Mmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mmax * 16)) ||
+      (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(4 * 8)))
+    return rc;
+  HIP_TRY(hipMemsetAsync(c->Rbits.p, 0, 4, c->st));
+  HIP_TRY(hipMemsetAsync(c->counters.p, 0, 4 * 8, c->st));
+
+  Imgs Aim{(const double *)dAc, (const double *)dA, (const double *)dApc, (const double *)dAp,
+           g.ah, g.aw, g.ahc, g.awc, (int64_t)nA, (int64_t)nAc};
+  Imgs Bim{(const double *)dBc, (const double *)dB, (const double *)dBpc, dBp, g.bh, g.bw, g.bhc, g.bwc, 0, 0};
+
+  HIP_TRY(hipEventRecord(c->lv0, c->st));
+  ia_launch_means(g.ch, Aim, g.n_ap, c->mu.as<double>(), c->st);
+  if (ns > 0) ia_launch_db_build(g, Aim, c->mu.as<double>(), c->db.as<float4>(), c->Rbits.as<unsigned>(), c->st);
+  HIP_TRY(hipEventRecord(c->lv1, c->st));
+
+  MergeArgs ma;
+  ma.rec = c->rec.as<float4>();
+  ma.recT = c->recT.as<float>();
+  ma.q64 = c->q64.as<double>();
+  ma.qn2 = c->qn2.as<double>();
+  ma.Rbits = c->Rbits.as<unsigned>();
+  ma.nwg = g.nwg;
+  ma.tpw = g.tiles_per_wg;
+  ma.n_tiles_shard = ns;
+  ma.row0 = g.tile0 * IA_TILE;
+  ma.row_end = std::min<int64_t>(g.NA, (int64_t)g.tile1 * IA_TILE);
+  ma.counters = c->counters.as<unsigned long long>();
+  ma.eps_c = ia_eps_c(DP);
+
+  const int qtmax = ia_k3_qtmax(g.KH);
+  if (c->time_dist && (int64_t)c->evs.size() < 2 * T) {
+    size_t old = c->evs.size();
+    c->evs.resize(2 * T);
+    for (size_t i = old; i < c->evs.size(); i++) hipEventCreate(&c->evs[i]);
+  }
+  int64_t dist_launches = 0;
+  double dist_flops = 0.;
+  for (int64_t t = 0; t < T; t++) {
+    StepDesc sd;
+    sd.t = (int)t;
+    const int64_t r_lo = std::max<int64_t>(0, (t - g.bw + 1 + 2) / 3);  // ceil((t - w + 1) / 3)
+    const int64_t r_hi = std::min<int64_t>(g.bh - 1, t / 3);
+    sd.r0 = (int)r_lo;
+    sd.M = (int)(r_hi - r_lo + 1);
+    sd.Mpad = (sd.M + IA_TILE - 1) / IA_TILE * IA_TILE;
+    ia_launch_gather(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(), c->st);
+    if (ns > 0) {
+      const int qtt = sd.Mpad / IA_TILE, nqb = (qtt + qtmax - 1) / qtmax;
+      if (c->time_dist) hipEventRecord(c->evs[2 * t], c->st);
+      int qt0 = 0;
+      for (int b = 0; b < nqb; b++) {
+        const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
+        ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.row0,
+                     c->rec.as<float4>(), c->recT.as<float>(), c->st);
+        const int mq = std::min(sd.M, (qt0 + qt) * IA_TILE) - qt0 * IA_TILE;
+        dist_flops += 2.0 * g.D * (double)(ma.row_end - ma.row0) * std::max(mq, 0);
+        dist_launches++;
+        qt0 += qt;
+      }
+      if (c->time_dist) hipEventRecord(c->evs[2 * t + 1], c->st);
+    }
+    if (!sharded) {
+      ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), dS, dIM, dBp, (const double *)dW, a->kappa_factor, true, c->st);
+    } else {
+      ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), dS, dIM, dBp, (const double *)dW, a->kappa_factor, false,
+                      c->st);
+      NCCL_TRY(ncclAllGather(c->win.p, c->allwin.p, (size_t)sd.M * sizeof(Winner), ncclUint8, c->comm, c->st));
+      ia_launch_finish(g, sd, Aim, c->q64.as<double>(), c->allwin.as<Winner>(), world, sd.M, dS, dIM, dBp,
+                       (const double *)dW, a->kappa_factor, c->counters.as<unsigned long long>(), c->st);
+    }
+  }
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipEventRecord(c->lv2, c->st));
+  if (a->mem == IA_MEM_HOST) {
+    HIP_TRY(hipMemcpyAsync(a->Bp, dBp, nB * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipMemcpyAsync(a->s_out, dS, (size_t)NB * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipMemcpyAsync(a->im_out, dIM, (size_t)NB * 4, hipMemcpyDeviceToHost, c->st));
+  }
+  HIP_TRY(hipStreamSynchronize(c->st));
+  if (stats) {
+    unsigned long long ctr[4];
+    HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
+    float ms_db = 0.f, ms_syn = 0.f;
+    hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
+    hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);
+    stats->pixels += NB;
+    stats->steps += T;
+    stats->reranked += (int64_t)ctr[0];
+    stats->fallbacks += (int64_t)ctr[1];
+    stats->coherence_wins += (int64_t)ctr[2];
+    stats->db_ms += ms_db;
+    stats->synth_ms += ms_syn;
+    stats->dist_launches += dist_launches;
+    stats->dist_flops += dist_flops;
+    if (c->time_dist && ns > 0) {
+      double tot = 0.;
+      for (int64_t t = 0; t < T; t++) {
+        float ms = 0.f;
+        hipEventElapsedTime(&ms, c->evs[2 * t], c->evs[2 * t + 1]);
+        tot += ms;
+      }
+      stats->dist_ms += tot;
+    }
+  }
+  return IA_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// FLANN-compatible exact index (algorithms.py:56,69,74)
+// ------------------------------------------------------------------------------------------
+int ia_index_build(ia_ctx *c, const double *pts, int64_t n, int d, ia_index **out) {
+  if (!c || !pts || !out || n < 1 || d < 1) return fail(IA_EINVAL, "ia_index_build: bad arguments");
+  const int KH = kh_for(d + 1);
+  if (KH < 0) return fail(IA_EINVAL, "ia_index_build: d must be <= 167");
+  if (n >= (int64_t)INT32_MAX) return fail(IA_EINVAL, "ia_index_build: n exceeds int32 row ids");
+  HIP_TRY(hipSetDevice(c->dev));
+  ia_index *x = new ia_index();
+  x->ctx = c;
+  x->n = n;
+  x->d = d;
+  x->KH = KH;
+  x->n_tiles = (int)((n + IA_TILE - 1) / IA_TILE);
+  x->tpw = std::max(4, (x->n_tiles + IA_WG_TARGET - 1) / IA_WG_TARGET);
+  x->nwg = (x->n_tiles + x->tpw - 1) / x->tpw;
+  // column means (host, fixed order): centre the fp32 copy, shrinking the MFMA error bound
+  std::vector<double> mu(d, 0.);
+  for (int64_t i = 0; i < n; i++)
+    for (int f = 0; f < d; f++) mu[f] += pts[i * d + f];
+  for (int f = 0; f < d; f++) mu[f] /= (double)n;
+  int rc;
+  if ((rc = x->pts.ensure((size_t)n * d * 8)) || (rc = x->db.ensure((size_t)x->n_tiles * IA_TILE * 2 * KH * 4)) ||
+      (rc = x->mu.ensure((size_t)d * 8)) || (rc = x->Rbits.ensure(4)) || (rc = x->counters.ensure(32))) {
+    delete x;
+    return rc;
+  }
+  hipMemcpyAsync(x->pts.p, pts, (size_t)n * d * 8, hipMemcpyHostToDevice, c->st);
+  hipMemcpyAsync(x->mu.p, mu.data(), (size_t)d * 8, hipMemcpyHostToDevice, c->st);
+  hipMemsetAsync(x->Rbits.p, 0, 4, c->st);
+  ia_launch_dense_db(KH, x->pts.as<double>(), n, d, x->n_tiles, x->mu.as<double>(), x->db.as<float4>(),
+                     x->Rbits.as<unsigned>(), c->st);
+  hipError_t e = hipStreamSynchronize(c->st);
+  if (e == hipSuccess) e = hipGetLastError();
+  if (e != hipSuccess) {
+    ia_index_destroy(x);
+    return fail(IA_EHIP, std::string("ia_index_build: ") + hipGetErrorString(e));
+  }
+  *out = x;
+  return IA_OK;
+}
+
+int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, double *dist_out) {
+  if (!x || !q || !idx_out || nq < 0) return fail(IA_EINVAL, "ia_index_query: bad arguments");
+  if (nq == 0) return IA_OK;
+  ia_ctx *c = x->ctx;
+  HIP_TRY(hipSetDevice(c->dev));
+  const int64_t BATCH = 4096;
+  const int64_t bmax = std::min(nq, BATCH), bpad = (bmax + IA_TILE - 1) / IA_TILE * IA_TILE;
+  const int DP = 2 * x->KH;
+  int rc;
+  if ((rc = x->q.ensure((size_t)bmax * x->d * 8)) || (rc = x->qn2.ensure((size_t)bpad * 8)) ||
+      (rc = x->qf.ensure((size_t)bpad * DP * 4)) || (rc = x->rec.ensure((size_t)bmax * x->nwg * 16)) ||
+      (rc = x->recT.ensure((size_t)bmax * x->nwg * 4)) || (rc = x->idx.ensure((size_t)bmax * 8)) ||
+      (rc = x->dist.ensure((size_t)bmax * 8)))
+    return rc;
+  HIP_TRY(hipMemsetAsync(x->counters.p, 0, 32, c->st));
+  MergeArgs ma;
+  ma.rec = x->rec.as<float4>();
+  ma.recT = x->recT.as<float>();
+  ma.q64 = nullptr;
+  ma.qn2 = x->qn2.as<double>();
+  ma.Rbits = x->Rbits.as<unsigned>();
+  ma.nwg = x->nwg;
+  ma.tpw = x->tpw;
+  ma.n_tiles_shard = x->n_tiles;
+  ma.row0 = 0;
+  ma.row_end = x->n;
+  ma.counters = x->counters.as<unsigned long long>();
+  ma.eps_c = ia_eps_c(DP);
+  const int qtmax = ia_k3_qtmax(x->KH);
+  for (int64_t b0 = 0; b0 < nq; b0 += BATCH) {
+    const int64_t nb = std::min(BATCH, nq - b0);
+    const int Mpad = (int)((nb + IA_TILE - 1) / IA_TILE * IA_TILE);
+    HIP_TRY(hipMemcpyAsync(x->q.p, q + b0 * x->d, (size_t)nb * x->d * 8, hipMemcpyHostToDevice, c->st));
+    ia_launch_dense_query(x->KH, x->q.as<double>(), nb, x->d, Mpad, x->mu.as<double>(), x->qn2.as<double>(),
+                          x->qf.as<float>(), c->st);
+    const int qtt = Mpad / IA_TILE;
+    for (int qt0 = 0; qt0 < qtt; qt0 += qtmax) {
+      const int qt = std::min(qtmax, qtt - qt0);
+      ia_launch_k3(x->KH, qt, x->db.as<float4>(), x->qf.as<float4>(), x->n_tiles, x->tpw, qt0, (int)nb, x->nwg, 0,
+                   x->rec.as<float4>(), x->recT.as<float>(), c->st);
+    }
+    ia_launch_merge_dense(ma, x->pts.as<double>(), x->d, x->q.as<double>(), nb, x->idx.as<int64_t>(),
+                          x->dist.as<double>(), c->st);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipMemcpyAsync(idx_out + b0, x->idx.p, (size_t)nb * 8, hipMemcpyDeviceToHost, c->st));
+    if (dist_out) HIP_TRY(hipMemcpyAsync(dist_out + b0, x->dist.p, (size_t)nb * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+  }
+  return IA_OK;
+}
+
+void ia_index_destroy(ia_index *x) {
+  if (!x) return;
+  hipSetDevice(x->ctx->dev);
+  hipStreamSynchronize(x->ctx->st);
+  for (DevBuf *b : {&x->pts, &x->db, &x->mu, &x->Rbits, &x->q, &x->q64, &x->qn2, &x->qf, &x->rec, &x->recT, &x->idx,
+                    &x->dist, &x->counters})
+    b->release();
+  delete x;
+}
+
+}  // extern "C"

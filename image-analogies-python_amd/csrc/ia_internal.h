@@ -1,0 +1,88 @@
+// ia_internal.h — shared host/device definitions of libia (MI355X / gfx950 only).
+//
+// Data layout in HBM:
+//   * pyramid levels: row-major fp64 (h, w, ch), exactly the reference's arrays.
+//   * feature DB of a level (create_index, algorithms.py:50-70): N_A rows of D = 55*ch
+//     features, centred by a per-(part, channel) mean mu and stored fp32 together with the
+//     row norm |a'|^2 in column D, zero padded to DP = 2*KH columns.  Rows are grouped in
+//     tiles of 32 and each tile is stored in MFMA-fragment order:
+//         float4 piece p (0..KH/4-1), lane L (0..63):  row  = tile*32 + (L & 31)
+//                                                       cols = (L >> 5)*KH + 4p .. +3
+//     so one wave loads a tile with KH/4 fully coalesced 1 KiB global_load_dwordx4.
+//   * queries of a wavefront step use the same fragment order with values -2*q' and 1.0 in
+//     column D, so one v_mfma_f32_32x32x2_f32 chain yields |a'|^2 - 2 q'.a' = |q-a|^2 - |q'|^2.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define IA_WAVE 64
+#define IA_TILE 32          // DB rows per MFMA tile (M side of 32x32x2)
+#define IA_WG 256           // threads per workgroup for every kernel
+#define IA_MAX_D 168        // max padded feature width (3 channels: 165 + norm -> 168)
+#define IA_WG_TARGET 512    // distance-kernel workgroups per step (2 per CU on 256 CUs)
+#define IA_PAD_NORM 1.0e30f // norm of padding rows: never a candidate
+
+// feature descriptor: which image part, offset and channel
+//   part 0: coarse 3x3 of A (level l-1)   part 1: fine 5x5 of A (level l)
+//   part 2: coarse 3x3 of A'              part 3: first 12 of fine 5x5 of A'
+struct FeatDesc {
+  int8_t part, dy, dx, c;
+};
+
+struct LevelGeo {
+  int ch, D, KH, n_ap;
+  int ah, aw, ahc, awc;     // A level l / l-1 dims
+  int bh, bw, bhc, bwc;     // B level l / l-1 dims
+  int64_t NA;               // DB rows = n_ap * ah * aw
+  int n_tiles;              // ceil(NA / 32) over the whole DB
+  int tile0, tile1;         // this rank's shard [tile0, tile1)
+  int tiles_per_wg, nwg;    // distance-kernel decomposition of the shard
+};
+
+struct Imgs {        // the four pyramid images a feature row reads (see FeatDesc parts)
+  const double *p0;  // coarse (level l-1) of A or B
+  const double *p1;  // fine (level l) of A or B
+  const double *p2;  // coarse of A' or B'
+  const double *p3;  // fine of A' or B'
+  int h, w, hc, wc;  // fine / coarse dims
+  int64_t img_stride_f, img_stride_c;  // per-A'-image strides (0 for B')
+};
+
+struct MergeArgs {
+  const float4 *rec;
+  const float *recT;
+  const double *q64;   // Mpad x D query rows (fp64)
+  const double *qn2;   // |q'|^2 per query
+  const unsigned *Rbits;
+  int nwg, tpw, n_tiles_shard, row0;  // K3 decomposition of this rank's shard
+  int64_t row_end;                    // first row past this rank's shard (clamped to NA)
+  unsigned long long *counters;       // [0] reranked [1] fallbacks [2] coherence wins
+  double eps_c;                       // 1.05 * gamma_(DP+2), see DESIGN.md §4
+};
+
+// per-step wavefront description: pixels (r, t - 3r), r in [r0, r0 + M)
+struct StepDesc {
+  int t, r0, M, Mpad;
+};
+
+// single-rank certified winner of one query
+struct Winner {
+  double d;
+  int64_t idx;
+};
+
+__host__ __device__ inline int ia_reflect(int i, int n) {
+  // np.pad(mode='symmetric') index map for any pad width (img_preprocess.py:81-83)
+  int m = 2 * n;
+  i %= m;
+  if (i < 0) i += m;
+  return i >= n ? m - 1 - i : i;
+}
+
+// error bound of the fp32 MFMA value |a'|^2 - 2q'.a' against exact arithmetic:
+//   |err| <= gamma_n * (|a'|^2 + 2 sum|q'_k a'_k|) <= gamma_n * (R^2 + 2 R |q'|),  n = DP + 2
+// with u = 2^-24, gamma_n = n u / (1 - n u); 5% margin on top.
+inline double ia_eps_c(int DP) {
+  const double nu = (DP + 2) * 5.9604644775390625e-08;
+  return 1.05 * nu / (1.0 - nu);
+}

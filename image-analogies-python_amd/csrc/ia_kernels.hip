@@ -1,0 +1,839 @@
+// ia_kernels.hip — CDNA4 (gfx950) kernels of the Image Analogies best-match path.
+//
+//   K0 k_part_means      deterministic per-(part, channel) means used to centre features
+//   K1 k_db_build        create_index's DB rows (algorithms.py:11-47,50-70) -> fp32 MFMA
+//                        fragment tiles in HBM (+ row norms, + max row norm R)
+//   K2 k_gather_query    BBp_feat of every pixel of one wavefront step
+//                        (image_analogies.py:166-168, algorithms.py:78-89) -> fp64 rows +
+//                        fp32 fragments staged for K3
+//   K3 k3_dist           best_approximate_match's distance scan (algorithms.py:73-75) as a
+//                        v_mfma_f32_32x32x2_f32 contraction |a'|^2 - 2 q'.a' with a fused
+//                        per-query top-2 + certification threshold kept in registers
+//   K4 k_merge_level     exact fp64 rerank of the MFMA candidates (numpy pairwise-sum order,
+//                        lowest-index ties), certification with exact fallback rescan,
+//                        best_coherence_match (algorithms.py:92-130), compute_distance
+//                        (:133-135), the kappa rule (image_analogies.py:206) and the
+//                        B'/s/im writeback (:214-220), one wave per query pixel
+//   dense variants for the FLANN-compatible index (ia_index_*).
+//
+// Build: hipcc --offload-arch=gfx950 -O3 -ffp-contract=off (no FMA contraction: the exact
+// fp64 paths must round exactly like numpy's separate multiply and add).
+#include <hip/hip_runtime.h>
+#include <float.h>
+#include <stdint.h>
+
+#include "ia_internal.h"
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ------------------------------------------------------------------------------------------
+// feature geometry, compile-time per channel count
+// ------------------------------------------------------------------------------------------
+template <int CH>
+struct Geo {
+  static constexpr int D = 55 * CH;
+  static constexpr int DP = ((D + 1 + 7) / 8) * 8;  // + norm column, 16-B aligned halves
+  static constexpr int KH = DP / 2;                 // k-steps of the 32x32x2 chain
+  static constexpr int KP = KH / 4;                 // float4 pieces per lane
+};
+
+// reflected (symmetric-pad) offsets of the 3x3 coarse and 5x5 fine windows of pixel (r, c)
+struct Px {
+  int64_t yc[3], yf[5];  // row offsets (already * width * CH)
+  int xc[3], xf[5];      // column offsets (already * CH)
+};
+template <int CH>
+__device__ __forceinline__ Px make_px(const Imgs &I, int r, int c) {
+  Px P;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    P.yc[k] = (int64_t)ia_reflect((r >> 1) + k - 1, I.hc) * I.wc * CH;
+    P.xc[k] = ia_reflect((c >> 1) + k - 1, I.wc) * CH;
+  }
+#pragma unroll
+  for (int k = 0; k < 5; k++) {
+    P.yf[k] = (int64_t)ia_reflect(r + k - 2, I.h) * I.w * CH;
+    P.xf[k] = ia_reflect(c + k - 2, I.w) * CH;
+  }
+  return P;
+}
+// value of feature f (reference order) of pixel P of image `img`
+// (A' index; 0 on the B side)
+template <int CH>
+__device__ __forceinline__ double featp(const Imgs &I, const Px &P, int f, int img) {
+  if (f < 9 * CH) {
+    const int k = f / CH, ch = f % CH;
+    return I.p0[P.yc[k / 3] + P.xc[k % 3] + ch];
+  } else if (f < 34 * CH) {
+    const int k = (f - 9 * CH) / CH, ch = (f - 9 * CH) % CH;
+    return I.p1[P.yf[k / 5] + P.xf[k % 5] + ch];
+  } else if (f < 43 * CH) {
+    const int k = (f - 34 * CH) / CH, ch = (f - 34 * CH) % CH;
+    return I.p2[img * I.img_stride_c + P.yc[k / 3] + P.xc[k % 3] + ch];
+  } else {
+    const int k = (f - 43 * CH) / CH, ch = (f - 43 * CH) % CH;
+    return I.p3[img * I.img_stride_f + P.yf[k / 5] + P.xf[k % 5] + ch];
+  }
+}
+template <int CH>
+__device__ __forceinline__ double feat(const Imgs &I, int f, int r, int c, int img) {
+  int part, k, ch;
+  if (f < 9 * CH) {
+    part = 0; k = f / CH; ch = f % CH;
+  } else if (f < 34 * CH) {
+    part = 1; k = (f - 9 * CH) / CH; ch = (f - 9 * CH) % CH;
+  } else if (f < 43 * CH) {
+    part = 2; k = (f - 34 * CH) / CH; ch = (f - 34 * CH) % CH;
+  } else {
+    part = 3; k = (f - 43 * CH) / CH; ch = (f - 43 * CH) % CH;
+  }
+  if (part == 0 || part == 2) {  // 3x3 at (floor(r/2), floor(c/2)) of the padded coarse level
+    int y = ia_reflect((r >> 1) + k / 3 - 1, I.hc), x = ia_reflect((c >> 1) + k % 3 - 1, I.wc);
+    const double *b = part == 0 ? I.p0 : I.p2 + img * I.img_stride_c;
+    return b[((int64_t)y * I.wc + x) * CH + ch];
+  } else {  // 5x5 at (r, c) of the padded fine level (part 3 only reaches k < 12)
+    int y = ia_reflect(r + k / 5 - 2, I.h), x = ia_reflect(c + k % 5 - 2, I.w);
+    const double *b = part == 1 ? I.p1 : I.p3 + img * I.img_stride_f;
+    return b[((int64_t)y * I.w + x) * CH + ch];
+  }
+}
+
+template <int CH>
+__device__ __forceinline__ int feat_part(int f) {
+  return f < 9 * CH ? 0 : f < 34 * CH ? 1 : f < 43 * CH ? 2 : 3;
+}
+template <int CH>
+__device__ __forceinline__ int feat_ch(int f) {
+  return (f < 9 * CH ? f : f < 34 * CH ? f - 9 * CH : f < 43 * CH ? f - 34 * CH : f - 43 * CH) % CH;
+}
+
+// numpy pairwise_sum (loops_utils.h.src) over n <= 128 terms produced in order by term(i)
+template <int N, class T>
+__device__ __forceinline__ double pw_block(T &&term, int off) {
+  static_assert(N <= 128, "block");
+  if constexpr (N < 8) {
+    double res = 0.;
+#pragma unroll
+    for (int i = 0; i < N; i++) res += term(off + i);
+    return res;
+  } else {
+    double r[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[j] = term(off + j);
+    constexpr int NB = N - (N % 8);
+#pragma unroll
+    for (int i = 8; i < NB; i += 8) {
+#pragma unroll
+      for (int j = 0; j < 8; j++) r[j] += term(off + i + j);
+    }
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+    for (int i = NB; i < N; i++) res += term(off + i);
+    return res;
+  }
+}
+template <int N, class T>
+__device__ __forceinline__ double pw_sum(T &&term) {
+  if constexpr (N <= 128) {
+    return pw_block<N>(term, 0);
+  } else {
+    constexpr int N2 = N / 2 - (N / 2) % 8;
+    static_assert(N - N2 <= 128, "single split");
+    return pw_block<N2>(term, 0) + pw_block<N - N2>(term, N2);
+  }
+}
+// runtime-length version (dense index path, n <= 167)
+template <class T>
+__device__ double pw_block_rt(T &&term, int off, int n) {
+  if (n < 8) {
+    double res = 0.;
+    for (int i = 0; i < n; i++) res += term(off + i);
+    return res;
+  }
+  double r[8];
+#pragma unroll
+  for (int j = 0; j < 8; j++) r[j] = term(off + j);
+  int nb = n - (n % 8), i = 8;
+  for (; i < nb; i += 8) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) r[j] += term(off + i + j);
+  }
+  double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; i++) res += term(off + i);
+  return res;
+}
+template <class T>
+__device__ double pw_sum_rt(T &&term, int n) {
+  if (n <= 128) return pw_block_rt(term, 0, n);
+  int n2 = n / 2;
+  n2 -= n2 % 8;
+  return pw_block_rt(term, 0, n2) + pw_block_rt(term, n2, n - n2);
+}
+
+// ------------------------------------------------------------------------------------------
+// wave helpers (64 lanes)
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ float wave_min_f(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fminf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double wave_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+// lexicographic (d, idx) minimum across the wave; every lane gets the result
+__device__ __forceinline__ void wave_min_di(double &d, int64_t &idx) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    double od = __shfl_xor(d, o, 64);
+    int64_t oi = __shfl_xor(idx, o, 64);
+    if (od < d || (od == d && oi < idx)) {
+      d = od;
+      idx = oi;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K0: per-(part, channel) means of the A-side images (deterministic tree reduction)
+// ------------------------------------------------------------------------------------------
+template <int CH>
+__global__ void __launch_bounds__(IA_WG) k_part_means(Imgs A, int n_ap, double *mu_part) {
+  const int part = blockIdx.x / CH, ch = blockIdx.x % CH;
+  const double *base = part == 0 ? A.p0 : part == 1 ? A.p1 : part == 2 ? A.p2 : A.p3;
+  int64_t npx = (part & 1) ? (int64_t)A.h * A.w : (int64_t)A.hc * A.wc;
+  if (part >= 2) npx *= n_ap;  // A' images are contiguous
+  double s = 0.;
+  for (int64_t i = threadIdx.x; i < npx; i += IA_WG) s += base[i * CH + ch];
+  __shared__ double red[IA_WG];
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = IA_WG / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) mu_part[blockIdx.x] = red[0] / (double)npx;
+}
+
+// ------------------------------------------------------------------------------------------
+// K1: DB tiles of this rank's shard (one thread per DB row)
+// ------------------------------------------------------------------------------------------
+template <int CH>
+__global__ void __launch_bounds__(IA_WG) k_db_build(LevelGeo g, Imgs A, const double *__restrict__ mu_part,
+                                                     float4 *__restrict__ db, unsigned *__restrict__ Rbits) {
+  using G = Geo<CH>;
+  const int64_t row = (int64_t)g.tile0 * IA_TILE + (int64_t)blockIdx.x * IA_WG + threadIdx.x;
+  if (row >= (int64_t)g.tile1 * IA_TILE) return;
+  const int64_t ltile = row / IA_TILE - g.tile0;
+  const int j = (int)(row % IA_TILE);
+  const bool real = row < g.NA;
+  int img = 0, pr = 0, pc = 0;
+  if (real) {
+    const int64_t hw = (int64_t)g.ah * g.aw;
+    img = (int)(row / hw);
+    const int64_t rem = row - img * hw;
+    pr = (int)(rem / g.aw);
+    pc = (int)(rem % g.aw);
+  }
+  const Px P = make_px<CH>(A, pr, pc);
+  double norm = 0.;
+#pragma unroll
+  for (int h = 0; h < 2; h++) {
+#pragma unroll
+    for (int p = 0; p < G::KP; p++) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int f = h * G::KH + 4 * p + e;
+        if (f < G::D) {
+          double a = 0.;
+          if (real) {
+            a = featp<CH>(A, P, f, img) - mu_part[feat_part<CH>(f) * CH + feat_ch<CH>(f)];
+            norm += a * a;
+          }
+          v[e] = (float)a;
+        } else if (f == G::D) {
+          v[e] = real ? (float)norm : IA_PAD_NORM;
+        } else {
+          v[e] = 0.f;
+        }
+      }
+      db[(ltile * G::KP + p) * IA_WAVE + h * IA_TILE + j] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  if (real) {
+    // upper bound on |a'| (R of the certification bound), atomicMax on non-negative float bits
+    float R = (float)(sqrt(norm) * (1.0 + 1e-6)) ;
+    atomicMax(Rbits, __float_as_uint(R));
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K2: queries of one wavefront step (one wave per query pixel)
+// ------------------------------------------------------------------------------------------
+template <int CH>
+__device__ __forceinline__ void put_qfrag(float *qf, int m, int f, float v) {
+  using G = Geo<CH>;
+  const int qt = m / IA_TILE, j = m % IA_TILE, h = f / G::KH, s = f % G::KH;
+  qf[(((int64_t)qt * G::KP + s / 4) * IA_WAVE + h * IA_TILE + j) * 4 + (s % 4)] = v;
+}
+
+template <int CH>
+__global__ void __launch_bounds__(IA_WG) k_gather_query(LevelGeo g, StepDesc sd, Imgs B, const double *__restrict__ mu_part,
+                                                         double *__restrict__ q64, double *__restrict__ qn2,
+                                                         float *__restrict__ qf) {
+  using G = Geo<CH>;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  if (m >= sd.Mpad) return;
+  if (m >= sd.M) {
+    for (int f = lane; f < G::DP; f += IA_WAVE) put_qfrag<CH>(qf, m, f, 0.f);
+    return;
+  }
+  const int r = sd.r0 + m, c = sd.t - 3 * r;
+  double ss = 0.;
+  for (int f = lane; f < G::DP; f += IA_WAVE) {
+    if (f < G::D) {
+      const double v = feat<CH>(B, f, r, c, 0);
+      q64[(int64_t)m * G::D + f] = v;
+      const double qc = v - mu_part[feat_part<CH>(f) * CH + feat_ch<CH>(f)];
+      ss += qc * qc;
+      put_qfrag<CH>(qf, m, f, -2.f * (float)qc);
+    } else {
+      put_qfrag<CH>(qf, m, f, f == G::D ? 1.f : 0.f);
+    }
+  }
+  ss = wave_sum_d(ss);
+  if (lane == 0) qn2[m] = ss;
+}
+
+// ------------------------------------------------------------------------------------------
+// K3: MFMA distance scan with fused top-2 / threshold (the hot kernel)
+//
+// grid.x = nwg workgroups of 4 waves; WG w owns DB tiles [w*tpw, (w+1)*tpw) of the shard,
+// wave v takes tiles w*tpw + v, +4, ... .  QT query tiles (32 queries each) are staged in
+// LDS once; each DB tile is loaded once into registers (KH floats per lane) and contracted
+// against every query tile:  C[row][query] = sum_k DB[row][k] * Qf[k][query]
+//   A operand = DB row (lane & 31), B operand = query (lane & 31), k-half = lane >> 5;
+//   C layout: lane holds query (lane & 31), rows (r&3) + 8(r>>2) + 4(lane>>5), r = 0..15.
+// Each lane keeps, per query tile, the best (value, row) and the second-smallest value of
+// the rows it has seen ("subset" = lane half x wave); the workgroup merges its 8 subsets into
+// a top-2 list + threshold T (every unlisted row of the chunk has approx value >= T).
+// ------------------------------------------------------------------------------------------
+struct Top2 {
+  float v1, v2, T;
+  int i1, i2;
+};
+__device__ __forceinline__ bool lt(float va, int ia, float vb, int ib) {
+  return va < vb || (va == vb && ia < ib);
+}
+__device__ __forceinline__ void top2_insert(Top2 &a, float v, int i, float &third) {
+  if (lt(v, i, a.v1, a.i1)) {
+    third = fminf(third, a.v2);
+    a.v2 = a.v1; a.i2 = a.i1; a.v1 = v; a.i1 = i;
+  } else if (lt(v, i, a.v2, a.i2)) {
+    third = fminf(third, a.v2);
+    a.v2 = v; a.i2 = i;
+  } else {
+    third = fminf(third, v);
+  }
+}
+__device__ __forceinline__ Top2 top2_merge(Top2 a, const Top2 &b) {
+  float third = FLT_MAX;
+  top2_insert(a, b.v1, b.i1, third);
+  top2_insert(a, b.v2, b.i2, third);
+  a.T = fminf(fminf(a.T, b.T), third);
+  return a;
+}
+
+template <int KH, int QT>
+__global__ void __launch_bounds__(IA_WG, 2)
+k3_dist(const float4 *__restrict__ db, const float4 *__restrict__ qf, int n_tiles, int tpw, int qt0, int M,
+        int nwg, int row0, float4 *__restrict__ rec, float *__restrict__ recT) {
+  constexpr int KP = KH / 4;
+  extern __shared__ float4 lds[];  // QT * KP * 64 float4 (queries), reused for the merge
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
+  const int wg = blockIdx.x;
+
+  const float4 *qsrc = qf + (int64_t)qt0 * KP * IA_WAVE;
+  for (int i = threadIdx.x; i < QT * KP * IA_WAVE; i += IA_WG) lds[i] = qsrc[i];
+  __syncthreads();
+
+  float b1[QT], b2[QT];
+  int i1[QT];
+#pragma unroll
+  for (int q = 0; q < QT; q++) {
+    b1[q] = FLT_MAX;
+    b2[q] = FLT_MAX;
+    i1[q] = 0x7fffffff;
+  }
+
+  const int t_begin = wg * tpw, t_end = min(n_tiles, t_begin + tpw);
+  int t = t_begin + wave;
+  float a[KH], an[KH];
+  {
+    const int tl = min(t, n_tiles - 1);
+    const float4 *src = db + (int64_t)tl * KP * IA_WAVE + lane;
+#pragma unroll
+    for (int p = 0; p < KP; p++) {
+      float4 v = src[p * IA_WAVE];
+      a[4 * p] = v.x; a[4 * p + 1] = v.y; a[4 * p + 2] = v.z; a[4 * p + 3] = v.w;
+    }
+  }
+  for (; t < t_end; t += 4) {
+    {  // prefetch the next tile of this wave (clamped: always issue, never branch per load)
+      const int tl = min(t + 4, n_tiles - 1);
+      const float4 *src = db + (int64_t)tl * KP * IA_WAVE + lane;
+#pragma unroll
+      for (int p = 0; p < KP; p++) {
+        float4 v = src[p * IA_WAVE];
+        an[4 * p] = v.x; an[4 * p + 1] = v.y; an[4 * p + 2] = v.z; an[4 * p + 3] = v.w;
+      }
+    }
+    const int rbase = row0 + t * IA_TILE + 4 * half;
+    asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
+#pragma unroll
+    for (int q = 0; q < QT; q++) {
+      f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const float4 *qb = lds + q * KP * IA_WAVE + lane;
+#pragma unroll
+      for (int p = 0; p < KP; p++) {
+        const float4 bq = qb[p * IA_WAVE];
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p], bq.x, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 1], bq.y, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 2], bq.z, acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 3], bq.w, acc, 0, 0, 0);
+      }
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const float v = acc[r];
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        b2[q] = fminf(b2[q], fmaxf(b1[q], v));
+        const bool c = v < b1[q];
+        i1[q] = c ? row : i1[q];
+        b1[q] = fminf(b1[q], v);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < KH; k++) a[k] = an[k];
+  }
+
+  // ---- merge the 8 subsets of each query: lane halves by shuffle, waves through LDS
+  __syncthreads();  // queries no longer needed: reuse LDS
+  Top2 *red = reinterpret_cast<Top2 *>(lds);  // [4 waves][QT][32]
+#pragma unroll
+  for (int q = 0; q < QT; q++) {
+    Top2 mine = {b1[q], FLT_MAX, b2[q], i1[q], 0x7fffffff};
+    Top2 other;
+    other.v1 = __shfl_xor(b1[q], 32, 64);
+    other.i1 = __shfl_xor(i1[q], 32, 64);
+    other.T = __shfl_xor(b2[q], 32, 64);
+    other.v2 = FLT_MAX;
+    other.i2 = 0x7fffffff;
+    Top2 mrg = half == 0 ? top2_merge(mine, other) : top2_merge(other, mine);
+    if (half == 0) red[(wave * QT + q) * IA_TILE + lane] = mrg;
+  }
+  __syncthreads();
+  for (int x = threadIdx.x; x < QT * IA_TILE; x += IA_WG) {
+    Top2 m = red[x];
+#pragma unroll
+    for (int w = 1; w < 4; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
+    const int qg = qt0 * IA_TILE + x;
+    if (qg < M) {
+      rec[(int64_t)qg * nwg + wg] = make_float4(m.v1, __int_as_float(m.i1), m.v2, __int_as_float(m.i2));
+      recT[(int64_t)qg * nwg + wg] = m.T;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// K4: exact rerank + certification (+ coherence, kappa rule, writeback) — one wave / query
+// ------------------------------------------------------------------------------------------
+// exact DB-row distance of row `row` (level path): ((a - q)**2).sum() in numpy order
+template <int CH>
+__device__ __forceinline__ double exact_dist_level(const LevelGeo &g, const Imgs &A, int64_t row, const double *q) {
+  const int64_t hw = (int64_t)g.ah * g.aw;
+  const int img = (int)(row / hw);
+  const int64_t rem = row - img * hw;
+  const Px P = make_px<CH>(A, (int)(rem / g.aw), (int)(rem % g.aw));
+  return pw_sum<Geo<CH>::D>([&](int f) {
+    const double d = featp<CH>(A, P, f, img) - q[f];
+    return d * d;
+  });
+}
+
+// the certified single-rank winner of query m (exact NN over this rank's shard)
+template <class DistFn>
+__device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist) {
+  const int lane = threadIdx.x & 63;
+  const float4 *rr = a.rec + (int64_t)m * a.nwg;
+  const float *rT = a.recT + (int64_t)m * a.nwg;
+  float a1 = FLT_MAX;
+  for (int w = lane; w < a.nwg; w += IA_WAVE) a1 = fminf(a1, rr[w].x);
+  a1 = wave_min_f(a1);
+  const double R = (double)__uint_as_float(*a.Rbits);
+  const double qn2 = a.qn2[m];
+  const double eps = a.eps_c * (R * R + 2.0 * R * sqrt(qn2));
+  const double thr = (double)a1 + 2.0 * eps;
+
+  double bd = DBL_MAX;
+  int64_t bi = INT64_MAX;
+  unsigned long long nre = 0;
+  for (int w = lane; w < a.nwg; w += IA_WAVE) {
+    const float4 x = rr[w];
+    if ((double)x.x <= thr && __float_as_int(x.y) >= a.row0 && __float_as_int(x.y) < a.row_end) {
+      const int64_t i = __float_as_int(x.y);
+      const double d = dist(i);
+      nre++;
+      if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
+    }
+    if ((double)x.z <= thr && __float_as_int(x.w) >= a.row0 && __float_as_int(x.w) < a.row_end) {
+      const int64_t i = __float_as_int(x.w);
+      const double d = dist(i);
+      nre++;
+      if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
+    }
+  }
+  wave_min_di(bd, bi);
+
+  // certification: every unlisted row of chunk w has MFMA value >= T_w, hence true distance
+  // >= T_w + |q'|^2 - eps.  Chunks with T_w <= theta may hide a row that beats or ties bd.
+  const double theta = bd - qn2 + eps + 1e-13 * (bd + 1.0);
+  unsigned long long nfb = 0;
+  for (int base = 0; base < a.nwg; base += IA_WAVE) {
+    const int w = base + lane;
+    const bool unc = w < a.nwg && (double)rT[w] <= theta;
+    unsigned long long mask = __ballot(unc);
+    while (mask) {
+      const int j = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const int wgid = base + j;
+      const int64_t r0 = (int64_t)a.row0 + (int64_t)wgid * a.tpw * IA_TILE;
+      const int64_t r1 = min(a.row_end, r0 + (int64_t)a.tpw * IA_TILE);
+      double cd = DBL_MAX;
+      int64_t ci = INT64_MAX;
+      for (int64_t i = r0 + lane; i < r1; i += IA_WAVE) {
+        const double d = dist(i);
+        if (d < cd || (d == cd && i < ci)) { cd = d; ci = i; }
+      }
+      wave_min_di(cd, ci);
+      if (cd < bd || (cd == bd && ci < bi)) { bd = cd; bi = ci; }
+      nfb++;
+    }
+  }
+  // stats: one atomic per wave
+  unsigned long long tot = nre;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
+  if (lane == 0) {
+    atomicAdd(&a.counters[0], tot);
+    if (nfb) atomicAdd(&a.counters[1], nfb);
+  }
+  return Winner{bd, bi};
+}
+
+// coherence + kappa + writeback for query pixel (r, c) whose NN row is app_ix
+// (image_analogies.py:182-220, algorithms.py:92-135)
+template <int CH>
+__device__ void finish_pixel(const LevelGeo &g, const Imgs &A, int r, int c, int64_t app_ix, const double *q,
+                             int32_t *__restrict__ s, int32_t *__restrict__ im, double *__restrict__ Bp,
+                             const double *__restrict__ weights, double kf, unsigned long long *counters) {
+  constexpr int D = Geo<CH>::D;
+  const int lane = threadIdx.x & 63;
+  const int64_t hw = (int64_t)g.ah * g.aw;
+  const int qi = r * g.bw + c;
+  int img = (int)(app_ix / hw);
+  int64_t rem = app_ix - img * hw;
+  int pr = (int)(rem / g.aw), pc = (int)(rem % g.aw);
+  bool coh_won = false;
+  if (qi > 0) {
+    // best_coherence_match: candidates in product(rows, cols) order, first argmin of the norm
+    double dk = DBL_MAX;
+    int64_t kk = INT64_MAX;
+    int cpr = -1, cpc = -1, cim = 0;
+    if (lane < 15) {
+      const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
+      if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
+        const int nb = nr * g.bw + nc;
+        const int tr = s[2 * nb] + r - nr, tc = s[2 * nb + 1] + c - nc;
+        if (tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) {
+          cim = im[nb];
+          cpr = tr;
+          cpc = tc;
+          const int64_t row = (int64_t)cim * hw + (int64_t)tr * g.aw + tc;
+          dk = sqrt(exact_dist_level<CH>(g, A, row, q));
+          kk = lane;
+        }
+      }
+    }
+    wave_min_di(dk, kk);
+    if (kk != INT64_MAX) {
+      const int src = (int)kk;
+      cpr = __shfl(cpr, src, 64);
+      cpc = __shfl(cpc, src, 64);
+      cim = __shfl(cim, src, 64);
+      // compute_distance(AAp_feat, BBp_feat, weights) = norm((a - q) * w)**2 for app and coh
+      double part = 0.;
+      if (lane < 2) {
+        const int ii = lane == 0 ? img : cim, rr_ = lane == 0 ? pr : cpr, cc_ = lane == 0 ? pc : cpc;
+        const Px P = make_px<CH>(A, rr_, cc_);
+#pragma unroll
+        for (int f = 0; f < D; f++) {
+          const double x = (featp<CH>(A, P, f, ii) - q[f]) * weights[f];
+          part += x * x;
+        }
+        part = sqrt(part);
+        part = part * part;
+      }
+      const double d_app = __shfl(part, 0, 64), d_coh = __shfl(part, 1, 64);
+      if (d_coh <= d_app * kf) {
+        img = cim;
+        pr = cpr;
+        pc = cpc;
+        coh_won = true;
+      }
+    }
+  }
+  if (lane < CH) Bp[(int64_t)qi * CH + lane] = A.p3[img * A.img_stride_f + ((int64_t)pr * g.aw + pc) * CH + lane];
+  if (lane == 0) {
+    s[2 * qi] = pr;
+    s[2 * qi + 1] = pc;
+    im[qi] = img;
+    if (coh_won) atomicAdd(&counters[2], 1ull);
+  }
+}
+
+template <int CH, bool FUSED>
+__global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, Winner *__restrict__ win,
+                                                        int32_t *__restrict__ s, int32_t *__restrict__ im,
+                                                        double *__restrict__ Bp, const double *__restrict__ weights,
+                                                        double kf) {
+  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  if (m >= sd.M) return;
+  const double *q = ma.q64 + (int64_t)m * Geo<CH>::D;
+  const Winner wn = certified_winner(ma, m, [&](int64_t row) { return exact_dist_level<CH>(g, A, row, q); });
+  if constexpr (FUSED) {
+    const int r = sd.r0 + m;
+    finish_pixel<CH>(g, A, r, sd.t - 3 * r, wn.idx, q, s, im, Bp, weights, kf, ma.counters);
+  } else {
+    if ((threadIdx.x & 63) == 0) win[m] = wn;
+  }
+}
+
+// multi-rank finish: global winner over the all-gathered per-rank winners, then coherence
+template <int CH>
+__global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd, Imgs A, const double *__restrict__ q64,
+                                                         const Winner *__restrict__ allwin, int world, int Mstride,
+                                                         int32_t *__restrict__ s, int32_t *__restrict__ im,
+                                                         double *__restrict__ Bp, const double *__restrict__ weights,
+                                                         double kf, unsigned long long *counters) {
+  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  if (m >= sd.M) return;
+  double bd = DBL_MAX;
+  int64_t bi = INT64_MAX;
+  for (int k = 0; k < world; k++) {  // same order on every rank -> identical replicas
+    const Winner w = allwin[(int64_t)k * Mstride + m];
+    if (w.d < bd || (w.d == bd && w.idx < bi)) { bd = w.d; bi = w.idx; }
+  }
+  const int r = sd.r0 + m;
+  finish_pixel<CH>(g, A, r, sd.t - 3 * r, bi, q64 + (int64_t)m * Geo<CH>::D, s, im, Bp, weights, kf, counters);
+}
+
+// ------------------------------------------------------------------------------------------
+// dense (FLANN-compatible index) variants: rows given as n x d fp64
+// ------------------------------------------------------------------------------------------
+template <int KH>
+__global__ void __launch_bounds__(IA_WG) k_dense_db_build(const double *__restrict__ pts, int64_t n, int d, int n_tiles,
+                                                           const double *__restrict__ mu, float4 *__restrict__ db,
+                                                           unsigned *__restrict__ Rbits) {
+  constexpr int KP = KH / 4;
+  const int64_t row = (int64_t)blockIdx.x * IA_WG + threadIdx.x;
+  if (row >= (int64_t)n_tiles * IA_TILE) return;
+  const bool real = row < n;
+  const int64_t tile = row / IA_TILE;
+  const int j = (int)(row % IA_TILE);
+  double norm = 0.;
+  for (int h = 0; h < 2; h++) {
+    for (int p = 0; p < KP; p++) {
+      float v[4];
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        const int f = h * KH + 4 * p + e;
+        if (f < d) {
+          double a = real ? pts[row * d + f] - mu[f] : 0.;
+          norm += a * a;
+          v[e] = (float)a;
+        } else if (f == d) {
+          v[e] = real ? (float)norm : IA_PAD_NORM;
+        } else {
+          v[e] = 0.f;
+        }
+      }
+      db[(tile * KP + p) * IA_WAVE + h * IA_TILE + j] = make_float4(v[0], v[1], v[2], v[3]);
+    }
+  }
+  if (real) atomicMax(Rbits, __float_as_uint((float)(sqrt(norm) * (1.0 + 1e-6))));
+}
+
+template <int KH>
+__global__ void __launch_bounds__(IA_WG) k_dense_query(const double *__restrict__ q, int64_t nq, int d, int Mpad,
+                                                        const double *__restrict__ mu, double *__restrict__ qn2,
+                                                        float *__restrict__ qf) {
+  constexpr int KP = KH / 4;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  if (m >= Mpad) return;
+  double ss = 0.;
+  for (int f = lane; f < 2 * KH; f += IA_WAVE) {
+    float v = 0.f;
+    if (m < nq && f < d) {
+      const double qc = q[(int64_t)m * d + f] - mu[f];
+      ss += qc * qc;
+      v = -2.f * (float)qc;
+    } else if (m < nq && f == d) {
+      v = 1.f;
+    }
+    const int qt = m / IA_TILE, j = m % IA_TILE, h = f / KH, s = f % KH;
+    qf[(((int64_t)qt * KP + s / 4) * IA_WAVE + h * IA_TILE + j) * 4 + (s % 4)] = v;
+  }
+  ss = wave_sum_d(ss);
+  if (lane == 0 && m < nq) qn2[m] = ss;
+}
+
+__global__ void __launch_bounds__(IA_WG) k_merge_dense(MergeArgs ma, const double *__restrict__ pts, int d, const double *__restrict__ q,
+                                                        int64_t nq, int64_t *__restrict__ idx_out, double *__restrict__ dist_out) {
+  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  if (m >= nq) return;
+  const double *qm = q + (int64_t)m * d;
+  const Winner wn = certified_winner(ma, m, [&](int64_t row) {
+    const double *a = pts + row * d;
+    return pw_sum_rt([&](int f) {
+      const double x = a[f] - qm[f];
+      return x * x;
+    }, d);
+  });
+  if ((threadIdx.x & 63) == 0) {
+    idx_out[m] = wn.idx;
+    dist_out[m] = wn.d;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host-side launchers (called from ia_capi.cpp)
+// ------------------------------------------------------------------------------------------
+#include "ia_launch.h"
+
+static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
+template <int CH>
+static void launch_means_t(const Imgs &A, int n_ap, double *mu, hipStream_t st) {
+  hipLaunchKernelGGL(k_part_means<CH>, dim3(4 * CH), dim3(IA_WG), 0, st, A, n_ap, mu);
+}
+void ia_launch_means(int ch, const Imgs &A, int n_ap, double *mu, hipStream_t st) {
+  if (ch == 1) launch_means_t<1>(A, n_ap, mu, st);
+  else if (ch == 2) launch_means_t<2>(A, n_ap, mu, st);
+  else launch_means_t<3>(A, n_ap, mu, st);
+}
+
+template <int CH>
+static void launch_db_t(const LevelGeo &g, const Imgs &A, const double *mu, float4 *db, unsigned *Rbits, hipStream_t st) {
+  const int64_t rows = (int64_t)(g.tile1 - g.tile0) * IA_TILE;
+  hipLaunchKernelGGL(k_db_build<CH>, dim3(cdiv(rows, IA_WG)), dim3(IA_WG), 0, st, g, A, mu, db, Rbits);
+}
+void ia_launch_db_build(const LevelGeo &g, const Imgs &A, const double *mu, float4 *db, unsigned *Rbits, hipStream_t st) {
+  if (g.ch == 1) launch_db_t<1>(g, A, mu, db, Rbits, st);
+  else if (g.ch == 2) launch_db_t<2>(g, A, mu, db, Rbits, st);
+  else launch_db_t<3>(g, A, mu, db, Rbits, st);
+}
+
+template <int CH>
+static void launch_gather_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64,
+                            double *qn2, float *qf, hipStream_t st) {
+  hipLaunchKernelGGL(k_gather_query<CH>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, mu, q64,
+                     qn2, qf);
+}
+void ia_launch_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64, double *qn2,
+                      float *qf, hipStream_t st) {
+  if (g.ch == 1) launch_gather_t<1>(g, sd, B, mu, q64, qn2, qf, st);
+  else if (g.ch == 2) launch_gather_t<2>(g, sd, B, mu, q64, qn2, qf, st);
+  else launch_gather_t<3>(g, sd, B, mu, q64, qn2, qf, st);
+}
+
+// K3 dispatch table: QT query tiles per launch (1..QTMAX(KH))
+typedef void (*k3_fn)(const float4 *, const float4 *, int, int, int, int, int, int, float4 *, float *);
+template <int KH, int... QTs>
+struct K3Table {
+  static k3_fn get(int qt) {
+    static const k3_fn tab[] = {k3_dist<KH, QTs>...};
+    return tab[qt - 1];
+  }
+};
+int ia_k3_qtmax(int KH) { return KH == 28 ? 11 : KH == 56 ? 5 : 3; }
+
+void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tiles, int tpw, int qt0, int M, int nwg,
+                  int row0, float4 *rec, float *recT, hipStream_t st) {
+  k3_fn fn;
+  if (KH == 28) fn = K3Table<28, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11>::get(qt);
+  else if (KH == 56) fn = K3Table<56, 1, 2, 3, 4, 5>::get(qt);
+  else fn = K3Table<84, 1, 2, 3>::get(qt);
+  const size_t lds = (size_t)qt * (KH / 4) * IA_WAVE * sizeof(float4);
+  static bool attr_set[3][16] = {};
+  const int ki = KH == 28 ? 0 : KH == 56 ? 1 : 2;
+  if (!attr_set[ki][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
+    (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set[ki][qt] = true;
+  }
+  hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WG), lds, st, db, qf, n_tiles, tpw, qt0, M, nwg, row0, rec, recT);
+}
+
+template <int CH>
+static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
+                           int32_t *s, int32_t *im, double *Bp, const double *w, double kf, bool fused, hipStream_t st) {
+  dim3 grid(cdiv(sd.M, IA_WG / IA_WAVE));
+  if (fused)
+    hipLaunchKernelGGL((k_merge_level<CH, true>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, s, im, Bp, w, kf);
+  else
+    hipLaunchKernelGGL((k_merge_level<CH, false>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, s, im, Bp, w, kf);
+}
+void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win, int32_t *s,
+                     int32_t *im, double *Bp, const double *w, double kf, bool fused, hipStream_t st) {
+  if (g.ch == 1) launch_merge_t<1>(g, sd, A, ma, win, s, im, Bp, w, kf, fused, st);
+  else if (g.ch == 2) launch_merge_t<2>(g, sd, A, ma, win, s, im, Bp, w, kf, fused, st);
+  else launch_merge_t<3>(g, sd, A, ma, win, s, im, Bp, w, kf, fused, st);
+}
+
+template <int CH>
+static void launch_finish_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *q64, const Winner *allwin,
+                            int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w, double kf,
+                            unsigned long long *ctr, hipStream_t st) {
+  hipLaunchKernelGGL(k_finish_level<CH>, dim3(cdiv(sd.M, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, A, q64, allwin,
+                     world, Mstride, s, im, Bp, w, kf, ctr);
+}
+void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *q64, const Winner *allwin,
+                      int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w, double kf,
+                      unsigned long long *ctr, hipStream_t st) {
+  if (g.ch == 1) launch_finish_t<1>(g, sd, A, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
+  else if (g.ch == 2) launch_finish_t<2>(g, sd, A, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
+  else launch_finish_t<3>(g, sd, A, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
+}
+
+void ia_launch_dense_db(int KH, const double *pts, int64_t n, int d, int n_tiles, const double *mu, float4 *db,
+                        unsigned *Rbits, hipStream_t st) {
+  dim3 grid(cdiv((int64_t)n_tiles * IA_TILE, IA_WG));
+  if (KH == 28) hipLaunchKernelGGL(k_dense_db_build<28>, grid, dim3(IA_WG), 0, st, pts, n, d, n_tiles, mu, db, Rbits);
+  else if (KH == 56) hipLaunchKernelGGL(k_dense_db_build<56>, grid, dim3(IA_WG), 0, st, pts, n, d, n_tiles, mu, db, Rbits);
+  else hipLaunchKernelGGL(k_dense_db_build<84>, grid, dim3(IA_WG), 0, st, pts, n, d, n_tiles, mu, db, Rbits);
+}
+void ia_launch_dense_query(int KH, const double *q, int64_t nq, int d, int Mpad, const double *mu, double *qn2, float *qf,
+                           hipStream_t st) {
+  dim3 grid(cdiv(Mpad, IA_WG / IA_WAVE));
+  if (KH == 28) hipLaunchKernelGGL(k_dense_query<28>, grid, dim3(IA_WG), 0, st, q, nq, d, Mpad, mu, qn2, qf);
+  else if (KH == 56) hipLaunchKernelGGL(k_dense_query<56>, grid, dim3(IA_WG), 0, st, q, nq, d, Mpad, mu, qn2, qf);
+  else hipLaunchKernelGGL(k_dense_query<84>, grid, dim3(IA_WG), 0, st, q, nq, d, Mpad, mu, qn2, qf);
+}
+void ia_launch_merge_dense(const MergeArgs &ma, const double *pts, int d, const double *q, int64_t nq, int64_t *idx,
+                           double *dist, hipStream_t st) {
+  hipLaunchKernelGGL(k_merge_dense, dim3(cdiv(nq, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, ma, pts, d, q, nq, idx, dist);
+}

@@ -1,0 +1,24 @@
+// ia_launch.h — host launchers of the kernels in ia_kernels.hip (used by ia_capi.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "ia_internal.h"
+
+void ia_launch_means(int ch, const Imgs &A, int n_ap, double *mu, hipStream_t st);
+void ia_launch_db_build(const LevelGeo &g, const Imgs &A, const double *mu, float4 *db, unsigned *Rbits, hipStream_t st);
+void ia_launch_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64, double *qn2,
+                      float *qf, hipStream_t st);
+int ia_k3_qtmax(int KH);
+void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tiles, int tpw, int qt0, int M, int nwg,
+                  int row0, float4 *rec, float *recT, hipStream_t st);
+void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win, int32_t *s,
+                     int32_t *im, double *Bp, const double *w, double kf, bool fused, hipStream_t st);
+void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *q64, const Winner *allwin,
+                      int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w, double kf,
+                      unsigned long long *ctr, hipStream_t st);
+void ia_launch_dense_db(int KH, const double *pts, int64_t n, int d, int n_tiles, const double *mu, float4 *db,
+                        unsigned *Rbits, hipStream_t st);
+void ia_launch_dense_query(int KH, const double *q, int64_t nq, int d, int Mpad, const double *mu, double *qn2, float *qf,
+                           hipStream_t st);
+void ia_launch_merge_dense(const MergeArgs &ma, const double *pts, int d, const double *q, int64_t nq, int64_t *idx,
+                           double *dist, hipStream_t st);

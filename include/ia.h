@@ -1,0 +1,117 @@
+/*
+ * ia.h — C ABI of the MI355X-native Image Analogies best-match core (libia.so).
+ *
+ * The reference (flair2005/image-analogies-python) reaches native code in exactly one place:
+ * pyflann, a ctypes shim over libflann's C ABI, called from algorithms.py:56 (pf.FLANN()),
+ * algorithms.py:69 (build_index) and algorithms.py:74 (nn_index).  Everything else on the hot
+ * path is the Python raster loop image_analogies.py:130-239.  This header replaces both:
+ *
+ *   ia_index_*            drop-in for the FLANN object API (algorithms.py:56,69,74):
+ *                         build an exact-NN index over caller rows, query it in batches.
+ *   ia_synthesize_level   drop-in for one iteration of the per-level loop
+ *                         (image_analogies.py:130-239 incl. create_index's DB for that level,
+ *                         algorithms.py:50-70): DB build, skewed-wavefront schedule, exact NN,
+ *                         coherence, kappa selection and B'/s/im writeback, all on the GPU.
+ *
+ * Conventions (pyflann's, kept): caller-owned C-contiguous buffers, library-owned opaque
+ * handles, integer status returns (0 = ok, negative IA_E* on error, never throws across the
+ * ABI), thread-local ia_last_error().  Images are row-major (h, w[, ch]) fp64 in [0,1] scale
+ * exactly as the reference keeps them; index outputs are int32/int64.
+ * A context is not thread-safe; one host thread drives one context (one GPU).
+ */
+#ifndef IA_H_
+#define IA_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define IA_OK 0
+#define IA_EINVAL -1   /* bad argument / shape contract violated */
+#define IA_EHIP -2     /* HIP runtime error */
+#define IA_ENOMEM -3   /* device allocation failed */
+#define IA_ENODEV -4   /* no usable gfx950 device */
+#define IA_ECOMM -5    /* RCCL error */
+
+#define IA_MEM_HOST 0   /* pointers in ia_level_args are host (numpy) memory */
+#define IA_MEM_DEVICE 1 /* pointers are device memory already resident in HBM */
+
+typedef struct ia_ctx ia_ctx;
+typedef struct ia_index ia_index;
+
+/* Per-call statistics (SURVEY §5 'Metrics'). */
+typedef struct {
+  int64_t pixels;          /* B' pixels synthesised */
+  int64_t steps;           /* wavefront steps executed */
+  int64_t coherence_wins;  /* pixels whose source came from best_coherence_match */
+  int64_t reranked;        /* exact fp64 reranks of MFMA candidates */
+  int64_t fallbacks;       /* uncertified DB chunks rescanned exactly */
+  double db_ms;            /* DB build time (device) */
+  double synth_ms;         /* wavefront time (device) */
+  double dist_ms;          /* time inside the MFMA distance kernel (device events) */
+  int64_t dist_launches;   /* MFMA distance kernel launches */
+  double dist_flops;       /* algorithmic flops 2*D*N_A*(queries) of those launches */
+} ia_stats;
+
+/* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
+ * level l-1 is (ceil(a_h/2), ceil(a_w/2)[, ch]); same for B.  Ap / Apc stack n_ap images.
+ * Bp: in = initial B' level (initialize_Bp, img_preprocess.py:66-78), out = synthesised.
+ * s_out (N x 2, row/col in A) and im_out (N) are the reference's s / im lists for this level. */
+typedef struct {
+  int ch;          /* channels per pixel: 1 (luminance / grayscale) or 3 */
+  int n_ap;        /* number of A' images (Ap_fname_list) */
+  int a_h, a_w;    /* A level l */
+  int b_h, b_w;    /* B level l */
+  const double *A, *Ac;     /* A level l, l-1 (already AB_weight-compressed, image_analogies.py:65) */
+  const double *Ap, *Apc;   /* A' level l, l-1, n_ap stacked */
+  const double *B, *Bc;     /* B level l, l-1 (compressed) */
+  const double *Bpc;        /* B' level l-1, complete */
+  double *Bp;               /* B' level l: in init, out synthesised */
+  const double *weights;    /* compute_distance weights (config.py:68-79), 55*ch */
+  double kappa_factor;      /* 1 + 2^(level - max_levels) * k   (image_analogies.py:206) */
+  int32_t *s_out;           /* N x 2 */
+  int32_t *im_out;          /* N */
+  int mem;                  /* IA_MEM_HOST or IA_MEM_DEVICE for every pointer above */
+} ia_level_args;
+
+/* ---- context ---------------------------------------------------------------------------- */
+int ia_init(int device, ia_ctx **out);
+void ia_destroy(ia_ctx *ctx);
+const char *ia_last_error(void);
+int ia_version(void);
+/* Options: "time_dist" (0/1) brackets every MFMA distance launch with HIP events so that
+ * ia_stats.dist_ms holds the kernel's measured device time (bench.py roofline). */
+int ia_set_option(ia_ctx *ctx, const char *name, int value);
+/* Multi-GPU (one process per GPU): A rows of every level are split into `world` contiguous
+ * shards; per wavefront step each rank exchanges its certified per-query winners with one
+ * RCCL all-gather and every rank picks the same global winner (lowest index on ties).
+ * ia_comm_unique_id fills 128 bytes on rank 0; broadcast them (torch.distributed) and call
+ * ia_comm_init on every rank. */
+int ia_comm_unique_id(unsigned char id_out[128]);
+int ia_comm_init(ia_ctx *ctx, int rank, int world, const unsigned char id[128]);
+
+/* ---- fast path: one level ----------------------------------------------------------------- */
+int ia_synthesize_level(ia_ctx *ctx, const ia_level_args *args, ia_stats *stats);
+
+/* ---- FLANN-compatible exact index (algorithms.py:56,69,74) -------------------------------- */
+/* build_index(pts): pts is n x d fp64 (row-major), d <= 167. */
+int ia_index_build(ia_ctx *ctx, const double *pts, int64_t n, int d, ia_index **out);
+/* nn_index(q, 1): exact 1-NN, squared L2 in fp64 with numpy's pairwise summation order,
+ * lowest index on ties.  q is nq x d fp64; idx_out (nq) int64, dist_out (nq) fp64 (may be NULL). */
+int ia_index_query(ia_index *index, const double *q, int64_t nq, int64_t *idx_out, double *dist_out);
+void ia_index_destroy(ia_index *index);
+
+/* ---- host-side helpers (no GPU needed) ---------------------------------------------------- */
+/* Merge per-rank candidate winners (dist fp64, global row) into the global winner per query:
+ * smallest distance, then smallest row.  cand is world x nq (dist, row) pairs, rank-major. */
+int ia_merge_winners(const double *dist, const int64_t *row, int world, int64_t nq,
+                     double *dist_out, int64_t *row_out);
+/* Wavefront schedule of a level (t = col + 3*row): number of steps and max queries per step. */
+int ia_wavefront_shape(int h, int w, int64_t *steps, int64_t *max_queries);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* IA_H_ */
