@@ -1,0 +1,208 @@
+#!/usr/bin/env python3
+"""bench.py — BASELINE.json metric: B' pixels synthesised per second, exact NN, synthetic
+1024x1024 A/A'/B (cfg3, full 10-level pyramid), on the MI355X HIP path.
+
+One "step" = one complete synthesis of B' (every level 1..L-1: DB build, skewed-wavefront
+exact-NN + coherence + kappa synthesis) for the synthetic job, with every input already
+resident in HBM (pyramids uploaded once, before timing; B' is re-initialised on the device at
+the start of each step).  `value` = B' pixels of all ranks / wall time of K timed steps.
+
+  python bench.py [--gpus N --steps K --warmup W]           # N=1 default
+  torchrun --nproc-per-node N bench.py --gpus N ...         # one process per GPU
+
+Multi-GPU: --mode replicas (default) runs one independent job per GPU (multi_script-style,
+no collective, "scaling": "weak"); --mode shard splits each level's A database across the
+ranks with one RCCL all-gather of certified winners per wavefront step ("strong").
+
+Besides the contract fields the JSON line carries:
+  roofline     the MFMA distance kernel (k3_dist): algorithmic flops sum 2*D*N_A*M over
+               launches / its device time, sampled live with HIP events (every --time-stride-th
+               wavefront step), against the fp32 MFMA dense peak (MI355X_MICROARCH.md).
+  cpu_baseline the oracle's restatement of the reference loop (per-pixel pad + exact fp64 NN,
+               1 thread) timed on bounded samples of the same job on this host, extrapolated to
+               the whole job (rank 0 at N=1 only).
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "B' pixels synthesized/sec, exact NN, 1024² A/A'/B, 1/2/4/8 GPUs; % MFMA peak"
+FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+HBM_PEAK = 8.0e12
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+class DeviceJob(object):
+    """The job's pyramids as torch device tensors + per-level output buffers."""
+
+    def __init__(self, job, torch, dev):
+        t = lambda x: torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64)).to(dev)
+        self.job = job
+        self.A = [t(x) for x in job.A_pyr]
+        self.Ap = [t(np.stack([p[l] for p in job.Ap_pyr_list])) for l in range(job.L)]
+        self.B = [t(x) for x in job.B_pyr[:job.L]]
+        self.Bp0 = [t(x) for x in job.Bp_init[:job.L]]
+        self.Bp = [x.clone() for x in self.Bp0]
+        self.W = t(job.weights)
+        self.S = [torch.empty((int(np.prod(x.shape[:2])), 2), dtype=torch.int32, device=dev) for x in self.B]
+        self.IM = [torch.empty(int(np.prod(x.shape[:2])), dtype=torch.int32, device=dev) for x in self.B]
+        self.ch = 1 if job.A_pyr[0].ndim == 2 else job.A_pyr[0].shape[2]
+
+    def run(self, ctx, torch, stats):
+        for l in range(self.job.L):
+            self.Bp[l].copy_(self.Bp0[l])
+        torch.cuda.synchronize()   # libia runs on its own stream
+        for l in range(1, self.job.L):
+            ptrs = dict(A=self.A[l].data_ptr(), Ac=self.A[l - 1].data_ptr(), Ap=self.Ap[l].data_ptr(),
+                        Apc=self.Ap[l - 1].data_ptr(), B=self.B[l].data_ptr(), Bc=self.B[l - 1].data_ptr(),
+                        Bpc=self.Bp[l - 1].data_ptr(), Bp=self.Bp[l].data_ptr(), weights=self.W.data_ptr(),
+                        s_out=self.S[l].data_ptr(), im_out=self.IM[l].data_ptr())
+            ctx.synthesize_level_device(self.ch, len(self.job.Ap_pyr_list), self.A[l].shape[:2], self.B[l].shape[:2],
+                                        ptrs, self.job.kappa_factor(l), stats)
+
+
+def cpu_baseline(job, seconds):
+    """Reference loop (oracle restatement: per-pixel np.pad + exact fp64 numpy NN, 1 thread)
+    timed on bounded raster samples of the three finest levels; coarser levels are priced by
+    scaling the smallest sampled level's per-pixel cost with the DB size (the per-pixel cost is
+    a full DB scan + a full-level pad, position independent)."""
+    from oracle import ia_oracle as O
+    L = job.L
+    lv = [l for l in range(L - 1, 0, -1)][:3]
+    budget = seconds / len(lv)
+    per_px, sample = {}, []
+    for l in lv:
+        n_b = int(np.prod(job.B_pyr[l].shape[:2]))
+        t2 = O.time_sample(job.A_pyr, job.Ap_pyr_list, job.B_pyr, job.Bp_init, l, L, job.k, job.weights, 2)
+        n = int(max(2, min(n_b, budget / max(t2, 1e-9))))
+        per_px[l] = O.time_sample(job.A_pyr, job.Ap_pyr_list, job.B_pyr, job.Bp_init, l, L, job.k, job.weights, n)
+        sample.append('%d px of level %d (%dx%d)' % (n, l, job.B_pyr[l].shape[0], job.B_pyr[l].shape[1]))
+    lmin = min(lv)
+    na_min = np.prod(job.A_pyr[lmin].shape[:2])
+    total = 0.
+    for l in range(1, L):
+        n_b = np.prod(job.B_pyr[l].shape[:2])
+        t = per_px[l] if l in per_px else per_px[lmin] * np.prod(job.A_pyr[l].shape[:2]) / na_min
+        total += n_b * t
+    return {'value': job.pixels / total, 'unit': "B' px/s", 'cores': 1, 'kind': 'port',
+            'sample': 'oracle/ia_oracle.py reference-loop restatement (per-pixel pad, exact fp64 NN), '
+                      'timed on ' + ', '.join(sample) + '; coarser levels scaled by DB size; '
+                      'extrapolated whole-job time %.0f s' % total}
+
+
+def main():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=3)
+    ap.add_argument('--warmup', type=int, default=1)
+    ap.add_argument('--config', default='cfg3', help='synthetic workload (ia_amd.synth.CONFIGS)')
+    ap.add_argument('--mode', default='replicas', choices=['replicas', 'shard'])
+    ap.add_argument('--time-stride', type=int, default=4, help='sample K3 timing every S-th wavefront step')
+    ap.add_argument('--cpu-seconds', type=float, default=20.0)
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'k3_traffic.json'),
+                    help='per-launch HBM bytes of k3_dist from a rocprofv3 --pmc pass (optional)')
+    args = ap.parse_args()
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    import torch
+    import ia_amd  # noqa: F401
+    from ia_amd import _native, synth
+
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    dev = torch.device('cuda', local)
+
+    kw, desc = synth.CONFIGS[args.config]
+    t0 = time.time()
+    job = synth.make_job(**kw)
+    log('[bench] rank %d: job %s built in %.1fs: L=%d, %d B\' px/step, %.3e NN flops/step'
+        % (rank, args.config, time.time() - t0, job.L, job.pixels, job.flops()))
+
+    ctx = _native.Context(local)
+    if args.mode == 'shard' and world > 1:
+        uid = [_native.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        ctx.comm_init(rank, world, uid[0])
+    dj = DeviceJob(job, torch, dev)
+
+    for _ in range(args.warmup):
+        dj.run(ctx, torch, _native.Stats())
+    ctx.set_option('time_dist', args.time_stride)
+    stats = _native.Stats()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    t_start = time.perf_counter()
+    for _ in range(args.steps):
+        dj.run(ctx, torch, stats)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t_start
+    ctx.set_option('time_dist', 0)
+    if dist:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    jobs = world if (args.mode == 'replicas') else 1
+    pixels = job.pixels * args.steps * jobs
+    value = pixels / elapsed
+    st = stats.as_dict()
+    log('[bench] rank %d stats: %s' % (rank, json.dumps(st)))
+
+    k3_ms_per_launch = st['dist_ms'] / max(st['dist_launches_timed'], 1)
+    flops_per_launch = st['dist_flops_timed'] / max(st['dist_launches_timed'], 1)
+    achieved = flops_per_launch / (k3_ms_per_launch * 1e-3) if k3_ms_per_launch > 0 else 0.
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            traffic = json.load(open(args.traffic_json)).get('hbm_bytes_per_launch')
+        except Exception:
+            traffic = None
+    roofline = {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': FP32_MFMA_PEAK / 1e12, 'unit': 'TFLOP/s',
+                'frac': achieved / FP32_MFMA_PEAK, 'traffic': traffic,
+                'kernel': 'k3_dist (v_mfma_f32_32x32x2_f32 distance scan + fused top-2)',
+                'k3_us_per_launch': k3_ms_per_launch * 1e3, 'k3_launches_sampled': st['dist_launches_timed'],
+                'k3_share_of_step': st['dist_ms'] * (st['dist_flops'] / max(st['dist_flops_timed'], 1)) /
+                max(elapsed * 1e3, 1e-9)}
+
+    out = {'metric': METRIC, 'value': value, 'unit': "B' px/s", 'n_gpus': world, 'steps': args.steps,
+           'warmup': args.warmup, 'ms_per_step': elapsed * 1e3 / args.steps, 'higher_is_better': True,
+           'scaling': 'weak' if args.mode == 'replicas' else 'strong', 'vs_baseline': None, 'dtype': 'f32',
+           'data': 'synthetic', 'config': {'workload': '%s: %s' % (args.config, desc),
+                                           'a_shape': list(job.A_pyr[-1].shape), 'pyramid_levels': job.L,
+                                           'px_per_step': job.pixels, 'nn_flops_per_step': job.flops(),
+                                           'mode': args.mode, 'parallelism': ('replicas%d' if args.mode == 'replicas'
+                                                                              else 'dbshard%d') % world,
+                                           'nn': 'exact: fp32 MFMA candidates + certified fp64 rerank'},
+           'roofline': roofline,
+           'stats': {k: st[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
+                                        'synth_ms')}}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        out['cpu_baseline'] = cpu_baseline(job, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -32,8 +32,9 @@ class LevelArgs(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [('pixels', ctypes.c_int64), ('steps', ctypes.c_int64), ('coherence_wins', ctypes.c_int64),
                 ('reranked', ctypes.c_int64), ('fallbacks', ctypes.c_int64), ('db_ms', ctypes.c_double),
-                ('synth_ms', ctypes.c_double), ('dist_ms', ctypes.c_double), ('dist_launches', ctypes.c_int64),
-                ('dist_flops', ctypes.c_double)]
+                ('synth_ms', ctypes.c_double), ('dist_launches', ctypes.c_int64), ('dist_flops', ctypes.c_double),
+                ('dist_ms', ctypes.c_double), ('dist_launches_timed', ctypes.c_int64),
+                ('dist_flops_timed', ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

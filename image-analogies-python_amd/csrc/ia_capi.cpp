@@ -312,13 +312,15 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   ma.eps_c = ia_eps_c(DP);
 
   const int qtmax = ia_k3_qtmax(g.KH);
-  if (c->time_dist && (int64_t)c->evs.size() < 2 * T) {
+  const int stride = c->time_dist > 0 ? c->time_dist : 0;
+  const int64_t n_timed = stride ? (T + stride - 1) / stride : 0;
+  if ((int64_t)c->evs.size() < 2 * n_timed) {
     size_t old = c->evs.size();
-    c->evs.resize(2 * T);
+    c->evs.resize(2 * n_timed);
     for (size_t i = old; i < c->evs.size(); i++) hipEventCreate(&c->evs[i]);
   }
-  int64_t dist_launches = 0;
-  double dist_flops = 0.;
+  int64_t dist_launches = 0, launches_timed = 0;
+  double dist_flops = 0., flops_timed = 0.;
   for (int64_t t = 0; t < T; t++) {
     StepDesc sd;
     sd.t = (int)t;
@@ -330,18 +332,24 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     ia_launch_gather(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(), c->st);
     if (ns > 0) {
       const int qtt = sd.Mpad / IA_TILE, nqb = (qtt + qtmax - 1) / qtmax;
-      if (c->time_dist) hipEventRecord(c->evs[2 * t], c->st);
+      const bool timed = stride && t % stride == 0;
+      if (timed) hipEventRecord(c->evs[2 * (t / stride)], c->st);
       int qt0 = 0;
       for (int b = 0; b < nqb; b++) {
         const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
         ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.row0,
                      c->rec.as<float4>(), c->recT.as<float>(), c->st);
         const int mq = std::min(sd.M, (qt0 + qt) * IA_TILE) - qt0 * IA_TILE;
-        dist_flops += 2.0 * g.D * (double)(ma.row_end - ma.row0) * std::max(mq, 0);
+        const double fl = 2.0 * g.D * (double)(ma.row_end - ma.row0) * std::max(mq, 0);
+        dist_flops += fl;
         dist_launches++;
+        if (timed) {
+          flops_timed += fl;
+          launches_timed++;
+        }
         qt0 += qt;
       }
-      if (c->time_dist) hipEventRecord(c->evs[2 * t + 1], c->st);
+      if (timed) hipEventRecord(c->evs[2 * (t / stride) + 1], c->st);
     }
     if (!sharded) {
       ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), dS, dIM, dBp, (const double *)dW, a->kappa_factor, true, c->st);
@@ -376,14 +384,16 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     stats->synth_ms += ms_syn;
     stats->dist_launches += dist_launches;
     stats->dist_flops += dist_flops;
-    if (c->time_dist && ns > 0) {
+    if (stride && ns > 0) {
       double tot = 0.;
-      for (int64_t t = 0; t < T; t++) {
+      for (int64_t i = 0; i < n_timed; i++) {
         float ms = 0.f;
-        hipEventElapsedTime(&ms, c->evs[2 * t], c->evs[2 * t + 1]);
+        hipEventElapsedTime(&ms, c->evs[2 * i], c->evs[2 * i + 1]);
         tot += ms;
       }
       stats->dist_ms += tot;
+      stats->dist_launches_timed += launches_timed;
+      stats->dist_flops_timed += flops_timed;
     }
   }
   return IA_OK;
