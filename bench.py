@@ -143,7 +143,8 @@ def main():
 
     for _ in range(args.warmup):
         dj.run(ctx, torch, _native.Stats())
-    ctx.set_option('time_dist', args.time_stride)
+    if args.time_stride > 0:
+        ctx.set_option('time_dist', args.time_stride)
     stats = _native.Stats()
     torch.cuda.synchronize()
     if dist:

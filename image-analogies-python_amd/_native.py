@@ -10,7 +10,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, 'libia.so')
+LIB_PATH = os.environ.get('IA_LIBIA', os.path.join(_HERE, 'libia.so'))  # override: diagnostic builds
 
 IA_MEM_HOST, IA_MEM_DEVICE = 0, 1
 _ERRNAMES = {-1: 'IA_EINVAL', -2: 'IA_EHIP', -3: 'IA_ENOMEM', -4: 'IA_ENODEV', -5: 'IA_ECOMM'}
@@ -58,6 +58,10 @@ EXPORTS = {
                                         ctypes.c_void_p, ctypes.c_void_p]),
     'ia_wavefront_shape': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
                                           ctypes.POINTER(ctypes.c_int64)]),
+    'ia_wavefront_step': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
+                                         ctypes.POINTER(ctypes.c_int)]),
+    'ia_shard_tiles': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
+                                      ctypes.POINTER(ctypes.c_int64)]),
 }
 
 _lib = None
@@ -207,6 +211,28 @@ def merge_winners(dist, row):
     ro = np.empty(nq, dtype=np.int64)
     check(lib().ia_merge_winners(_ptr(dist), _ptr(row), world, nq, _ptr(do), _ptr(ro)), 'ia_merge_winners')
     return do, ro
+
+
+def wavefront_step(h, w, t):
+    """(r0, M): step t covers pixels (r, t - 3r) for r in r0 .. r0 + M - 1."""
+    r0, m = ctypes.c_int(), ctypes.c_int()
+    check(lib().ia_wavefront_step(h, w, t, ctypes.byref(r0), ctypes.byref(m)), 'ia_wavefront_step')
+    return r0.value, m.value
+
+
+def shard_tiles(n_rows, world, rank):
+    """Tiles [t0, t1) of `rank`; position j of tile t holds DB row j * ceil(n_rows/32) + t."""
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    check(lib().ia_shard_tiles(n_rows, world, rank, ctypes.byref(a), ctypes.byref(b)), 'ia_shard_tiles')
+    return a.value, b.value
+
+
+def shard_rows(n_rows, world, rank):
+    """Sorted DB rows owned by `rank` (tile-strided layout, see shard_tiles)."""
+    t0, t1 = shard_tiles(n_rows, world, rank)
+    nt = (n_rows + 31) // 32
+    rows = (np.arange(32)[:, None] * nt + np.arange(t0, t1)[None, :]).ravel()
+    return np.sort(rows[rows < n_rows])
 
 
 def wavefront_shape(h, w):

@@ -75,7 +75,7 @@ struct ia_ctx {
   hipStream_t st = nullptr;
   // uploads (IA_MEM_HOST) and per-level scratch
   DevBuf A, Ac, Ap, Apc, B, Bc, Bpc, Bp, S, IM, W;
-  DevBuf db, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters;
+  DevBuf db, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, pstat;
   // per-step K3 timing (optional)
   int time_dist = 0;
   std::vector<hipEvent_t> evs;
@@ -125,7 +125,7 @@ void ia_destroy(ia_ctx *c) {
   hipSetDevice(c->dev);
   hipStreamSynchronize(c->st);
   for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->B, &c->Bc, &c->Bpc, &c->Bp, &c->S, &c->IM, &c->W, &c->db,
-                    &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters})
+                    &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->pstat})
     b->release();
   for (hipEvent_t e : c->evs) hipEventDestroy(e);
   hipEventDestroy(c->lv0);
@@ -171,6 +171,31 @@ int ia_wavefront_shape(int h, int w, int64_t *steps, int64_t *max_queries) {
   if (h < 1 || w < 1) return fail(IA_EINVAL, "ia_wavefront_shape: empty level");
   if (steps) *steps = (int64_t)w + 3 * (int64_t)(h - 1);
   if (max_queries) *max_queries = std::min<int64_t>(h, (w + 2) / 3);
+  return IA_OK;
+}
+
+int ia_wavefront_step(int h, int w, int64_t t, int *r0, int *M) {
+  if (h < 1 || w < 1 || t < 0 || t >= (int64_t)w + 3 * (int64_t)(h - 1)) return fail(IA_EINVAL, "ia_wavefront_step: bad step");
+  const int64_t r_lo = std::max<int64_t>(0, (t - w + 1 + 2) / 3);  // ceil((t - w + 1) / 3), t - w + 3 > 0
+  const int64_t r_hi = std::min<int64_t>(h - 1, t / 3);
+  *r0 = (int)r_lo;
+  *M = (int)(r_hi - r_lo + 1);
+  return IA_OK;
+}
+
+static bool shard_level(int64_t n_tiles, int world) { return world > 1 && n_tiles >= 64 * (int64_t)world; }
+
+int ia_shard_tiles(int64_t n_rows, int world, int rank, int64_t *tile0, int64_t *tile1) {
+  if (n_rows < 1 || world < 1 || rank < 0 || rank >= world || !tile0 || !tile1)
+    return fail(IA_EINVAL, "ia_shard_tiles: bad args");
+  const int64_t n_tiles = (n_rows + IA_TILE - 1) / IA_TILE;
+  if (!shard_level(n_tiles, world)) {
+    *tile0 = 0;
+    *tile1 = n_tiles;
+    return IA_OK;
+  }
+  *tile0 = n_tiles * rank / world;
+  *tile1 = n_tiles * (rank + 1) / world;
   return IA_OK;
 }
 
@@ -239,10 +264,14 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   g.NA = (int64_t)g.n_ap * g.ah * g.aw;
   g.n_tiles = (int)((g.NA + IA_TILE - 1) / IA_TILE);
   // shard the DB over ranks unless the level is too small to be worth an exchange per step
-  const bool sharded = c->world > 1 && g.n_tiles >= 64 * c->world;
+  const bool sharded = shard_level(g.n_tiles, c->world);
   const int world = sharded ? c->world : 1, rank = sharded ? c->rank : 0;
-  g.tile0 = (int)((int64_t)g.n_tiles * rank / world);
-  g.tile1 = (int)((int64_t)g.n_tiles * (rank + 1) / world);
+  {
+    int64_t t0, t1;
+    ia_shard_tiles(g.NA, c->world, c->rank, &t0, &t1);
+    g.tile0 = (int)t0;
+    g.tile1 = (int)t1;
+  }
   const int ns = g.tile1 - g.tile0;
   g.tiles_per_wg = std::max(4, (ns + IA_WG_TARGET - 1) / IA_WG_TARGET);
   g.nwg = (ns + g.tiles_per_wg - 1) / g.tiles_per_wg;
@@ -283,10 +312,12 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       (rc = c->qn2.ensure((size_t)Mpad_max * 8)) || (rc = c->qf.ensure((size_t)Mpad_max * DP * 4)) ||
       (rc = c->rec.ensure((size_t)Mmax * std::max(g.nwg, 1) * 16)) ||
       (rc = c->recT.ensure((size_t)Mmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mmax * 16)) ||
-      (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(4 * 8)))
+      (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(4 * 8)) ||
+      (rc = c->pstat.ensure((size_t)NB * 4)))
     return rc;
   HIP_TRY(hipMemsetAsync(c->Rbits.p, 0, 4, c->st));
   HIP_TRY(hipMemsetAsync(c->counters.p, 0, 4 * 8, c->st));
+  HIP_TRY(hipMemsetAsync(c->pstat.p, 0, (size_t)NB * 4, c->st));
 
   Imgs Aim{(const double *)dAc, (const double *)dA, (const double *)dApc, (const double *)dAp,
            g.ah, g.aw, g.ahc, g.awc, (int64_t)nA, (int64_t)nAc};
@@ -305,10 +336,13 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   ma.Rbits = c->Rbits.as<unsigned>();
   ma.nwg = g.nwg;
   ma.tpw = g.tiles_per_wg;
-  ma.n_tiles_shard = ns;
-  ma.row0 = g.tile0 * IA_TILE;
-  ma.row_end = std::min<int64_t>(g.NA, (int64_t)g.tile1 * IA_TILE);
-  ma.counters = c->counters.as<unsigned long long>();
+  ma.pos0 = g.tile0 * IA_TILE;
+  ma.pos_end = g.tile1 * IA_TILE;
+  ma.NT = g.n_tiles;
+  ma.NA = (int)g.NA;
+  int64_t shard_rows = 0;  // real DB rows in this shard's tiles (strided layout)
+  for (int t = g.tile0; t < g.tile1; t++) shard_rows += std::min<int64_t>(IA_TILE, (g.NA - t + g.n_tiles - 1) / g.n_tiles);
+  ma.pstat = c->pstat.as<unsigned>();
   ma.eps_c = ia_eps_c(DP);
 
   const int qtmax = ia_k3_qtmax(g.KH);
@@ -319,28 +353,26 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     c->evs.resize(2 * n_timed);
     for (size_t i = old; i < c->evs.size(); i++) hipEventCreate(&c->evs[i]);
   }
-  int64_t dist_launches = 0, launches_timed = 0;
+  int64_t dist_launches = 0, launches_timed = 0, n_rec = 0;
   double dist_flops = 0., flops_timed = 0.;
   for (int64_t t = 0; t < T; t++) {
     StepDesc sd;
     sd.t = (int)t;
-    const int64_t r_lo = std::max<int64_t>(0, (t - g.bw + 1 + 2) / 3);  // ceil((t - w + 1) / 3)
-    const int64_t r_hi = std::min<int64_t>(g.bh - 1, t / 3);
-    sd.r0 = (int)r_lo;
-    sd.M = (int)(r_hi - r_lo + 1);
+    ia_wavefront_step(g.bh, g.bw, t, &sd.r0, &sd.M);
+    if (sd.M <= 0) continue;  // levels narrower than 3 columns have empty steps
     sd.Mpad = (sd.M + IA_TILE - 1) / IA_TILE * IA_TILE;
     ia_launch_gather(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(), c->st);
     if (ns > 0) {
       const int qtt = sd.Mpad / IA_TILE, nqb = (qtt + qtmax - 1) / qtmax;
       const bool timed = stride && t % stride == 0;
-      if (timed) hipEventRecord(c->evs[2 * (t / stride)], c->st);
+      if (timed) hipEventRecord(c->evs[2 * n_rec], c->st);
       int qt0 = 0;
       for (int b = 0; b < nqb; b++) {
         const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
-        ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.row0,
+        ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0, ma.NT,
                      c->rec.as<float4>(), c->recT.as<float>(), c->st);
         const int mq = std::min(sd.M, (qt0 + qt) * IA_TILE) - qt0 * IA_TILE;
-        const double fl = 2.0 * g.D * (double)(ma.row_end - ma.row0) * std::max(mq, 0);
+        const double fl = 2.0 * g.D * (double)shard_rows * std::max(mq, 0);
         dist_flops += fl;
         dist_launches++;
         if (timed) {
@@ -349,7 +381,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
         }
         qt0 += qt;
       }
-      if (timed) hipEventRecord(c->evs[2 * (t / stride) + 1], c->st);
+      if (timed) hipEventRecord(c->evs[2 * n_rec++ + 1], c->st);
     }
     if (!sharded) {
       ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), dS, dIM, dBp, (const double *)dW, a->kappa_factor, true, c->st);
@@ -358,11 +390,12 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
                       c->st);
       NCCL_TRY(ncclAllGather(c->win.p, c->allwin.p, (size_t)sd.M * sizeof(Winner), ncclUint8, c->comm, c->st));
       ia_launch_finish(g, sd, Aim, c->q64.as<double>(), c->allwin.as<Winner>(), world, sd.M, dS, dIM, dBp,
-                       (const double *)dW, a->kappa_factor, c->counters.as<unsigned long long>(), c->st);
+                       (const double *)dW, a->kappa_factor, c->pstat.as<unsigned>(), c->st);
     }
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->lv2, c->st));
+  if (stats) ia_launch_reduce_stats(c->pstat.as<unsigned>(), NB, c->counters.as<unsigned long long>(), c->st);
   if (a->mem == IA_MEM_HOST) {
     HIP_TRY(hipMemcpyAsync(a->Bp, dBp, nB * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipMemcpyAsync(a->s_out, dS, (size_t)NB * 8, hipMemcpyDeviceToHost, c->st));
@@ -386,7 +419,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     stats->dist_flops += dist_flops;
     if (stride && ns > 0) {
       double tot = 0.;
-      for (int64_t i = 0; i < n_timed; i++) {
+      for (int64_t i = 0; i < n_rec; i++) {
         float ms = 0.f;
         hipEventElapsedTime(&ms, c->evs[2 * i], c->evs[2 * i + 1]);
         tot += ms;
@@ -465,10 +498,11 @@ int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, d
   ma.Rbits = x->Rbits.as<unsigned>();
   ma.nwg = x->nwg;
   ma.tpw = x->tpw;
-  ma.n_tiles_shard = x->n_tiles;
-  ma.row0 = 0;
-  ma.row_end = x->n;
-  ma.counters = x->counters.as<unsigned long long>();
+  ma.pos0 = 0;
+  ma.pos_end = x->n_tiles * IA_TILE;
+  ma.NT = x->n_tiles;
+  ma.NA = (int)x->n;
+  ma.pstat = nullptr;
   ma.eps_c = ia_eps_c(DP);
   const int qtmax = ia_k3_qtmax(x->KH);
   for (int64_t b0 = 0; b0 < nq; b0 += BATCH) {
@@ -480,7 +514,7 @@ int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, d
     const int qtt = Mpad / IA_TILE;
     for (int qt0 = 0; qt0 < qtt; qt0 += qtmax) {
       const int qt = std::min(qtmax, qtt - qt0);
-      ia_launch_k3(x->KH, qt, x->db.as<float4>(), x->qf.as<float4>(), x->n_tiles, x->tpw, qt0, (int)nb, x->nwg, 0,
+      ia_launch_k3(x->KH, qt, x->db.as<float4>(), x->qf.as<float4>(), x->n_tiles, x->tpw, qt0, (int)nb, x->nwg, 0, x->n_tiles,
                    x->rec.as<float4>(), x->recT.as<float>(), c->st);
     }
     ia_launch_merge_dense(ma, x->pts.as<double>(), x->d, x->q.as<double>(), nb, x->idx.as<int64_t>(),

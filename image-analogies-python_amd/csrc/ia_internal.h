@@ -54,11 +54,20 @@ struct MergeArgs {
   const double *q64;   // Mpad x D query rows (fp64)
   const double *qn2;   // |q'|^2 per query
   const unsigned *Rbits;
-  int nwg, tpw, n_tiles_shard, row0;  // K3 decomposition of this rank's shard
-  int64_t row_end;                    // first row past this rank's shard (clamped to NA)
-  unsigned long long *counters;       // [0] reranked [1] fallbacks [2] coherence wins
+  int nwg, tpw;        // K3 decomposition of this rank's shard
+  int pos0, pos_end;   // this rank's DB positions [tile0*32, tile1*32)
+  int NT;              // tiles of the whole DB: position p holds row ia_pos_row(p, NT)
+  int NA;              // DB rows
+  unsigned *pstat;                    // per-pixel stats word of the level (nullptr: none):
+                                      // bits 0-15 reranked, 16-29 fallbacks, 30 coherence won
   double eps_c;                       // 1.05 * gamma_(DP+2), see DESIGN.md §4
 };
+
+// DB positions are tile-strided: slot j of tile t holds row j*NT + t, so spatially adjacent A
+// pixels (near-identical features, near-tied distances) land in different tiles and hence in
+// different K3 subsets; every subset's runner-up threshold then stays clear of the winner and
+// certification rarely needs an exact chunk rescan.
+__host__ __device__ inline int64_t ia_pos_row(int64_t pos, int64_t NT) { return (pos & 31) * NT + (pos >> 5); }
 
 // per-step wavefront description: pixels (r, t - 3r), r in [r0, r0 + M)
 struct StepDesc {
@@ -72,8 +81,13 @@ struct Winner {
 };
 
 __host__ __device__ inline int ia_reflect(int i, int n) {
-  // np.pad(mode='symmetric') index map for any pad width (img_preprocess.py:81-83)
-  int m = 2 * n;
+  // np.pad(mode='symmetric') index map (img_preprocess.py:81-83).  Windows reach at most 2
+  // pixels past an edge, so two folds suffice unless the image is narrower than the window;
+  // only then take the (slow, integer-modulo) periodic form.
+  int j = i < 0 ? -i - 1 : i;
+  j = j >= n ? 2 * n - 1 - j : j;
+  if ((unsigned)j < (unsigned)n) return j;
+  const int m = 2 * n;
   i %= m;
   if (i < 0) i += m;
   return i >= n ? m - 1 - i : i;

@@ -24,6 +24,10 @@
 
 #include "ia_internal.h"
 
+#ifndef IA_PROBE
+#define IA_PROBE 0  // diagnostic phase-skipping builds (never set in the product build)
+#endif
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------------------------------
@@ -224,18 +228,19 @@ template <int CH>
 __global__ void __launch_bounds__(IA_WG) k_db_build(LevelGeo g, Imgs A, const double *__restrict__ mu_part,
                                                      float4 *__restrict__ db, unsigned *__restrict__ Rbits) {
   using G = Geo<CH>;
-  const int64_t row = (int64_t)g.tile0 * IA_TILE + (int64_t)blockIdx.x * IA_WG + threadIdx.x;
-  if (row >= (int64_t)g.tile1 * IA_TILE) return;
-  const int64_t ltile = row / IA_TILE - g.tile0;
-  const int j = (int)(row % IA_TILE);
+  const int64_t pos = (int64_t)g.tile0 * IA_TILE + (int64_t)blockIdx.x * IA_WG + threadIdx.x;
+  if (pos >= (int64_t)g.tile1 * IA_TILE) return;
+  const int64_t ltile = pos / IA_TILE - g.tile0;
+  const int j = (int)(pos % IA_TILE);
+  const int64_t row = ia_pos_row(pos, g.n_tiles);
   const bool real = row < g.NA;
   int img = 0, pr = 0, pc = 0;
   if (real) {
-    const int64_t hw = (int64_t)g.ah * g.aw;
-    img = (int)(row / hw);
-    const int64_t rem = row - img * hw;
-    pr = (int)(rem / g.aw);
-    pc = (int)(rem % g.aw);
+    const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
+    img = (int)((unsigned)row / hw);
+    const unsigned rem = (unsigned)row - (unsigned)img * hw;
+    pr = (int)(rem / (unsigned)g.aw);
+    pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
   }
   const Px P = make_px<CH>(A, pr, pc);
   double norm = 0.;
@@ -351,7 +356,7 @@ __device__ __forceinline__ Top2 top2_merge(Top2 a, const Top2 &b) {
 template <int KH, int QT>
 __global__ void __launch_bounds__(IA_WG, 2)
 k3_dist(const float4 *__restrict__ db, const float4 *__restrict__ qf, int n_tiles, int tpw, int qt0, int M,
-        int nwg, int row0, float4 *__restrict__ rec, float *__restrict__ recT) {
+        int nwg, int row0, int NT, float4 *__restrict__ rec, float *__restrict__ recT) {
   constexpr int KP = KH / 4;
   extern __shared__ float4 lds[];  // QT * KP * 64 float4 (queries), reused for the merge
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
@@ -394,27 +399,54 @@ k3_dist(const float4 *__restrict__ db, const float4 *__restrict__ qf, int n_tile
     }
     const int rbase = row0 + t * IA_TILE + 4 * half;
     asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-#pragma unroll
-    for (int q = 0; q < QT; q++) {
-      f32x16 acc = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      const float4 *qb = lds + q * KP * IA_WAVE + lane;
-#pragma unroll
-      for (int p = 0; p < KP; p++) {
-        const float4 bq = qb[p * IA_WAVE];
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p], bq.x, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 1], bq.y, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 2], bq.z, acc, 0, 0, 0);
-        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 3], bq.w, acc, 0, 0, 0);
-      }
+    // Query tiles go in pairs (two independent accumulation chains share each DB operand);
+    // the top-2 epilogue of pair j is issued after the MFMAs of pair j+1 so the scheduler can
+    // fill the MFMA gaps with it (distinct accumulators, no dependency).
+    // Epilogue per value v (4 VALU): c = v < b1;  b2 = med3(b1, b2, v) (b1 <= b2 => the
+    // second smallest of the three);  b1 = c ? v : b1;  i1 = c ? row : i1.
+    f32x16 e0, e1;
+    auto epilogue = [&](const f32x16 &acc, int q) {
 #pragma unroll
       for (int r = 0; r < 16; r++) {
         const float v = acc[r];
         const int row = rbase + (r & 3) + 8 * (r >> 2);
-        b2[q] = fminf(b2[q], fmaxf(b1[q], v));
         const bool c = v < b1[q];
+        b2[q] = __builtin_amdgcn_fmed3f(b1[q], b2[q], v);
+        b1[q] = c ? v : b1[q];
         i1[q] = c ? row : i1[q];
-        b1[q] = fminf(b1[q], v);
       }
+    };
+#pragma unroll
+    for (int qp = 0; qp < QT; qp += 2) {
+      constexpr f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const bool two = qp + 1 < QT;
+      f32x16 c0 = zero, c1 = zero;
+      const float4 *qb0 = lds + qp * KP * IA_WAVE + lane;
+      const float4 *qb1 = qb0 + KP * IA_WAVE;
+#pragma unroll
+      for (int p = 0; p < KP; p++) {
+        const float4 x0 = qb0[p * IA_WAVE];
+        const float4 x1 = two ? qb1[p * IA_WAVE] : x0;
+        c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p], x0.x, c0, 0, 0, 0);
+        if (two) c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p], x1.x, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 1], x0.y, c0, 0, 0, 0);
+        if (two) c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 1], x1.y, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 2], x0.z, c0, 0, 0, 0);
+        if (two) c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 2], x1.z, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 3], x0.w, c0, 0, 0, 0);
+        if (two) c1 = __builtin_amdgcn_mfma_f32_32x32x2f32(a[4 * p + 3], x1.w, c1, 0, 0, 0);
+      }
+      if (qp >= 2) {
+        epilogue(e0, qp - 2);
+        epilogue(e1, qp - 1);
+      }
+      e0 = c0;
+      e1 = c1;
+    }
+    {
+      constexpr int ql = ((QT - 1) / 2) * 2;  // first tile of the last pair
+      epilogue(e0, ql);
+      if (ql + 1 < QT) epilogue(e1, ql + 1);
     }
 #pragma unroll
     for (int k = 0; k < KH; k++) a[k] = an[k];
@@ -441,8 +473,10 @@ k3_dist(const float4 *__restrict__ db, const float4 *__restrict__ qf, int n_tile
 #pragma unroll
     for (int w = 1; w < 4; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
     const int qg = qt0 * IA_TILE + x;
-    if (qg < M) {
-      rec[(int64_t)qg * nwg + wg] = make_float4(m.v1, __int_as_float(m.i1), m.v2, __int_as_float(m.i2));
+    if (qg < M) {  // positions -> DB rows (ia_pos_row); never-set entries stay out of range
+      const int r1 = m.i1 == 0x7fffffff ? m.i1 : (int)ia_pos_row(m.i1, NT);
+      const int r2 = m.i2 == 0x7fffffff ? m.i2 : (int)ia_pos_row(m.i2, NT);
+      rec[(int64_t)qg * nwg + wg] = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
       recT[(int64_t)qg * nwg + wg] = m.T;
     }
   }
@@ -454,10 +488,12 @@ k3_dist(const float4 *__restrict__ db, const float4 *__restrict__ qf, int n_tile
 // exact DB-row distance of row `row` (level path): ((a - q)**2).sum() in numpy order
 template <int CH>
 __device__ __forceinline__ double exact_dist_level(const LevelGeo &g, const Imgs &A, int64_t row, const double *q) {
-  const int64_t hw = (int64_t)g.ah * g.aw;
-  const int img = (int)(row / hw);
-  const int64_t rem = row - img * hw;
-  const Px P = make_px<CH>(A, (int)(rem / g.aw), (int)(rem % g.aw));
+  // 32-bit row decode (row ids < 2^31 are enforced by the host); no 64-bit division
+  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
+  const unsigned img = (unsigned)row / hw;
+  const unsigned rem = (unsigned)row - img * hw;
+  const unsigned pr = rem / (unsigned)g.aw;
+  const Px P = make_px<CH>(A, (int)pr, (int)(rem - pr * (unsigned)g.aw));
   return pw_sum<Geo<CH>::D>([&](int f) {
     const double d = featp<CH>(A, P, f, img) - q[f];
     return d * d;
@@ -466,31 +502,48 @@ __device__ __forceinline__ double exact_dist_level(const LevelGeo &g, const Imgs
 
 // the certified single-rank winner of query m (exact NN over this rank's shard)
 template <class DistFn>
-__device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist) {
+__device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, unsigned *stat_out) {
+  constexpr int RPL = IA_WG_TARGET / IA_WAVE;  // records per lane (nwg <= IA_WG_TARGET)
   const int lane = threadIdx.x & 63;
   const float4 *rr = a.rec + (int64_t)m * a.nwg;
   const float *rT = a.recT + (int64_t)m * a.nwg;
-  float a1 = FLT_MAX;
-  for (int w = lane; w < a.nwg; w += IA_WAVE) a1 = fminf(a1, rr[w].x);
-  a1 = wave_min_f(a1);
+  // issue every record load at once (clamped index, no per-load branch), mask afterwards
+  float v1[RPL], v2[RPL], tt[RPL];
+#pragma unroll
+  for (int j = 0; j < RPL; j++) {
+    const int w = min(lane + IA_WAVE * j, a.nwg - 1);
+    const float4 x = rr[w];
+    const float t = rT[w];
+    const bool ok = lane + IA_WAVE * j < a.nwg;
+    v1[j] = ok ? x.x : FLT_MAX;
+    v2[j] = ok ? x.z : FLT_MAX;
+    tt[j] = ok ? t : FLT_MAX;
+  }
   const double R = (double)__uint_as_float(*a.Rbits);
   const double qn2 = a.qn2[m];
+  float a1 = FLT_MAX;
+#pragma unroll
+  for (int j = 0; j < RPL; j++) a1 = fminf(a1, v1[j]);
+  a1 = wave_min_f(a1);
   const double eps = a.eps_c * (R * R + 2.0 * R * sqrt(qn2));
   const double thr = (double)a1 + 2.0 * eps;
 
+  // rerank every listed candidate that could be the exact winner
+  unsigned cmask = 0;
+#pragma unroll
+  for (int j = 0; j < RPL; j++) {
+    if ((double)v1[j] <= thr) cmask |= 1u << (2 * j);
+    if ((double)v2[j] <= thr) cmask |= 1u << (2 * j + 1);
+  }
   double bd = DBL_MAX;
   int64_t bi = INT64_MAX;
   unsigned long long nre = 0;
-  for (int w = lane; w < a.nwg; w += IA_WAVE) {
-    const float4 x = rr[w];
-    if ((double)x.x <= thr && __float_as_int(x.y) >= a.row0 && __float_as_int(x.y) < a.row_end) {
-      const int64_t i = __float_as_int(x.y);
-      const double d = dist(i);
-      nre++;
-      if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
-    }
-    if ((double)x.z <= thr && __float_as_int(x.w) >= a.row0 && __float_as_int(x.w) < a.row_end) {
-      const int64_t i = __float_as_int(x.w);
+  while (cmask) {
+    const int b = __ffs(cmask) - 1;
+    cmask &= cmask - 1;
+    const float4 x = rr[lane + IA_WAVE * (b >> 1)];  // L2-hot re-read of the record
+    const int64_t i = __float_as_int((b & 1) ? x.w : x.y);
+    if (i >= 0 && i < a.NA) {
       const double d = dist(i);
       nre++;
       if (d < bd || (d == bd && i < bi)) { bd = d; bi = i; }
@@ -502,19 +555,21 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist) {
   // >= T_w + |q'|^2 - eps.  Chunks with T_w <= theta may hide a row that beats or ties bd.
   const double theta = bd - qn2 + eps + 1e-13 * (bd + 1.0);
   unsigned long long nfb = 0;
-  for (int base = 0; base < a.nwg; base += IA_WAVE) {
-    const int w = base + lane;
-    const bool unc = w < a.nwg && (double)rT[w] <= theta;
-    unsigned long long mask = __ballot(unc);
+#pragma unroll
+  for (int jb = 0; jb < RPL; jb++) {
+    const int base = jb * IA_WAVE;
+    unsigned long long mask = __ballot((double)tt[jb] <= theta);
     while (mask) {
       const int j = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
       const int wgid = base + j;
-      const int64_t r0 = (int64_t)a.row0 + (int64_t)wgid * a.tpw * IA_TILE;
-      const int64_t r1 = min(a.row_end, r0 + (int64_t)a.tpw * IA_TILE);
+      const int64_t p0 = (int64_t)a.pos0 + (int64_t)wgid * a.tpw * IA_TILE;
+      const int64_t p1 = min((int64_t)a.pos_end, p0 + (int64_t)a.tpw * IA_TILE);
       double cd = DBL_MAX;
       int64_t ci = INT64_MAX;
-      for (int64_t i = r0 + lane; i < r1; i += IA_WAVE) {
+      for (int64_t p = p0 + lane; p < p1; p += IA_WAVE) {
+        const int64_t i = ia_pos_row(p, a.NT);
+        if (i >= a.NA) continue;
         const double d = dist(i);
         if (d < cd || (d == cd && i < ci)) { cd = d; ci = i; }
       }
@@ -523,14 +578,10 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist) {
       nfb++;
     }
   }
-  // stats: one atomic per wave
   unsigned long long tot = nre;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-  if (lane == 0) {
-    atomicAdd(&a.counters[0], tot);
-    if (nfb) atomicAdd(&a.counters[1], nfb);
-  }
+  *stat_out = (unsigned)min((unsigned long long)0xffff, tot) | ((unsigned)min((unsigned long long)0x3fff, nfb) << 16);
   return Winner{bd, bi};
 }
 
@@ -539,14 +590,14 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist) {
 template <int CH>
 __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, int r, int c, int64_t app_ix, const double *q,
                              int32_t *__restrict__ s, int32_t *__restrict__ im, double *__restrict__ Bp,
-                             const double *__restrict__ weights, double kf, unsigned long long *counters) {
+                             const double *__restrict__ weights, double kf, unsigned *pstat, unsigned stat) {
   constexpr int D = Geo<CH>::D;
   const int lane = threadIdx.x & 63;
-  const int64_t hw = (int64_t)g.ah * g.aw;
+  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
   const int qi = r * g.bw + c;
-  int img = (int)(app_ix / hw);
-  int64_t rem = app_ix - img * hw;
-  int pr = (int)(rem / g.aw), pc = (int)(rem % g.aw);
+  int img = (int)((unsigned)app_ix / hw);
+  const unsigned rem = (unsigned)app_ix - (unsigned)img * hw;
+  int pr = (int)(rem / (unsigned)g.aw), pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
   bool coh_won = false;
   if (qi > 0) {
     // best_coherence_match: candidates in product(rows, cols) order, first argmin of the norm
@@ -601,7 +652,239 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, int r, int c, int
     s[2 * qi] = pr;
     s[2 * qi + 1] = pc;
     im[qi] = img;
-    if (coh_won) atomicAdd(&counters[2], 1ull);
+    if (pstat) pstat[qi] = stat | (coh_won ? 1u << 30 : 0u);
+  }
+}
+
+// Both distances of DB row `row` against query q from ONE set of feature loads:
+//   unw = ((a - q)**2).sum()  in numpy's pairwise order (NN rerank / coherence ranking)
+//   wsq = sum(((a - q) * w)**2) sequentially (compute_distance before its sqrt / square)
+template <int CH>
+__device__ __forceinline__ void row_dists(const LevelGeo &g, const Imgs &A, int row, const double *q,
+                                          const double *w, double &unw, double &wsq) {
+  constexpr int D = Geo<CH>::D;
+  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
+  const unsigned img = (unsigned)row / hw;
+  const unsigned rem = (unsigned)row - img * hw;
+  const unsigned pr = rem / (unsigned)g.aw;
+  const Px P = make_px<CH>(A, (int)pr, (int)(rem - pr * (unsigned)g.aw));
+  if constexpr (CH == 1) {
+    double t[D];
+#pragma unroll
+    for (int f = 0; f < D; f++) t[f] = featp<CH>(A, P, f, (int)img) - q[f];
+    unw = pw_sum<D>([&](int f) { return t[f] * t[f]; });
+    double s = 0.;
+#pragma unroll
+    for (int f = 0; f < D; f++) {
+      const double x = t[f] * w[f];
+      s += x * x;
+    }
+    wsq = s;
+  } else {  // 165 doubles do not fit in registers: gather twice
+    unw = pw_sum<D>([&](int f) {
+      const double d = featp<CH>(A, P, f, (int)img) - q[f];
+      return d * d;
+    });
+    double s = 0.;
+    for (int f = 0; f < D; f++) {
+      const double x = (featp<CH>(A, P, f, (int)img) - q[f]) * w[f];
+      s += x * x;
+    }
+    wsq = s;
+  }
+}
+
+// row of the lowest set candidate bit (bit 2j: record j's best, bit 2j+1: its runner-up)
+template <int RPL>
+__device__ __forceinline__ int lowest_cand(unsigned cmask, const int (&i1)[RPL], const int (&i2)[RPL]) {
+  int row = -1;
+#pragma unroll
+  for (int j = RPL - 1; j >= 0; j--) {
+    row = (cmask >> (2 * j + 1)) & 1 ? i2[j] : row;
+    row = (cmask >> (2 * j)) & 1 ? i1[j] : row;
+  }
+  return row;
+}
+
+// Fused single-rank merge of query m: certified exact NN + coherence + kappa + writeback.
+// Memory is touched in two dependent rounds: (1) the K3 records and the coherence
+// neighbours' s/im, (2) ONE feature gather in which lane k < 15 evaluates coherence candidate
+// k and lanes 15..63 the MFMA candidates worth an exact rerank; every lane gets both the exact
+// unweighted distance (ranking) and the weighted one (kappa rule) from the same loads.
+template <int CH>
+__device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &a, int m,
+                            int32_t *__restrict__ s, int32_t *__restrict__ im, double *__restrict__ Bp,
+                            const double *__restrict__ weights, double kf) {
+  constexpr int RPL = IA_WG_TARGET / IA_WAVE;
+  constexpr int NCOH = 15, NRR = IA_WAVE - NCOH;  // lanes for coherence / rerank candidates
+  const int lane = threadIdx.x & 63;
+  const int r = sd.r0 + m, c = sd.t - 3 * r, qi = r * g.bw + c;
+  const double *q = a.q64 + (int64_t)m * Geo<CH>::D;
+  const float4 *rr = a.rec + (int64_t)m * a.nwg;
+  const float *rT = a.recT + (int64_t)m * a.nwg;
+
+  // ---- round 1: records (clamped, unconditional loads) and coherence neighbours
+  float v1[RPL], v2[RPL], tt[RPL];
+  int i1[RPL], i2[RPL];
+#pragma unroll
+  for (int j = 0; j < RPL; j++) {
+    const int w = min(lane + IA_WAVE * j, a.nwg - 1);
+    const float4 x = rr[w];
+    const float t = rT[w];
+    const bool ok = lane + IA_WAVE * j < a.nwg;
+    v1[j] = ok ? x.x : FLT_MAX;
+    v2[j] = ok ? x.z : FLT_MAX;
+    tt[j] = ok ? t : FLT_MAX;
+    i1[j] = __float_as_int(x.y);
+    i2[j] = __float_as_int(x.w);
+  }
+  int crow = -1, cpr = -1, cpc = -1, cim = 0;
+  if (qi > 0 && lane < NCOH) {  // best_coherence_match candidates, product(rows, cols) order
+    const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
+    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
+      const int nb = nr * g.bw + nc;
+      const int tr = s[2 * nb] + r - nr, tc = s[2 * nb + 1] + c - nc;
+      const int ti = im[nb];
+      if (tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) {
+        cpr = tr;
+        cpc = tc;
+        cim = ti;
+        crow = (ti * g.ah + tr) * g.aw + tc;
+      }
+    }
+  }
+  const double R = (double)__uint_as_float(*a.Rbits);
+  const double qn2 = a.qn2[m];
+
+  // ---- MFMA candidates that may be the exact winner -> lanes 15..63
+  float a1 = FLT_MAX;
+#pragma unroll
+  for (int j = 0; j < RPL; j++) a1 = fminf(a1, v1[j]);
+  a1 = wave_min_f(a1);
+  const double eps = a.eps_c * (R * R + 2.0 * R * sqrt(qn2));
+  const double thr = (double)a1 + 2.0 * eps;
+  unsigned cmask = 0;
+#pragma unroll
+  for (int j = 0; j < RPL; j++) {
+    if ((double)v1[j] <= thr && i1[j] >= 0 && i1[j] < a.NA) cmask |= 1u << (2 * j);
+    if ((double)v2[j] <= thr && i2[j] >= 0 && i2[j] < a.NA) cmask |= 1u << (2 * j + 1);
+  }
+  int my_row = lane < NCOH ? crow : -1;
+  int nxt = lowest_cand<RPL>(cmask, i1, i2);
+  int slot = 0;
+  unsigned long long pend = __ballot(cmask != 0);
+  while (pend && slot < NRR) {
+    const int L = __ffsll((long long)pend) - 1;
+    const int row = __shfl(nxt, L, 64);
+    if (lane == NCOH + slot) my_row = row;
+    slot++;
+    if (lane == L) {
+      cmask &= cmask - 1;
+      nxt = lowest_cand<RPL>(cmask, i1, i2);
+    }
+    pend = __ballot(cmask != 0);
+  }
+
+  // ---- round 2: one feature gather per lane
+  double unw = DBL_MAX, wsq = 0.;
+  if (my_row >= 0) row_dists<CH>(g, A, my_row, q, weights, unw, wsq);
+
+  // exact NN winner among the reranked candidates (+ any overflow beyond 49, rare)
+  double bd = (lane >= NCOH && my_row >= 0) ? unw : DBL_MAX;
+  int64_t bi = (lane >= NCOH && my_row >= 0) ? (int64_t)my_row : INT64_MAX;
+  bool recompute_app = false;
+  while (pend) {  // overflow: remaining candidates one at a time
+    const int L = __ffsll((long long)pend) - 1;
+    const int row = __shfl(nxt, L, 64);
+    double u, wq;
+    row_dists<CH>(g, A, row, q, weights, u, wq);
+    if (u < bd || (u == bd && row < bi)) {
+      bd = u;
+      bi = row;
+    }
+    slot++;
+    recompute_app = true;
+    if (lane == L) {
+      cmask &= cmask - 1;
+      nxt = lowest_cand<RPL>(cmask, i1, i2);
+    }
+    pend = __ballot(cmask != 0);
+  }
+  wave_min_di(bd, bi);
+  double wsq_app = 0.;
+  {
+    const unsigned long long own = __ballot(lane >= NCOH && my_row >= 0 && (int64_t)my_row == bi && unw == bd);
+    if (own) wsq_app = __shfl(wsq, __ffsll((long long)own) - 1, 64);
+    else recompute_app = true;
+  }
+
+  // certification (see certified_winner): rescan chunks whose threshold does not clear bd
+  const double theta = bd - qn2 + eps + 1e-13 * (bd + 1.0);
+  unsigned long long nfb = 0;
+#pragma unroll
+  for (int jb = 0; jb < RPL; jb++) {
+    unsigned long long mask = __ballot((double)tt[jb] <= theta);
+    while (mask) {
+      const int j = __ffsll((long long)mask) - 1;
+      mask &= mask - 1;
+      const int64_t p0 = (int64_t)a.pos0 + (int64_t)(jb * IA_WAVE + j) * a.tpw * IA_TILE;
+      const int64_t p1 = min((int64_t)a.pos_end, p0 + (int64_t)a.tpw * IA_TILE);
+      double cd = DBL_MAX;
+      int64_t ci = INT64_MAX;
+      for (int64_t p = p0 + lane; p < p1; p += IA_WAVE) {
+        const int64_t i = ia_pos_row(p, a.NT);
+        if (i >= a.NA) continue;
+        const double d = exact_dist_level<CH>(g, A, i, q);
+        if (d < cd || (d == cd && i < ci)) { cd = d; ci = i; }
+      }
+      wave_min_di(cd, ci);
+      if (cd < bd || (cd == bd && ci < bi)) {
+        bd = cd;
+        bi = ci;
+        recompute_app = true;
+      }
+      nfb++;
+    }
+  }
+
+  // coherence winner: first argmin of the norm over lanes 0..14
+  double dk = (lane < NCOH && my_row >= 0) ? sqrt(unw) : DBL_MAX;
+  int64_t kk = (lane < NCOH && my_row >= 0) ? (int64_t)lane : INT64_MAX;
+  wave_min_di(dk, kk);
+
+  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
+  int img = (int)((unsigned)bi / hw);
+  const unsigned rem = (unsigned)bi - (unsigned)img * hw;
+  int pr = (int)(rem / (unsigned)g.aw), pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
+  bool coh_won = false;
+  if (kk != INT64_MAX) {  // a coherence candidate exists (never for the level's first pixel)
+    const int src = (int)kk;
+    const int kpr = __shfl(cpr, src, 64), kpc = __shfl(cpc, src, 64), kim = __shfl(cim, src, 64);
+    const double wsq_coh = __shfl(wsq, src, 64);
+    if (recompute_app) {
+      double u, wq = 0.;
+      if (lane == 0) row_dists<CH>(g, A, (int)bi, q, weights, u, wq);
+      wsq_app = __shfl(wq, 0, 64);
+    }
+    // compute_distance = norm(x)**2 = sqrt(sum x^2)**2 ; kappa rule image_analogies.py:206
+    double d_app = sqrt(wsq_app), d_coh = sqrt(wsq_coh);
+    d_app = d_app * d_app;
+    d_coh = d_coh * d_coh;
+    if (d_coh <= d_app * kf) {
+      img = kim;
+      pr = kpr;
+      pc = kpc;
+      coh_won = true;
+    }
+  }
+  if (lane < CH) Bp[(int64_t)qi * CH + lane] = A.p3[img * A.img_stride_f + ((int64_t)pr * g.aw + pc) * CH + lane];
+  if (lane == 0) {
+    s[2 * qi] = pr;
+    s[2 * qi + 1] = pc;
+    im[qi] = img;
+    // per-pixel stats word (no shared-counter atomics: hundreds of waves adding to one
+    // address serialise at L2 and dominated this kernel); reduced once per level
+    a.pstat[qi] = (unsigned)min(slot, 0xffff) | ((unsigned)min((int)nfb, 0x3fff) << 16) | (coh_won ? 1u << 30 : 0u);
   }
 }
 
@@ -612,13 +895,37 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
                                                         double kf) {
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
   if (m >= sd.M) return;
+#if IA_PROBE == 0
+  if constexpr (FUSED) {
+    merge_fused<CH>(g, sd, A, ma, m, s, im, Bp, weights, kf);
+    return;
+  }
+#endif
   const double *q = ma.q64 + (int64_t)m * Geo<CH>::D;
-  const Winner wn = certified_winner(ma, m, [&](int64_t row) { return exact_dist_level<CH>(g, A, row, q); });
+#if IA_PROBE & 1  // diagnostic build only: take the first record's candidate, no rerank
+  const Winner wn{0., (int64_t)__float_as_int(ma.rec[(int64_t)m * ma.nwg].y)};
+#else
+  unsigned stat = 0;
+  const Winner wn = certified_winner(ma, m, [&](int64_t row) { return exact_dist_level<CH>(g, A, row, q); }, &stat);
+#endif
+#if IA_PROBE & 2  // diagnostic build only: no coherence / kappa
+  if ((threadIdx.x & 63) == 0) {
+    const int r = sd.r0 + m, qi = r * g.bw + sd.t - 3 * r;
+    s[2 * qi] = (int)(wn.idx / g.aw) % g.ah;
+    s[2 * qi + 1] = (int)(wn.idx % g.aw);
+    im[qi] = 0;
+  }
+  return;
+#endif
   if constexpr (FUSED) {
     const int r = sd.r0 + m;
-    finish_pixel<CH>(g, A, r, sd.t - 3 * r, wn.idx, q, s, im, Bp, weights, kf, ma.counters);
+    finish_pixel<CH>(g, A, r, sd.t - 3 * r, wn.idx, q, s, im, Bp, weights, kf, ma.pstat, stat);
   } else {
-    if ((threadIdx.x & 63) == 0) win[m] = wn;
+    if ((threadIdx.x & 63) == 0) {
+      win[m] = wn;
+      const int r = sd.r0 + m;
+      if (ma.pstat) ma.pstat[r * g.bw + sd.t - 3 * r] = stat;  // finish adds the coherence bit
+    }
   }
 }
 
@@ -628,7 +935,7 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
                                                          const Winner *__restrict__ allwin, int world, int Mstride,
                                                          int32_t *__restrict__ s, int32_t *__restrict__ im,
                                                          double *__restrict__ Bp, const double *__restrict__ weights,
-                                                         double kf, unsigned long long *counters) {
+                                                         double kf, unsigned *pstat) {
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
   if (m >= sd.M) return;
   double bd = DBL_MAX;
@@ -638,7 +945,32 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
     if (w.d < bd || (w.d == bd && w.idx < bi)) { bd = w.d; bi = w.idx; }
   }
   const int r = sd.r0 + m;
-  finish_pixel<CH>(g, A, r, sd.t - 3 * r, bi, q64 + (int64_t)m * Geo<CH>::D, s, im, Bp, weights, kf, counters);
+  const int qi = r * g.bw + sd.t - 3 * r;
+  const unsigned prev = pstat ? pstat[qi] : 0u;
+  finish_pixel<CH>(g, A, r, sd.t - 3 * r, bi, q64 + (int64_t)m * Geo<CH>::D, s, im, Bp, weights, kf, pstat, prev);
+}
+
+// per-level statistics: sum the per-pixel stats words (one workgroup, fixed order)
+__global__ void __launch_bounds__(IA_WG) k_reduce_stats(const unsigned *__restrict__ pstat, int64_t n,
+                                                         unsigned long long *__restrict__ counters) {
+  unsigned long long rr = 0, fb = 0, cw = 0;
+  for (int64_t i = threadIdx.x; i < n; i += IA_WG) {
+    const unsigned v = pstat[i];
+    rr += v & 0xffff;
+    fb += (v >> 16) & 0x3fff;
+    cw += (v >> 30) & 1;
+  }
+  __shared__ unsigned long long red[3][IA_WG];
+  red[0][threadIdx.x] = rr;
+  red[1][threadIdx.x] = fb;
+  red[2][threadIdx.x] = cw;
+  __syncthreads();
+  for (int o = IA_WG / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o)
+      for (int k = 0; k < 3; k++) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x < 3) counters[threadIdx.x] = red[threadIdx.x][0];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -649,11 +981,12 @@ __global__ void __launch_bounds__(IA_WG) k_dense_db_build(const double *__restri
                                                            const double *__restrict__ mu, float4 *__restrict__ db,
                                                            unsigned *__restrict__ Rbits) {
   constexpr int KP = KH / 4;
-  const int64_t row = (int64_t)blockIdx.x * IA_WG + threadIdx.x;
-  if (row >= (int64_t)n_tiles * IA_TILE) return;
+  const int64_t pos = (int64_t)blockIdx.x * IA_WG + threadIdx.x;
+  if (pos >= (int64_t)n_tiles * IA_TILE) return;
+  const int64_t row = ia_pos_row(pos, n_tiles);
   const bool real = row < n;
-  const int64_t tile = row / IA_TILE;
-  const int j = (int)(row % IA_TILE);
+  const int64_t tile = pos / IA_TILE;
+  const int j = (int)(pos % IA_TILE);
   double norm = 0.;
   for (int h = 0; h < 2; h++) {
     for (int p = 0; p < KP; p++) {
@@ -707,13 +1040,14 @@ __global__ void __launch_bounds__(IA_WG) k_merge_dense(MergeArgs ma, const doubl
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
   if (m >= nq) return;
   const double *qm = q + (int64_t)m * d;
+  unsigned stat;
   const Winner wn = certified_winner(ma, m, [&](int64_t row) {
     const double *a = pts + row * d;
     return pw_sum_rt([&](int f) {
       const double x = a[f] - qm[f];
       return x * x;
     }, d);
-  });
+  }, &stat);
   if ((threadIdx.x & 63) == 0) {
     idx_out[m] = wn.idx;
     dist_out[m] = wn.d;
@@ -762,7 +1096,7 @@ void ia_launch_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &B, cons
 }
 
 // K3 dispatch table: QT query tiles per launch (1..QTMAX(KH))
-typedef void (*k3_fn)(const float4 *, const float4 *, int, int, int, int, int, int, float4 *, float *);
+typedef void (*k3_fn)(const float4 *, const float4 *, int, int, int, int, int, int, int, float4 *, float *);
 template <int KH, int... QTs>
 struct K3Table {
   static k3_fn get(int qt) {
@@ -773,7 +1107,7 @@ struct K3Table {
 int ia_k3_qtmax(int KH) { return KH == 28 ? 11 : KH == 56 ? 5 : 3; }
 
 void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tiles, int tpw, int qt0, int M, int nwg,
-                  int row0, float4 *rec, float *recT, hipStream_t st) {
+                  int row0, int NT, float4 *rec, float *recT, hipStream_t st) {
   k3_fn fn;
   if (KH == 28) fn = K3Table<28, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11>::get(qt);
   else if (KH == 56) fn = K3Table<56, 1, 2, 3, 4, 5>::get(qt);
@@ -785,7 +1119,7 @@ void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tile
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_set[ki][qt] = true;
   }
-  hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WG), lds, st, db, qf, n_tiles, tpw, qt0, M, nwg, row0, rec, recT);
+  hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WG), lds, st, db, qf, n_tiles, tpw, qt0, M, nwg, row0, NT, rec, recT);
 }
 
 template <int CH>
@@ -807,16 +1141,20 @@ void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const
 template <int CH>
 static void launch_finish_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *q64, const Winner *allwin,
                             int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w, double kf,
-                            unsigned long long *ctr, hipStream_t st) {
+                            unsigned *ctr, hipStream_t st) {
   hipLaunchKernelGGL(k_finish_level<CH>, dim3(cdiv(sd.M, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, A, q64, allwin,
                      world, Mstride, s, im, Bp, w, kf, ctr);
 }
 void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *q64, const Winner *allwin,
                       int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w, double kf,
-                      unsigned long long *ctr, hipStream_t st) {
+                      unsigned *ctr, hipStream_t st) {
   if (g.ch == 1) launch_finish_t<1>(g, sd, A, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
   else if (g.ch == 2) launch_finish_t<2>(g, sd, A, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
   else launch_finish_t<3>(g, sd, A, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
+}
+
+void ia_launch_reduce_stats(const unsigned *pstat, int64_t n, unsigned long long *counters, hipStream_t st) {
+  hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(IA_WG), 0, st, pstat, n, counters);
 }
 
 void ia_launch_dense_db(int KH, const double *pts, int64_t n, int d, int n_tiles, const double *mu, float4 *db,

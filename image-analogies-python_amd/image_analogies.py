@@ -1,0 +1,151 @@
+"""Driver with the reference's entry points (image_analogies.py:17-268):
+img_setup(A_fname, Ap_fname_list, B_fname, out_path, c) and
+image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=False).
+
+Setup (image reading, scaling, YIQ, remap, compression, pyramids, B' initialisation) is host
+numpy as in the reference.  The per-level loop (image_analogies.py:130-239) is one
+ia_synthesize_level call per level on the GPU: create_index's DB for the level, the skewed
+wavefront over B', exact NN, coherence, the kappa rule and the B'/s/im writeback.  There is no
+CPU path.
+"""
+import os
+import pickle
+import time
+import warnings
+
+import numpy as np
+
+from . import _native
+from .algorithms import default_context
+from .config import save_metadata, setup_vars
+from .img_preprocess import (compress_values, compute_gaussian_pyramid, convert_to_RGB, convert_to_YIQ,
+                             initialize_Bp, remap_luminance)
+
+
+def _imread(src):
+    if isinstance(src, np.ndarray):
+        return src
+    import matplotlib.image as mpimg
+    return mpimg.imread(src)
+
+
+def _imsave(path, img):
+    import matplotlib.image as mpimg
+    mpimg.imsave(path, np.clip(img, 0, 1))
+
+
+def img_setup(A_fname, Ap_fname_list, B_fname, out_path, c):
+    """image_analogies.py:17-94.  File names may also be numpy arrays."""
+    os.makedirs(out_path, exist_ok=True)
+    A_orig, B_orig = _imread(A_fname), _imread(B_fname)
+    if A_orig.ndim != B_orig.ndim:
+        raise ValueError('A and B must have the same number of channels')
+    Ap_orig_list = [_imread(f) for f in Ap_fname_list]
+    for Ap_orig in Ap_orig_list:
+        if Ap_orig.shape != A_orig.shape:
+            raise ValueError("every A' must be aligned with A (same shape)")
+    # 0..255 vs 0..1 detection; the reference tests the FIRST ROW of the LAST A' (quirk, :33)
+    scale = lambda x: 255. if np.max(x) > 1.0 else 1.0
+    sA, sB, sAp = scale(A_orig), scale(B_orig), scale(Ap_orig_list[-1][0])
+
+    if c.convert:
+        A = convert_to_YIQ(A_orig / sA)[:, :, 0]
+        B_yiq = convert_to_YIQ(B_orig / sB)
+        B = B_yiq[:, :, 0]
+        Ap_list = [convert_to_YIQ(x / sAp)[:, :, 0] for x in Ap_orig_list]
+    else:
+        A, B = A_orig / sA, B_orig / sB
+        Ap_list = [x / sAp for x in Ap_orig_list]
+    if c.remap_lum:
+        A, Ap_list = remap_luminance(A, Ap_list, B)
+    if not c.init_rand:
+        B_orig_pyr = compute_gaussian_pyramid(B, c.n_sm, c.n_levels)
+    A, B = compress_values(A, B, c.AB_weight)
+    c.num_ch, c.padding_sm, c.padding_lg, c.weights = setup_vars(A)
+
+    A_pyr = compute_gaussian_pyramid(A, c.n_sm, c.n_levels)
+    B_pyr = compute_gaussian_pyramid(B, c.n_sm, c.n_levels)
+    Ap_pyr_list = [compute_gaussian_pyramid(x, c.n_sm, c.n_levels) for x in Ap_list]
+    if c.convert:
+        color_pyr_list = [compute_gaussian_pyramid(B_yiq, c.n_sm, c.n_levels)]
+    else:
+        color_pyr_list = [compute_gaussian_pyramid(x, c.n_sm, c.n_levels) for x in Ap_list]
+
+    if len(A_pyr) != len(B_pyr):
+        c.max_levels = min(len(A_pyr), len(B_pyr))
+        warnings.warn('Warning: input images are very different sizes! The minimum number of levels will be used.')
+        if getattr(c, 'level_align', 'coarse') == 'fine' and len(B_pyr) > len(A_pyr):
+            # extension: pair B's finest levels with A's (B level k+d <-> A level k)
+            d = len(B_pyr) - len(A_pyr)
+            B_pyr = B_pyr[d:]
+            if c.convert:
+                color_pyr_list = [p[d:] for p in color_pyr_list]
+            if not c.init_rand:
+                B_orig_pyr = B_orig_pyr[d:]
+    else:
+        c.max_levels = len(B_pyr)
+    src = B_pyr if c.init_rand else B_orig_pyr
+    Bp_pyr = initialize_Bp(src, init_rand=c.init_rand, seed=getattr(c, 'seed', None))
+    return A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list, c
+
+
+def synthesize_pyramid(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c, ctx=None, stats=None, on_level=None):
+    """The level loop of image_analogies_main (image_analogies.py:130-239) on the GPU.
+    Bp_pyr levels 1..max_levels-1 are synthesised in place; returns ({level: s}, {level: im})."""
+    ctx = ctx or default_context()
+    L = c.max_levels
+    S, IM = {}, {}
+    for level in range(1, L):
+        Bp_pyr[level] = np.ascontiguousarray(Bp_pyr[level], dtype=np.float64)
+        kf = 1 + (2 ** (level - L)) * c.k          # image_analogies.py:206
+        S[level], IM[level] = ctx.synthesize_level(
+            A_pyr[level], A_pyr[level - 1], [p[level] for p in Ap_pyr_list], [p[level - 1] for p in Ap_pyr_list],
+            B_pyr[level], B_pyr[level - 1], Bp_pyr[level - 1], Bp_pyr[level], c.weights, kf, stats)
+        if on_level is not None:
+            on_level(level, S, IM)
+    return S, IM
+
+
+def level_colour(level, Bp_pyr, S, IM, color_pyr_list, c):
+    """Colour output of a level (image_analogies.py:216-217, 255-258)."""
+    if c.convert:
+        return np.clip(convert_to_RGB(np.dstack([Bp_pyr[level], color_pyr_list[0][level][:, :, 1:]])), 0, 1)
+    h, w = Bp_pyr[level].shape[:2]
+    src = np.stack([p[level] for p in color_pyr_list])[IM[level], S[level][:, 0], S[level][:, 1]]
+    out = np.empty((h * w, 3))
+    out[:] = src.reshape(h * w, -1)
+    return out.reshape(h, w, 3)
+
+
+def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=False):
+    """image_analogies.py:97-268.  Writes metadata.txt, level_<l>_color.jpg and
+    <dirname>.jpg per level like the reference; debug=True additionally pickles [s, im] per
+    level (the reference's [sa, sc, rstars, s, im] debug lists are not produced: the GPU level
+    path keeps no per-pixel candidate log).  Returns {'Bp_pyr', 's', 'im', 'stats'}."""
+    begin = time.time()
+    A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list, c = img_setup(A_fname, Ap_fname_list, B_fname, out_path, c)
+    names = ['A_fname', 'Ap_fname_list', 'B_fname', 'c.convert', 'c.remap_lum', 'c.init_rand', 'c.AB_weight', 'c.k']
+    vals = [A_fname if isinstance(A_fname, str) else '<array>',
+            [f if isinstance(f, str) else '<array>' for f in Ap_fname_list],
+            B_fname if isinstance(B_fname, str) else '<array>', c.convert, c.remap_lum, c.init_rand, c.AB_weight, c.k]
+    save_metadata(out_path, names, vals)
+    print('Environment Setup: %f' % (time.time() - begin))
+
+    stats = _native.Stats()
+    state = {'t': time.time()}
+
+    def on_level(level, S, IM):
+        col = level_colour(level, Bp_pyr, S, IM, color_pyr_list, c)
+        _imsave(out_path + 'level_%d_color.jpg' % level, col)
+        _imsave(out_path + out_path.rstrip('/').split('/')[-1] + '.jpg', col)
+        if debug:
+            with open(out_path + '%d_srcs.pickle' % level, 'wb') as f:
+                pickle.dump([S[level], IM[level]], f)
+        now = time.time()
+        print('Level %d time: %f' % (level, now - state['t']))
+        state['t'] = now
+
+    S, IM = synthesize_pyramid(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c, stats=stats, on_level=on_level)
+    print('Total time: %f' % (time.time() - begin))
+    print('GPU synthesis time: %f (DB build %f)' % (stats.synth_ms / 1e3, stats.db_ms / 1e3))
+    return {'Bp_pyr': Bp_pyr, 's': S, 'im': IM, 'stats': stats.as_dict()}

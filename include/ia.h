@@ -50,9 +50,13 @@ typedef struct {
   int64_t fallbacks;       /* uncertified DB chunks rescanned exactly */
   double db_ms;            /* DB build time (device) */
   double synth_ms;         /* wavefront time (device) */
-  double dist_ms;          /* time inside the MFMA distance kernel (device events) */
   int64_t dist_launches;   /* MFMA distance kernel launches */
   double dist_flops;       /* algorithmic flops 2*D*N_A*(queries) of those launches */
+  /* sampled timing of the MFMA distance kernel (option "time_dist" = sampling stride S > 0:
+   * every S-th wavefront step's distance launches are bracketed by HIP events) */
+  double dist_ms;          /* device time of the sampled launches */
+  int64_t dist_launches_timed;
+  double dist_flops_timed; /* algorithmic flops of the sampled launches */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
@@ -81,8 +85,9 @@ int ia_init(int device, ia_ctx **out);
 void ia_destroy(ia_ctx *ctx);
 const char *ia_last_error(void);
 int ia_version(void);
-/* Options: "time_dist" (0/1) brackets every MFMA distance launch with HIP events so that
- * ia_stats.dist_ms holds the kernel's measured device time (bench.py roofline). */
+/* Options: "time_dist" = S (0 = off): bracket the MFMA distance launches of every S-th
+ * wavefront step with HIP events; ia_stats.dist_ms / dist_flops_timed then give the kernel's
+ * measured device time and algorithmic flops (bench.py roofline). */
 int ia_set_option(ia_ctx *ctx, const char *name, int value);
 /* Multi-GPU (one process per GPU): A rows of every level are split into `world` contiguous
  * shards; per wavefront step each rank exchanges its certified per-query winners with one
@@ -110,6 +115,13 @@ int ia_merge_winners(const double *dist, const int64_t *row, int world, int64_t 
                      double *dist_out, int64_t *row_out);
 /* Wavefront schedule of a level (t = col + 3*row): number of steps and max queries per step. */
 int ia_wavefront_shape(int h, int w, int64_t *steps, int64_t *max_queries);
+/* Pixels of step t: rows r0 .. r0+M-1, pixel (r, t - 3r).  Used by the level driver. */
+int ia_wavefront_step(int h, int w, int64_t t, int *r0, int *M);
+/* DB tiles [tile0, tile1) owned by `rank` of `world` for a level of n_rows DB rows.  The DB is
+ * stored in ceil(n_rows/32) tiles of 32 positions; position j of tile t holds row j*n_tiles + t
+ * (tile-strided, so neighbouring A pixels sit in different tiles).  Tiles are split contiguously
+ * over ranks; levels under 64*world tiles are not sharded (every rank owns every tile). */
+int ia_shard_tiles(int64_t n_rows, int world, int rank, int64_t *tile0, int64_t *tile1);
 
 #ifdef __cplusplus
 }

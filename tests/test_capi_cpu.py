@@ -1,0 +1,98 @@
+"""The C ABI without a GPU: libia.so loads, exports every entry point include/ia.h declares,
+fails loudly (IA_ENODEV) instead of falling back to the CPU, and its host-side helpers (wavefront
+schedule, shard split, winner merge) are right."""
+import os
+import re
+
+import numpy as np
+import pytest
+
+import ia_amd  # noqa: F401
+from ia_amd import _native
+from conftest import ROOT
+
+
+def _declared():
+    hdr = open(os.path.join(ROOT, 'include', 'ia.h')).read()
+    return sorted(set(re.findall(r'\b(ia_[a-z_]+)\s*\(', hdr)))
+
+
+def test_library_exports_every_declared_symbol():
+    L = _native.lib()
+    names = _declared()
+    assert len(names) >= 14
+    for n in names:
+        assert hasattr(L, n), n
+        assert n in _native.EXPORTS, n
+
+
+def test_no_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('a GPU is visible')
+    with pytest.raises(_native.IAError, match='IA_ENODEV'):
+        _native.Context(0)
+
+
+def test_last_error_and_einval():
+    with pytest.raises(_native.IAError, match='IA_EINVAL'):
+        _native.wavefront_step(4, 4, 999)
+    with pytest.raises(_native.IAError, match='IA_EINVAL'):
+        _native.shard_rows(0, 2, 0)
+
+
+@pytest.mark.parametrize('h,w', [(1, 1), (1, 7), (7, 1), (2, 2), (3, 5), (4, 6), (8, 8), (15, 23), (59, 90),
+                                 (117, 180), (64, 64), (1024, 1024)])
+def test_wavefront_covers_level_in_causal_order(h, w):
+    """with t = c + 3r every pixel appears exactly once, every causal read
+    (rows r-2..r-1 x cols c-2..c+2, and (r, c-2), (r, c-1)) lies in an earlier step, and no
+    reflected read of a raster-later pixel lies in the same step."""
+    T, M = _native.wavefront_shape(h, w)
+    assert T == w + 3 * (h - 1) and M == min(h, (w + 2) // 3)
+    step = -np.ones((h, w), dtype=np.int64)
+    for t in range(T):
+        r0, m = _native.wavefront_step(h, w, t)
+        assert 0 <= m <= M and (m >= 1 or w < 3)
+        for r in range(r0, r0 + m):
+            c = t - 3 * r
+            assert 0 <= c < w and step[r, c] == -1
+            step[r, c] = t
+    assert (step >= 0).all()
+    if h * w > 4096:
+        return
+    refl = lambda i, n: (i % (2 * n)) if (i % (2 * n)) < n else 2 * n - 1 - (i % (2 * n))
+    for r in range(h):
+        for c in range(w):
+            t = step[r, c]
+            reads = [(r + dy, c + dx) for dy in (-2, -1) for dx in range(-2, 3)] + [(r, c - 2), (r, c - 1)]
+            for (y, x) in reads:
+                yy, xx = refl(y, h), refl(x, w)
+                if yy * w + xx < r * w + c:
+                    assert step[yy, xx] < t          # synthesised before (reference sees final)
+                elif (yy, xx) != (r, c):
+                    assert step[yy, xx] > t          # still initial in both orders
+
+
+def test_shard_tiles_partition():
+    """Tiles split contiguously over ranks; the rows they hold (tile-strided layout) partition
+    0..n_rows-1 exactly; small levels are replicated."""
+    for n in (1, 31, 32, 100, 64 * 32 * 8, 70000, 1 << 16):
+        nt = (n + 31) // 32
+        for world in (1, 2, 4, 8):
+            parts = [_native.shard_tiles(n, world, k) for k in range(world)]
+            if parts[0] == (0, nt):
+                assert all(p == (0, nt) for p in parts)        # replicated level
+                continue
+            assert parts[0][0] == 0 and parts[-1][1] == nt
+            for a, b in zip(parts, parts[1:]):
+                assert a[1] == b[0]
+            rows = np.concatenate([_native.shard_rows(n, world, k) for k in range(world)])
+            assert np.array_equal(np.sort(rows), np.arange(n))
+
+
+def test_merge_winners_lowest_index_on_ties():
+    d = np.array([[1.0, 2.0, 3.0, 0.5], [1.0, 1.5, 3.0, 0.5], [0.9, 2.0, 3.0, 0.5]])
+    r = np.array([[10, 20, 30, 7], [5, 21, 31, 3], [11, 22, 29, 9]])
+    do, ro = _native.merge_winners(d, r)
+    assert list(do) == [0.9, 1.5, 3.0, 0.5]
+    assert list(ro) == [11, 21, 29, 3]
