@@ -35,6 +35,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "B' pixels synthesized/sec, exact NN, 1024² A/A'/B, 1/2/4/8 GPUs; % MFMA peak"
 FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
+F16_MFMA_PEAK = 2.5e15      # MI355X_MICROARCH.md: BF16/F16 ~2.5 PF dense (same cycles for f16)
 HBM_PEAK = 8.0e12
 
 
@@ -107,6 +108,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=1)
     ap.add_argument('--config', default='cfg3', help='synthetic workload (ia_amd.synth.CONFIGS)')
     ap.add_argument('--mode', default='replicas', choices=['replicas', 'shard'])
+    ap.add_argument('--matcher', default='f16x3', choices=['f16x3', 'f32'],
+                    help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
     ap.add_argument('--time-stride', type=int, default=4, help='sample K3 timing every S-th wavefront step')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -135,6 +138,7 @@ def main():
         % (rank, args.config, time.time() - t0, job.L, job.pixels, job.flops()))
 
     ctx = _native.Context(local)
+    ctx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
     if args.mode == 'shard' and world > 1:
         uid = [_native.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -177,25 +181,36 @@ def main():
             traffic = json.load(open(args.traffic_json)).get('hbm_bytes_per_launch')
         except Exception:
             traffic = None
-    roofline = {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': FP32_MFMA_PEAK / 1e12, 'unit': 'TFLOP/s',
-                'frac': achieved / FP32_MFMA_PEAK, 'traffic': traffic,
-                'kernel': 'k3_dist (v_mfma_f32_32x32x2_f32 distance scan + fused top-2)',
+    f16 = st['f16_levels'] > 0
+    peak = F16_MFMA_PEAK if f16 else FP32_MFMA_PEAK
+    ch = dj.ch
+    D = 55 * ch
+    # MFMA flops the kernel issues per algorithmic flop: 3 f16 passes over 16*KS padded k
+    # (split-f16) or 2*KH padded k (fp32); query-tile padding to 32 not included
+    issued = 3.0 * 16 * {1: 4, 2: 7}.get(ch, 0) / D if f16 else (56 if ch == 1 else 112 if ch == 2 else 168) / D
+    roofline = {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': peak / 1e12, 'unit': 'TFLOP/s',
+                'frac': achieved / peak, 'traffic': traffic,
+                'mfma_issue_frac': achieved * issued / peak,
+                'kernel': ('k3h_dist (3 x v_mfma_f32_32x32x16_f16 on hi/lo-split operands, fused top-2)' if f16 else
+                           'k3_dist (v_mfma_f32_32x32x2_f32 distance scan + fused top-2)'),
                 'k3_us_per_launch': k3_ms_per_launch * 1e3, 'k3_launches_sampled': st['dist_launches_timed'],
                 'k3_share_of_step': st['dist_ms'] * (st['dist_flops'] / max(st['dist_flops_timed'], 1)) /
                 max(elapsed * 1e3, 1e-9)}
 
     out = {'metric': METRIC, 'value': value, 'unit': "B' px/s", 'n_gpus': world, 'steps': args.steps,
            'warmup': args.warmup, 'ms_per_step': elapsed * 1e3 / args.steps, 'higher_is_better': True,
-           'scaling': 'weak' if args.mode == 'replicas' else 'strong', 'vs_baseline': None, 'dtype': 'f32',
+           'scaling': 'weak' if args.mode == 'replicas' else 'strong', 'vs_baseline': None,
+           'dtype': 'f16x3' if f16 else 'f32',
            'data': 'synthetic', 'config': {'workload': '%s: %s' % (args.config, desc),
                                            'a_shape': list(job.A_pyr[-1].shape), 'pyramid_levels': job.L,
                                            'px_per_step': job.pixels, 'nn_flops_per_step': job.flops(),
                                            'mode': args.mode, 'parallelism': ('replicas%d' if args.mode == 'replicas'
                                                                               else 'dbshard%d') % world,
-                                           'nn': 'exact: fp32 MFMA candidates + certified fp64 rerank'},
+                                           'nn': 'exact: %s MFMA candidates + certified fp64 rerank'
+                                                 % ('split-f16 (hi/lo x3)' if f16 else 'fp32')},
            'roofline': roofline,
            'stats': {k: st[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
-                                        'synth_ms')}}
+                                        'synth_ms', 'bound_violations', 'f16_levels')}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(job, args.cpu_seconds)
     if rank == 0:

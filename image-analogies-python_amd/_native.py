@@ -13,6 +13,7 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get('IA_LIBIA', os.path.join(_HERE, 'libia.so'))  # override: diagnostic builds
 
 IA_MEM_HOST, IA_MEM_DEVICE = 0, 1
+IA_MATCH_F32, IA_MATCH_F16X3 = 0, 1   # option "matcher" (include/ia.h)
 _ERRNAMES = {-1: 'IA_EINVAL', -2: 'IA_EHIP', -3: 'IA_ENOMEM', -4: 'IA_ENODEV', -5: 'IA_ECOMM'}
 
 
@@ -34,7 +35,8 @@ class Stats(ctypes.Structure):
                 ('reranked', ctypes.c_int64), ('fallbacks', ctypes.c_int64), ('db_ms', ctypes.c_double),
                 ('synth_ms', ctypes.c_double), ('dist_launches', ctypes.c_int64), ('dist_flops', ctypes.c_double),
                 ('dist_ms', ctypes.c_double), ('dist_launches_timed', ctypes.c_int64),
-                ('dist_flops_timed', ctypes.c_double)]
+                ('dist_flops_timed', ctypes.c_double), ('bound_violations', ctypes.c_int64),
+                ('f16_levels', ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -75,7 +75,8 @@ struct ia_ctx {
   hipStream_t st = nullptr;
   // uploads (IA_MEM_HOST) and per-level scratch
   DevBuf A, Ac, Ap, Apc, B, Bc, Bpc, Bp, S, IM, W;
-  DevBuf db, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, pstat;
+  DevBuf db, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, pstat, absmax;
+  int matcher = IA_MATCH_F16X3;  // option "matcher"
   // per-step K3 timing (optional)
   int time_dist = 0;
   std::vector<hipEvent_t> evs;
@@ -125,7 +126,7 @@ void ia_destroy(ia_ctx *c) {
   hipSetDevice(c->dev);
   hipStreamSynchronize(c->st);
   for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->B, &c->Bc, &c->Bpc, &c->Bp, &c->S, &c->IM, &c->W, &c->db,
-                    &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->pstat})
+                    &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->pstat, &c->absmax})
     b->release();
   for (hipEvent_t e : c->evs) hipEventDestroy(e);
   hipEventDestroy(c->lv0);
@@ -140,6 +141,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!c || !name) return fail(IA_EINVAL, "ia_set_option: NULL argument");
   if (!std::strcmp(name, "time_dist")) {
     c->time_dist = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "matcher")) {
+    if (value != IA_MATCH_F32 && value != IA_MATCH_F16X3) return fail(IA_EINVAL, "ia_set_option: matcher must be 0 or 1");
+    c->matcher = value;
     return IA_OK;
   }
   return fail(IA_EINVAL, std::string("ia_set_option: unknown option ") + name);
@@ -303,13 +309,38 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     HIP_TRY(hipMemcpyAsync(dBp, a->Bp, nB * 8, hipMemcpyHostToDevice, c->st));
   }
 
+  // matcher: split-f16 when the channel count has a K3h instance and every image value fits
+  // (IA_F16_MAXABS, one 4-byte read-back per level); otherwise the fp32 MFMA scan
+  bool use_h = false;
+  if (c->matcher == IA_MATCH_F16X3 && ia_ks_for(g.ch) > 0) {
+    if ((rc = c->absmax.ensure(4))) return rc;
+    HIP_TRY(hipMemsetAsync(c->absmax.p, 0, 4, c->st));
+    const double *arrs[8] = {(const double *)dA, (const double *)dAc, (const double *)dAp, (const double *)dApc,
+                             (const double *)dB, (const double *)dBc, (const double *)dBpc, dBp};
+    const int64_t ns8[8] = {(int64_t)nA, (int64_t)nAc, (int64_t)(nA * g.n_ap), (int64_t)(nAc * g.n_ap),
+                            (int64_t)nB, (int64_t)nBc, (int64_t)nBc, (int64_t)nB};
+    ia_launch_absmax(arrs, ns8, c->absmax.as<unsigned>(), c->st);
+    unsigned mbits = 0;
+    HIP_TRY(hipMemcpyAsync(&mbits, c->absmax.p, 4, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    float mx;
+    std::memcpy(&mx, &mbits, 4);
+    use_h = mx <= IA_F16_MAXABS;
+  }
+  g.KS = use_h ? ia_ks_for(g.ch) : 0;
+  if (use_h) {
+    g.tiles_per_wg = std::max(IA_WGH / IA_WAVE, (ns + IA_NWG_H - 1) / IA_NWG_H);
+    g.nwg = (ns + g.tiles_per_wg - 1) / g.tiles_per_wg;
+  }
+  const size_t db_row_bytes = use_h ? (size_t)16 * g.KS * 4 : (size_t)DP * 4;  // hi+lo f16 / fp32 per column
+
   // per-level scratch
   int64_t T, Mmax;
   ia_wavefront_shape(g.bh, g.bw, &T, &Mmax);
   const int64_t Mpad_max = (Mmax + IA_TILE - 1) / IA_TILE * IA_TILE;
-  if ((rc = c->db.ensure((size_t)std::max(ns, 1) * IA_TILE * DP * 4)) || (rc = c->mu.ensure(4 * g.ch * 8)) ||
+  if ((rc = c->db.ensure((size_t)std::max(ns, 1) * IA_TILE * db_row_bytes)) || (rc = c->mu.ensure(4 * g.ch * 8)) ||
       (rc = c->Rbits.ensure(4)) || (rc = c->q64.ensure((size_t)Mpad_max * g.D * 8)) ||
-      (rc = c->qn2.ensure((size_t)Mpad_max * 8)) || (rc = c->qf.ensure((size_t)Mpad_max * DP * 4)) ||
+      (rc = c->qn2.ensure((size_t)Mpad_max * 8)) || (rc = c->qf.ensure((size_t)Mpad_max * db_row_bytes)) ||
       (rc = c->rec.ensure((size_t)Mmax * std::max(g.nwg, 1) * 16)) ||
       (rc = c->recT.ensure((size_t)Mmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mmax * 16)) ||
       (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(4 * 8)) ||
@@ -325,7 +356,10 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
 
   HIP_TRY(hipEventRecord(c->lv0, c->st));
   ia_launch_means(g.ch, Aim, g.n_ap, c->mu.as<double>(), c->st);
-  if (ns > 0) ia_launch_db_build(g, Aim, c->mu.as<double>(), c->db.as<float4>(), c->Rbits.as<unsigned>(), c->st);
+  if (ns > 0) {
+    if (use_h) ia_launch_db_build_h(g, Aim, c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
+    else ia_launch_db_build(g, Aim, c->mu.as<double>(), c->db.as<float4>(), c->Rbits.as<unsigned>(), c->st);
+  }
   HIP_TRY(hipEventRecord(c->lv1, c->st));
 
   MergeArgs ma;
@@ -343,9 +377,10 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   int64_t shard_rows = 0;  // real DB rows in this shard's tiles (strided layout)
   for (int t = g.tile0; t < g.tile1; t++) shard_rows += std::min<int64_t>(IA_TILE, (g.NA - t + g.n_tiles - 1) / g.n_tiles);
   ma.pstat = c->pstat.as<unsigned>();
-  ma.eps_c = ia_eps_c(DP);
+  ma.eps_c = use_h ? ia_eps_c_h(g.KS) : ia_eps_c(DP);
+  ma.eps_a = use_h ? ia_eps_a_h() : 0.;
 
-  const int qtmax = ia_k3_qtmax(g.KH);
+  const int qtmax = use_h ? ia_k3h_qtmax(g.KS) : ia_k3_qtmax(g.KH);
   const int stride = c->time_dist > 0 ? c->time_dist : 0;
   const int64_t n_timed = stride ? (T + stride - 1) / stride : 0;
   if ((int64_t)c->evs.size() < 2 * n_timed) {
@@ -361,7 +396,10 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     ia_wavefront_step(g.bh, g.bw, t, &sd.r0, &sd.M);
     if (sd.M <= 0) continue;  // levels narrower than 3 columns have empty steps
     sd.Mpad = (sd.M + IA_TILE - 1) / IA_TILE * IA_TILE;
-    ia_launch_gather(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(), c->st);
+    if (use_h)
+      ia_launch_gather_h(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p, c->st);
+    else
+      ia_launch_gather(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(), c->st);
     if (ns > 0) {
       const int qtt = sd.Mpad / IA_TILE, nqb = (qtt + qtmax - 1) / qtmax;
       const bool timed = stride && t % stride == 0;
@@ -369,8 +407,12 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       int qt0 = 0;
       for (int b = 0; b < nqb; b++) {
         const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
-        ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0, ma.NT,
-                     c->rec.as<float4>(), c->recT.as<float>(), c->st);
+        if (use_h)
+          ia_launch_k3h(g.KS, qt, c->db.p, c->qf.p, ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0, ma.NT, c->rec.as<float4>(),
+                        c->recT.as<float>(), c->st);
+        else
+          ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0,
+                       ma.NT, c->rec.as<float4>(), c->recT.as<float>(), c->st);
         const int mq = std::min(sd.M, (qt0 + qt) * IA_TILE) - qt0 * IA_TILE;
         const double fl = 2.0 * g.D * (double)shard_rows * std::max(mq, 0);
         dist_flops += fl;
@@ -413,6 +455,8 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     stats->reranked += (int64_t)ctr[0];
     stats->fallbacks += (int64_t)ctr[1];
     stats->coherence_wins += (int64_t)ctr[2];
+    stats->bound_violations += (int64_t)ctr[3];
+    stats->f16_levels += use_h ? 1 : 0;
     stats->db_ms += ms_db;
     stats->synth_ms += ms_syn;
     stats->dist_launches += dist_launches;
@@ -504,6 +548,7 @@ int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, d
   ma.NA = (int)x->n;
   ma.pstat = nullptr;
   ma.eps_c = ia_eps_c(DP);
+  ma.eps_a = 0.;
   const int qtmax = ia_k3_qtmax(x->KH);
   for (int64_t b0 = 0; b0 < nq; b0 += BATCH) {
     const int64_t nb = std::min(BATCH, nq - b0);

@@ -21,6 +21,14 @@
 #define IA_MAX_D 168        // max padded feature width (3 channels: 165 + norm -> 168)
 #define IA_WG_TARGET 512    // distance-kernel workgroups per step (2 per CU on 256 CUs)
 #define IA_PAD_NORM 1.0e30f // norm of padding rows: never a candidate
+#define IA_WGH 512          // threads per workgroup of the split-f16 distance kernel (8 waves)
+#define IA_NWG_H 256        // its workgroups per step (1 per CU: the step's queries fill LDS)
+#define IA_NORM_SCALE 256.0 // split-f16 DB stores |a'|^2 / 256 (query column D holds 256)
+#define IA_F16_MAXABS 64.0  // split-f16 matcher only when every image value is within +-64
+
+// nearest-neighbour matcher of the distance scan (option "matcher")
+#define IA_MATCH_F32 0      // v_mfma_f32_32x32x2_f32 on fp32 operands
+#define IA_MATCH_F16X3 1    // v_mfma_f32_32x32x16_f16 x3 on hi/lo-split f16 operands
 
 // feature descriptor: which image part, offset and channel
 //   part 0: coarse 3x3 of A (level l-1)   part 1: fine 5x5 of A (level l)
@@ -31,6 +39,7 @@ struct FeatDesc {
 
 struct LevelGeo {
   int ch, D, KH, n_ap;
+  int KS;                   // split-f16 k-steps of 16 (0: fp32 matcher)
   int ah, aw, ahc, awc;     // A level l / l-1 dims
   int bh, bw, bhc, bwc;     // B level l / l-1 dims
   int64_t NA;               // DB rows = n_ap * ah * aw
@@ -59,8 +68,10 @@ struct MergeArgs {
   int NT;              // tiles of the whole DB: position p holds row ia_pos_row(p, NT)
   int NA;              // DB rows
   unsigned *pstat;                    // per-pixel stats word of the level (nullptr: none):
-                                      // bits 0-15 reranked, 16-29 fallbacks, 30 coherence won
-  double eps_c;                       // 1.05 * gamma_(DP+2), see DESIGN.md §4
+                                      // bits 0-15 reranked, 16-29 fallbacks, 30 coherence won,
+                                      // 31 an MFMA value outside the certified error bound
+  double eps_c;                       // relative error coefficient of the MFMA value
+  double eps_a;                       // absolute (f16 subnormal) error coefficient
 };
 
 // DB positions are tile-strided: slot j of tile t holds row j*NT + t, so spatially adjacent A
@@ -100,3 +111,17 @@ inline double ia_eps_c(int DP) {
   const double nu = (DP + 2) * 5.9604644775390625e-08;
   return 1.05 * nu / (1.0 - nu);
 }
+
+// Split-f16 MFMA value: x = a' or |a'|^2/256, y = -2q' or 256, each split as
+// hi = f16(f32(x)), lo = f16(f32(x) - hi); the kernel sums hi*hi + lo*hi + hi*lo (exact f16
+// products) in fp32 over n <= 48*KS + 4 terms.  Per term |x*y - computed| <= 3.5*2^-22 |x y| +
+// 2^-25 (|x| + |y|) (representation + dropped lo*lo; 2^-25 = half the f16 subnormal spacing),
+// and the fp32 accumulation, whatever its internal order or rounding (round-to-nearest or
+// truncation, hence u = 2^-23), adds gamma_n * sum|terms|.  With sum|x y| <= R^2 + 2R|q'| and
+// sum(|x| + |y|) <= R^2/256 + sqrt(D)(R + 2|q'|) + 256 + 1 (D <= 176):
+//   eps = eps_c (R^2 + 2R|q'|) + eps_a (R^2 + 14 R + 28|q'| + 260)
+inline double ia_eps_c_h(int KS) {
+  const double nu = (48.0 * KS + 4) * 1.1920928955078125e-07;
+  return 1.05 * (nu / (1.0 - nu) * (1.0 + 1.0 / 512) + 3.5 * 2.384185791015625e-07);
+}
+inline double ia_eps_a_h() { return 1.05 * 2.9802322387695312e-08; }

@@ -483,6 +483,261 @@ k3_dist(const float4 *__restrict__ db, const float4 *__restrict__ qf, int n_tile
 }
 
 // ------------------------------------------------------------------------------------------
+// Split-f16 matcher (IA_MATCH_F16X3): K1h / K2h / K3h
+//
+// Every operand x (centred DB feature a', |a'|^2/256, query -2q', 256) is split into
+// hi = f16(f32(x)) and lo = f16(f32(x) - hi) (22 significant bits together); K3h sums
+// lo_a*hi_q + hi_a*lo_q + hi_a*hi_q with v_mfma_f32_32x32x16_f16 (f16 products are exact in
+// fp32), i.e. 3 f16 MFMAs replace 8 f32 ones per 16 k.  The value carries a larger, still
+// rigorous, error bound (ia_eps_c_h), so K4's certification keeps the NN exact.
+// Fragment order (tile of 32 DB rows or 32 queries, k-step s of 16, part 0 = hi / 1 = lo):
+//   h16x8 piece p = 2s + part, lane L:  row (L & 31), k = 16s + 8(L >> 5) + e, e = 0..7
+// ------------------------------------------------------------------------------------------
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ void split_h(double x, _Float16 &hi, _Float16 &lo) {
+  const float xf = (float)x;
+  const _Float16 h = (_Float16)xf;
+  hi = h;
+  lo = (_Float16)(xf - (float)h);  // exact in fp32: xf and h share the leading bits
+}
+
+// max |x| over the level's images (decides whether every operand fits f16, IA_F16_MAXABS)
+struct AbsArrays {
+  const double *p[8];
+  int64_t n[8];
+};
+__global__ void __launch_bounds__(IA_WG) k_absmax(AbsArrays arr, unsigned *__restrict__ out) {
+  float m = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; k++) {
+    const double *p = arr.p[k];
+    const int64_t n = arr.n[k];
+    for (int64_t i = (int64_t)blockIdx.x * IA_WG + threadIdx.x; i < n; i += (int64_t)gridDim.x * IA_WG)
+      m = fmaxf(m, (float)fabs(p[i]));  // NaN propagates as "not finite" below
+  }
+  if (!(m <= 3.0e38f)) m = 3.4e38f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+  if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
+}
+
+template <int CH, int KS>
+__global__ void __launch_bounds__(IA_WG) k_db_build_h(LevelGeo g, Imgs A, const double *__restrict__ mu_part,
+                                                       h16x8 *__restrict__ db, unsigned *__restrict__ Rbits) {
+  constexpr int D = 55 * CH, NP = 2 * KS;
+  static_assert(16 * KS >= D + 1, "k-steps must hold D features + the norm column");
+  const int64_t pos = (int64_t)g.tile0 * IA_TILE + (int64_t)blockIdx.x * IA_WG + threadIdx.x;
+  const bool inr = pos < (int64_t)g.tile1 * IA_TILE;
+  const int64_t ltile = pos / IA_TILE - g.tile0;
+  const int j = (int)(pos % IA_TILE);
+  const int64_t row = ia_pos_row(pos, g.n_tiles);
+  const bool real = inr && row < g.NA;
+  int img = 0, pr = 0, pc = 0;
+  if (real) {
+    const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
+    img = (int)((unsigned)row / hw);
+    const unsigned rem = (unsigned)row - (unsigned)img * hw;
+    pr = (int)(rem / (unsigned)g.aw);
+    pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
+  }
+  const Px P = make_px<CH>(A, pr, pc);
+  double norm = 0.;
+#pragma unroll
+  for (int s = 0; s < KS; s++) {
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+      h16x8 vh, vl;
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const int f = 16 * s + 8 * h + e;
+        double a = 0.;
+        if (f < D) {
+          if (real) {
+            a = featp<CH>(A, P, f, img) - mu_part[feat_part<CH>(f) * CH + feat_ch<CH>(f)];
+            norm += a * a;
+          }
+        } else if (f == D) {
+          a = real ? norm * (1.0 / IA_NORM_SCALE) : 60000.0;  // padding rows: never a candidate
+        }
+        _Float16 hi, lo;
+        split_h(a, hi, lo);
+        vh[e] = hi;
+        vl[e] = lo;
+      }
+      if (inr) {
+        db[(ltile * NP + 2 * s) * IA_WAVE + h * IA_TILE + j] = vh;
+        db[(ltile * NP + 2 * s + 1) * IA_WAVE + h * IA_TILE + j] = vl;
+      }
+    }
+  }
+  // R = max |a'| (certification bound): wave max first, one atomic per wave
+  float R = real ? (float)(sqrt(norm) * (1.0 + 1e-6)) : 0.f;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) R = fmaxf(R, __shfl_xor(R, o, 64));
+  if ((threadIdx.x & 63) == 0 && R > 0.f) atomicMax(Rbits, __float_as_uint(R));
+}
+
+template <int KS>
+__device__ __forceinline__ void put_qh(_Float16 *qf, int m, int f, double v) {
+  const int qt = m / IA_TILE, j = m % IA_TILE, s = f >> 4, h = (f >> 3) & 1, e = f & 7;
+  _Float16 hi, lo;
+  split_h(v, hi, lo);
+  const int64_t base = (((int64_t)qt * 2 * KS + 2 * s) * IA_WAVE + h * IA_TILE + j) * 8 + e;
+  qf[base] = hi;
+  qf[base + IA_WAVE * 8] = lo;
+}
+
+template <int CH, int KS>
+__global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc sd, Imgs B,
+                                                           const double *__restrict__ mu_part,
+                                                           double *__restrict__ q64, double *__restrict__ qn2,
+                                                           _Float16 *__restrict__ qf) {
+  constexpr int D = 55 * CH, KD = 16 * KS;
+  const int lane = threadIdx.x & 63;
+  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  if (m >= sd.Mpad) return;
+  if (m >= sd.M) {
+    for (int f = lane; f < KD; f += IA_WAVE) put_qh<KS>(qf, m, f, 0.);
+    return;
+  }
+  const int r = sd.r0 + m, c = sd.t - 3 * r;
+  double ss = 0.;
+  for (int f = lane; f < KD; f += IA_WAVE) {
+    if (f < D) {
+      const double v = feat<CH>(B, f, r, c, 0);
+      q64[(int64_t)m * D + f] = v;
+      const double qc = v - mu_part[feat_part<CH>(f) * CH + feat_ch<CH>(f)];
+      ss += qc * qc;
+      put_qh<KS>(qf, m, f, -2.0 * qc);
+    } else {
+      put_qh<KS>(qf, m, f, f == D ? IA_NORM_SCALE : 0.);
+    }
+  }
+  ss = wave_sum_d(ss);
+  if (lane == 0) qn2[m] = ss;
+}
+
+// K3h: grid = nwg workgroups of 8 waves (one per CU); WG w owns DB tiles [w*tpw, (w+1)*tpw),
+// wave v takes tiles w*tpw + v, +8, ...; the step's QT query tiles sit in LDS (QT*KS*2 KiB);
+// each DB tile (hi+lo, 2*KS h16x8 per lane) is loaded once into registers with a one-tile
+// prefetch and contracted against every query tile: per 16 k, 3 MFMAs into one accumulator.
+// Epilogue, subset merge and records exactly as k3_dist (16 subsets per WG).
+template <int KS, int QT>
+__global__ void __launch_bounds__(IA_WGH, 1)
+k3h_dist(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, int n_tiles, int tpw, int qt0, int M, int nwg,
+         int row0, int NT, float4 *__restrict__ rec, float *__restrict__ recT) {
+  constexpr int NP = 2 * KS, NW = IA_WGH / IA_WAVE;
+  extern __shared__ h16x8 ldsh[];  // QT * NP * 64 (queries), reused for the merge
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
+  const int wg = blockIdx.x;
+
+  const h16x8 *qsrc = qf + (int64_t)qt0 * NP * IA_WAVE;
+  for (int i = threadIdx.x; i < QT * NP * IA_WAVE; i += IA_WGH) ldsh[i] = qsrc[i];
+  __syncthreads();
+
+  float b1[QT], b2[QT];
+  int i1[QT];
+#pragma unroll
+  for (int q = 0; q < QT; q++) {
+    b1[q] = FLT_MAX;
+    b2[q] = FLT_MAX;
+    i1[q] = 0x7fffffff;
+  }
+
+  const int t_begin = wg * tpw, t_end = min(n_tiles, t_begin + tpw);
+  int t = t_begin + wave;
+  h16x8 a[NP], an[NP];
+  {
+    const h16x8 *src = db + (int64_t)min(t, n_tiles - 1) * NP * IA_WAVE + lane;
+#pragma unroll
+    for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+  }
+  for (; t < t_end; t += NW) {
+    {  // prefetch this wave's next tile (clamped: always issued)
+      const h16x8 *src = db + (int64_t)min(t + NW, n_tiles - 1) * NP * IA_WAVE + lane;
+#pragma unroll
+      for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
+    }
+    const int rbase = row0 + t * IA_TILE + 4 * half;
+    asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
+    f32x16 e0, e1;
+    auto epilogue = [&](const f32x16 &acc, int q) {
+#pragma unroll
+      for (int r = 0; r < 16; r++) {
+        const float v = acc[r];
+        const int row = rbase + (r & 3) + 8 * (r >> 2);
+        const bool c = v < b1[q];
+        b2[q] = __builtin_amdgcn_fmed3f(b1[q], b2[q], v);
+        b1[q] = c ? v : b1[q];
+        i1[q] = c ? row : i1[q];
+      }
+    };
+#pragma unroll
+    for (int qp = 0; qp < QT; qp += 2) {
+      constexpr f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+      const bool two = qp + 1 < QT;
+      f32x16 c0 = zero, c1 = zero;
+      const h16x8 *qb0 = ldsh + qp * NP * IA_WAVE + lane;
+      const h16x8 *qb1 = qb0 + NP * IA_WAVE;
+#pragma unroll
+      for (int s = 0; s < KS; s++) {
+        const h16x8 x0h = qb0[(2 * s) * IA_WAVE], x0l = qb0[(2 * s + 1) * IA_WAVE];
+        const h16x8 x1h = two ? qb1[(2 * s) * IA_WAVE] : x0h, x1l = two ? qb1[(2 * s + 1) * IA_WAVE] : x0l;
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x0h, c0, 0, 0, 0);
+        if (two) c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x1h, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0l, c0, 0, 0, 0);
+        if (two) c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1l, c1, 0, 0, 0);
+        c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0h, c0, 0, 0, 0);
+        if (two) c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1h, c1, 0, 0, 0);
+      }
+      if (qp >= 2) {
+        epilogue(e0, qp - 2);
+        epilogue(e1, qp - 1);
+      }
+      e0 = c0;
+      e1 = c1;
+    }
+    {
+      constexpr int ql = ((QT - 1) / 2) * 2;
+      epilogue(e0, ql);
+      if (ql + 1 < QT) epilogue(e1, ql + 1);
+    }
+#pragma unroll
+    for (int p = 0; p < NP; p++) a[p] = an[p];
+  }
+
+  // ---- merge the 16 subsets of each query: lane halves by shuffle, waves through LDS
+  __syncthreads();
+  Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32]
+#pragma unroll
+  for (int q = 0; q < QT; q++) {
+    Top2 mine = {b1[q], FLT_MAX, b2[q], i1[q], 0x7fffffff};
+    Top2 other;
+    other.v1 = __shfl_xor(b1[q], 32, 64);
+    other.i1 = __shfl_xor(i1[q], 32, 64);
+    other.T = __shfl_xor(b2[q], 32, 64);
+    other.v2 = FLT_MAX;
+    other.i2 = 0x7fffffff;
+    Top2 mrg = half == 0 ? top2_merge(mine, other) : top2_merge(other, mine);
+    if (half == 0) red[(wave * QT + q) * IA_TILE + lane] = mrg;
+  }
+  __syncthreads();
+  for (int x = threadIdx.x; x < QT * IA_TILE; x += IA_WGH) {
+    Top2 m = red[x];
+#pragma unroll
+    for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
+    const int qg = qt0 * IA_TILE + x;
+    if (qg < M) {
+      const int r1 = m.i1 == 0x7fffffff ? m.i1 : (int)ia_pos_row(m.i1, NT);
+      const int r2 = m.i2 == 0x7fffffff ? m.i2 : (int)ia_pos_row(m.i2, NT);
+      rec[(int64_t)qg * nwg + wg] = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
+      recT[(int64_t)qg * nwg + wg] = m.T;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // K4: exact rerank + certification (+ coherence, kappa rule, writeback) — one wave / query
 // ------------------------------------------------------------------------------------------
 // exact DB-row distance of row `row` (level path): ((a - q)**2).sum() in numpy order
@@ -525,7 +780,8 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
 #pragma unroll
   for (int j = 0; j < RPL; j++) a1 = fminf(a1, v1[j]);
   a1 = wave_min_f(a1);
-  const double eps = a.eps_c * (R * R + 2.0 * R * sqrt(qn2));
+  const double qn = sqrt(qn2);
+  const double eps = a.eps_c * (R * R + 2.0 * R * qn) + a.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0);
   const double thr = (double)a1 + 2.0 * eps;
 
   // rerank every listed candidate that could be the exact winner
@@ -696,12 +952,17 @@ __device__ __forceinline__ void row_dists(const LevelGeo &g, const Imgs &A, int 
 
 // row of the lowest set candidate bit (bit 2j: record j's best, bit 2j+1: its runner-up)
 template <int RPL>
-__device__ __forceinline__ int lowest_cand(unsigned cmask, const int (&i1)[RPL], const int (&i2)[RPL]) {
+__device__ __forceinline__ int lowest_cand(unsigned cmask, const int (&i1)[RPL], const int (&i2)[RPL],
+                                           const float (&v1)[RPL], const float (&v2)[RPL], float &v) {
   int row = -1;
+  v = FLT_MAX;
 #pragma unroll
   for (int j = RPL - 1; j >= 0; j--) {
-    row = (cmask >> (2 * j + 1)) & 1 ? i2[j] : row;
-    row = (cmask >> (2 * j)) & 1 ? i1[j] : row;
+    const bool b2 = (cmask >> (2 * j + 1)) & 1, b1 = (cmask >> (2 * j)) & 1;
+    row = b2 ? i2[j] : row;
+    v = b2 ? v2[j] : v;
+    row = b1 ? i1[j] : row;
+    v = b1 ? v1[j] : v;
   }
   return row;
 }
@@ -761,7 +1022,8 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
 #pragma unroll
   for (int j = 0; j < RPL; j++) a1 = fminf(a1, v1[j]);
   a1 = wave_min_f(a1);
-  const double eps = a.eps_c * (R * R + 2.0 * R * sqrt(qn2));
+  const double qn = sqrt(qn2);
+  const double eps = a.eps_c * (R * R + 2.0 * R * qn) + a.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0);
   const double thr = (double)a1 + 2.0 * eps;
   unsigned cmask = 0;
 #pragma unroll
@@ -770,17 +1032,22 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
     if ((double)v2[j] <= thr && i2[j] >= 0 && i2[j] < a.NA) cmask |= 1u << (2 * j + 1);
   }
   int my_row = lane < NCOH ? crow : -1;
-  int nxt = lowest_cand<RPL>(cmask, i1, i2);
+  float my_v = FLT_MAX, nxv;  // MFMA value of the candidate a rerank lane evaluates (bound audit)
+  int nxt = lowest_cand<RPL>(cmask, i1, i2, v1, v2, nxv);
   int slot = 0;
   unsigned long long pend = __ballot(cmask != 0);
   while (pend && slot < NRR) {
     const int L = __ffsll((long long)pend) - 1;
     const int row = __shfl(nxt, L, 64);
-    if (lane == NCOH + slot) my_row = row;
+    const float rv = __shfl(nxv, L, 64);
+    if (lane == NCOH + slot) {
+      my_row = row;
+      my_v = rv;
+    }
     slot++;
     if (lane == L) {
       cmask &= cmask - 1;
-      nxt = lowest_cand<RPL>(cmask, i1, i2);
+      nxt = lowest_cand<RPL>(cmask, i1, i2, v1, v2, nxv);
     }
     pend = __ballot(cmask != 0);
   }
@@ -788,6 +1055,10 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
   // ---- round 2: one feature gather per lane
   double unw = DBL_MAX, wsq = 0.;
   if (my_row >= 0) row_dists<CH>(g, A, my_row, q, weights, unw, wsq);
+  // bound audit: the exact distance of every reranked candidate must lie within eps of its
+  // MFMA value + |q'|^2 (a violation would void the certification; counted, never expected)
+  const bool viol = lane >= NCOH && my_row >= 0 && fabs(unw - qn2 - (double)my_v) > eps;
+  const bool any_viol = __ballot(viol) != 0;
 
   // exact NN winner among the reranked candidates (+ any overflow beyond 49, rare)
   double bd = (lane >= NCOH && my_row >= 0) ? unw : DBL_MAX;
@@ -806,7 +1077,7 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
     recompute_app = true;
     if (lane == L) {
       cmask &= cmask - 1;
-      nxt = lowest_cand<RPL>(cmask, i1, i2);
+      nxt = lowest_cand<RPL>(cmask, i1, i2, v1, v2, nxv);
     }
     pend = __ballot(cmask != 0);
   }
@@ -884,7 +1155,8 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
     im[qi] = img;
     // per-pixel stats word (no shared-counter atomics: hundreds of waves adding to one
     // address serialise at L2 and dominated this kernel); reduced once per level
-    a.pstat[qi] = (unsigned)min(slot, 0xffff) | ((unsigned)min((int)nfb, 0x3fff) << 16) | (coh_won ? 1u << 30 : 0u);
+    a.pstat[qi] = (unsigned)min(slot, 0xffff) | ((unsigned)min((int)nfb, 0x3fff) << 16) | (coh_won ? 1u << 30 : 0u) |
+                  (any_viol ? 1u << 31 : 0u);
   }
 }
 
@@ -953,24 +1225,26 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
 // per-level statistics: sum the per-pixel stats words (one workgroup, fixed order)
 __global__ void __launch_bounds__(IA_WG) k_reduce_stats(const unsigned *__restrict__ pstat, int64_t n,
                                                          unsigned long long *__restrict__ counters) {
-  unsigned long long rr = 0, fb = 0, cw = 0;
+  unsigned long long rr = 0, fb = 0, cw = 0, bv = 0;
   for (int64_t i = threadIdx.x; i < n; i += IA_WG) {
     const unsigned v = pstat[i];
     rr += v & 0xffff;
     fb += (v >> 16) & 0x3fff;
     cw += (v >> 30) & 1;
+    bv += v >> 31;
   }
-  __shared__ unsigned long long red[3][IA_WG];
+  __shared__ unsigned long long red[4][IA_WG];
   red[0][threadIdx.x] = rr;
   red[1][threadIdx.x] = fb;
   red[2][threadIdx.x] = cw;
+  red[3][threadIdx.x] = bv;
   __syncthreads();
   for (int o = IA_WG / 2; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o)
-      for (int k = 0; k < 3; k++) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+      for (int k = 0; k < 4; k++) red[k][threadIdx.x] += red[k][threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x < 3) counters[threadIdx.x] = red[threadIdx.x][0];
+  if (threadIdx.x < 4) counters[threadIdx.x] = red[threadIdx.x][0];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1174,4 +1448,65 @@ void ia_launch_dense_query(int KH, const double *q, int64_t nq, int d, int Mpad,
 void ia_launch_merge_dense(const MergeArgs &ma, const double *pts, int d, const double *q, int64_t nq, int64_t *idx,
                            double *dist, hipStream_t st) {
   hipLaunchKernelGGL(k_merge_dense, dim3(cdiv(nq, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, ma, pts, d, q, nq, idx, dist);
+}
+
+// ---- split-f16 matcher launchers -----------------------------------------------------------
+int ia_ks_for(int ch) { return ch == 1 ? 4 : ch == 2 ? 7 : 0; }  // 3 channels: fp32 matcher
+int ia_k3h_qtmax(int KS) { return KS == 4 ? 11 : 8; }
+size_t ia_k3h_lds(int KS, int qt) {
+  const size_t q = (size_t)qt * 2 * KS * IA_WAVE * 16, m = (size_t)(IA_WGH / IA_WAVE) * qt * IA_TILE * sizeof(Top2);
+  return q > m ? q : m;
+}
+
+void ia_launch_absmax(const double *const *p, const int64_t *n, unsigned *out, hipStream_t st) {
+  AbsArrays arr;
+  for (int k = 0; k < 8; k++) {
+    arr.p[k] = p[k];
+    arr.n[k] = p[k] ? n[k] : 0;
+  }
+  hipLaunchKernelGGL(k_absmax, dim3(512), dim3(IA_WG), 0, st, arr, out);
+}
+
+template <int CH, int KS>
+static void launch_db_h_t(const LevelGeo &g, const Imgs &A, const double *mu, void *db, unsigned *Rbits, hipStream_t st) {
+  const int64_t rows = (int64_t)(g.tile1 - g.tile0) * IA_TILE;
+  hipLaunchKernelGGL((k_db_build_h<CH, KS>), dim3(cdiv(rows, IA_WG)), dim3(IA_WG), 0, st, g, A, mu, (h16x8 *)db, Rbits);
+}
+void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *mu, void *db, unsigned *Rbits, hipStream_t st) {
+  if (g.ch == 1) launch_db_h_t<1, 4>(g, A, mu, db, Rbits, st);
+  else launch_db_h_t<2, 7>(g, A, mu, db, Rbits, st);
+}
+
+template <int CH, int KS>
+static void launch_gather_h_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64,
+                              double *qn2, void *qf, hipStream_t st) {
+  hipLaunchKernelGGL((k_gather_query_h<CH, KS>), dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, mu,
+                     q64, qn2, (_Float16 *)qf);
+}
+void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64, double *qn2,
+                        void *qf, hipStream_t st) {
+  if (g.ch == 1) launch_gather_h_t<1, 4>(g, sd, B, mu, q64, qn2, qf, st);
+  else launch_gather_h_t<2, 7>(g, sd, B, mu, q64, qn2, qf, st);
+}
+
+typedef void (*k3h_fn)(const h16x8 *, const h16x8 *, int, int, int, int, int, int, int, float4 *, float *);
+template <int KS, int... QTs>
+struct K3hTable {
+  static k3h_fn get(int qt) {
+    static const k3h_fn tab[] = {k3h_dist<KS, QTs>...};
+    return tab[qt - 1];
+  }
+};
+void ia_launch_k3h(int KS, int qt, const void *db, const void *qf, int n_tiles, int tpw, int qt0, int M, int nwg, int row0,
+                   int NT, float4 *rec, float *recT, hipStream_t st) {
+  k3h_fn fn = KS == 4 ? K3hTable<4, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11>::get(qt) : K3hTable<7, 1, 2, 3, 4, 5, 6, 7, 8>::get(qt);
+  const size_t lds = ia_k3h_lds(KS, qt);
+  static bool attr_set[2][16] = {};
+  const int ki = KS == 4 ? 0 : 1;
+  if (!attr_set[ki][qt]) {
+    (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_set[ki][qt] = true;
+  }
+  hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WGH), lds, st, (const h16x8 *)db, (const h16x8 *)qf, n_tiles, tpw, qt0, M, nwg,
+                     row0, NT, rec, recT);
 }

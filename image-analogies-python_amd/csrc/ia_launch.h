@@ -23,3 +23,13 @@ void ia_launch_dense_query(int KH, const double *q, int64_t nq, int d, int Mpad,
                            hipStream_t st);
 void ia_launch_merge_dense(const MergeArgs &ma, const double *pts, int d, const double *q, int64_t nq, int64_t *idx,
                            double *dist, hipStream_t st);
+// split-f16 matcher (IA_MATCH_F16X3)
+int ia_ks_for(int ch);
+int ia_k3h_qtmax(int KS);
+size_t ia_k3h_lds(int KS, int qt);
+void ia_launch_absmax(const double *const *p, const int64_t *n, unsigned *out, hipStream_t st);
+void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *mu, void *db, unsigned *Rbits, hipStream_t st);
+void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64, double *qn2,
+                        void *qf, hipStream_t st);
+void ia_launch_k3h(int KS, int qt, const void *db, const void *qf, int n_tiles, int tpw, int qt0, int M, int nwg, int row0,
+                   int NT, float4 *rec, float *recT, hipStream_t st);

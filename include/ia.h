@@ -57,6 +57,9 @@ typedef struct {
   double dist_ms;          /* device time of the sampled launches */
   int64_t dist_launches_timed;
   double dist_flops_timed; /* algorithmic flops of the sampled launches */
+  int64_t bound_violations; /* pixels where a reranked candidate's exact distance fell outside
+                             * the certified MFMA error bound (audit; expected 0) */
+  int64_t f16_levels;       /* levels run on the split-f16 matcher */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
@@ -87,7 +90,11 @@ const char *ia_last_error(void);
 int ia_version(void);
 /* Options: "time_dist" = S (0 = off): bracket the MFMA distance launches of every S-th
  * wavefront step with HIP events; ia_stats.dist_ms / dist_flops_timed then give the kernel's
- * measured device time and algorithmic flops (bench.py roofline). */
+ * measured device time and algorithmic flops (bench.py roofline).
+ * "matcher" = IA_MATCH_F16X3 (default: split-f16 MFMA scan, 1 and 2 channels, image values
+ * within +-64) or IA_MATCH_F32 (fp32 MFMA scan).  Both are certified exact: identical results. */
+#define IA_MATCH_F32 0
+#define IA_MATCH_F16X3 1
 int ia_set_option(ia_ctx *ctx, const char *name, int value);
 /* Multi-GPU (one process per GPU): A rows of every level are split into `world` contiguous
  * shards; per wavefront step each rank exchanges its certified per-query winners with one

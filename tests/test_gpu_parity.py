@@ -15,21 +15,58 @@ from golden_util import E2E_CASES, load_e2e
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize('name', E2E_CASES)
-def test_level_path_matches_reference(ctx, name):
+@pytest.fixture(params=['f16x3', 'f32'])
+def matcher(request, ctx):
+    """Both certified matchers (split-f16 MFMA, fp32 MFMA) must give the reference's decisions."""
     from ia_amd import _native
-    z = load_e2e(name)
+    ctx.set_option('matcher', _native.IA_MATCH_F16X3 if request.param == 'f16x3' else _native.IA_MATCH_F32)
+    yield request.param
+    ctx.set_option('matcher', _native.IA_MATCH_F16X3)
+
+
+def _run_levels(ctx, z, Bp, A_pyr=None, Ap_pyr=None, B_pyr=None):
+    from ia_amd import _native
+    A_pyr, Ap_pyr, B_pyr = A_pyr or z['A_pyr'], Ap_pyr or z['Ap_pyr'], B_pyr or z['B_pyr']
     L, k = z['L'], float(z['k'])
-    Bp = [x.copy() for x in z['Bp_init']]
+    st = _native.Stats()
+    out = {}
     for level in range(1, L):
         kf = 1 + (2 ** (level - L)) * k
-        s, im = ctx.synthesize_level(z['A_pyr'][level], z['A_pyr'][level - 1],
-                                     [p[level] for p in z['Ap_pyr']], [p[level - 1] for p in z['Ap_pyr']],
-                                     z['B_pyr'][level], z['B_pyr'][level - 1], Bp[level - 1], Bp[level],
-                                     z['weights'], kf)
+        out[level] = ctx.synthesize_level(A_pyr[level], A_pyr[level - 1], [p[level] for p in Ap_pyr],
+                                          [p[level - 1] for p in Ap_pyr], B_pyr[level], B_pyr[level - 1],
+                                          Bp[level - 1], Bp[level], z['weights'], kf, st)
+    return out, st
+
+
+@pytest.mark.parametrize('name', E2E_CASES)
+def test_level_path_matches_reference(ctx, matcher, name):
+    z = load_e2e(name)
+    Bp = [x.copy() for x in z['Bp_init']]
+    out, st = _run_levels(ctx, z, Bp)
+    for level, (s, im) in out.items():
         assert np.array_equal(s, z['s'][level]), 'level %d source map differs' % level
         assert np.array_equal(im, z['im'][level]), 'level %d image map differs' % level
         assert np.array_equal(Bp[level], z['Bp_final'][level]), 'level %d B\' differs' % level
+    assert st.bound_violations == 0
+    ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]
+    assert st.f16_levels == (z['L'] - 1 if (matcher == 'f16x3' and ch < 3) else 0)
+
+
+def test_split_f16_falls_back_to_fp32_outside_f16_range(ctx):
+    """Image values beyond +-64 would overflow the split-f16 operands: the level runs on the
+    fp32 matcher instead, with the same (oracle) decisions."""
+    from oracle import ia_oracle as O
+    z = load_e2e('g24k5')
+    sc = lambda pyr: [x * 100.0 for x in pyr]
+    A_pyr, Ap_pyr, B_pyr = sc(z['A_pyr']), [sc(p) for p in z['Ap_pyr']], sc(z['B_pyr'])
+    Bp0 = sc(z['Bp_init'])
+    Bp_gpu, Bp_cpu = [x.copy() for x in Bp0], [x.copy() for x in Bp0]
+    out, st = _run_levels(ctx, z, Bp_gpu, A_pyr, Ap_pyr, B_pyr)
+    S, IM = O.run_all_levels(A_pyr, Ap_pyr, B_pyr, Bp_cpu, float(z['k']), z['weights'])
+    assert st.f16_levels == 0
+    for level, (s, im) in out.items():
+        assert np.array_equal(s, S[level]) and np.array_equal(im, IM[level])
+        assert np.array_equal(Bp_gpu[level], Bp_cpu[level])
 
 
 def _numpy_nn(pts, q):

@@ -76,6 +76,7 @@ def test_teacher_forced_1024_finest_level(ctx):
     assert all(near for _, near, _, _ in mism), mism
     assert len(mism) <= 1, mism
     assert st.fallbacks < 0.01 * st.pixels
+    assert st.bound_violations == 0 and st.f16_levels == L - 1   # default matcher: split-f16
 
 
 def test_driver_end_to_end_matches_oracle(tmp_path):
