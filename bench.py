@@ -110,6 +110,8 @@ def main():
     ap.add_argument('--mode', default='replicas', choices=['replicas', 'shard'])
     ap.add_argument('--matcher', default='f16x3', choices=['f16x3', 'f32'],
                     help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
+    ap.add_argument('--k3-variant', type=int, default=1, choices=[0, 1],
+                    help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select')
     ap.add_argument('--time-stride', type=int, default=4, help='sample K3 timing every S-th wavefront step')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -139,6 +141,7 @@ def main():
 
     ctx = _native.Context(local)
     ctx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
+    ctx.set_option('k3_variant', args.k3_variant)
     if args.mode == 'shard' and world > 1:
         uid = [_native.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)

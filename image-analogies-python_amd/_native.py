@@ -56,6 +56,8 @@ EXPORTS = {
     'ia_index_query': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                       ctypes.c_void_p]),
     'ia_index_destroy': (None, [ctypes.c_void_p]),
+    'ia_k3_microbench': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                        ctypes.POINTER(ctypes.c_double)]),
     'ia_merge_winners': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
                                         ctypes.c_void_p, ctypes.c_void_p]),
     'ia_wavefront_shape': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
@@ -128,6 +130,12 @@ class Context(object):
 
     def set_option(self, name, value):
         check(lib().ia_set_option(self._h, name.encode(), int(value)), 'ia_set_option')
+
+    def k3_microbench(self, n_rows, M, reps=20):
+        """Mean device microseconds of one split-f16 distance-scan launch (random operands)."""
+        us = ctypes.c_double()
+        check(lib().ia_k3_microbench(self._h, int(n_rows), int(M), int(reps), ctypes.byref(us)), 'ia_k3_microbench')
+        return us.value
 
     def comm_init(self, rank, world, uid):
         check(lib().ia_comm_init(self._h, rank, world, bytes(uid)), 'ia_comm_init')

@@ -77,6 +77,7 @@ struct ia_ctx {
   DevBuf A, Ac, Ap, Apc, B, Bc, Bpc, Bp, S, IM, W;
   DevBuf db, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, pstat, absmax;
   int matcher = IA_MATCH_F16X3;  // option "matcher"
+  int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   // per-step K3 timing (optional)
   int time_dist = 0;
   std::vector<hipEvent_t> evs;
@@ -141,6 +142,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!c || !name) return fail(IA_EINVAL, "ia_set_option: NULL argument");
   if (!std::strcmp(name, "time_dist")) {
     c->time_dist = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "k3_variant")) {
+    if (value < 0 || value > 3) return fail(IA_EINVAL, "ia_set_option: k3_variant must be 0..3 (2, 3: diagnostic builds)");
+    c->k3_variant = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "matcher")) {
@@ -377,7 +383,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   int64_t shard_rows = 0;  // real DB rows in this shard's tiles (strided layout)
   for (int t = g.tile0; t < g.tile1; t++) shard_rows += std::min<int64_t>(IA_TILE, (g.NA - t + g.n_tiles - 1) / g.n_tiles);
   ma.pstat = c->pstat.as<unsigned>();
-  ma.eps_c = use_h ? ia_eps_c_h(g.KS) : ia_eps_c(DP);
+  ma.eps_c = use_h ? ia_eps_c_h(g.KS, c->k3_variant == 1) : ia_eps_c(DP);
   ma.eps_a = use_h ? ia_eps_a_h() : 0.;
 
   const int qtmax = use_h ? ia_k3h_qtmax(g.KS) : ia_k3_qtmax(g.KH);
@@ -409,7 +415,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
         const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
         if (use_h)
           ia_launch_k3h(g.KS, qt, c->db.p, c->qf.p, ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0, ma.NT, c->rec.as<float4>(),
-                        c->recT.as<float>(), c->st);
+                        c->recT.as<float>(), c->k3_variant, c->st);
         else
           ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0,
                        ma.NT, c->rec.as<float4>(), c->recT.as<float>(), c->st);
@@ -473,6 +479,42 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       stats->dist_flops_timed += flops_timed;
     }
   }
+  return IA_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// K3h microbenchmark (kernel tuning): the split-f16 distance scan alone on random operands
+// ------------------------------------------------------------------------------------------
+int ia_k3_microbench(ia_ctx *c, int64_t n_rows, int M, int reps, double *us_per_launch) {
+  if (!c || n_rows < 1 || M < 1 || reps < 1 || !us_per_launch) return fail(IA_EINVAL, "ia_k3_microbench: bad arguments");
+  const int KS = ia_ks_for(1), qtmax = ia_k3h_qtmax(KS);
+  const int qt = (M + IA_TILE - 1) / IA_TILE;
+  if (qt > qtmax) return fail(IA_EINVAL, "ia_k3_microbench: M exceeds one launch");
+  if (n_rows >= (int64_t)INT32_MAX) return fail(IA_EINVAL, "ia_k3_microbench: n_rows exceeds int32 row ids");
+  HIP_TRY(hipSetDevice(c->dev));
+  const int n_tiles = (int)((n_rows + IA_TILE - 1) / IA_TILE);
+  const int tpw = std::max(IA_WGH / IA_WAVE, (n_tiles + IA_NWG_H - 1) / IA_NWG_H);
+  const int nwg = (n_tiles + tpw - 1) / tpw;
+  const size_t row_bytes = (size_t)16 * KS * 4;
+  int rc;
+  if ((rc = c->db.ensure((size_t)n_tiles * IA_TILE * row_bytes)) || (rc = c->qf.ensure((size_t)qt * IA_TILE * row_bytes)) ||
+      (rc = c->rec.ensure((size_t)M * nwg * 16)) || (rc = c->recT.ensure((size_t)M * nwg * 4)))
+    return rc;
+  ia_launch_fill_random_f16(c->db.p, (int64_t)n_tiles * IA_TILE * row_bytes / 2, 12345u, c->st);
+  ia_launch_fill_random_f16(c->qf.p, (int64_t)qt * IA_TILE * row_bytes / 2, 777u, c->st);
+  auto launch = [&]() {
+    ia_launch_k3h(KS, qt, c->db.p, c->qf.p, n_tiles, tpw, 0, M, nwg, 0, n_tiles, c->rec.as<float4>(), c->recT.as<float>(),
+                  c->k3_variant, c->st);
+  };
+  for (int i = 0; i < 3; i++) launch();
+  HIP_TRY(hipEventRecord(c->lv0, c->st));
+  for (int i = 0; i < reps; i++) launch();
+  HIP_TRY(hipEventRecord(c->lv1, c->st));
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipStreamSynchronize(c->st));
+  float ms = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms, c->lv0, c->lv1));
+  *us_per_launch = 1e3 * ms / reps;
   return IA_OK;
 }
 

@@ -120,8 +120,11 @@ inline double ia_eps_c(int DP) {
 // truncation, hence u = 2^-23), adds gamma_n * sum|terms|.  With sum|x y| <= R^2 + 2R|q'| and
 // sum(|x| + |y|) <= R^2/256 + sqrt(D)(R + 2|q'|) + 256 + 1 (D <= 176):
 //   eps = eps_c (R^2 + 2R|q'|) + eps_a (R^2 + 14 R + 28|q'| + 260)
-inline double ia_eps_c_h(int KS) {
+// packed: the packed-index K3h epilogue replaces each value's 4 low mantissa bits by a row
+// index, moving it by < 16 ulp <= 2^-19 |v| <= 2^-19 (R^2 + 2R|q'|) (1 + 1e-2 headroom).
+inline double ia_eps_c_h(int KS, bool packed) {
   const double nu = (48.0 * KS + 4) * 1.1920928955078125e-07;
-  return 1.05 * (nu / (1.0 - nu) * (1.0 + 1.0 / 512) + 3.5 * 2.384185791015625e-07);
+  return 1.05 * (nu / (1.0 - nu) * (1.0 + 1.0 / 512) + 3.5 * 2.384185791015625e-07) +
+         (packed ? 1.01 * 1.9073486328125e-06 : 0.0);
 }
 inline double ia_eps_a_h() { return 1.05 * 2.9802322387695312e-08; }

@@ -28,7 +28,6 @@
 #define IA_PROBE 0  // diagnostic phase-skipping builds (never set in the product build)
 #endif
 
-typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 // ------------------------------------------------------------------------------------------
 // feature geometry, compile-time per channel count
@@ -327,31 +326,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query(LevelGeo g, StepDesc sd,
 // the rows it has seen ("subset" = lane half x wave); the workgroup merges its 8 subsets into
 // a top-2 list + threshold T (every unlisted row of the chunk has approx value >= T).
 // ------------------------------------------------------------------------------------------
-struct Top2 {
-  float v1, v2, T;
-  int i1, i2;
-};
-__device__ __forceinline__ bool lt(float va, int ia, float vb, int ib) {
-  return va < vb || (va == vb && ia < ib);
-}
-__device__ __forceinline__ void top2_insert(Top2 &a, float v, int i, float &third) {
-  if (lt(v, i, a.v1, a.i1)) {
-    third = fminf(third, a.v2);
-    a.v2 = a.v1; a.i2 = a.i1; a.v1 = v; a.i1 = i;
-  } else if (lt(v, i, a.v2, a.i2)) {
-    third = fminf(third, a.v2);
-    a.v2 = v; a.i2 = i;
-  } else {
-    third = fminf(third, v);
-  }
-}
-__device__ __forceinline__ Top2 top2_merge(Top2 a, const Top2 &b) {
-  float third = FLT_MAX;
-  top2_insert(a, b.v1, b.i1, third);
-  top2_insert(a, b.v2, b.i2, third);
-  a.T = fminf(fminf(a.T, b.T), third);
-  return a;
-}
+#include "ia_top2.h"
 
 template <int KH, int QT>
 __global__ void __launch_bounds__(IA_WG, 2)
@@ -493,7 +468,6 @@ k3_dist(const float4 *__restrict__ db, const float4 *__restrict__ qf, int n_tile
 // Fragment order (tile of 32 DB rows or 32 queries, k-step s of 16, part 0 = hi / 1 = lo):
 //   h16x8 piece p = 2s + part, lane L:  row (L & 31), k = 16s + 8(L >> 5) + e, e = 0..7
 // ------------------------------------------------------------------------------------------
-typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 
 __device__ __forceinline__ void split_h(double x, _Float16 &hi, _Float16 &lo) {
   const float xf = (float)x;
@@ -616,125 +590,6 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc s
   }
   ss = wave_sum_d(ss);
   if (lane == 0) qn2[m] = ss;
-}
-
-// K3h: grid = nwg workgroups of 8 waves (one per CU); WG w owns DB tiles [w*tpw, (w+1)*tpw),
-// wave v takes tiles w*tpw + v, +8, ...; the step's QT query tiles sit in LDS (QT*KS*2 KiB);
-// each DB tile (hi+lo, 2*KS h16x8 per lane) is loaded once into registers with a one-tile
-// prefetch and contracted against every query tile: per 16 k, 3 MFMAs into one accumulator.
-// Epilogue, subset merge and records exactly as k3_dist (16 subsets per WG).
-template <int KS, int QT>
-__global__ void __launch_bounds__(IA_WGH, 1)
-k3h_dist(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, int n_tiles, int tpw, int qt0, int M, int nwg,
-         int row0, int NT, float4 *__restrict__ rec, float *__restrict__ recT) {
-  constexpr int NP = 2 * KS, NW = IA_WGH / IA_WAVE;
-  extern __shared__ h16x8 ldsh[];  // QT * NP * 64 (queries), reused for the merge
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, half = lane >> 5;
-  const int wg = blockIdx.x;
-
-  const h16x8 *qsrc = qf + (int64_t)qt0 * NP * IA_WAVE;
-  for (int i = threadIdx.x; i < QT * NP * IA_WAVE; i += IA_WGH) ldsh[i] = qsrc[i];
-  __syncthreads();
-
-  float b1[QT], b2[QT];
-  int i1[QT];
-#pragma unroll
-  for (int q = 0; q < QT; q++) {
-    b1[q] = FLT_MAX;
-    b2[q] = FLT_MAX;
-    i1[q] = 0x7fffffff;
-  }
-
-  const int t_begin = wg * tpw, t_end = min(n_tiles, t_begin + tpw);
-  int t = t_begin + wave;
-  h16x8 a[NP], an[NP];
-  {
-    const h16x8 *src = db + (int64_t)min(t, n_tiles - 1) * NP * IA_WAVE + lane;
-#pragma unroll
-    for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
-  }
-  for (; t < t_end; t += NW) {
-    {  // prefetch this wave's next tile (clamped: always issued)
-      const h16x8 *src = db + (int64_t)min(t + NW, n_tiles - 1) * NP * IA_WAVE + lane;
-#pragma unroll
-      for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
-    }
-    const int rbase = row0 + t * IA_TILE + 4 * half;
-    asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-    f32x16 e0, e1;
-    auto epilogue = [&](const f32x16 &acc, int q) {
-#pragma unroll
-      for (int r = 0; r < 16; r++) {
-        const float v = acc[r];
-        const int row = rbase + (r & 3) + 8 * (r >> 2);
-        const bool c = v < b1[q];
-        b2[q] = __builtin_amdgcn_fmed3f(b1[q], b2[q], v);
-        b1[q] = c ? v : b1[q];
-        i1[q] = c ? row : i1[q];
-      }
-    };
-#pragma unroll
-    for (int qp = 0; qp < QT; qp += 2) {
-      constexpr f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-      const bool two = qp + 1 < QT;
-      f32x16 c0 = zero, c1 = zero;
-      const h16x8 *qb0 = ldsh + qp * NP * IA_WAVE + lane;
-      const h16x8 *qb1 = qb0 + NP * IA_WAVE;
-#pragma unroll
-      for (int s = 0; s < KS; s++) {
-        const h16x8 x0h = qb0[(2 * s) * IA_WAVE], x0l = qb0[(2 * s + 1) * IA_WAVE];
-        const h16x8 x1h = two ? qb1[(2 * s) * IA_WAVE] : x0h, x1l = two ? qb1[(2 * s + 1) * IA_WAVE] : x0l;
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x0h, c0, 0, 0, 0);
-        if (two) c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x1h, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0l, c0, 0, 0, 0);
-        if (two) c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1l, c1, 0, 0, 0);
-        c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0h, c0, 0, 0, 0);
-        if (two) c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1h, c1, 0, 0, 0);
-      }
-      if (qp >= 2) {
-        epilogue(e0, qp - 2);
-        epilogue(e1, qp - 1);
-      }
-      e0 = c0;
-      e1 = c1;
-    }
-    {
-      constexpr int ql = ((QT - 1) / 2) * 2;
-      epilogue(e0, ql);
-      if (ql + 1 < QT) epilogue(e1, ql + 1);
-    }
-#pragma unroll
-    for (int p = 0; p < NP; p++) a[p] = an[p];
-  }
-
-  // ---- merge the 16 subsets of each query: lane halves by shuffle, waves through LDS
-  __syncthreads();
-  Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32]
-#pragma unroll
-  for (int q = 0; q < QT; q++) {
-    Top2 mine = {b1[q], FLT_MAX, b2[q], i1[q], 0x7fffffff};
-    Top2 other;
-    other.v1 = __shfl_xor(b1[q], 32, 64);
-    other.i1 = __shfl_xor(i1[q], 32, 64);
-    other.T = __shfl_xor(b2[q], 32, 64);
-    other.v2 = FLT_MAX;
-    other.i2 = 0x7fffffff;
-    Top2 mrg = half == 0 ? top2_merge(mine, other) : top2_merge(other, mine);
-    if (half == 0) red[(wave * QT + q) * IA_TILE + lane] = mrg;
-  }
-  __syncthreads();
-  for (int x = threadIdx.x; x < QT * IA_TILE; x += IA_WGH) {
-    Top2 m = red[x];
-#pragma unroll
-    for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
-    const int qg = qt0 * IA_TILE + x;
-    if (qg < M) {
-      const int r1 = m.i1 == 0x7fffffff ? m.i1 : (int)ia_pos_row(m.i1, NT);
-      const int r2 = m.i2 == 0x7fffffff ? m.i2 : (int)ia_pos_row(m.i2, NT);
-      rec[(int64_t)qg * nwg + wg] = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
-      recT[(int64_t)qg * nwg + wg] = m.T;
-    }
-  }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1453,9 +1308,34 @@ void ia_launch_merge_dense(const MergeArgs &ma, const double *pts, int d, const 
 // ---- split-f16 matcher launchers -----------------------------------------------------------
 int ia_ks_for(int ch) { return ch == 1 ? 4 : ch == 2 ? 7 : 0; }  // 3 channels: fp32 matcher
 int ia_k3h_qtmax(int KS) { return KS == 4 ? 11 : 8; }
+// waves per workgroup of the K3h instance selected by (KS, qt, variant) (ia_k3h.hip getters)
+static int k3h_waves(int KS, int qt, int variant) {
+#ifdef IA_K3H_DIAG
+  if (KS == 4 && qt == 11 && variant == 2) return 4;
+#endif
+  return IA_WGH / IA_WAVE;
+}
+static size_t k3h_lds(int KS, int qt, int nw) {
+  const size_t q = (size_t)qt * 2 * KS * IA_WAVE * 16, m = (size_t)nw * qt * IA_TILE * sizeof(Top2);
+  return q > m ? q : m;
+}
 size_t ia_k3h_lds(int KS, int qt) {
   const size_t q = (size_t)qt * 2 * KS * IA_WAVE * 16, m = (size_t)(IA_WGH / IA_WAVE) * qt * IA_TILE * sizeof(Top2);
   return q > m ? q : m;
+}
+
+// microbenchmark operands: pseudo-random f16 values in [-0.5, 0.5) (hash of the index)
+__global__ void __launch_bounds__(IA_WG) k_fill_random_f16(_Float16 *__restrict__ p, int64_t n, unsigned seed) {
+  for (int64_t i = (int64_t)blockIdx.x * IA_WG + threadIdx.x; i < n; i += (int64_t)gridDim.x * IA_WG) {
+    unsigned h = (unsigned)i * 2654435761u ^ seed;
+    h ^= h >> 15;
+    h *= 2246822519u;
+    h ^= h >> 13;
+    p[i] = (_Float16)((float)(h & 0xffff) * (1.f / 65536.f) - 0.5f);
+  }
+}
+void ia_launch_fill_random_f16(void *p, int64_t n, unsigned seed, hipStream_t st) {
+  hipLaunchKernelGGL(k_fill_random_f16, dim3(1024), dim3(IA_WG), 0, st, (_Float16 *)p, n, seed);
 }
 
 void ia_launch_absmax(const double *const *p, const int64_t *n, unsigned *out, hipStream_t st) {
@@ -1489,24 +1369,31 @@ void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
   else launch_gather_h_t<2, 7>(g, sd, B, mu, q64, qn2, qf, st);
 }
 
-typedef void (*k3h_fn)(const h16x8 *, const h16x8 *, int, int, int, int, int, int, int, float4 *, float *);
-template <int KS, int... QTs>
-struct K3hTable {
-  static k3h_fn get(int qt) {
-    static const k3h_fn tab[] = {k3h_dist<KS, QTs>...};
-    return tab[qt - 1];
-  }
-};
+// split-f16 distance kernels live in ia_k3h.hip, compiled once per (KS, QT) instance
+#define IA_K3H_DECL(ks, qt) k3h_fn ia_k3h_get_##ks##_##qt(int variant);
+IA_K3H_DECL(4, 1) IA_K3H_DECL(4, 2) IA_K3H_DECL(4, 3) IA_K3H_DECL(4, 4) IA_K3H_DECL(4, 5) IA_K3H_DECL(4, 6)
+IA_K3H_DECL(4, 7) IA_K3H_DECL(4, 8) IA_K3H_DECL(4, 9) IA_K3H_DECL(4, 10) IA_K3H_DECL(4, 11)
+IA_K3H_DECL(7, 1) IA_K3H_DECL(7, 2) IA_K3H_DECL(7, 3) IA_K3H_DECL(7, 4) IA_K3H_DECL(7, 5) IA_K3H_DECL(7, 6)
+IA_K3H_DECL(7, 7) IA_K3H_DECL(7, 8)
+static k3h_fn k3h_get(int KS, int qt, int variant) {
+  typedef k3h_fn (*getter)(int);
+  static const getter g4[] = {ia_k3h_get_4_1, ia_k3h_get_4_2, ia_k3h_get_4_3, ia_k3h_get_4_4,  ia_k3h_get_4_5, ia_k3h_get_4_6,
+                              ia_k3h_get_4_7, ia_k3h_get_4_8, ia_k3h_get_4_9, ia_k3h_get_4_10, ia_k3h_get_4_11};
+  static const getter g7[] = {ia_k3h_get_7_1, ia_k3h_get_7_2, ia_k3h_get_7_3, ia_k3h_get_7_4,
+                              ia_k3h_get_7_5, ia_k3h_get_7_6, ia_k3h_get_7_7, ia_k3h_get_7_8};
+  return KS == 4 ? g4[qt - 1](variant) : g7[qt - 1](variant);
+}
 void ia_launch_k3h(int KS, int qt, const void *db, const void *qf, int n_tiles, int tpw, int qt0, int M, int nwg, int row0,
-                   int NT, float4 *rec, float *recT, hipStream_t st) {
-  k3h_fn fn = KS == 4 ? K3hTable<4, 1, 2, 3, 4, 5, 6, 7, 8, 9, 10, 11>::get(qt) : K3hTable<7, 1, 2, 3, 4, 5, 6, 7, 8>::get(qt);
-  const size_t lds = ia_k3h_lds(KS, qt);
-  static bool attr_set[2][16] = {};
-  const int ki = KS == 4 ? 0 : 1;
-  if (!attr_set[ki][qt]) {
+                   int NT, float4 *rec, float *recT, int variant, hipStream_t st) {
+  const k3h_fn fn = k3h_get(KS, qt, variant);
+  const int nw = k3h_waves(KS, qt, variant);
+  const size_t lds = k3h_lds(KS, qt, nw);
+  static bool attr_set[4][2][16] = {};
+  const int ki = KS == 4 ? 0 : 1, vi = variant & 3;
+  if (!attr_set[vi][ki][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set[ki][qt] = true;
+    attr_set[vi][ki][qt] = true;
   }
-  hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WGH), lds, st, (const h16x8 *)db, (const h16x8 *)qf, n_tiles, tpw, qt0, M, nwg,
+  hipLaunchKernelGGL(fn, dim3(nwg), dim3(nw * IA_WAVE), lds, st, (const h16x8 *)db, (const h16x8 *)qf, n_tiles, tpw, qt0, M, nwg,
                      row0, NT, rec, recT);
 }

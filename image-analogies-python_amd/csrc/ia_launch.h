@@ -32,4 +32,5 @@ void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *mu, vo
 void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64, double *qn2,
                         void *qf, hipStream_t st);
 void ia_launch_k3h(int KS, int qt, const void *db, const void *qf, int n_tiles, int tpw, int qt0, int M, int nwg, int row0,
-                   int NT, float4 *rec, float *recT, hipStream_t st);
+                   int NT, float4 *rec, float *recT, int variant, hipStream_t st);
+void ia_launch_fill_random_f16(void *p, int64_t n, unsigned seed, hipStream_t st);

@@ -1,0 +1,39 @@
+// ia_top2.h — device types shared by the MFMA distance kernels (ia_kernels.hip, ia_k3h.hip):
+// MFMA operand/accumulator vectors and the per-subset top-2 record with its merge.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <float.h>
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
+
+// a K3 subset's best two (value, DB position) pairs and the threshold T: every position of
+// the subset that is not listed has an MFMA value >= T
+struct Top2 {
+  float v1, v2, T;
+  int i1, i2;
+};
+__device__ __forceinline__ bool lt(float va, int ia, float vb, int ib) {
+  return va < vb || (va == vb && ia < ib);
+}
+__device__ __forceinline__ void top2_insert(Top2 &a, float v, int i, float &third) {
+  if (lt(v, i, a.v1, a.i1)) {
+    third = fminf(third, a.v2);
+    a.v2 = a.v1; a.i2 = a.i1; a.v1 = v; a.i1 = i;
+  } else if (lt(v, i, a.v2, a.i2)) {
+    third = fminf(third, a.v2);
+    a.v2 = v; a.i2 = i;
+  } else {
+    third = fminf(third, v);
+  }
+}
+__device__ __forceinline__ Top2 top2_merge(Top2 a, const Top2 &b) {
+  float third = FLT_MAX;
+  top2_insert(a, b.v1, b.i1, third);
+  top2_insert(a, b.v2, b.i2, third);
+  a.T = fminf(fminf(a.T, b.T), third);
+  return a;
+}
+
+// split-f16 distance kernel entry (ia_k3h.hip)
+typedef void (*k3h_fn)(const h16x8 *, const h16x8 *, int, int, int, int, int, int, int, float4 *, float *);

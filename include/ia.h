@@ -115,6 +115,12 @@ int ia_index_build(ia_ctx *ctx, const double *pts, int64_t n, int d, ia_index **
 int ia_index_query(ia_index *index, const double *q, int64_t nq, int64_t *idx_out, double *dist_out);
 void ia_index_destroy(ia_index *index);
 
+/* ---- kernel tuning ------------------------------------------------------------------------- */
+/* Time the split-f16 distance scan (K3h, current "k3_variant") alone: n_rows random DB rows
+ * (1 channel), M <= 352 random queries, `reps` back-to-back launches on the context's stream;
+ * *us_per_launch = mean device time per launch (HIP events). */
+int ia_k3_microbench(ia_ctx *ctx, int64_t n_rows, int M, int reps, double *us_per_launch);
+
 /* ---- host-side helpers (no GPU needed) ---------------------------------------------------- */
 /* Merge per-rank candidate winners (dist fp64, global row) into the global winner per query:
  * smallest distance, then smallest row.  cand is world x nq (dist, row) pairs, rank-major. */

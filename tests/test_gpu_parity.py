@@ -15,13 +15,16 @@ from golden_util import E2E_CASES, load_e2e
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=['f16x3', 'f32'])
+@pytest.fixture(params=['f16x3', 'f16x3-cmpsel', 'f32'])
 def matcher(request, ctx):
-    """Both certified matchers (split-f16 MFMA, fp32 MFMA) must give the reference's decisions."""
+    """Every certified matcher (split-f16 MFMA with the packed-index or the compare/select K3
+    epilogue, fp32 MFMA) must give the reference's decisions."""
     from ia_amd import _native
-    ctx.set_option('matcher', _native.IA_MATCH_F16X3 if request.param == 'f16x3' else _native.IA_MATCH_F32)
-    yield request.param
+    ctx.set_option('matcher', _native.IA_MATCH_F32 if request.param == 'f32' else _native.IA_MATCH_F16X3)
+    ctx.set_option('k3_variant', 0 if request.param == 'f16x3-cmpsel' else 1)
+    yield request.param.split('-')[0]
     ctx.set_option('matcher', _native.IA_MATCH_F16X3)
+    ctx.set_option('k3_variant', 1)
 
 
 def _run_levels(ctx, z, Bp, A_pyr=None, Ap_pyr=None, B_pyr=None):
