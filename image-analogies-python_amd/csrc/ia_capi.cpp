@@ -75,7 +75,7 @@ struct ia_ctx {
   hipStream_t st = nullptr;
   // uploads (IA_MEM_HOST) and per-level scratch
   DevBuf A, Ac, Ap, Apc, B, Bc, Bpc, Bp, S, IM, W;
-  DevBuf db, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, pstat, absmax;
+  DevBuf db, db64, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, pstat, absmax;
   int matcher = IA_MATCH_F16X3;  // option "matcher"
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   // per-step K3 timing (optional)
@@ -126,7 +126,7 @@ void ia_destroy(ia_ctx *c) {
   if (!c) return;
   hipSetDevice(c->dev);
   hipStreamSynchronize(c->st);
-  for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->B, &c->Bc, &c->Bpc, &c->Bp, &c->S, &c->IM, &c->W, &c->db,
+  for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->B, &c->Bc, &c->Bpc, &c->Bp, &c->S, &c->IM, &c->W, &c->db, &c->db64,
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->pstat, &c->absmax})
     b->release();
   for (hipEvent_t e : c->evs) hipEventDestroy(e);
@@ -345,6 +345,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   ia_wavefront_shape(g.bh, g.bw, &T, &Mmax);
   const int64_t Mpad_max = (Mmax + IA_TILE - 1) / IA_TILE * IA_TILE;
   if ((rc = c->db.ensure((size_t)std::max(ns, 1) * IA_TILE * db_row_bytes)) || (rc = c->mu.ensure(4 * g.ch * 8)) ||
+      (rc = c->db64.ensure((size_t)g.NA * ia_db64_stride(g.ch) * 8)) ||
       (rc = c->Rbits.ensure(4)) || (rc = c->q64.ensure((size_t)Mpad_max * g.D * 8)) ||
       (rc = c->qn2.ensure((size_t)Mpad_max * 8)) || (rc = c->qf.ensure((size_t)Mpad_max * db_row_bytes)) ||
       (rc = c->rec.ensure((size_t)Mmax * std::max(g.nwg, 1) * 16)) ||
@@ -366,9 +367,11 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     if (use_h) ia_launch_db_build_h(g, Aim, c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
     else ia_launch_db_build(g, Aim, c->mu.as<double>(), c->db.as<float4>(), c->Rbits.as<unsigned>(), c->st);
   }
+  ia_launch_db64_build(g, Aim, c->db64.as<double>(), c->st);  // every row: coherence reads any row
   HIP_TRY(hipEventRecord(c->lv1, c->st));
 
   MergeArgs ma;
+  ma.db64 = c->db64.as<double>();
   ma.rec = c->rec.as<float4>();
   ma.recT = c->recT.as<float>();
   ma.q64 = c->q64.as<double>();
@@ -437,7 +440,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), dS, dIM, dBp, (const double *)dW, a->kappa_factor, false,
                       c->st);
       NCCL_TRY(ncclAllGather(c->win.p, c->allwin.p, (size_t)sd.M * sizeof(Winner), ncclUint8, c->comm, c->st));
-      ia_launch_finish(g, sd, Aim, c->q64.as<double>(), c->allwin.as<Winner>(), world, sd.M, dS, dIM, dBp,
+      ia_launch_finish(g, sd, Aim, c->db64.as<double>(), c->q64.as<double>(), c->allwin.as<Winner>(), world, sd.M, dS, dIM, dBp,
                        (const double *)dW, a->kappa_factor, c->pstat.as<unsigned>(), c->st);
     }
   }
@@ -577,6 +580,7 @@ int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, d
     return rc;
   HIP_TRY(hipMemsetAsync(x->counters.p, 0, 32, c->st));
   MergeArgs ma;
+  ma.db64 = nullptr;
   ma.rec = x->rec.as<float4>();
   ma.recT = x->recT.as<float>();
   ma.q64 = nullptr;

@@ -58,6 +58,7 @@ struct Imgs {        // the four pyramid images a feature row reads (see FeatDes
 };
 
 struct MergeArgs {
+  const double *db64;  // fp64 row-major feature DB of the level (K1b), stride ia_db64_stride(ch)
   const float4 *rec;
   const float *recT;
   const double *q64;   // Mpad x D query rows (fp64)

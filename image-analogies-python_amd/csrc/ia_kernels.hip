@@ -27,6 +27,12 @@
 #ifndef IA_PROBE
 #define IA_PROBE 0  // diagnostic phase-skipping builds (never set in the product build)
 #endif
+#if IA_PROBE & 8  // diagnostic build only: s_memtime phase stamps of sampled merge waves
+#define IA_STAMP(k) do { __builtin_amdgcn_sched_barrier(0); stamp[k] = __builtin_amdgcn_s_memtime(); \
+                         __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define IA_STAMP(k) do { } while (0)
+#endif
 
 
 // ------------------------------------------------------------------------------------------
@@ -38,6 +44,7 @@ struct Geo {
   static constexpr int DP = ((D + 1 + 7) / 8) * 8;  // + norm column, 16-B aligned halves
   static constexpr int KH = DP / 2;                 // k-steps of the 32x32x2 chain
   static constexpr int KP = KH / 4;                 // float4 pieces per lane
+  static constexpr int DS = ((D + 7) / 8) * 8;      // fp64 row-major DB row stride (doubles)
 };
 
 // reflected (symmetric-pad) offsets of the 3x3 coarse and 5x5 fine windows of pixel (r, c)
@@ -272,6 +279,36 @@ __global__ void __launch_bounds__(IA_WG) k_db_build(LevelGeo g, Imgs A, const do
     float R = (float)(sqrt(norm) * (1.0 + 1e-6)) ;
     atomicMax(Rbits, __float_as_uint(R));
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// K1b: the fp64 feature DB, row-major (row = img*h*w + r*w + c, stride Geo::DS doubles, the
+// tail zero), holding the exact pixel values of create_index's As rows (algorithms.py:63-67).
+// The merge reranks candidates from it with contiguous 16-byte loads instead of re-gathering
+// four symmetric-padded images per row.  One thread per (row, 8 features): coalesced stores.
+// ------------------------------------------------------------------------------------------
+template <int CH>
+__global__ void __launch_bounds__(IA_WG) k_db64_build(LevelGeo g, Imgs A, double *__restrict__ db64) {
+  using G = Geo<CH>;
+  constexpr int NCH = G::DS / 8;
+  const int64_t gid = (int64_t)blockIdx.x * IA_WG + threadIdx.x;
+  if (gid >= g.NA * NCH) return;
+  const int64_t row = gid / NCH;
+  const int chunk = (int)(gid - row * NCH);
+  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
+  const int img = (int)((unsigned)row / hw);
+  const unsigned rem = (unsigned)row - (unsigned)img * hw;
+  const int pr = (int)(rem / (unsigned)g.aw), pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
+  const Px P = make_px<CH>(A, pr, pc);
+  double v[8];
+#pragma unroll
+  for (int e = 0; e < 8; e++) {
+    const int f = chunk * 8 + e;
+    v[e] = f < G::D ? featp<CH>(A, P, f, img) : 0.;
+  }
+  double2 *dst = reinterpret_cast<double2 *>(db64 + row * G::DS + chunk * 8);
+#pragma unroll
+  for (int e = 0; e < 4; e++) dst[e] = make_double2(v[2 * e], v[2 * e + 1]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -595,17 +632,13 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc s
 // ------------------------------------------------------------------------------------------
 // K4: exact rerank + certification (+ coherence, kappa rule, writeback) — one wave / query
 // ------------------------------------------------------------------------------------------
-// exact DB-row distance of row `row` (level path): ((a - q)**2).sum() in numpy order
+// exact DB-row distance of row `row` (level path): ((a - q)**2).sum() in numpy order, the row
+// read from the fp64 DB (K1b)
 template <int CH>
-__device__ __forceinline__ double exact_dist_level(const LevelGeo &g, const Imgs &A, int64_t row, const double *q) {
-  // 32-bit row decode (row ids < 2^31 are enforced by the host); no 64-bit division
-  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
-  const unsigned img = (unsigned)row / hw;
-  const unsigned rem = (unsigned)row - img * hw;
-  const unsigned pr = rem / (unsigned)g.aw;
-  const Px P = make_px<CH>(A, (int)pr, (int)(rem - pr * (unsigned)g.aw));
+__device__ __forceinline__ double exact_dist_level(const double *__restrict__ db64, int64_t row, const double *q) {
+  const double *a = db64 + row * Geo<CH>::DS;
   return pw_sum<Geo<CH>::D>([&](int f) {
-    const double d = featp<CH>(A, P, f, img) - q[f];
+    const double d = a[f] - q[f];
     return d * d;
   });
 }
@@ -699,7 +732,8 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
 // coherence + kappa + writeback for query pixel (r, c) whose NN row is app_ix
 // (image_analogies.py:182-220, algorithms.py:92-135)
 template <int CH>
-__device__ void finish_pixel(const LevelGeo &g, const Imgs &A, int r, int c, int64_t app_ix, const double *q,
+__device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__restrict__ db64, int r, int c, int64_t app_ix,
+                             const double *q,
                              int32_t *__restrict__ s, int32_t *__restrict__ im, double *__restrict__ Bp,
                              const double *__restrict__ weights, double kf, unsigned *pstat, unsigned stat) {
   constexpr int D = Geo<CH>::D;
@@ -725,7 +759,7 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, int r, int c, int
           cpr = tr;
           cpc = tc;
           const int64_t row = (int64_t)cim * hw + (int64_t)tr * g.aw + tc;
-          dk = sqrt(exact_dist_level<CH>(g, A, row, q));
+          dk = sqrt(exact_dist_level<CH>(db64, row, q));
           kk = lane;
         }
       }
@@ -740,10 +774,10 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, int r, int c, int
       double part = 0.;
       if (lane < 2) {
         const int ii = lane == 0 ? img : cim, rr_ = lane == 0 ? pr : cpr, cc_ = lane == 0 ? pc : cpc;
-        const Px P = make_px<CH>(A, rr_, cc_);
+        const double *arow = db64 + ((int64_t)ii * hw + (int64_t)rr_ * g.aw + cc_) * Geo<CH>::DS;
 #pragma unroll
         for (int f = 0; f < D; f++) {
-          const double x = (featp<CH>(A, P, f, ii) - q[f]) * weights[f];
+          const double x = (arow[f] - q[f]) * weights[f];
           part += x * x;
         }
         part = sqrt(part);
@@ -767,22 +801,26 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, int r, int c, int
   }
 }
 
-// Both distances of DB row `row` against query q from ONE set of feature loads:
+// Both distances of DB row `row` against query q from ONE set of feature loads (the row of the
+// fp64 DB, K1b; q and w staged in LDS by the caller):
 //   unw = ((a - q)**2).sum()  in numpy's pairwise order (NN rerank / coherence ranking)
 //   wsq = sum(((a - q) * w)**2) sequentially (compute_distance before its sqrt / square)
 template <int CH>
-__device__ __forceinline__ void row_dists(const LevelGeo &g, const Imgs &A, int row, const double *q,
-                                          const double *w, double &unw, double &wsq) {
-  constexpr int D = Geo<CH>::D;
-  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
-  const unsigned img = (unsigned)row / hw;
-  const unsigned rem = (unsigned)row - img * hw;
-  const unsigned pr = rem / (unsigned)g.aw;
-  const Px P = make_px<CH>(A, (int)pr, (int)(rem - pr * (unsigned)g.aw));
+__device__ __forceinline__ void row_dists(const double *__restrict__ db64, int row, const double *q, const double *w,
+                                          double &unw, double &wsq) {
+  constexpr int D = Geo<CH>::D, DS = Geo<CH>::DS;
+  const double *a = db64 + (int64_t)row * DS;
   if constexpr (CH == 1) {
-    double t[D];
+    const double2 *a2 = reinterpret_cast<const double2 *>(a);
+    double t[D + 1];
 #pragma unroll
-    for (int f = 0; f < D; f++) t[f] = featp<CH>(A, P, f, (int)img) - q[f];
+    for (int k = 0; k < (D + 1) / 2; k++) {  // all 28 loads issued before any use
+      const double2 v = a2[k];
+      t[2 * k] = v.x;
+      t[2 * k + 1] = v.y;
+    }
+#pragma unroll
+    for (int f = 0; f < D; f++) t[f] -= q[f];
     unw = pw_sum<D>([&](int f) { return t[f] * t[f]; });
     double s = 0.;
 #pragma unroll
@@ -791,14 +829,14 @@ __device__ __forceinline__ void row_dists(const LevelGeo &g, const Imgs &A, int 
       s += x * x;
     }
     wsq = s;
-  } else {  // 165 doubles do not fit in registers: gather twice
+  } else {  // 165 doubles do not fit in registers: read the row twice
     unw = pw_sum<D>([&](int f) {
-      const double d = featp<CH>(A, P, f, (int)img) - q[f];
+      const double d = a[f] - q[f];
       return d * d;
     });
     double s = 0.;
     for (int f = 0; f < D; f++) {
-      const double x = (featp<CH>(A, P, f, (int)img) - q[f]) * w[f];
+      const double x = (a[f] - q[f]) * w[f];
       s += x * x;
     }
     wsq = s;
@@ -828,9 +866,14 @@ __device__ __forceinline__ int lowest_cand(unsigned cmask, const int (&i1)[RPL],
 // k and lanes 15..63 the MFMA candidates worth an exact rerank; every lane gets both the exact
 // unweighted distance (ranking) and the weighted one (kappa rule) from the same loads.
 template <int CH>
-__device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &a, int m,
-                            int32_t *__restrict__ s, int32_t *__restrict__ im, double *__restrict__ Bp,
-                            const double *__restrict__ weights, double kf) {
+__device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &a,
+                                            int m, int32_t *__restrict__ s, int32_t *__restrict__ im,
+                                            double *__restrict__ Bp, const double *__restrict__ weights, double kf,
+                                            double *qs, double *ws) {
+#if IA_PROBE & 8
+  unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  IA_STAMP(0);
   constexpr int RPL = IA_WG_TARGET / IA_WAVE;
   constexpr int NCOH = 15, NRR = IA_WAVE - NCOH;  // lanes for coherence / rerank candidates
   const int lane = threadIdx.x & 63;
@@ -854,6 +897,13 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
     i1[j] = __float_as_int(x.y);
     i2[j] = __float_as_int(x.w);
   }
+  // the query row and the weights, staged in this wave's LDS slice (read by every lane below;
+  // LDS operations of one wave complete in order)
+  for (int f = lane; f < Geo<CH>::D; f += IA_WAVE) {
+    qs[f] = q[f];
+    ws[f] = weights[f];
+  }
+  __builtin_amdgcn_wave_barrier();
   int crow = -1, cpr = -1, cpc = -1, cim = 0;
   if (qi > 0 && lane < NCOH) {  // best_coherence_match candidates, product(rows, cols) order
     const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
@@ -872,6 +922,10 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
   const double R = (double)__uint_as_float(*a.Rbits);
   const double qn2 = a.qn2[m];
 
+#if IA_PROBE & 8
+  if (v1[0] == 12345.f && crow == 7) stamp[7] = 1;  // force round 1 to land here
+#endif
+  IA_STAMP(1);
   // ---- MFMA candidates that may be the exact winner -> lanes 15..63
   float a1 = FLT_MAX;
 #pragma unroll
@@ -907,23 +961,31 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
     pend = __ballot(cmask != 0);
   }
 
+  IA_STAMP(2);
   // ---- round 2: one feature gather per lane
   double unw = DBL_MAX, wsq = 0.;
-  if (my_row >= 0) row_dists<CH>(g, A, my_row, q, weights, unw, wsq);
+  if (my_row >= 0) row_dists<CH>(a.db64, my_row, qs, ws, unw, wsq);
   // bound audit: the exact distance of every reranked candidate must lie within eps of its
   // MFMA value + |q'|^2 (a violation would void the certification; counted, never expected)
   const bool viol = lane >= NCOH && my_row >= 0 && fabs(unw - qn2 - (double)my_v) > eps;
   const bool any_viol = __ballot(viol) != 0;
 
+#if IA_PROBE & 8
+  if (unw == 12345.) stamp[7] = 2;
+#endif
+  IA_STAMP(3);
   // exact NN winner among the reranked candidates (+ any overflow beyond 49, rare)
   double bd = (lane >= NCOH && my_row >= 0) ? unw : DBL_MAX;
   int64_t bi = (lane >= NCOH && my_row >= 0) ? (int64_t)my_row : INT64_MAX;
   bool recompute_app = false;
+#if IA_PROBE & 4  // diagnostic build only: no overflow candidates, no certification rescans
+  pend = 0;
+#endif
   while (pend) {  // overflow: remaining candidates one at a time
     const int L = __ffsll((long long)pend) - 1;
     const int row = __shfl(nxt, L, 64);
     double u, wq;
-    row_dists<CH>(g, A, row, q, weights, u, wq);
+    row_dists<CH>(a.db64, row, qs, ws, u, wq);
     if (u < bd || (u == bd && row < bi)) {
       bd = u;
       bi = row;
@@ -944,12 +1006,16 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
     else recompute_app = true;
   }
 
+  IA_STAMP(4);
   // certification (see certified_winner): rescan chunks whose threshold does not clear bd
   const double theta = bd - qn2 + eps + 1e-13 * (bd + 1.0);
   unsigned long long nfb = 0;
 #pragma unroll
   for (int jb = 0; jb < RPL; jb++) {
     unsigned long long mask = __ballot((double)tt[jb] <= theta);
+#if IA_PROBE & 4
+    mask = 0;
+#endif
     while (mask) {
       const int j = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
@@ -960,7 +1026,7 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
       for (int64_t p = p0 + lane; p < p1; p += IA_WAVE) {
         const int64_t i = ia_pos_row(p, a.NT);
         if (i >= a.NA) continue;
-        const double d = exact_dist_level<CH>(g, A, i, q);
+        const double d = exact_dist_level<CH>(a.db64, i, qs);
         if (d < cd || (d == cd && i < ci)) { cd = d; ci = i; }
       }
       wave_min_di(cd, ci);
@@ -973,6 +1039,7 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
     }
   }
 
+  IA_STAMP(5);
   // coherence winner: first argmin of the norm over lanes 0..14
   double dk = (lane < NCOH && my_row >= 0) ? sqrt(unw) : DBL_MAX;
   int64_t kk = (lane < NCOH && my_row >= 0) ? (int64_t)lane : INT64_MAX;
@@ -989,7 +1056,7 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
     const double wsq_coh = __shfl(wsq, src, 64);
     if (recompute_app) {
       double u, wq = 0.;
-      if (lane == 0) row_dists<CH>(g, A, (int)bi, q, weights, u, wq);
+      if (lane == 0) row_dists<CH>(a.db64, (int)bi, qs, ws, u, wq);
       wsq_app = __shfl(wq, 0, 64);
     }
     // compute_distance = norm(x)**2 = sqrt(sum x^2)**2 ; kappa rule image_analogies.py:206
@@ -1003,6 +1070,7 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
       coh_won = true;
     }
   }
+  IA_STAMP(6);
   if (lane < CH) Bp[(int64_t)qi * CH + lane] = A.p3[img * A.img_stride_f + ((int64_t)pr * g.aw + pc) * CH + lane];
   if (lane == 0) {
     s[2 * qi] = pr;
@@ -1013,6 +1081,15 @@ __device__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A
     a.pstat[qi] = (unsigned)min(slot, 0xffff) | ((unsigned)min((int)nfb, 0x3fff) << 16) | (coh_won ? 1u << 30 : 0u) |
                   (any_viol ? 1u << 31 : 0u);
   }
+#if IA_PROBE & 8
+  if (lane == 0 && m == sd.M / 2 && (sd.t % 256) == 128) {
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t7 = __builtin_amdgcn_s_memtime();
+    printf("STAMP bw=%d t=%d M=%d slot=%d nfb=%d d1=%llu d2=%llu d3=%llu d4=%llu d5=%llu d6=%llu d7=%llu\n", g.bw, sd.t,
+           sd.M, slot, (int)nfb, stamp[1] - stamp[0], stamp[2] - stamp[1], stamp[3] - stamp[2], stamp[4] - stamp[3],
+           stamp[5] - stamp[4], stamp[6] - stamp[5], t7 - stamp[6]);
+  }
+#endif
 }
 
 template <int CH, bool FUSED>
@@ -1022,9 +1099,10 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
                                                         double kf) {
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
   if (m >= sd.M) return;
-#if IA_PROBE == 0
+#if (IA_PROBE & 3) == 0
   if constexpr (FUSED) {
-    merge_fused<CH>(g, sd, A, ma, m, s, im, Bp, weights, kf);
+    __shared__ double qsh[IA_WG / IA_WAVE][Geo<CH>::DS], wsh[IA_WG / IA_WAVE][Geo<CH>::DS];
+    merge_fused<CH>(g, sd, A, ma, m, s, im, Bp, weights, kf, qsh[threadIdx.x >> 6], wsh[threadIdx.x >> 6]);
     return;
   }
 #endif
@@ -1033,7 +1111,7 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
   const Winner wn{0., (int64_t)__float_as_int(ma.rec[(int64_t)m * ma.nwg].y)};
 #else
   unsigned stat = 0;
-  const Winner wn = certified_winner(ma, m, [&](int64_t row) { return exact_dist_level<CH>(g, A, row, q); }, &stat);
+  const Winner wn = certified_winner(ma, m, [&](int64_t row) { return exact_dist_level<CH>(ma.db64, row, q); }, &stat);
 #endif
 #if IA_PROBE & 2  // diagnostic build only: no coherence / kappa
   if ((threadIdx.x & 63) == 0) {
@@ -1046,7 +1124,7 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
 #endif
   if constexpr (FUSED) {
     const int r = sd.r0 + m;
-    finish_pixel<CH>(g, A, r, sd.t - 3 * r, wn.idx, q, s, im, Bp, weights, kf, ma.pstat, stat);
+    finish_pixel<CH>(g, A, ma.db64, r, sd.t - 3 * r, wn.idx, q, s, im, Bp, weights, kf, ma.pstat, stat);
   } else {
     if ((threadIdx.x & 63) == 0) {
       win[m] = wn;
@@ -1058,7 +1136,8 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
 
 // multi-rank finish: global winner over the all-gathered per-rank winners, then coherence
 template <int CH>
-__global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd, Imgs A, const double *__restrict__ q64,
+__global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd, Imgs A, const double *__restrict__ db64,
+                                                         const double *__restrict__ q64,
                                                          const Winner *__restrict__ allwin, int world, int Mstride,
                                                          int32_t *__restrict__ s, int32_t *__restrict__ im,
                                                          double *__restrict__ Bp, const double *__restrict__ weights,
@@ -1074,7 +1153,7 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
   const int r = sd.r0 + m;
   const int qi = r * g.bw + sd.t - 3 * r;
   const unsigned prev = pstat ? pstat[qi] : 0u;
-  finish_pixel<CH>(g, A, r, sd.t - 3 * r, bi, q64 + (int64_t)m * Geo<CH>::D, s, im, Bp, weights, kf, pstat, prev);
+  finish_pixel<CH>(g, A, db64, r, sd.t - 3 * r, bi, q64 + (int64_t)m * Geo<CH>::D, s, im, Bp, weights, kf, pstat, prev);
 }
 
 // per-level statistics: sum the per-pixel stats words (one workgroup, fixed order)
@@ -1268,19 +1347,31 @@ void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const
 }
 
 template <int CH>
-static void launch_finish_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *q64, const Winner *allwin,
-                            int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w, double kf,
-                            unsigned *ctr, hipStream_t st) {
-  hipLaunchKernelGGL(k_finish_level<CH>, dim3(cdiv(sd.M, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, A, q64, allwin,
+static void launch_finish_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
+                            const Winner *allwin, int world, int Mstride, int32_t *s, int32_t *im, double *Bp,
+                            const double *w, double kf, unsigned *ctr, hipStream_t st) {
+  hipLaunchKernelGGL(k_finish_level<CH>, dim3(cdiv(sd.M, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, A, db64, q64, allwin,
                      world, Mstride, s, im, Bp, w, kf, ctr);
 }
-void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *q64, const Winner *allwin,
-                      int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w, double kf,
-                      unsigned *ctr, hipStream_t st) {
-  if (g.ch == 1) launch_finish_t<1>(g, sd, A, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
-  else if (g.ch == 2) launch_finish_t<2>(g, sd, A, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
-  else launch_finish_t<3>(g, sd, A, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
+void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
+                      const Winner *allwin, int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w,
+                      double kf, unsigned *ctr, hipStream_t st) {
+  if (g.ch == 1) launch_finish_t<1>(g, sd, A, db64, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
+  else if (g.ch == 2) launch_finish_t<2>(g, sd, A, db64, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
+  else launch_finish_t<3>(g, sd, A, db64, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
 }
+
+template <int CH>
+static void launch_db64_t(const LevelGeo &g, const Imgs &A, double *db64, hipStream_t st) {
+  const int64_t n = g.NA * (Geo<CH>::DS / 8);
+  hipLaunchKernelGGL(k_db64_build<CH>, dim3(cdiv(n, IA_WG)), dim3(IA_WG), 0, st, g, A, db64);
+}
+void ia_launch_db64_build(const LevelGeo &g, const Imgs &A, double *db64, hipStream_t st) {
+  if (g.ch == 1) launch_db64_t<1>(g, A, db64, st);
+  else if (g.ch == 2) launch_db64_t<2>(g, A, db64, st);
+  else launch_db64_t<3>(g, A, db64, st);
+}
+int ia_db64_stride(int ch) { return ch == 1 ? Geo<1>::DS : ch == 2 ? Geo<2>::DS : Geo<3>::DS; }
 
 void ia_launch_reduce_stats(const unsigned *pstat, int64_t n, unsigned long long *counters, hipStream_t st) {
   hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(IA_WG), 0, st, pstat, n, counters);

@@ -13,9 +13,11 @@ void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tile
                   int row0, int NT, float4 *rec, float *recT, hipStream_t st);
 void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win, int32_t *s,
                      int32_t *im, double *Bp, const double *w, double kf, bool fused, hipStream_t st);
-void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *q64, const Winner *allwin,
-                      int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w, double kf,
-                      unsigned *pstat, hipStream_t st);
+void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
+                      const Winner *allwin, int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w,
+                      double kf, unsigned *pstat, hipStream_t st);
+void ia_launch_db64_build(const LevelGeo &g, const Imgs &A, double *db64, hipStream_t st);
+int ia_db64_stride(int ch);
 void ia_launch_reduce_stats(const unsigned *pstat, int64_t n, unsigned long long *counters, hipStream_t st);
 void ia_launch_dense_db(int KH, const double *pts, int64_t n, int d, int n_tiles, const double *mu, float4 *db,
                         unsigned *Rbits, hipStream_t st);
