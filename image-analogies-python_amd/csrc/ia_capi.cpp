@@ -384,7 +384,10 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   ma.NT = g.n_tiles;
   ma.NA = (int)g.NA;
   int64_t shard_rows = 0;  // real DB rows in this shard's tiles (strided layout)
-  for (int t = g.tile0; t < g.tile1; t++) shard_rows += std::min<int64_t>(IA_TILE, (g.NA - t + g.n_tiles - 1) / g.n_tiles);
+  for (int t = g.tile0; t < g.tile1; t++) {
+    const int64_t tr = ia_tile_perm(t, g.n_tiles);
+    shard_rows += std::min<int64_t>(IA_TILE, (g.NA - tr + g.n_tiles - 1) / g.n_tiles);
+  }
   ma.pstat = c->pstat.as<unsigned>();
   ma.eps_c = use_h ? ia_eps_c_h(g.KS, c->k3_variant == 1) : ia_eps_c(DP);
   ma.eps_a = use_h ? ia_eps_a_h() : 0.;

@@ -75,11 +75,25 @@ struct MergeArgs {
   double eps_a;                       // absolute (f16 subnormal) error coefficient
 };
 
-// DB positions are tile-strided: slot j of tile t holds row j*NT + t, so spatially adjacent A
-// pixels (near-identical features, near-tied distances) land in different tiles and hence in
-// different K3 subsets; every subset's runner-up threshold then stays clear of the winner and
-// certification rarely needs an exact chunk rescan.
-__host__ __device__ inline int64_t ia_pos_row(int64_t pos, int64_t NT) { return (pos & 31) * NT + (pos >> 5); }
+// DB positions are tile-strided and tile-scattered: slot j of tile t holds row j*NT + perm(t)
+// with perm(t) = t * (IA_TILE_MUL mod NT) mod NT (a bijection: IA_TILE_MUL is a prime above any
+// NT).  Spatially adjacent A pixels (near-identical features, near-tied distances) thereby land
+// in different tiles AND far-apart tiles, i.e. in different K3 workgroup chunks: every chunk's
+// runner-up threshold then stays clear of the winner and certification rarely needs an exact
+// chunk rescan (with contiguous tiles, three near-ties of a smooth neighbourhood shared a chunk).
+#define IA_TILE_MUL 2654435761LL
+__host__ __device__ inline int64_t ia_tile_perm(int64_t t, int64_t NT) {
+  const int64_t k = IA_TILE_MUL % NT;
+  const int64_t p = t * k;  // < 2^52: exact in double
+  int64_t q = (int64_t)((double)p / (double)NT);
+  int64_t r = p - q * NT;
+  r += r < 0 ? NT : 0;
+  r -= r >= NT ? NT : 0;
+  return r;
+}
+__host__ __device__ inline int64_t ia_pos_row(int64_t pos, int64_t NT) {
+  return (pos & 31) * NT + ia_tile_perm(pos >> 5, NT);
+}
 
 // per-step wavefront description: pixels (r, t - 3r), r in [r0, r0 + M)
 struct StepDesc {

@@ -131,9 +131,10 @@ int ia_wavefront_shape(int h, int w, int64_t *steps, int64_t *max_queries);
 /* Pixels of step t: rows r0 .. r0+M-1, pixel (r, t - 3r).  Used by the level driver. */
 int ia_wavefront_step(int h, int w, int64_t t, int *r0, int *M);
 /* DB tiles [tile0, tile1) owned by `rank` of `world` for a level of n_rows DB rows.  The DB is
- * stored in ceil(n_rows/32) tiles of 32 positions; position j of tile t holds row j*n_tiles + t
- * (tile-strided, so neighbouring A pixels sit in different tiles).  Tiles are split contiguously
- * over ranks; levels under 64*world tiles are not sharded (every rank owns every tile). */
+ * stored in NT = ceil(n_rows/32) tiles of 32 positions; position j of tile t holds row
+ * j*NT + (t * (2654435761 mod NT) mod NT) (tile-strided and tile-scattered, so neighbouring A
+ * pixels sit in far-apart tiles).  Tiles are split contiguously over ranks; levels under
+ * 64*world tiles are not sharded (every rank owns every tile). */
 int ia_shard_tiles(int64_t n_rows, int world, int rank, int64_t *tile0, int64_t *tile1);
 
 #ifdef __cplusplus
