@@ -860,16 +860,68 @@ __device__ __forceinline__ int lowest_cand(unsigned cmask, const int (&i1)[RPL],
   return row;
 }
 
+// ---- cross-lane exchange without LDS: partner of step k of a 64-lane butterfly -----------------
+// steps 0-3 stay inside a 16-lane row (DPP quad_perm xor 1, xor 2, row_half_mirror,
+// row_mirror), 4 pairs rows 0-1 / 2-3 (v_permlane16_swap), 5 the two wave halves
+// (v_permlane32_swap).  Every lane's partner differs from it and the pairing at each step
+// joins two groups that are each already reduced, so after step 5 every lane holds the
+// reduction of all 64.
+template <int STEP>
+__device__ __forceinline__ int lane_xchg(int v) {
+  if constexpr (STEP == 0) return __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false);
+  else if constexpr (STEP == 1) return __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false);
+  else if constexpr (STEP == 2) return __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false);
+  else if constexpr (STEP == 3) return __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false);
+  else if constexpr (STEP == 4) {
+    const auto r = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)(((threadIdx.x >> 4) & 1) ? r[0] : r[1]);
+  } else {
+    const auto r = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    return (int)((threadIdx.x & 32) ? r[0] : r[1]);
+  }
+}
+template <int STEP>
+__device__ __forceinline__ double lane_xchg_d(double v) {
+  const int lo = lane_xchg<STEP>(__double2loint(v)), hi = lane_xchg<STEP>(__double2hiint(v));
+  return __hiloint2double(hi, lo);
+}
+template <int STEP>
+__device__ __forceinline__ float lane_xchg_f(float v) {
+  return __int_as_float(lane_xchg<STEP>(__float_as_int(v)));
+}
+// lexicographic (d, i) minimum across the wave for TWO independent keys at once
+template <int STEP = 0>
+__device__ __forceinline__ void wave_min2_di(double &d0, int &i0, double &d1, int &i1) {
+  if constexpr (STEP < 6) {
+    const double e0 = lane_xchg_d<STEP>(d0), e1 = lane_xchg_d<STEP>(d1);
+    const int j0 = lane_xchg<STEP>(i0), j1 = lane_xchg<STEP>(i1);
+    if (e0 < d0 || (e0 == d0 && j0 < i0)) { d0 = e0; i0 = j0; }
+    if (e1 < d1 || (e1 == d1 && j1 < i1)) { d1 = e1; i1 = j1; }
+    wave_min2_di<STEP + 1>(d0, i0, d1, i1);
+  }
+}
+template <int STEP = 0>
+__device__ __forceinline__ float wave_min_f_x(float v) {
+  if constexpr (STEP < 6) return wave_min_f_x<STEP + 1>(fminf(v, lane_xchg_f<STEP>(v)));
+  else return v;
+}
+__device__ __forceinline__ int lane_prefix(unsigned long long bal) {  // set bits of bal below this lane
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
+}
+
 // Fused single-rank merge of query m: certified exact NN + coherence + kappa + writeback.
-// Memory is touched in two dependent rounds: (1) the K3 records and the coherence
-// neighbours' s/im, (2) ONE feature gather in which lane k < 15 evaluates coherence candidate
-// k and lanes 15..63 the MFMA candidates worth an exact rerank; every lane gets both the exact
-// unweighted distance (ranking) and the weighted one (kappa rule) from the same loads.
+// Memory is touched in two dependent rounds: (1) the K3 records, the coherence neighbours'
+// s/im and the query/weights (staged in LDS), (2) ONE fp64-DB row per lane, in which lane
+// k < 15 evaluates coherence candidate k and lanes 15..63 the MFMA candidates worth an exact
+// rerank (placed by mbcnt rounds); every lane gets the exact unweighted distance (ranking),
+// the weighted one (kappa rule) and its row's A' value (the B' write) from the same round.
+// Candidates beyond the 49 rerank lanes (rare) are evaluated by the lanes that listed them.
+// Wave reductions use DPP / permlane exchanges (no LDS round trips).
 template <int CH>
 __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &a,
                                             int m, int32_t *__restrict__ s, int32_t *__restrict__ im,
                                             double *__restrict__ Bp, const double *__restrict__ weights, double kf,
-                                            double *qs, double *ws) {
+                                            double *qs, double *ws, int *cand_row, float *cand_v) {
 #if IA_PROBE & 8
   unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -881,8 +933,9 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   const double *q = a.q64 + (int64_t)m * Geo<CH>::D;
   const float4 *rr = a.rec + (int64_t)m * a.nwg;
   const float *rT = a.recT + (int64_t)m * a.nwg;
+  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
 
-  // ---- round 1: records (clamped, unconditional loads) and coherence neighbours
+  // ---- round 1: records (clamped, unconditional loads), coherence neighbours, query/weights
   float v1[RPL], v2[RPL], tt[RPL];
   int i1[RPL], i2[RPL];
 #pragma unroll
@@ -897,13 +950,10 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     i1[j] = __float_as_int(x.y);
     i2[j] = __float_as_int(x.w);
   }
-  // the query row and the weights, staged in this wave's LDS slice (read by every lane below;
-  // LDS operations of one wave complete in order)
   for (int f = lane; f < Geo<CH>::D; f += IA_WAVE) {
     qs[f] = q[f];
     ws[f] = weights[f];
   }
-  __builtin_amdgcn_wave_barrier();
   int crow = -1, cpr = -1, cpc = -1, cim = 0;
   if (qi > 0 && lane < NCOH) {  // best_coherence_match candidates, product(rows, cols) order
     const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
@@ -921,16 +971,16 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   }
   const double R = (double)__uint_as_float(*a.Rbits);
   const double qn2 = a.qn2[m];
-
 #if IA_PROBE & 8
   if (v1[0] == 12345.f && crow == 7) stamp[7] = 1;  // force round 1 to land here
 #endif
   IA_STAMP(1);
-  // ---- MFMA candidates that may be the exact winner -> lanes 15..63
+
+  // ---- MFMA candidates that may be the exact winner -> lanes 15..63 (mbcnt placement rounds)
   float a1 = FLT_MAX;
 #pragma unroll
   for (int j = 0; j < RPL; j++) a1 = fminf(a1, v1[j]);
-  a1 = wave_min_f(a1);
+  a1 = wave_min_f_x(a1);
   const double qn = sqrt(qn2);
   const double eps = a.eps_c * (R * R + 2.0 * R * qn) + a.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0);
   const double thr = (double)a1 + 2.0 * eps;
@@ -940,96 +990,103 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     if ((double)v1[j] <= thr && i1[j] >= 0 && i1[j] < a.NA) cmask |= 1u << (2 * j);
     if ((double)v2[j] <= thr && i2[j] >= 0 && i2[j] < a.NA) cmask |= 1u << (2 * j + 1);
   }
-  int my_row = lane < NCOH ? crow : -1;
-  float my_v = FLT_MAX, nxv;  // MFMA value of the candidate a rerank lane evaluates (bound audit)
-  int nxt = lowest_cand<RPL>(cmask, i1, i2, v1, v2, nxv);
-  int slot = 0;
-  unsigned long long pend = __ballot(cmask != 0);
-  while (pend && slot < NRR) {
-    const int L = __ffsll((long long)pend) - 1;
-    const int row = __shfl(nxt, L, 64);
-    const float rv = __shfl(nxv, L, 64);
-    if (lane == NCOH + slot) {
-      my_row = row;
-      my_v = rv;
-    }
-    slot++;
-    if (lane == L) {
+  int placed = 0;  // candidates given a rerank lane so far (wave-uniform)
+  unsigned long long bal = __ballot(cmask != 0);
+  while (bal && placed < NRR) {
+    const int pos = placed + lane_prefix(bal);
+    if (cmask != 0 && pos < NRR) {
+      float v;
+      cand_row[pos] = lowest_cand<RPL>(cmask, i1, i2, v1, v2, v);
+      cand_v[pos] = v;
       cmask &= cmask - 1;
-      nxt = lowest_cand<RPL>(cmask, i1, i2, v1, v2, nxv);
     }
-    pend = __ballot(cmask != 0);
+    placed += __popcll(bal);
+    bal = __ballot(cmask != 0);
   }
-
+  const int n_cand = min(placed, NRR);
+  __builtin_amdgcn_wave_barrier();
+  int my_row = lane < NCOH ? crow : (lane - NCOH < n_cand ? cand_row[lane - NCOH] : -1);
+  const float my_v = lane >= NCOH && my_row >= 0 ? cand_v[lane - NCOH] : FLT_MAX;
   IA_STAMP(2);
-  // ---- round 2: one feature gather per lane
+
+  // ---- round 2: one fp64-DB row + its A' value per lane
   double unw = DBL_MAX, wsq = 0.;
-  if (my_row >= 0) row_dists<CH>(a.db64, my_row, qs, ws, unw, wsq);
+  double av[CH];
+#pragma unroll
+  for (int k = 0; k < CH; k++) av[k] = 0.;
+  if (my_row >= 0) {
+    const unsigned img = (unsigned)my_row / hw;
+    const double *src = A.p3 + img * A.img_stride_f + (int64_t)((unsigned)my_row - img * hw) * CH;
+#pragma unroll
+    for (int k = 0; k < CH; k++) av[k] = src[k];
+    row_dists<CH>(a.db64, my_row, qs, ws, unw, wsq);
+  }
   // bound audit: the exact distance of every reranked candidate must lie within eps of its
   // MFMA value + |q'|^2 (a violation would void the certification; counted, never expected)
   const bool viol = lane >= NCOH && my_row >= 0 && fabs(unw - qn2 - (double)my_v) > eps;
   const bool any_viol = __ballot(viol) != 0;
-
 #if IA_PROBE & 8
   if (unw == 12345.) stamp[7] = 2;
 #endif
   IA_STAMP(3);
-  // exact NN winner among the reranked candidates (+ any overflow beyond 49, rare)
-  double bd = (lane >= NCOH && my_row >= 0) ? unw : DBL_MAX;
-  int64_t bi = (lane >= NCOH && my_row >= 0) ? (int64_t)my_row : INT64_MAX;
+
+  // exact NN candidates of this lane: its rerank row, then any overflow it listed (rare)
+  double nd = (lane >= NCOH && my_row >= 0) ? unw : DBL_MAX;
+  int ni = (lane >= NCOH && my_row >= 0) ? my_row : INT_MAX;
   bool recompute_app = false;
-#if IA_PROBE & 4  // diagnostic build only: no overflow candidates, no certification rescans
-  pend = 0;
-#endif
-  while (pend) {  // overflow: remaining candidates one at a time
-    const int L = __ffsll((long long)pend) - 1;
-    const int row = __shfl(nxt, L, 64);
+  int n_over = 0;
+  while (cmask) {
+    float v;
+    const int row = lowest_cand<RPL>(cmask, i1, i2, v1, v2, v);
+    cmask &= cmask - 1;
     double u, wq;
     row_dists<CH>(a.db64, row, qs, ws, u, wq);
-    if (u < bd || (u == bd && row < bi)) {
-      bd = u;
-      bi = row;
+    if (u < nd || (u == nd && row < ni)) {
+      nd = u;
+      ni = row;
     }
-    slot++;
-    recompute_app = true;
-    if (lane == L) {
-      cmask &= cmask - 1;
-      nxt = lowest_cand<RPL>(cmask, i1, i2, v1, v2, nxv);
-    }
-    pend = __ballot(cmask != 0);
+    n_over++;
   }
-  wave_min_di(bd, bi);
+  if (__ballot(n_over > 0)) recompute_app = true;
+  // NN winner (lowest index on ties) and coherence winner (first argmin of the norm) together
+  double dk = (lane < NCOH && my_row >= 0) ? sqrt(unw) : DBL_MAX;
+  int kk = (lane < NCOH && my_row >= 0) ? lane : INT_MAX;
+  double bd = nd;
+  int bi = ni;
+  wave_min2_di(bd, bi, dk, kk);
+  const unsigned long long own = __ballot(lane >= NCOH && my_row >= 0 && my_row == bi && unw == bd);
   double wsq_app = 0.;
-  {
-    const unsigned long long own = __ballot(lane >= NCOH && my_row >= 0 && (int64_t)my_row == bi && unw == bd);
-    if (own) wsq_app = __shfl(wsq, __ffsll((long long)own) - 1, 64);
-    else recompute_app = true;
+  int app_lane = 0;
+  if (own) {
+    app_lane = __ffsll((long long)own) - 1;
+    wsq_app = __shfl(wsq, app_lane, 64);
+  } else {
+    recompute_app = true;
   }
-
   IA_STAMP(4);
+
   // certification (see certified_winner): rescan chunks whose threshold does not clear bd
   const double theta = bd - qn2 + eps + 1e-13 * (bd + 1.0);
   unsigned long long nfb = 0;
 #pragma unroll
   for (int jb = 0; jb < RPL; jb++) {
     unsigned long long mask = __ballot((double)tt[jb] <= theta);
-#if IA_PROBE & 4
-    mask = 0;
-#endif
     while (mask) {
       const int j = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
       const int64_t p0 = (int64_t)a.pos0 + (int64_t)(jb * IA_WAVE + j) * a.tpw * IA_TILE;
       const int64_t p1 = min((int64_t)a.pos_end, p0 + (int64_t)a.tpw * IA_TILE);
       double cd = DBL_MAX;
-      int64_t ci = INT64_MAX;
+      int ci = INT_MAX;
       for (int64_t p = p0 + lane; p < p1; p += IA_WAVE) {
         const int64_t i = ia_pos_row(p, a.NT);
         if (i >= a.NA) continue;
         const double d = exact_dist_level<CH>(a.db64, i, qs);
-        if (d < cd || (d == cd && i < ci)) { cd = d; ci = i; }
+        if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
       }
-      wave_min_di(cd, ci);
+      double du = DBL_MAX;
+      int iu = INT_MAX;
+      wave_min2_di(cd, ci, du, iu);
       if (cd < bd || (cd == bd && ci < bi)) {
         bd = cd;
         bi = ci;
@@ -1038,25 +1095,19 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
       nfb++;
     }
   }
-
   IA_STAMP(5);
-  // coherence winner: first argmin of the norm over lanes 0..14
-  double dk = (lane < NCOH && my_row >= 0) ? sqrt(unw) : DBL_MAX;
-  int64_t kk = (lane < NCOH && my_row >= 0) ? (int64_t)lane : INT64_MAX;
-  wave_min_di(dk, kk);
 
-  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
   int img = (int)((unsigned)bi / hw);
   const unsigned rem = (unsigned)bi - (unsigned)img * hw;
   int pr = (int)(rem / (unsigned)g.aw), pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
   bool coh_won = false;
-  if (kk != INT64_MAX) {  // a coherence candidate exists (never for the level's first pixel)
-    const int src = (int)kk;
-    const int kpr = __shfl(cpr, src, 64), kpc = __shfl(cpc, src, 64), kim = __shfl(cim, src, 64);
-    const double wsq_coh = __shfl(wsq, src, 64);
+  int src_lane = recompute_app ? -1 : app_lane;  // lane holding the chosen row's A' value
+  if (kk != INT_MAX) {  // a coherence candidate exists (never for the level's first pixel)
+    const int kpr = __shfl(cpr, kk, 64), kpc = __shfl(cpc, kk, 64), kim = __shfl(cim, kk, 64);
+    const double wsq_coh = __shfl(wsq, kk, 64);
     if (recompute_app) {
       double u, wq = 0.;
-      if (lane == 0) row_dists<CH>(a.db64, (int)bi, qs, ws, u, wq);
+      if (lane == 0) row_dists<CH>(a.db64, bi, qs, ws, u, wq);
       wsq_app = __shfl(wq, 0, 64);
     }
     // compute_distance = norm(x)**2 = sqrt(sum x^2)**2 ; kappa rule image_analogies.py:206
@@ -1068,16 +1119,26 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
       pr = kpr;
       pc = kpc;
       coh_won = true;
+      src_lane = kk;
     }
   }
   IA_STAMP(6);
-  if (lane < CH) Bp[(int64_t)qi * CH + lane] = A.p3[img * A.img_stride_f + ((int64_t)pr * g.aw + pc) * CH + lane];
+  double val[CH];
+#pragma unroll
+  for (int k = 0; k < CH; k++) val[k] = src_lane >= 0 ? __shfl(av[k], src_lane, 64) : 0.;
+  if (src_lane < 0) {  // winner from an overflow candidate or a rescan: fetch its A' value
+#pragma unroll
+    for (int k = 0; k < CH; k++) val[k] = A.p3[img * A.img_stride_f + ((int64_t)pr * g.aw + pc) * CH + k];
+  }
   if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < CH; k++) Bp[(int64_t)qi * CH + k] = val[k];
     s[2 * qi] = pr;
     s[2 * qi + 1] = pc;
     im[qi] = img;
     // per-pixel stats word (no shared-counter atomics: hundreds of waves adding to one
     // address serialise at L2 and dominated this kernel); reduced once per level
+    const int slot = placed + 0;
     a.pstat[qi] = (unsigned)min(slot, 0xffff) | ((unsigned)min((int)nfb, 0x3fff) << 16) | (coh_won ? 1u << 30 : 0u) |
                   (any_viol ? 1u << 31 : 0u);
   }
@@ -1086,7 +1147,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     __builtin_amdgcn_s_waitcnt(0);
     const unsigned long long t7 = __builtin_amdgcn_s_memtime();
     printf("STAMP bw=%d t=%d M=%d slot=%d nfb=%d d1=%llu d2=%llu d3=%llu d4=%llu d5=%llu d6=%llu d7=%llu\n", g.bw, sd.t,
-           sd.M, slot, (int)nfb, stamp[1] - stamp[0], stamp[2] - stamp[1], stamp[3] - stamp[2], stamp[4] - stamp[3],
+           sd.M, placed, (int)nfb, stamp[1] - stamp[0], stamp[2] - stamp[1], stamp[3] - stamp[2], stamp[4] - stamp[3],
            stamp[5] - stamp[4], stamp[6] - stamp[5], t7 - stamp[6]);
   }
 #endif
@@ -1102,7 +1163,10 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
 #if (IA_PROBE & 3) == 0
   if constexpr (FUSED) {
     __shared__ double qsh[IA_WG / IA_WAVE][Geo<CH>::DS], wsh[IA_WG / IA_WAVE][Geo<CH>::DS];
-    merge_fused<CH>(g, sd, A, ma, m, s, im, Bp, weights, kf, qsh[threadIdx.x >> 6], wsh[threadIdx.x >> 6]);
+    __shared__ int crsh[IA_WG / IA_WAVE][IA_WAVE];
+    __shared__ float cvsh[IA_WG / IA_WAVE][IA_WAVE];
+    const int wv = threadIdx.x >> 6;
+    merge_fused<CH>(g, sd, A, ma, m, s, im, Bp, weights, kf, qsh[wv], wsh[wv], crsh[wv], cvsh[wv]);
     return;
   }
 #endif
