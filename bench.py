@@ -194,7 +194,7 @@ def main():
     roofline = {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': peak / 1e12, 'unit': 'TFLOP/s',
                 'frac': achieved / peak, 'traffic': traffic,
                 'mfma_issue_frac': achieved * issued / peak,
-                'kernel': ('k3h_dist (3 x v_mfma_f32_32x32x16_f16 on hi/lo-split operands, fused top-2)' if f16 else
+                'kernel': ('k3h_scan (3 x v_mfma_f32_32x32x16_f16 on hi/lo-split operands, fused packed-index top-2)' if f16 else
                            'k3_dist (v_mfma_f32_32x32x2_f32 distance scan + fused top-2)'),
                 'k3_us_per_launch': k3_ms_per_launch * 1e3, 'k3_launches_sampled': st['dist_launches_timed'],
                 'k3_share_of_step': st['dist_ms'] * (st['dist_flops'] / max(st['dist_flops_timed'], 1)) /
