@@ -237,11 +237,15 @@ def shard_tiles(n_rows, world, rank):
     return a.value, b.value
 
 
+TILE_MUL = 2654435761  # IA_TILE_MUL of ia_internal.h
+
+
 def shard_rows(n_rows, world, rank):
     """Sorted DB rows owned by `rank` (tile-strided layout, see shard_tiles)."""
     t0, t1 = shard_tiles(n_rows, world, rank)
     nt = (n_rows + 31) // 32
-    rows = (np.arange(32)[:, None] * nt + np.arange(t0, t1)[None, :]).ravel()
+    perm = np.arange(t0, t1, dtype=np.int64) * (TILE_MUL % nt) % nt  # ia_tile_perm (ia_internal.h)
+    rows = (np.arange(32)[:, None] * nt + perm[None, :]).ravel()
     return np.sort(rows[rows < n_rows])
 
 

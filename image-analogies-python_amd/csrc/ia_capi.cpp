@@ -260,6 +260,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   HIP_TRY(hipSetDevice(c->dev));
 
   LevelGeo g;
+  g.pos2row = nullptr;
   g.ch = a->ch;
   g.D = 55 * a->ch;
   g.KH = kh_for(g.D + 1);
@@ -383,6 +384,8 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   ma.pos_end = g.tile1 * IA_TILE;
   ma.NT = g.n_tiles;
   ma.NA = (int)g.NA;
+  ma.pos2row = nullptr;
+  ma.rr = 0;
   int64_t shard_rows = 0;  // real DB rows in this shard's tiles (strided layout)
   for (int t = g.tile0; t < g.tile1; t++) {
     const int64_t tr = ia_tile_perm(t, g.n_tiles);
@@ -595,6 +598,8 @@ int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, d
   ma.pos_end = x->n_tiles * IA_TILE;
   ma.NT = x->n_tiles;
   ma.NA = (int)x->n;
+  ma.pos2row = nullptr;
+  ma.rr = 0;
   ma.pstat = nullptr;
   ma.eps_c = ia_eps_c(DP);
   ma.eps_a = 0.;

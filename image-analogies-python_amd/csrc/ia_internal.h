@@ -46,6 +46,7 @@ struct LevelGeo {
   int n_tiles;              // ceil(NA / 32) over the whole DB
   int tile0, tile1;         // this rank's shard [tile0, tile1)
   int tiles_per_wg, nwg;    // distance-kernel decomposition of the shard
+  const int *pos2row;       // pruned levels: position -> row table (ia_prune.hip); nullptr: ia_pos_row
 };
 
 struct Imgs {        // the four pyramid images a feature row reads (see FeatDesc parts)
@@ -73,6 +74,9 @@ struct MergeArgs {
                                       // 31 an MFMA value outside the certified error bound
   double eps_c;                       // relative error coefficient of the MFMA value
   double eps_a;                       // absolute (f16 subnormal) error coefficient
+  const int *pos2row;                 // position -> row table (pruned levels) or nullptr
+  int rr;                             // 1: workgroup w's chunk is tiles {w, w + nwg, ...} (pruned
+                                      // scan); 0: the contiguous range [w*tpw, (w+1)*tpw)
 };
 
 // DB positions are tile-strided and tile-scattered: slot j of tile t holds row j*NT + perm(t)
@@ -94,6 +98,14 @@ __host__ __device__ inline int64_t ia_tile_perm(int64_t t, int64_t NT) {
 __host__ __device__ inline int64_t ia_pos_row(int64_t pos, int64_t NT) {
   return (pos & 31) * NT + ia_tile_perm(pos >> 5, NT);
 }
+__host__ __device__ inline int64_t ia_pos_row_t(int64_t pos, int64_t NT, const int *tab) {
+  return tab ? (int64_t)tab[pos] : ia_pos_row(pos, NT);
+}
+
+// certified pruning of the distance scan (ia_prune.hip): projection basis size, smallest DB
+// that prunes
+#define IA_NPC 4
+#define IA_PRUNE_MIN_ROWS 262144
 
 // per-step wavefront description: pixels (r, t - 3r), r in [r0, r0 + M)
 struct StepDesc {

@@ -238,7 +238,7 @@ __global__ void __launch_bounds__(IA_WG) k_db_build(LevelGeo g, Imgs A, const do
   if (pos >= (int64_t)g.tile1 * IA_TILE) return;
   const int64_t ltile = pos / IA_TILE - g.tile0;
   const int j = (int)(pos % IA_TILE);
-  const int64_t row = ia_pos_row(pos, g.n_tiles);
+  const int64_t row = ia_pos_row_t(pos, g.n_tiles, g.pos2row);
   const bool real = row < g.NA;
   int img = 0, pr = 0, pc = 0;
   if (real) {
@@ -542,7 +542,7 @@ __global__ void __launch_bounds__(IA_WG) k_db_build_h(LevelGeo g, Imgs A, const 
   const bool inr = pos < (int64_t)g.tile1 * IA_TILE;
   const int64_t ltile = pos / IA_TILE - g.tile0;
   const int j = (int)(pos % IA_TILE);
-  const int64_t row = ia_pos_row(pos, g.n_tiles);
+  const int64_t row = inr ? ia_pos_row_t(pos, g.n_tiles, g.pos2row) : g.NA;
   const bool real = inr && row < g.NA;
   int img = 0, pr = 0, pc = 0;
   if (real) {
@@ -1074,15 +1074,27 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     while (mask) {
       const int j = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
-      const int64_t p0 = (int64_t)a.pos0 + (int64_t)(jb * IA_WAVE + j) * a.tpw * IA_TILE;
-      const int64_t p1 = min((int64_t)a.pos_end, p0 + (int64_t)a.tpw * IA_TILE);
+      const int wgid = jb * IA_WAVE + j;
       double cd = DBL_MAX;
       int ci = INT_MAX;
-      for (int64_t p = p0 + lane; p < p1; p += IA_WAVE) {
-        const int64_t i = ia_pos_row(p, a.NT);
-        if (i >= a.NA) continue;
-        const double d = exact_dist_level<CH>(a.db64, i, qs);
-        if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
+      if (a.rr) {  // chunk = tiles wgid, wgid + nwg, ... (pruned scan)
+        for (int64_t x = lane;; x += IA_WAVE) {
+          const int64_t t = wgid + (int64_t)a.nwg * (x >> 5);
+          if (t >= a.NT) break;
+          const int64_t i = ia_pos_row_t(t * IA_TILE + (x & 31), a.NT, a.pos2row);
+          if (i >= a.NA) continue;
+          const double d = exact_dist_level<CH>(a.db64, i, qs);
+          if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
+        }
+      } else {
+        const int64_t p0 = (int64_t)a.pos0 + (int64_t)wgid * a.tpw * IA_TILE;
+        const int64_t p1 = min((int64_t)a.pos_end, p0 + (int64_t)a.tpw * IA_TILE);
+        for (int64_t p = p0 + lane; p < p1; p += IA_WAVE) {
+          const int64_t i = ia_pos_row_t(p, a.NT, a.pos2row);
+          if (i >= a.NA) continue;
+          const double d = exact_dist_level<CH>(a.db64, i, qs);
+          if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
+        }
       }
       double du = DBL_MAX;
       int iu = INT_MAX;

@@ -36,3 +36,13 @@ void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
 void ia_launch_k3h(int KS, int qt, const void *db, const void *qf, int n_tiles, int tpw, int qt0, int M, int nwg, int row0,
                    int NT, float4 *rec, float *recT, int variant, hipStream_t st);
 void ia_launch_fill_random_f16(void *p, int64_t n, unsigned seed, hipStream_t st);
+// certified pruned scan: per-level setup (ia_prune.hip)
+void ia_launch_cov(const double *db64, int64_t NA, int64_t stride, int nwg, const double *mu_part, double *part,
+                   double *cov, hipStream_t st);
+void ia_launch_proj_keys(const double *db64, int64_t NA, const double *mu_part, const double *basis, double *proj,
+                         unsigned *keys, int *rows, hipStream_t st);
+size_t ia_sort_temp_bytes(int64_t n);
+int ia_sort_pairs(void *temp, size_t temp_bytes, const unsigned *keys_in, unsigned *keys_out, const int *vals_in,
+                  int *vals_out, int64_t n, hipStream_t st);
+void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int *pos2row, float *boxes,
+                           hipStream_t st);

@@ -1,0 +1,219 @@
+// ia_prune.hip — per-level setup of the certified pruned distance scan.
+//
+// The exact NN of a query q can only be a DB row a with |a - q|^2 <= U, U = the exact fp64
+// distance of q's best coherence candidate (itself a DB row).  For an orthonormal basis u_1..u_k
+// of R^D, sum_i (u_i . (a - q))^2 <= |a - q|^2, so a row whose projection box lies further than
+// sqrt(U) from q's projection can be skipped without changing the result.  Per level:
+//   K5a/K5b  covariance of the centred fp64 DB rows (sampled, deterministic two-pass reduction);
+//            the host takes its top IA_NPC eigenvectors (Jacobi, ia_capi.cpp) as the basis
+//   K5c      projections of every row onto the basis + a Morton key of the quantised
+//            projections; hipCUB radix sort of (key, row) orders the DB so that 32-row tiles
+//            are compact in projection space
+//   K5d      position -> row table (sort neighbours alternate between the two lane halves of
+//            a tile, i.e. between K3 subsets) and per-tile projection boxes (fp32, rounded
+//            outward)
+// Only the 1-channel split-f16 path prunes (the bench configuration); everything else scans.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <float.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "ia_internal.h"
+#include "ia_launch.h"
+
+#define PR_WG 256
+#define PR_COV_ROWS 16  // rows staged in LDS per covariance pass
+
+__device__ __forceinline__ int prune_part1(int f) { return f < 9 ? 0 : f < 34 ? 1 : f < 43 ? 2 : 3; }
+
+// K5a: partial sums of x'_f x'_g (f <= g) over the sampled rows r = (wg + nwg*k) * stride
+__global__ void __launch_bounds__(PR_WG) k_cov_partial(const double *__restrict__ db64, int64_t NA, int64_t stride,
+                                                       const double *__restrict__ mu_part, double *__restrict__ part) {
+  constexpr int D = 55, DS = 56, NPAIR = D * (D + 1) / 2, PPT = (NPAIR + PR_WG - 1) / PR_WG;
+  __shared__ double xs[PR_COV_ROWS][DS];
+  int pf[PPT], pg[PPT];
+  double acc[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; k++) {
+    int p = threadIdx.x + PR_WG * k, f = 0;
+    if (p >= NPAIR) p = NPAIR - 1;
+    while (p >= D - f) {  // pair p -> (f, g), f <= g, row-major upper triangle
+      p -= D - f;
+      f++;
+    }
+    pf[k] = f;
+    pg[k] = f + p;
+    acc[k] = 0.;
+  }
+  const int64_t nsamp = (NA + stride - 1) / stride;
+  for (int64_t base = (int64_t)blockIdx.x * PR_COV_ROWS; base < nsamp; base += (int64_t)gridDim.x * PR_COV_ROWS) {
+    for (int i = threadIdx.x; i < PR_COV_ROWS * DS; i += PR_WG) {
+      const int rr = i / DS, f = i % DS;
+      const int64_t s = base + rr;
+      double v = 0.;
+      if (s < nsamp && f < D) v = db64[s * stride * DS + f] - mu_part[prune_part1(f)];
+      xs[rr][f] = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < PPT; k++) {
+#pragma unroll 4
+      for (int rr = 0; rr < PR_COV_ROWS; rr++) acc[k] += xs[rr][pf[k]] * xs[rr][pg[k]];
+    }
+    __syncthreads();
+  }
+#pragma unroll
+  for (int k = 0; k < PPT; k++) {
+    const int p = threadIdx.x + PR_WG * k;
+    if (p < NPAIR) part[(int64_t)blockIdx.x * NPAIR + p] = acc[k];
+  }
+}
+
+// K5b: fixed-order sum of the partials
+__global__ void __launch_bounds__(PR_WG) k_cov_reduce(const double *__restrict__ part, int nwg, double *__restrict__ cov) {
+  constexpr int NPAIR = 55 * 56 / 2;
+  for (int p = threadIdx.x; p < NPAIR; p += PR_WG) {
+    double s = 0.;
+    for (int w = 0; w < nwg; w++) s += part[(int64_t)w * NPAIR + p];
+    cov[p] = s;
+  }
+}
+
+// Morton key of the projections quantised to 8 bits each over [-4 sigma_i, 4 sigma_i]
+__device__ __forceinline__ unsigned prune_key(const double (&p)[IA_NPC], const double *__restrict__ scale) {
+  unsigned key = 0;
+  unsigned qv[IA_NPC];
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) {
+    const double t = (p[i] * scale[i] + 1.0) * 128.0;
+    qv[i] = t <= 0. ? 0u : t >= 255. ? 255u : (unsigned)t;
+  }
+#pragma unroll
+  for (int b = 7; b >= 0; b--) {
+#pragma unroll
+    for (int i = 0; i < IA_NPC; i++) key = (key << 1) | ((qv[i] >> b) & 1u);
+  }
+  return key;
+}
+
+// K5c: projections, keys and the identity row list of every DB row
+__global__ void __launch_bounds__(PR_WG) k_proj_keys(const double *__restrict__ db64, int64_t NA,
+                                                     const double *__restrict__ mu_part, const double *__restrict__ basis,
+                                                     double *__restrict__ proj, unsigned *__restrict__ keys,
+                                                     int *__restrict__ rows) {
+  constexpr int D = 55, DS = 56;
+  __shared__ double ub[IA_NPC * D + IA_NPC];
+  for (int i = threadIdx.x; i < IA_NPC * D + IA_NPC; i += PR_WG) ub[i] = basis[i];
+  __syncthreads();
+  const int64_t row = (int64_t)blockIdx.x * PR_WG + threadIdx.x;
+  if (row >= NA) return;
+  const double2 *a2 = reinterpret_cast<const double2 *>(db64 + row * DS);
+  double p[IA_NPC];
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) p[i] = 0.;
+#pragma unroll
+  for (int k = 0; k < DS / 2; k++) {
+    const double2 v = a2[k];
+    const int f0 = 2 * k, f1 = 2 * k + 1;
+    const double x0 = v.x - mu_part[prune_part1(f0)];
+#pragma unroll
+    for (int i = 0; i < IA_NPC; i++) p[i] += ub[i * D + f0] * x0;
+    if (f1 < D) {
+      const double x1 = v.y - mu_part[prune_part1(f1)];
+#pragma unroll
+      for (int i = 0; i < IA_NPC; i++) p[i] += ub[i * D + f1] * x1;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) proj[row * IA_NPC + i] = p[i];
+  keys[row] = prune_key(p, ub + IA_NPC * D);
+  rows[row] = (int)row;
+}
+
+// K5d: position -> row table.  Sorted index k of tile t sits in slot ((k >> 1) & 3) +
+// 8 * (k >> 3) + 4 * (k & 1): consecutive sorted rows alternate between the lane halves of the
+// MFMA output (half = (slot >> 2) & 1), i.e. between K3 subsets.  Positions past NA map to
+// rows >= NA (padding: never a candidate).
+__global__ void __launch_bounds__(PR_WG) k_make_table(const int *__restrict__ sorted_rows, int64_t NA, int n_tiles,
+                                                      int *__restrict__ pos2row) {
+  const int64_t p = (int64_t)blockIdx.x * PR_WG + threadIdx.x;
+  if (p >= (int64_t)n_tiles * IA_TILE) return;
+  const int j = (int)(p & 31);
+  const int k = (((j & 3) << 1) | ((j >> 2) & 1) | ((j >> 3) << 3));
+  const int64_t s = (p & ~(int64_t)31) + k;
+  pos2row[p] = s < NA ? sorted_rows[s] : (int)s;
+}
+
+__device__ __forceinline__ float round_down_f(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = nextafterf(f, -INFINITY);
+  return f;
+}
+__device__ __forceinline__ float round_up_f(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = nextafterf(f, INFINITY);
+  return f;
+}
+
+// K5d': per-tile boxes of the projections (lo[IA_NPC], hi[IA_NPC]) over the tile's real rows
+__global__ void __launch_bounds__(PR_WG) k_tile_boxes(const int *__restrict__ pos2row, const double *__restrict__ proj,
+                                                      int64_t NA, int n_tiles, float *__restrict__ boxes) {
+  const int t = blockIdx.x * PR_WG + threadIdx.x;
+  if (t >= n_tiles) return;
+  double lo[IA_NPC], hi[IA_NPC];
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) {
+    lo[i] = DBL_MAX;
+    hi[i] = -DBL_MAX;
+  }
+  for (int j = 0; j < IA_TILE; j++) {
+    const int row = pos2row[(int64_t)t * IA_TILE + j];
+    if (row >= NA) continue;
+#pragma unroll
+    for (int i = 0; i < IA_NPC; i++) {
+      const double v = proj[(int64_t)row * IA_NPC + i];
+      lo[i] = fmin(lo[i], v);
+      hi[i] = fmax(hi[i], v);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) {
+    const bool empty = lo[i] > hi[i];
+    boxes[(int64_t)t * 2 * IA_NPC + i] = empty ? INFINITY : round_down_f(lo[i]);
+    boxes[(int64_t)t * 2 * IA_NPC + IA_NPC + i] = empty ? -INFINITY : round_up_f(hi[i]);
+  }
+}
+
+// ---- host launchers ---------------------------------------------------------------------------
+static inline unsigned pr_cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+
+void ia_launch_cov(const double *db64, int64_t NA, int64_t stride, int nwg, const double *mu_part, double *part,
+                   double *cov, hipStream_t st) {
+  hipLaunchKernelGGL(k_cov_partial, dim3(nwg), dim3(PR_WG), 0, st, db64, NA, stride, mu_part, part);
+  hipLaunchKernelGGL(k_cov_reduce, dim3(1), dim3(PR_WG), 0, st, part, nwg, cov);
+}
+
+void ia_launch_proj_keys(const double *db64, int64_t NA, const double *mu_part, const double *basis, double *proj,
+                         unsigned *keys, int *rows, hipStream_t st) {
+  hipLaunchKernelGGL(k_proj_keys, dim3(pr_cdiv(NA, PR_WG)), dim3(PR_WG), 0, st, db64, NA, mu_part, basis, proj, keys, rows);
+}
+
+size_t ia_sort_temp_bytes(int64_t n) {
+  size_t bytes = 0;
+  hipcub::DeviceRadixSort::SortPairs(nullptr, bytes, (const unsigned *)nullptr, (unsigned *)nullptr, (const int *)nullptr,
+                                     (int *)nullptr, (int)n, 0, 32, (hipStream_t)0);
+  return bytes;
+}
+
+int ia_sort_pairs(void *temp, size_t temp_bytes, const unsigned *keys_in, unsigned *keys_out, const int *vals_in,
+                  int *vals_out, int64_t n, hipStream_t st) {
+  return (int)hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (int)n, 0, 32, st);
+}
+
+void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int *pos2row, float *boxes,
+                           hipStream_t st) {
+  hipLaunchKernelGGL(k_make_table, dim3(pr_cdiv((int64_t)n_tiles * IA_TILE, PR_WG)), dim3(PR_WG), 0, st, sorted_rows, NA,
+                     n_tiles, pos2row);
+  hipLaunchKernelGGL(k_tile_boxes, dim3(pr_cdiv(n_tiles, PR_WG)), dim3(PR_WG), 0, st, pos2row, proj, NA, n_tiles, boxes);
+}
