@@ -112,6 +112,8 @@ def main():
                     help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
     ap.add_argument('--k3-variant', type=int, default=1, choices=[0, 1],
                     help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select')
+    ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
+                    help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
     ap.add_argument('--time-stride', type=int, default=4, help='sample K3 timing every S-th wavefront step')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -142,6 +144,7 @@ def main():
     ctx = _native.Context(local)
     ctx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
     ctx.set_option('k3_variant', args.k3_variant)
+    ctx.set_option('prune', args.prune)
     if args.mode == 'shard' and world > 1:
         uid = [_native.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -213,7 +216,8 @@ def main():
                                                  % ('split-f16 (hi/lo x3)' if f16 else 'fp32')},
            'roofline': roofline,
            'stats': {k: st[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
-                                        'synth_ms', 'bound_violations', 'f16_levels')}}
+                                        'synth_ms', 'bound_violations', 'f16_levels', 'pruned_levels',
+                                        'dist_pairs', 'dist_pairs_full')}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(job, args.cpu_seconds)
     if rank == 0:

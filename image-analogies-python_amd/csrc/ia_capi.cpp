@@ -76,6 +76,10 @@ struct ia_ctx {
   // uploads (IA_MEM_HOST) and per-level scratch
   DevBuf A, Ac, Ap, Apc, B, Bc, Bpc, Bp, S, IM, W;
   DevBuf db, db64, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, pstat, absmax;
+  // certified pruned scan (option "prune"): per-level basis, sorted DB table, tile boxes
+  DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs;
+  std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
+  int prune = 1;
   int matcher = IA_MATCH_F16X3;  // option "matcher"
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   // per-step K3 timing (optional)
@@ -93,6 +97,109 @@ struct ia_index {
   int d = 0, KH = 0, n_tiles = 0, tpw = 0, nwg = 0;
   DevBuf pts, db, mu, Rbits, q, q64, qn2, qf, rec, recT, idx, dist, counters;
 };
+
+namespace {
+
+// cyclic Jacobi eigen-decomposition of a symmetric n x n matrix (row-major, overwritten);
+// V's column k is the eigenvector of eigenvalue w[k]
+void jacobi_eig(int n, std::vector<double> &A, std::vector<double> &V, std::vector<double> &w) {
+  V.assign((size_t)n * n, 0.);
+  for (int i = 0; i < n; i++) V[(size_t)i * n + i] = 1.;
+  auto a = [&](int i, int j) -> double & { return A[(size_t)i * n + j]; };
+  for (int sweep = 0; sweep < 100; sweep++) {
+    double off = 0., dia = 0.;
+    for (int p = 0; p < n; p++) {
+      dia += a(p, p) * a(p, p);
+      for (int q = p + 1; q < n; q++) off += a(p, q) * a(p, q);
+    }
+    if (off <= 1e-32 * dia || off == 0.) break;
+    for (int p = 0; p < n - 1; p++) {
+      for (int q = p + 1; q < n; q++) {
+        const double apq = a(p, q);
+        if (apq == 0.) continue;
+        const double theta = (a(q, q) - a(p, p)) / (2. * apq);
+        const double t = (theta >= 0. ? 1. : -1.) / (std::fabs(theta) + std::sqrt(theta * theta + 1.));
+        const double cs = 1. / std::sqrt(t * t + 1.), sn = t * cs;
+        for (int k = 0; k < n; k++) {  // columns p, q
+          const double akp = a(k, p), akq = a(k, q);
+          a(k, p) = cs * akp - sn * akq;
+          a(k, q) = sn * akp + cs * akq;
+        }
+        for (int k = 0; k < n; k++) {  // rows p, q
+          const double apk = a(p, k), aqk = a(q, k);
+          a(p, k) = cs * apk - sn * aqk;
+          a(q, k) = sn * apk + cs * aqk;
+        }
+        for (int k = 0; k < n; k++) {
+          const double vkp = V[(size_t)k * n + p], vkq = V[(size_t)k * n + q];
+          V[(size_t)k * n + p] = cs * vkp - sn * vkq;
+          V[(size_t)k * n + q] = sn * vkp + cs * vkq;
+        }
+      }
+    }
+  }
+  w.resize(n);
+  for (int i = 0; i < n; i++) w[i] = a(i, i);
+}
+
+// Per-level setup of the certified pruned scan (ia_prune.hip): covariance of
+// the centred fp64 DB (sampled) -> top IA_NPC eigenvectors (host Jacobi) -> projections and
+// Morton keys of every row -> radix sort -> position -> row table + per-tile projection boxes.
+// Sets g.pos2row; *ufac = the U' factor of ia_prune.h.  One host sync (the covariance).
+int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, double *ufac) {
+  constexpr int D = 55, NPAIR = D * (D + 1) / 2, NWG_COV = 256;
+  const int64_t NA = g.NA, NT = g.n_tiles;
+  const int64_t stride = std::max<int64_t>(1, NA / 65536), nsamp = (NA + stride - 1) / stride;
+  int rc;
+  if ((rc = c->pr_part.ensure((size_t)NWG_COV * NPAIR * 8)) || (rc = c->pr_cov.ensure((size_t)NPAIR * 8)) ||
+      (rc = c->pr_basis.ensure((size_t)(IA_NPC * D + IA_NPC) * 8)) || (rc = c->pr_proj.ensure((size_t)NA * IA_NPC * 8)) ||
+      (rc = c->pr_keys.ensure((size_t)NA * 8)) || (rc = c->pr_rows.ensure((size_t)NA * 8)) ||
+      (rc = c->pos2row.ensure((size_t)NT * IA_TILE * 4)) || (rc = c->boxes.ensure((size_t)NT * 2 * IA_NPC * 4)))
+    return rc;
+  const size_t sort_bytes = ia_sort_temp_bytes(NA);
+  if ((rc = c->pr_tmp.ensure(sort_bytes))) return rc;
+  ia_launch_cov(c->db64.as<double>(), NA, stride, NWG_COV, mu, c->pr_part.as<double>(), c->pr_cov.as<double>(), c->st);
+  std::vector<double> cov(NPAIR);
+  HIP_TRY(hipMemcpyAsync(cov.data(), c->pr_cov.p, NPAIR * 8, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(hipStreamSynchronize(c->st));
+  std::vector<double> A((size_t)D * D), V, w;
+  for (int f = 0, p = 0; f < D; f++)
+    for (int h = f; h < D; h++, p++) A[(size_t)f * D + h] = A[(size_t)h * D + f] = cov[p] / (double)nsamp;
+  jacobi_eig(D, A, V, w);
+  std::vector<int> idx(D);
+  for (int i = 0; i < D; i++) idx[i] = i;
+  std::stable_sort(idx.begin(), idx.end(), [&](int x, int y) { return w[x] > w[y]; });
+  c->basis_h.assign((size_t)IA_NPC * D + IA_NPC, 0.);
+  for (int i = 0; i < IA_NPC; i++) {
+    double nrm = 0.;
+    for (int f = 0; f < D; f++) nrm += V[(size_t)f * D + idx[i]] * V[(size_t)f * D + idx[i]];
+    nrm = std::sqrt(nrm);
+    for (int f = 0; f < D; f++) c->basis_h[(size_t)i * D + f] = V[(size_t)f * D + idx[i]] / nrm;
+    const double lam = w[idx[i]];
+    c->basis_h[(size_t)IA_NPC * D + i] = lam > 0. ? 1. / (4. * std::sqrt(lam)) : 0.;
+  }
+  // deviation of the basis from orthonormality: lambda_max(U^T U) <= 1 + sum |G - I|
+  long double delta = 0.L;
+  for (int i = 0; i < IA_NPC; i++)
+    for (int j = 0; j < IA_NPC; j++) {
+      long double gij = 0.L;
+      for (int f = 0; f < D; f++) gij += (long double)c->basis_h[(size_t)i * D + f] * c->basis_h[(size_t)j * D + f];
+      delta += std::fabs((double)(gij - (i == j ? 1.L : 0.L)));
+    }
+  *ufac = (1.0 + 2.0 * (double)delta + 1e-15) * (1.0 + std::ldexp(1.0, -17)) * (1.0 + std::ldexp(1.0, -19));
+  HIP_TRY(hipMemcpyAsync(c->pr_basis.p, c->basis_h.data(), c->basis_h.size() * 8, hipMemcpyHostToDevice, c->st));
+  unsigned *keys = c->pr_keys.as<unsigned>();
+  int *rows = c->pr_rows.as<int>();
+  ia_launch_proj_keys(c->db64.as<double>(), NA, mu, c->pr_basis.as<double>(), c->pr_proj.as<double>(), keys, rows, c->st);
+  if (ia_sort_pairs(c->pr_tmp.p, sort_bytes, keys, keys + NA, rows, rows + NA, NA, c->st) != 0)
+    return fail(IA_EHIP, "prepare_prune: radix sort failed");
+  ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, c->pos2row.as<int>(), c->boxes.as<float>(), c->st);
+  HIP_TRY(hipGetLastError());
+  g.pos2row = c->pos2row.as<int>();
+  return IA_OK;
+}
+
+}  // namespace
 
 extern "C" {
 
@@ -127,7 +234,9 @@ void ia_destroy(ia_ctx *c) {
   hipSetDevice(c->dev);
   hipStreamSynchronize(c->st);
   for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->B, &c->Bc, &c->Bpc, &c->Bp, &c->S, &c->IM, &c->W, &c->db, &c->db64,
-                    &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->pstat, &c->absmax})
+                    &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->pstat, &c->absmax,
+                    &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
+                    &c->boxes, &c->qinfo, &c->pairs})
     b->release();
   for (hipEvent_t e : c->evs) hipEventDestroy(e);
   hipEventDestroy(c->lv0);
@@ -147,6 +256,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "k3_variant")) {
     if (value < 0 || value > 3) return fail(IA_EINVAL, "ia_set_option: k3_variant must be 0..3 (2, 3: diagnostic builds)");
     c->k3_variant = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "prune")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: prune must be 0 or 1");
+    c->prune = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "matcher")) {
@@ -339,12 +453,16 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     g.tiles_per_wg = std::max(IA_WGH / IA_WAVE, (ns + IA_NWG_H - 1) / IA_NWG_H);
     g.nwg = (ns + g.tiles_per_wg - 1) / g.tiles_per_wg;
   }
-  const size_t db_row_bytes = use_h ? (size_t)16 * g.KS * 4 : (size_t)DP * 4;  // hi+lo f16 / fp32 per column
-
-  // per-level scratch
+  // certified pruned scan (1 channel, single rank, large DBs; every query of a step sorted in
+  // one workgroup's LDS)
   int64_t T, Mmax;
   ia_wavefront_shape(g.bh, g.bw, &T, &Mmax);
   const int64_t Mpad_max = (Mmax + IA_TILE - 1) / IA_TILE * IA_TILE;
+  const bool prune = c->prune && use_h && g.ch == 1 && !sharded && g.NA >= IA_PRUNE_MIN_ROWS && Mpad_max <= 4096;
+  if (prune) g.nwg = std::min(IA_NWG_H, g.n_tiles);  // round-robin chunks: WG w owns tiles w + nwg*k
+  const size_t db_row_bytes = use_h ? (size_t)16 * g.KS * 4 : (size_t)DP * 4;  // hi+lo f16 / fp32 per column
+
+  // per-level scratch
   if ((rc = c->db.ensure((size_t)std::max(ns, 1) * IA_TILE * db_row_bytes)) || (rc = c->mu.ensure(4 * g.ch * 8)) ||
       (rc = c->db64.ensure((size_t)g.NA * ia_db64_stride(g.ch) * 8)) ||
       (rc = c->Rbits.ensure(4)) || (rc = c->q64.ensure((size_t)Mpad_max * g.D * 8)) ||
@@ -352,8 +470,10 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       (rc = c->rec.ensure((size_t)Mmax * std::max(g.nwg, 1) * 16)) ||
       (rc = c->recT.ensure((size_t)Mmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mmax * 16)) ||
       (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(4 * 8)) ||
-      (rc = c->pstat.ensure((size_t)NB * 4)))
+      (rc = c->pstat.ensure((size_t)NB * 4)) || (rc = c->pairs.ensure(2 * 8)) ||
+      (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 : 16)))
     return rc;
+  HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 2 * 8, c->st));
   HIP_TRY(hipMemsetAsync(c->Rbits.p, 0, 4, c->st));
   HIP_TRY(hipMemsetAsync(c->counters.p, 0, 4 * 8, c->st));
   HIP_TRY(hipMemsetAsync(c->pstat.p, 0, (size_t)NB * 4, c->st));
@@ -364,11 +484,13 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
 
   HIP_TRY(hipEventRecord(c->lv0, c->st));
   ia_launch_means(g.ch, Aim, g.n_ap, c->mu.as<double>(), c->st);
+  ia_launch_db64_build(g, Aim, c->db64.as<double>(), c->st);  // every row: coherence reads any row
+  double ufac = 0.;
+  if (prune && (rc = prepare_prune(c, g, c->mu.as<double>(), &ufac))) return rc;  // sets g.pos2row
   if (ns > 0) {
     if (use_h) ia_launch_db_build_h(g, Aim, c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
     else ia_launch_db_build(g, Aim, c->mu.as<double>(), c->db.as<float4>(), c->Rbits.as<unsigned>(), c->st);
   }
-  ia_launch_db64_build(g, Aim, c->db64.as<double>(), c->st);  // every row: coherence reads any row
   HIP_TRY(hipEventRecord(c->lv1, c->st));
 
   MergeArgs ma;
@@ -384,15 +506,18 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   ma.pos_end = g.tile1 * IA_TILE;
   ma.NT = g.n_tiles;
   ma.NA = (int)g.NA;
-  ma.pos2row = nullptr;
-  ma.rr = 0;
+  ma.pos2row = g.pos2row;
+  ma.rr = prune ? 1 : 0;
+  ma.qinfo = prune ? c->qinfo.as<float4>() : nullptr;
+  ma.boxes = prune ? c->boxes.as<float4>() : nullptr;
+  ma.ufac = ufac;
   int64_t shard_rows = 0;  // real DB rows in this shard's tiles (strided layout)
   for (int t = g.tile0; t < g.tile1; t++) {
     const int64_t tr = ia_tile_perm(t, g.n_tiles);
     shard_rows += std::min<int64_t>(IA_TILE, (g.NA - tr + g.n_tiles - 1) / g.n_tiles);
   }
   ma.pstat = c->pstat.as<unsigned>();
-  ma.eps_c = use_h ? ia_eps_c_h(g.KS, c->k3_variant == 1) : ia_eps_c(DP);
+  ma.eps_c = use_h ? ia_eps_c_h(g.KS, prune || c->k3_variant == 1) : ia_eps_c(DP);
   ma.eps_a = use_h ? ia_eps_a_h() : 0.;
 
   const int qtmax = use_h ? ia_k3h_qtmax(g.KS) : ia_k3_qtmax(g.KH);
@@ -404,14 +529,17 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     for (size_t i = old; i < c->evs.size(); i++) hipEventCreate(&c->evs[i]);
   }
   int64_t dist_launches = 0, launches_timed = 0, n_rec = 0;
-  double dist_flops = 0., flops_timed = 0.;
+  double dist_flops = 0., flops_timed = 0., pairs_full = 0.;
   for (int64_t t = 0; t < T; t++) {
     StepDesc sd;
     sd.t = (int)t;
     ia_wavefront_step(g.bh, g.bw, t, &sd.r0, &sd.M);
     if (sd.M <= 0) continue;  // levels narrower than 3 columns have empty steps
     sd.Mpad = (sd.M + IA_TILE - 1) / IA_TILE * IA_TILE;
-    if (use_h)
+    if (prune)
+      ia_launch_gather_p(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
+                         c->db64.as<double>(), dS, dIM, c->pr_basis.as<double>(), ufac, c->qinfo.as<float4>(), c->st);
+    else if (use_h)
       ia_launch_gather_h(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p, c->st);
     else
       ia_launch_gather(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(), c->st);
@@ -422,15 +550,20 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       int qt0 = 0;
       for (int b = 0; b < nqb; b++) {
         const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
-        if (use_h)
+        if (prune)
+          ia_launch_k3p(qt, c->db.p, c->qf.p, c->qinfo.as<float4>(), c->boxes.as<float4>(), g.pos2row, g.n_tiles, qt0, sd.M,
+                        sd.Mpad, g.nwg, c->rec.as<float4>(), c->recT.as<float>(),
+                        c->pairs.as<unsigned long long>() + (timed ? 1 : 0), c->st);
+        else if (use_h)
           ia_launch_k3h(g.KS, qt, c->db.p, c->qf.p, ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0, ma.NT, c->rec.as<float4>(),
                         c->recT.as<float>(), c->k3_variant, c->st);
         else
           ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0,
                        ma.NT, c->rec.as<float4>(), c->recT.as<float>(), c->st);
         const int mq = std::min(sd.M, (qt0 + qt) * IA_TILE) - qt0 * IA_TILE;
-        const double fl = 2.0 * g.D * (double)shard_rows * std::max(mq, 0);
+        const double fl = prune ? 0. : 2.0 * g.D * (double)shard_rows * std::max(mq, 0);  // pruned: pair counters
         dist_flops += fl;
+        pairs_full += (double)ns * qt;
         dist_launches++;
         if (timed) {
           flops_timed += fl;
@@ -460,8 +593,17 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   }
   HIP_TRY(hipStreamSynchronize(c->st));
   if (stats) {
-    unsigned long long ctr[4];
+    unsigned long long ctr[4], prs[2];
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
+    HIP_TRY(hipMemcpy(prs, c->pairs.p, sizeof(prs), hipMemcpyDeviceToHost));
+    const double pair_flops = 2.0 * g.D * IA_TILE * IA_TILE;  // one (DB tile, query tile) pair
+    if (prune) {
+      dist_flops = pair_flops * (double)(prs[0] + prs[1]);
+      flops_timed = pair_flops * (double)prs[1];
+    }
+    stats->pruned_levels += prune ? 1 : 0;
+    stats->dist_pairs += prune ? (double)(prs[0] + prs[1]) : pairs_full;
+    stats->dist_pairs_full += pairs_full;
     float ms_db = 0.f, ms_syn = 0.f;
     hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
     hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);
@@ -600,6 +742,9 @@ int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, d
   ma.NA = (int)x->n;
   ma.pos2row = nullptr;
   ma.rr = 0;
+  ma.qinfo = nullptr;
+  ma.boxes = nullptr;
+  ma.ufac = 0.;
   ma.pstat = nullptr;
   ma.eps_c = ia_eps_c(DP);
   ma.eps_a = 0.;

@@ -77,6 +77,9 @@ struct MergeArgs {
   const int *pos2row;                 // position -> row table (pruned levels) or nullptr
   int rr;                             // 1: workgroup w's chunk is tiles {w, w + nwg, ...} (pruned
                                       // scan); 0: the contiguous range [w*tpw, (w+1)*tpw)
+  const float4 *qinfo;                // pruned levels: the step's query projection intervals (K2p)
+  const float4 *boxes;                // pruned levels: per-tile projection boxes (ia_prune.hip)
+  double ufac;                        // pruned levels: bound factor of ia_prune.h
 };
 
 // DB positions are tile-strided and tile-scattered: slot j of tile t holds row j*NT + perm(t)

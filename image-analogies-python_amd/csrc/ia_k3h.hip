@@ -11,6 +11,7 @@
 
 #include "ia_internal.h"
 #include "ia_top2.h"
+#include "ia_prune.h"
 
 // K3h: grid = nwg workgroups of NW waves (one workgroup per CU); WG w owns DB tiles
 // [w*tpw, (w+1)*tpw), wave v takes tiles w*tpw + v, +NW, ...; the step's QT query tiles sit in
@@ -193,6 +194,281 @@ k3h_scan(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, int n_tiles
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// K3p: the certified pruned scan (1 channel).  The level's DB is Morton-sorted
+// in the projection space of its top IA_NPC principal axes (ia_prune.hip: position -> row table
+// pos2row, per-tile projection boxes); K2p wrote each query's projection interval, bound U' and
+// key (ia_prune.h).  Per workgroup:
+//   1. rank-sort the step's queries by key in LDS (deterministic: ties by query index) and
+//      gather this launch's QT query tiles in sorted order, so a query tile is compact in
+//      projection space too; per query tile a bounding box of its intervals and max U'
+//   2. DB tiles round-robin: WG w, wave v takes tiles w + nwg*(v + NW*k) (the merge rescans the
+//      same chunk, MergeArgs::rr); per tile a need mask over the query tiles: a coarse
+//      tile-box test (lanes = query tiles), then for the survivors the per-query test
+//      LB(q, tile) <= U'_q (lanes = queries, ballot).  Tiles nobody needs are never loaded; the
+//      next needed tile is prefetched while the current one is contracted
+//   3. only the needed (DB tile, query tile) pairs run the 12-MFMA chain (two chains at once
+//      when both tiles of a query-tile pair are needed) with the packed-index epilogue
+//   4. per-query records as K3h, written to the queries' original slots with DB rows taken
+//      from pos2row; the WG adds its computed pair count to *pairs (flop accounting)
+// Skipped rows are strictly farther than the query's coherence candidate (ia_prune.h), so
+// they can neither be nor tie the exact NN; K4's certification over the computed rows stands.
+// ------------------------------------------------------------------------------------------
+template <int KS>
+__device__ __forceinline__ f32x16 k3p_chain(const h16x8 (&a)[2 * KS], const h16x8 *qb) {
+  f32x16 c = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; s++) {
+    const h16x8 xh = qb[(2 * s) * IA_WAVE], xl = qb[(2 * s + 1) * IA_WAVE];
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], xh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], xl, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], xh, c, 0, 0, 0);
+  }
+  return c;
+}
+template <int KS>
+__device__ __forceinline__ void k3p_chain2(const h16x8 (&a)[2 * KS], const h16x8 *qb0, const h16x8 *qb1, f32x16 &c0,
+                                           f32x16 &c1) {
+  constexpr f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  c0 = zero;
+  c1 = zero;
+#pragma unroll
+  for (int s = 0; s < KS; s++) {
+    const h16x8 x0h = qb0[(2 * s) * IA_WAVE], x0l = qb0[(2 * s + 1) * IA_WAVE];
+    const h16x8 x1h = qb1[(2 * s) * IA_WAVE], x1l = qb1[(2 * s + 1) * IA_WAVE];
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x0h, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x1h, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0l, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1l, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0h, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1h, c1, 0, 0, 0);
+  }
+}
+// packed epilogue of one accumulator into one query's (b1, b2, tile)
+__device__ __forceinline__ void k3p_epi1(const f32x16 &e, int t, float &b1, float &b2, int &i1) {
+  const float o = b1;
+#pragma unroll
+  for (int r = 0; r < 16; r++) {
+    const float p = k3h_pack(e[r], r);
+    b2 = k3h_med3(b1, b2, p);
+    b1 = k3h_min(b1, p);
+  }
+  i1 = b1 != o ? t : i1;
+}
+// query-tile pairs QP.. of one DB tile t; m2 = the pair's two need bits (wave-uniform).  A pair
+// with one needed tile runs one chain on it; its query state is selected with v_cndmask (never
+// a dynamically indexed register array, which would live in scratch)
+template <int KS, int QT, int QP>
+__device__ __forceinline__ void k3p_pairs(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, int t, float (&b1)[QT],
+                                          float (&b2)[QT], int (&i1)[QT]) {
+  if constexpr (2 * QP < QT) {
+    constexpr int NP = 2 * KS, q0 = 2 * QP, q1 = 2 * QP + 1;
+    const unsigned m2 = (msk >> q0) & 3u;
+    const h16x8 *qb0 = lq + q0 * NP * IA_WAVE;
+    if constexpr (q1 < QT) {
+      if (m2 == 3u) {
+        f32x16 c0, c1;
+        k3p_chain2<KS>(a, qb0, qb0 + NP * IA_WAVE, c0, c1);
+        k3h_epi2<QT, true>(c0, c1, q0, true, 0, t, b1, b2, i1);
+      } else if (m2 != 0u) {
+        const bool sel = m2 == 2u;
+        const f32x16 c = k3p_chain<KS>(a, sel ? qb0 + NP * IA_WAVE : qb0);
+        float x1 = sel ? b1[q1] : b1[q0], x2 = sel ? b2[q1] : b2[q0];
+        int xi = sel ? i1[q1] : i1[q0];
+        k3p_epi1(c, t, x1, x2, xi);
+        b1[q0] = sel ? b1[q0] : x1;
+        b2[q0] = sel ? b2[q0] : x2;
+        i1[q0] = sel ? i1[q0] : xi;
+        b1[q1] = sel ? x1 : b1[q1];
+        b2[q1] = sel ? x2 : b2[q1];
+        i1[q1] = sel ? xi : i1[q1];
+      }
+    } else {
+      if (m2 == 1u) {
+        const f32x16 c = k3p_chain<KS>(a, qb0);
+        k3p_epi1(c, t, b1[q0], b2[q0], i1[q0]);
+      }
+    }
+    k3p_pairs<KS, QT, QP + 1>(a, lq, msk, t, b1, b2, i1);
+  }
+}
+
+template <int KS, int QT, int NW>
+__global__ void __launch_bounds__(NW * IA_WAVE, 1)
+k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
+          const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
+          float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs) {
+  constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
+  static_assert(QT <= 32, "need masks are 32-bit");
+  extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
+  float4 *qlo = reinterpret_cast<float4 *>(ldsh + QT * NP * IA_WAVE);  // [NQ]
+  float4 *qhi = qlo + NQ;                                               // [NQ]
+  float *qU = reinterpret_cast<float *>(qhi + NQ);                     // [NQ]
+  float4 *tlo = reinterpret_cast<float4 *>(qU + NQ);                   // [QT] query-tile boxes
+  float4 *thi = tlo + QT;                                               // [QT]
+  float *tU = reinterpret_cast<float *>(thi + QT);                     // [QT] max U' of the tile
+  unsigned *skey = reinterpret_cast<unsigned *>(tU + ((QT + 3) & ~3));  // [Mpad]
+  int *order = reinterpret_cast<int *>(skey + Mpad);                    // [Mpad] sorted -> query
+  __shared__ unsigned wpairs[NW];
+  const int lane = threadIdx.x & 63, half = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wg = blockIdx.x, tstep = nwg * NW;
+  int t = wg + nwg * wave;
+
+  h16x8 a[NP], an[NP];
+  {  // speculative first tile (usually needed), overlapping the query setup
+    const h16x8 *src = db + (int64_t)min(t, NT - 1) * NP * IA_WAVE + lane;
+#pragma unroll
+    for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+  }
+  // 1. rank sort of the step's queries by key (index breaks ties)
+  for (int i = threadIdx.x; i < Mpad; i += WGT) skey[i] = __float_as_uint(qinfo[3 * i + 2].y);
+  __syncthreads();
+  for (int i = threadIdx.x; i < Mpad; i += WGT) {
+    const unsigned k = skey[i];
+    int rank = 0;
+    for (int j = 0; j < Mpad; j += 4) {
+      const uint4 kk = *reinterpret_cast<const uint4 *>(skey + j);
+      rank += (kk.x < k || (kk.x == k && j < i)) + (kk.y < k || (kk.y == k && j + 1 < i)) +
+              (kk.z < k || (kk.z == k && j + 2 < i)) + (kk.w < k || (kk.w == k && j + 3 < i));
+    }
+    order[rank] = i;
+  }
+  __syncthreads();
+  const int s0 = qt0 * IA_TILE;
+  for (int x = threadIdx.x; x < NQ; x += WGT) {
+    const int mq = order[s0 + x];
+    qlo[x] = qinfo[3 * mq];
+    qhi[x] = qinfo[3 * mq + 1];
+    qU[x] = qinfo[3 * mq + 2].x;
+  }
+  for (int e = threadIdx.x; e < QT * NP * IA_WAVE; e += WGT) {
+    const int L = e & 63, pq = e >> 6, qt = pq / NP, p = pq - qt * NP;
+    const int mq = order[s0 + qt * IA_TILE + (L & 31)];
+    ldsh[e] = qf[((int64_t)(mq >> 5) * NP + p) * IA_WAVE + (L & 32) + (mq & 31)];
+  }
+  __syncthreads();
+  if (threadIdx.x < QT) {
+    float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    float u = -INFINITY;
+    for (int q = 0; q < IA_TILE; q++) {
+      const int x = threadIdx.x * IA_TILE + q;
+      if (qU[x] == -INFINITY) continue;  // padding slot
+      const float4 l = qlo[x], h = qhi[x];
+      lo = make_float4(fminf(lo.x, l.x), fminf(lo.y, l.y), fminf(lo.z, l.z), fminf(lo.w, l.w));
+      hi = make_float4(fmaxf(hi.x, h.x), fmaxf(hi.y, h.y), fmaxf(hi.z, h.z), fmaxf(hi.w, h.w));
+      u = fmaxf(u, qU[x]);
+    }
+    tlo[threadIdx.x] = lo;
+    thi[threadIdx.x] = hi;
+    tU[threadIdx.x] = u;
+  }
+  __syncthreads();
+
+  // 2. need mask of DB tile tt over the QT query tiles (wave-uniform)
+  auto need = [&](int tt) -> unsigned {
+    const float4 blo = boxes[2 * tt], bhi = boxes[2 * tt + 1];
+    bool c = false;
+    if (lane < QT) c = prune_lb(blo, bhi, tlo[lane], thi[lane]) <= tU[lane];
+    const unsigned coarse = (unsigned)__ballot(c);
+    unsigned msk = 0;
+#pragma unroll
+    for (int pr = 0; pr < NPAIR; pr++) {
+      if ((coarse >> (2 * pr)) & 3u) {
+        const int j = 2 * pr + half, x = j * IA_TILE + (lane & 31);
+        bool nd = false;
+        if (j < QT) nd = prune_lb(blo, bhi, qlo[x], qhi[x]) <= qU[x];
+        const unsigned long long b = __ballot(nd);
+        msk |= (((unsigned)b != 0u ? 1u : 0u) | ((unsigned)(b >> 32) != 0u ? 2u : 0u)) << (2 * pr);
+      }
+    }
+    return msk & coarse;
+  };
+  auto next_needed = [&](int tt, unsigned &msk) -> int {
+    for (; tt < NT; tt += tstep) {
+      msk = need(tt);
+      if (msk) return tt;
+    }
+    msk = 0;
+    return tt;
+  };
+
+  float b1[QT], b2[QT];
+  int i1[QT];  // tile of b1 (packed epilogue)
+#pragma unroll
+  for (int q = 0; q < QT; q++) {
+    b1[q] = FLT_MAX;
+    b2[q] = FLT_MAX;
+    i1[q] = 0x7fffffff;
+  }
+  unsigned msk = t < NT ? need(t) : 0u;
+  if (!msk && t < NT) {
+    t = next_needed(t + tstep, msk);
+    const h16x8 *src = db + (int64_t)min(t, NT - 1) * NP * IA_WAVE + lane;
+#pragma unroll
+    for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+  }
+  unsigned cnt = 0;
+  while (t < NT) {
+    unsigned mn;
+    const int tn = next_needed(t + tstep, mn);
+    {
+      const h16x8 *src = db + (int64_t)min(tn, NT - 1) * NP * IA_WAVE + lane;
+#pragma unroll
+      for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
+    }
+    asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
+    // 3. the needed pairs of tile t
+    k3p_pairs<KS, QT, 0>(a, ldsh + lane, msk, t, b1, b2, i1);
+    cnt += __popc(msk);
+#pragma unroll
+    for (int p = 0; p < NP; p++) a[p] = an[p];
+    t = tn;
+    msk = mn;
+  }
+#pragma unroll
+  for (int q = 0; q < QT; q++) {  // tile + packed in-tile index -> DB position
+    const int r = (int)(__float_as_uint(b1[q]) & 15u);
+    i1[q] = b1[q] == FLT_MAX ? 0x7fffffff : i1[q] * IA_TILE + 4 * half + (r & 3) + 8 * (r >> 2);
+  }
+
+  // 4. merge the 2*NW subsets of each query (as K3h); records go to the original query slots
+  __syncthreads();
+  if (lane == 0) wpairs[wave] = cnt;
+  Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32], inside the query-fragment area
+#pragma unroll
+  for (int q = 0; q < QT; q++) {
+    Top2 mine = {b1[q], FLT_MAX, b2[q], i1[q], 0x7fffffff};
+    Top2 other;
+    other.v1 = __shfl_xor(b1[q], 32, 64);
+    other.i1 = __shfl_xor(i1[q], 32, 64);
+    other.T = __shfl_xor(b2[q], 32, 64);
+    other.v2 = FLT_MAX;
+    other.i2 = 0x7fffffff;
+    Top2 mrg = half == 0 ? top2_merge(mine, other) : top2_merge(other, mine);
+    if (half == 0) red[(wave * QT + q) * IA_TILE + lane] = mrg;
+  }
+  __syncthreads();
+  for (int x = threadIdx.x; x < NQ; x += WGT) {
+    Top2 m = red[x];
+#pragma unroll
+    for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
+    const int mq = order[s0 + x];
+    if (mq < M) {
+      const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
+      const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
+      rec[(int64_t)mq * nwg + wg] = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
+      recT[(int64_t)mq * nwg + wg] = m.T;
+    }
+  }
+  if (threadIdx.x == 0) {
+    unsigned long long s = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) s += wpairs[w];
+    atomicAdd(pairs, s);
+  }
+}
+
 #if defined(IA_K3H_KS) && defined(IA_K3H_QT)
 #define IA_K3H_CAT2(a, b, c) a##b##_##c
 #define IA_K3H_CAT(a, b, c) IA_K3H_CAT2(a, b, c)
@@ -206,5 +482,13 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
   }
 #endif
   return k3h_scan<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, false>;
+}
+#endif
+
+#if defined(IA_K3H_KS) && defined(IA_K3H_QT)
+// pruned scan instance (1 channel only: KS = 4)
+k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)() {
+  if constexpr (IA_K3H_KS == 4) return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE>;
+  else return nullptr;
 }
 #endif

@@ -23,6 +23,7 @@
 #include <stdint.h>
 
 #include "ia_internal.h"
+#include "ia_prune.h"
 
 #ifndef IA_PROBE
 #define IA_PROBE 0  // diagnostic phase-skipping builds (never set in the product build)
@@ -908,6 +909,95 @@ __device__ __forceinline__ float wave_min_f_x(float v) {
 __device__ __forceinline__ int lane_prefix(unsigned long long bal) {  // set bits of bal below this lane
   return __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
 }
+template <int STEP = 0>
+__device__ __forceinline__ double wave_min_d_x(double v) {
+  if constexpr (STEP < 6) return wave_min_d_x<STEP + 1>(fmin(v, lane_xchg_d<STEP>(v)));
+  else return v;
+}
+template <int STEP = 0>
+__device__ __forceinline__ double wave_sum_d_x(double v) {  // fixed butterfly order: deterministic
+  if constexpr (STEP < 6) return wave_sum_d_x<STEP + 1>(v + lane_xchg_d<STEP>(v));
+  else return v;
+}
+
+// ------------------------------------------------------------------------------------------
+// K2p: K2h for the pruned scan (1 channel) — one wave per query.  Besides the split-f16 query
+// fragments it writes the query's pruning record (ia_prune.h), qinfo[3m .. 3m+2]:
+//   (qlo_0..3), (qhi_0..3): f32 interval around the fp64 projection onto the level's basis
+//   (U', key bits, 0, 0):   U' from the exact fp64 distance of the best coherence candidate
+//                           (best_coherence_match's candidate set: the causal 5x5 neighbours'
+//                           shifted source pixels, all final at this wavefront step), the
+//                           Morton key of the projection (sort order of the query tiles)
+// ------------------------------------------------------------------------------------------
+template <int KS>
+__global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc sd, Imgs B, const double *__restrict__ mu_part,
+                                                          double *__restrict__ q64, double *__restrict__ qn2,
+                                                          _Float16 *__restrict__ qf, const double *__restrict__ db64,
+                                                          const int32_t *__restrict__ s, const int32_t *__restrict__ im,
+                                                          const double *__restrict__ basis, double ufac,
+                                                          float4 *__restrict__ qinfo) {
+  constexpr int D = 55, KD = 16 * KS;
+  static_assert(KD <= IA_WAVE, "one feature per lane");
+  __shared__ double qsh[IA_WG / IA_WAVE][Geo<1>::DS];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int m = blockIdx.x * (IA_WG / IA_WAVE) + wv;
+  if (m >= sd.Mpad) return;
+  if (m >= sd.M) {
+    if (lane < KD) put_qh<KS>(qf, m, lane, 0.);
+    if (lane == 0) {
+      qinfo[3 * m] = make_float4(0.f, 0.f, 0.f, 0.f);
+      qinfo[3 * m + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      qinfo[3 * m + 2] = make_float4(-INFINITY, __uint_as_float(IA_PRUNE_KEY_PAD), 0.f, 0.f);
+    }
+    return;
+  }
+  const int r = sd.r0 + m, c = sd.t - 3 * r, qi = r * g.bw + c;
+  // coherence candidate of this lane (lanes 0..14, product(rows, cols) order as merge_fused)
+  int crow = -1;
+  if (qi > 0 && lane < 15) {
+    const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
+    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
+      const int nb = nr * g.bw + nc;
+      const int tr = s[2 * nb] + r - nr, tc = s[2 * nb + 1] + c - nc;
+      if (tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) crow = (im[nb] * g.ah + tr) * g.aw + tc;
+    }
+  }
+  double ss = 0., p[IA_NPC];
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) p[i] = 0.;
+  if (lane < KD) {
+    const int f = lane;
+    if (f < D) {
+      const double v = feat<1>(B, f, r, c, 0);
+      q64[(int64_t)m * D + f] = v;
+      qsh[wv][f] = v;
+      const double qc = v - mu_part[feat_part<1>(f)];
+      ss = qc * qc;
+      put_qh<KS>(qf, m, f, -2.0 * qc);
+#pragma unroll
+      for (int i = 0; i < IA_NPC; i++) p[i] = basis[i * D + f] * qc;
+    } else {
+      put_qh<KS>(qf, m, f, f == D ? IA_NORM_SCALE : 0.);
+    }
+  }
+  ss = wave_sum_d(ss);
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) p[i] = wave_sum_d_x(p[i]);
+  __builtin_amdgcn_wave_barrier();  // qsh written by this wave's lanes, read below
+  double u = DBL_MAX;
+  if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh[wv]);
+  u = wave_min_d_x(u);
+  if (lane == 0) {
+    qn2[m] = ss;
+    qinfo[3 * m] = make_float4(round_down_f(p[0] - IA_PRUNE_MABS), round_down_f(p[1] - IA_PRUNE_MABS),
+                               round_down_f(p[2] - IA_PRUNE_MABS), round_down_f(p[3] - IA_PRUNE_MABS));
+    qinfo[3 * m + 1] = make_float4(round_up_f(p[0] + IA_PRUNE_MABS), round_up_f(p[1] + IA_PRUNE_MABS),
+                                   round_up_f(p[2] + IA_PRUNE_MABS), round_up_f(p[3] + IA_PRUNE_MABS));
+    const bool fin = u < DBL_MAX;
+    const unsigned key = fin ? prune_key(p, basis + IA_NPC * D) : IA_PRUNE_KEY_INF;
+    qinfo[3 * m + 2] = make_float4(fin ? round_up_f(u * ufac) : INFINITY, __uint_as_float(key), 0.f, 0.f);
+  }
+}
 
 // Fused single-rank merge of query m: certified exact NN + coherence + kappa + writeback.
 // Memory is touched in two dependent rounds: (1) the K3 records, the coherence neighbours'
@@ -1077,14 +1167,35 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
       const int wgid = jb * IA_WAVE + j;
       double cd = DBL_MAX;
       int ci = INT_MAX;
-      if (a.rr) {  // chunk = tiles wgid, wgid + nwg, ... (pruned scan)
-        for (int64_t x = lane;; x += IA_WAVE) {
-          const int64_t t = wgid + (int64_t)a.nwg * (x >> 5);
-          if (t >= a.NT) break;
-          const int64_t i = ia_pos_row_t(t * IA_TILE + (x & 31), a.NT, a.pos2row);
-          if (i >= a.NA) continue;
-          const double d = exact_dist_level<CH>(a.db64, i, qs);
-          if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
+      if (a.rr) {
+        // pruned scan: chunk = tiles wgid, wgid + nwg, ...  Only rows with exact distance <= bd
+        // can displace the winner, and such a row's tile has a projection lower bound
+        // <= bd * ufac (ia_prune.h), so the rescan visits just the tiles that pass that box
+        // test (one tile per lane), two tiles per wave pass
+        const float4 ql = a.qinfo[3 * m], qh = a.qinfo[3 * m + 1];
+        const float ub = round_up_f(bd * a.ufac);
+        for (int64_t tb = 0; wgid + (int64_t)a.nwg * tb < a.NT; tb += IA_WAVE) {
+          const int64_t t = wgid + (int64_t)a.nwg * (tb + lane);
+          bool nd = false;
+          if (t < a.NT) nd = prune_lb(a.boxes[2 * t], a.boxes[2 * t + 1], ql, qh) <= ub;
+          unsigned long long nm = __ballot(nd);
+          while (nm) {
+            const int j0 = __ffsll((long long)nm) - 1;
+            nm &= nm - 1;
+            int j1 = -1;
+            if (nm) {
+              j1 = __ffsll((long long)nm) - 1;
+              nm &= nm - 1;
+            }
+            const int j = lane < 32 ? j0 : j1;
+            if (j >= 0) {
+              const int64_t i = a.pos2row[(wgid + (int64_t)a.nwg * (tb + j)) * IA_TILE + (lane & 31)];
+              if (i < a.NA) {
+                const double d = exact_dist_level<CH>(a.db64, i, qs);
+                if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
+              }
+            }
+          }
         }
       } else {
         const int64_t p0 = (int64_t)a.pos0 + (int64_t)wgid * a.tpw * IA_TILE;
@@ -1536,6 +1647,13 @@ void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
   else launch_gather_h_t<2, 7>(g, sd, B, mu, q64, qn2, qf, st);
 }
 
+void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64, double *qn2,
+                        void *qf, const double *db64, const int32_t *s, const int32_t *im, const double *basis, double ufac,
+                        float4 *qinfo, hipStream_t st) {
+  hipLaunchKernelGGL(k_gather_query_p<4>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, mu, q64, qn2,
+                     (_Float16 *)qf, db64, s, im, basis, ufac, qinfo);
+}
+
 // split-f16 distance kernels live in ia_k3h.hip, compiled once per (KS, QT) instance
 #define IA_K3H_DECL(ks, qt) k3h_fn ia_k3h_get_##ks##_##qt(int variant);
 IA_K3H_DECL(4, 1) IA_K3H_DECL(4, 2) IA_K3H_DECL(4, 3) IA_K3H_DECL(4, 4) IA_K3H_DECL(4, 5) IA_K3H_DECL(4, 6)
@@ -1563,4 +1681,30 @@ void ia_launch_k3h(int KS, int qt, const void *db, const void *qf, int n_tiles, 
   }
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(nw * IA_WAVE), lds, st, (const h16x8 *)db, (const h16x8 *)qf, n_tiles, tpw, qt0, M, nwg,
                      row0, NT, rec, recT);
+}
+
+// pruned split-f16 distance kernels (ia_k3h.hip k3h_prune, 1 channel)
+#define IA_K3P_DECL(qt) k3p_fn ia_k3p_get_4_##qt();
+IA_K3P_DECL(1) IA_K3P_DECL(2) IA_K3P_DECL(3) IA_K3P_DECL(4) IA_K3P_DECL(5) IA_K3P_DECL(6) IA_K3P_DECL(7) IA_K3P_DECL(8)
+IA_K3P_DECL(9) IA_K3P_DECL(10) IA_K3P_DECL(11)
+size_t ia_k3p_lds(int qt, int Mpad) {
+  const size_t NQ = (size_t)qt * IA_TILE;
+  const size_t qfrag = (size_t)qt * 8 * IA_WAVE * 16;  // KS = 4: NP = 8 h16x8 per lane
+  return qfrag + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + (size_t)Mpad * 8;
+}
+void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
+                   int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
+                   hipStream_t st) {
+  typedef k3p_fn (*getter)();
+  static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
+                              ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
+  const k3p_fn fn = g4[qt - 1]();
+  const size_t lds = ia_k3p_lds(qt, Mpad);
+  static int attr_lds[16] = {};
+  if ((int)lds > attr_lds[qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
+    (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    attr_lds[qt] = (int)lds;
+  }
+  hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WGH), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row, NT,
+                     qt0, M, Mpad, nwg, rec, recT, pairs);
 }

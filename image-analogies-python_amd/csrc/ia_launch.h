@@ -46,3 +46,10 @@ int ia_sort_pairs(void *temp, size_t temp_bytes, const unsigned *keys_in, unsign
                   int *vals_out, int64_t n, hipStream_t st);
 void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int *pos2row, float *boxes,
                            hipStream_t st);
+void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64, double *qn2,
+                        void *qf, const double *db64, const int32_t *s, const int32_t *im, const double *basis, double ufac,
+                        float4 *qinfo, hipStream_t st);
+size_t ia_k3p_lds(int qt, int Mpad);
+void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
+                   int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
+                   hipStream_t st);

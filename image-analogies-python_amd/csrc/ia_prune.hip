@@ -21,6 +21,7 @@
 
 #include "ia_internal.h"
 #include "ia_launch.h"
+#include "ia_prune.h"
 
 #define PR_WG 256
 #define PR_COV_ROWS 16  // rows staged in LDS per covariance pass
@@ -80,23 +81,6 @@ __global__ void __launch_bounds__(PR_WG) k_cov_reduce(const double *__restrict__
   }
 }
 
-// Morton key of the projections quantised to 8 bits each over [-4 sigma_i, 4 sigma_i]
-__device__ __forceinline__ unsigned prune_key(const double (&p)[IA_NPC], const double *__restrict__ scale) {
-  unsigned key = 0;
-  unsigned qv[IA_NPC];
-#pragma unroll
-  for (int i = 0; i < IA_NPC; i++) {
-    const double t = (p[i] * scale[i] + 1.0) * 128.0;
-    qv[i] = t <= 0. ? 0u : t >= 255. ? 255u : (unsigned)t;
-  }
-#pragma unroll
-  for (int b = 7; b >= 0; b--) {
-#pragma unroll
-    for (int i = 0; i < IA_NPC; i++) key = (key << 1) | ((qv[i] >> b) & 1u);
-  }
-  return key;
-}
-
 // K5c: projections, keys and the identity row list of every DB row
 __global__ void __launch_bounds__(PR_WG) k_proj_keys(const double *__restrict__ db64, int64_t NA,
                                                      const double *__restrict__ mu_part, const double *__restrict__ basis,
@@ -143,17 +127,6 @@ __global__ void __launch_bounds__(PR_WG) k_make_table(const int *__restrict__ so
   const int k = (((j & 3) << 1) | ((j >> 2) & 1) | ((j >> 3) << 3));
   const int64_t s = (p & ~(int64_t)31) + k;
   pos2row[p] = s < NA ? sorted_rows[s] : (int)s;
-}
-
-__device__ __forceinline__ float round_down_f(double x) {
-  float f = (float)x;
-  if ((double)f > x) f = nextafterf(f, -INFINITY);
-  return f;
-}
-__device__ __forceinline__ float round_up_f(double x) {
-  float f = (float)x;
-  if ((double)f < x) f = nextafterf(f, INFINITY);
-  return f;
 }
 
 // K5d': per-tile boxes of the projections (lo[IA_NPC], hi[IA_NPC]) over the tile's real rows

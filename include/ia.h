@@ -60,6 +60,9 @@ typedef struct {
   int64_t bound_violations; /* pixels where a reranked candidate's exact distance fell outside
                              * the certified MFMA error bound (audit; expected 0) */
   int64_t f16_levels;       /* levels run on the split-f16 matcher */
+  int64_t pruned_levels;    /* levels run on the certified pruned scan (option "prune") */
+  double dist_pairs;        /* (DB tile, query tile) pairs the distance kernel contracted */
+  double dist_pairs_full;   /* pairs an unpruned scan contracts (dist_pairs / this = work left) */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
@@ -92,7 +95,10 @@ int ia_version(void);
  * wavefront step with HIP events; ia_stats.dist_ms / dist_flops_timed then give the kernel's
  * measured device time and algorithmic flops (bench.py roofline).
  * "matcher" = IA_MATCH_F16X3 (default: split-f16 MFMA scan, 1 and 2 channels, image values
- * within +-64) or IA_MATCH_F32 (fp32 MFMA scan).  Both are certified exact: identical results. */
+ * within +-64) or IA_MATCH_F32 (fp32 MFMA scan).  Both are certified exact: identical results.
+ * "prune" = 1 (default) / 0: certified pruned scan on 1-channel split-f16 levels with >= 2^18
+ * DB rows: (DB tile, query tile) pairs a projection bound proves farther than
+ * the query's best coherence candidate are skipped.  Identical results either way. */
 #define IA_MATCH_F32 0
 #define IA_MATCH_F16X3 1
 int ia_set_option(ia_ctx *ctx, const char *name, int value);

@@ -1,0 +1,51 @@
+"""Certified pruned scan: the synthesis with pruning on must be bit-identical to
+the unpruned exact scan on every level (source maps and B'), while contracting fewer
+(DB tile, query tile) pairs.  The 512^2 job prunes its finest level, the 1024^2 job (cfg3, the
+bench configuration) its two finest."""
+import numpy as np
+import pytest
+
+import ia_amd  # noqa: F401
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(ctx, job, prune):
+    from ia_amd import _native
+    ctx.set_option('prune', prune)
+    Bp = [x.copy() for x in job.Bp_init]
+    S, IM = {}, {}
+    st = _native.Stats()
+    try:
+        for level in range(1, job.L):
+            S[level], IM[level] = ctx.synthesize_level(
+                job.A_pyr[level], job.A_pyr[level - 1], [p[level] for p in job.Ap_pyr_list],
+                [p[level - 1] for p in job.Ap_pyr_list], job.B_pyr[level], job.B_pyr[level - 1], Bp[level - 1],
+                Bp[level], job.weights, job.kappa_factor(level), st)
+    finally:
+        ctx.set_option('prune', 1)
+    return Bp, S, IM, st
+
+
+@pytest.mark.parametrize('size,n_pruned', [(512, 1), (1024, 2)])
+def test_pruned_equals_unpruned(ctx, size, n_pruned):
+    from ia_amd import synth
+    job = synth.make_job(size)
+    Bp0, S0, IM0, st0 = _run(ctx, job, 0)
+    Bp1, S1, IM1, st1 = _run(ctx, job, 1)
+    assert st0.pruned_levels == 0 and st1.pruned_levels == n_pruned
+    for level in range(1, job.L):
+        assert np.array_equal(S0[level], S1[level]), level
+        assert np.array_equal(IM0[level], IM1[level]), level
+        assert np.array_equal(Bp0[level], Bp1[level]), level
+    assert st1.bound_violations == 0 and st0.bound_violations == 0
+    assert st1.dist_pairs < st1.dist_pairs_full
+    assert st1.dist_pairs_full == st0.dist_pairs_full
+    print('size %d: pairs left %.3f, fallbacks %d -> %d' % (size, st1.dist_pairs / st1.dist_pairs_full,
+                                                            st0.fallbacks, st1.fallbacks))
+
+
+def test_prune_option_rejects_bad_values(ctx):
+    from ia_amd import _native
+    with pytest.raises(_native.IAError):
+        ctx.set_option('prune', 2)
