@@ -114,6 +114,10 @@ def main():
                     help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
+    ap.add_argument('--k3p-variant', type=int, default=6, choices=[0, 1, 2, 3, 4, 5, 6],
+                    help='pruned-scan kernel version (ia_k3h.hip k3h_prune*): 0 = first version, 1 = boxes in '
+                         'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
+                         'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically')
     ap.add_argument('--time-stride', type=int, default=4, help='sample K3 timing every S-th wavefront step')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -145,6 +149,7 @@ def main():
     ctx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
     ctx.set_option('k3_variant', args.k3_variant)
     ctx.set_option('prune', args.prune)
+    ctx.set_option('k3p_variant', args.k3p_variant)
     if args.mode == 'shard' and world > 1:
         uid = [_native.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -197,7 +202,8 @@ def main():
     roofline = {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': peak / 1e12, 'unit': 'TFLOP/s',
                 'frac': achieved / peak, 'traffic': traffic,
                 'mfma_issue_frac': achieved * issued / peak,
-                'kernel': ('k3h_scan (3 x v_mfma_f32_32x32x16_f16 on hi/lo-split operands, fused packed-index top-2)' if f16 else
+                'kernel': (('k3h_prune (certified pruned scan; ' if st['pruned_levels'] else 'k3h_scan (') +
+                           '3 x v_mfma_f32_32x32x16_f16 on hi/lo-split operands, fused packed-index top-2)' if f16 else
                            'k3_dist (v_mfma_f32_32x32x2_f32 distance scan + fused top-2)'),
                 'k3_us_per_launch': k3_ms_per_launch * 1e3, 'k3_launches_sampled': st['dist_launches_timed'],
                 'k3_share_of_step': st['dist_ms'] * (st['dist_flops'] / max(st['dist_flops_timed'], 1)) /
@@ -217,7 +223,7 @@ def main():
            'roofline': roofline,
            'stats': {k: st[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
                                         'synth_ms', 'bound_violations', 'f16_levels', 'pruned_levels',
-                                        'dist_pairs', 'dist_pairs_full')}}
+                                        'dist_pairs', 'dist_pairs_full', 'dist_tiles', 'dist_tiles_full')}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(job, args.cpu_seconds)
     if rank == 0:

@@ -15,6 +15,10 @@
 #include "ia_internal.h"
 #include "ia_launch.h"
 
+#if IA_PROBE & 16
+void ia_k3p_probe_dump();
+#endif
+
 namespace {
 
 thread_local std::string g_last_error;
@@ -81,6 +85,7 @@ struct ia_ctx {
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
   int prune = 1;
   int matcher = IA_MATCH_F16X3;  // option "matcher"
+  int k3p_variant = 6;           // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   // per-step K3 timing (optional)
   int time_dist = 0;
@@ -251,6 +256,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!c || !name) return fail(IA_EINVAL, "ia_set_option: NULL argument");
   if (!std::strcmp(name, "time_dist")) {
     c->time_dist = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "k3p_variant")) {
+    if (value < 0 || value > 6) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..6");
+    c->k3p_variant = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "k3_variant")) {
@@ -470,10 +480,10 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       (rc = c->rec.ensure((size_t)Mmax * std::max(g.nwg, 1) * 16)) ||
       (rc = c->recT.ensure((size_t)Mmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mmax * 16)) ||
       (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(4 * 8)) ||
-      (rc = c->pstat.ensure((size_t)NB * 4)) || (rc = c->pairs.ensure(2 * 8)) ||
+      (rc = c->pstat.ensure((size_t)NB * 4)) || (rc = c->pairs.ensure(3 * IA_NWG_H * 8)) ||
       (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 : 16)))
     return rc;
-  HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 2 * 8, c->st));
+  HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 3 * IA_NWG_H * 8, c->st));  // [untimed pairs | timed pairs | tiles][wg]
   HIP_TRY(hipMemsetAsync(c->Rbits.p, 0, 4, c->st));
   HIP_TRY(hipMemsetAsync(c->counters.p, 0, 4 * 8, c->st));
   HIP_TRY(hipMemsetAsync(c->pstat.p, 0, (size_t)NB * 4, c->st));
@@ -529,7 +539,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     for (size_t i = old; i < c->evs.size(); i++) hipEventCreate(&c->evs[i]);
   }
   int64_t dist_launches = 0, launches_timed = 0, n_rec = 0;
-  double dist_flops = 0., flops_timed = 0., pairs_full = 0.;
+  double dist_flops = 0., flops_timed = 0., pairs_full = 0., tiles_full = 0.;
   for (int64_t t = 0; t < T; t++) {
     StepDesc sd;
     sd.t = (int)t;
@@ -553,7 +563,8 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
         if (prune)
           ia_launch_k3p(qt, c->db.p, c->qf.p, c->qinfo.as<float4>(), c->boxes.as<float4>(), g.pos2row, g.n_tiles, qt0, sd.M,
                         sd.Mpad, g.nwg, c->rec.as<float4>(), c->recT.as<float>(),
-                        c->pairs.as<unsigned long long>() + (timed ? 1 : 0), c->st);
+                        c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0), c->pairs.as<unsigned long long>() + 2 * IA_NWG_H,
+                        c->k3p_variant, c->st);
         else if (use_h)
           ia_launch_k3h(g.KS, qt, c->db.p, c->qf.p, ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0, ma.NT, c->rec.as<float4>(),
                         c->recT.as<float>(), c->k3_variant, c->st);
@@ -564,6 +575,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
         const double fl = prune ? 0. : 2.0 * g.D * (double)shard_rows * std::max(mq, 0);  // pruned: pair counters
         dist_flops += fl;
         pairs_full += (double)ns * qt;
+        tiles_full += (double)ns;
         dist_launches++;
         if (timed) {
           flops_timed += fl;
@@ -592,10 +604,20 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     HIP_TRY(hipMemcpyAsync(a->im_out, dIM, (size_t)NB * 4, hipMemcpyDeviceToHost, c->st));
   }
   HIP_TRY(hipStreamSynchronize(c->st));
+#if IA_PROBE & 16
+  if (prune) ia_k3p_probe_dump();
+#endif
   if (stats) {
-    unsigned long long ctr[4], prs[2];
+    unsigned long long ctr[4], prs[3];
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
-    HIP_TRY(hipMemcpy(prs, c->pairs.p, sizeof(prs), hipMemcpyDeviceToHost));
+    {  // per-workgroup counter slots (no same-address atomics in the distance kernel)
+      std::vector<unsigned long long> slots(3 * IA_NWG_H);
+      HIP_TRY(hipMemcpy(slots.data(), c->pairs.p, slots.size() * 8, hipMemcpyDeviceToHost));
+      for (int j = 0; j < 3; j++) {
+        prs[j] = 0;
+        for (int w = 0; w < IA_NWG_H; w++) prs[j] += slots[j * IA_NWG_H + w];
+      }
+    }
     const double pair_flops = 2.0 * g.D * IA_TILE * IA_TILE;  // one (DB tile, query tile) pair
     if (prune) {
       dist_flops = pair_flops * (double)(prs[0] + prs[1]);
@@ -604,6 +626,8 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     stats->pruned_levels += prune ? 1 : 0;
     stats->dist_pairs += prune ? (double)(prs[0] + prs[1]) : pairs_full;
     stats->dist_pairs_full += pairs_full;
+    stats->dist_tiles += prune ? (double)prs[2] : tiles_full;
+    stats->dist_tiles_full += tiles_full;
     float ms_db = 0.f, ms_syn = 0.f;
     hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
     hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);

@@ -8,10 +8,21 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 #include <stdint.h>
+#include <stdio.h>
 
 #include "ia_internal.h"
 #include "ia_top2.h"
 #include "ia_prune.h"
+
+#ifndef IA_PROBE
+#define IA_PROBE 0
+#endif
+#if IA_PROBE & 16  // diagnostic build only: per-wave phase cycle sums of the pruned scan (K3p, V >= 1)
+__device__ unsigned long long k3p_prof[12];
+#define K3P_T(x) do { __builtin_amdgcn_sched_barrier(0); x = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define K3P_T(x) do { } while (0)
+#endif
 
 // K3h: grid = nwg workgroups of NW waves (one workgroup per CU); WG w owns DB tiles
 // [w*tpw, (w+1)*tpw), wave v takes tiles w*tpw + v, +NW, ...; the step's QT query tiles sit in
@@ -293,11 +304,16 @@ __device__ __forceinline__ void k3p_pairs(const h16x8 (&a)[2 * KS], const h16x8 
   }
 }
 
-template <int KS, int QT, int NW>
+// V (option "k3p_variant"): 0 = per-tile box loads and a full-key rank sort (first version);
+// 1 = the wave's tile boxes held in registers (one coalesced load per 64 tiles, read back with
+// v_readlane: the tile walk has no memory latency left), unique 20-bit-key rank sort;
+// 2 = as 1 with the coarse query-tile test only (diagnostic: no per-query test)
+template <int KS, int QT, int NW, int V>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
           const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
-          float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs) {
+          float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
+          unsigned long long *__restrict__ tiles) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   static_assert(QT <= 32, "need masks are 32-bit");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
@@ -309,11 +325,13 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
   float *tU = reinterpret_cast<float *>(thi + QT);                     // [QT] max U' of the tile
   unsigned *skey = reinterpret_cast<unsigned *>(tU + ((QT + 3) & ~3));  // [Mpad]
   int *order = reinterpret_cast<int *>(skey + Mpad);                    // [Mpad] sorted -> query
-  __shared__ unsigned wpairs[NW];
+  __shared__ unsigned wpairs[NW], wtiles[NW];
   const int lane = threadIdx.x & 63, half = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wg = blockIdx.x, tstep = nwg * NW;
   int t = wg + nwg * wave;
+  unsigned long long pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0, pneed = 0, px = 0, py = 0;
+  K3P_T(pt0);
 
   h16x8 a[NP], an[NP];
   {  // speculative first tile (usually needed), overlapping the query setup
@@ -321,18 +339,44 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
 #pragma unroll
     for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
   }
-  // 1. rank sort of the step's queries by key (index breaks ties)
-  for (int i = threadIdx.x; i < Mpad; i += WGT) skey[i] = __float_as_uint(qinfo[3 * i + 2].y);
-  __syncthreads();
-  for (int i = threadIdx.x; i < Mpad; i += WGT) {
-    const unsigned k = skey[i];
-    int rank = 0;
-    for (int j = 0; j < Mpad; j += 4) {
-      const uint4 kk = *reinterpret_cast<const uint4 *>(skey + j);
-      rank += (kk.x < k || (kk.x == k && j < i)) + (kk.y < k || (kk.y == k && j + 1 < i)) +
-              (kk.z < k || (kk.z == k && j + 2 < i)) + (kk.w < k || (kk.w == k && j + 3 < i));
+  float4 rlo = make_float4(0.f, 0.f, 0.f, 0.f), rhi = rlo;  // V >= 1: boxes of the wave's tiles
+  int chunk = -1;
+  if constexpr (V >= 1) {  // the first 64 of them, also overlapping the query setup
+    const int tt = t + tstep * lane;
+    if (tt < NT) {
+      rlo = boxes[2 * tt];
+      rhi = boxes[2 * tt + 1];
     }
-    order[rank] = i;
+    chunk = 0;
+  }
+  // 1. rank sort of the step's queries by key (index breaks ties)
+  if constexpr (V == 0) {
+    for (int i = threadIdx.x; i < Mpad; i += WGT) skey[i] = __float_as_uint(qinfo[3 * i + 2].y);
+    __syncthreads();
+    for (int i = threadIdx.x; i < Mpad; i += WGT) {
+      const unsigned k = skey[i];
+      int rank = 0;
+      for (int j = 0; j < Mpad; j += 4) {
+        const uint4 kk = *reinterpret_cast<const uint4 *>(skey + j);
+        rank += (kk.x < k || (kk.x == k && j < i)) + (kk.y < k || (kk.y == k && j + 1 < i)) +
+                (kk.z < k || (kk.z == k && j + 2 < i)) + (kk.w < k || (kk.w == k && j + 3 < i));
+      }
+      order[rank] = i;
+    }
+  } else {
+    // unique keys: the key's top 20 bits (5 per axis) above the 12-bit query index (Mpad <= 4096),
+    // so a rank is one unsigned compare per key
+    for (int i = threadIdx.x; i < Mpad; i += WGT) skey[i] = (__float_as_uint(qinfo[3 * i + 2].y) & 0xFFFFF000u) | (unsigned)i;
+    __syncthreads();
+    for (int i = threadIdx.x; i < Mpad; i += WGT) {
+      const unsigned k = skey[i];
+      int rank = 0;
+      for (int j = 0; j < Mpad; j += 4) {
+        const uint4 kk = *reinterpret_cast<const uint4 *>(skey + j);
+        rank += (int)(kk.x < k) + (int)(kk.y < k) + (int)(kk.z < k) + (int)(kk.w < k);
+      }
+      order[rank] = i;
+    }
   }
   __syncthreads();
   const int s0 = qt0 * IA_TILE;
@@ -366,11 +410,11 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
   __syncthreads();
 
   // 2. need mask of DB tile tt over the QT query tiles (wave-uniform)
-  auto need = [&](int tt) -> unsigned {
-    const float4 blo = boxes[2 * tt], bhi = boxes[2 * tt + 1];
+  auto need_box = [&](const float4 &blo, const float4 &bhi) -> unsigned {
     bool c = false;
     if (lane < QT) c = prune_lb(blo, bhi, tlo[lane], thi[lane]) <= tU[lane];
     const unsigned coarse = (unsigned)__ballot(c);
+    if constexpr (V == 2) return coarse;
     unsigned msk = 0;
 #pragma unroll
     for (int pr = 0; pr < NPAIR; pr++) {
@@ -383,6 +427,10 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
       }
     }
     return msk & coarse;
+  };
+  auto need = [&](int tt) -> unsigned {
+    const float4 blo = boxes[2 * tt], bhi = boxes[2 * tt + 1];
+    return need_box(blo, bhi);
   };
   auto next_needed = [&](int tt, unsigned &msk) -> int {
     for (; tt < NT; tt += tstep) {
@@ -401,30 +449,94 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
     b2[q] = FLT_MAX;
     i1[q] = 0x7fffffff;
   }
-  unsigned msk = t < NT ? need(t) : 0u;
-  if (!msk && t < NT) {
-    t = next_needed(t + tstep, msk);
-    const h16x8 *src = db + (int64_t)min(t, NT - 1) * NP * IA_WAVE + lane;
+  unsigned cnt = 0, ntl = 0;  // pairs contracted, DB tiles loaded
+  if constexpr (V == 0) {
+    unsigned msk = t < NT ? need(t) : 0u;
+    if (!msk && t < NT) {
+      t = next_needed(t + tstep, msk);
+      const h16x8 *src = db + (int64_t)min(t, NT - 1) * NP * IA_WAVE + lane;
 #pragma unroll
-    for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
-  }
-  unsigned cnt = 0;
-  while (t < NT) {
-    unsigned mn;
-    const int tn = next_needed(t + tstep, mn);
-    {
-      const h16x8 *src = db + (int64_t)min(tn, NT - 1) * NP * IA_WAVE + lane;
-#pragma unroll
-      for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
+      for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
     }
-    asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-    // 3. the needed pairs of tile t
-    k3p_pairs<KS, QT, 0>(a, ldsh + lane, msk, t, b1, b2, i1);
-    cnt += __popc(msk);
+    while (t < NT) {
+      unsigned mn;
+      const int tn = next_needed(t + tstep, mn);
+      {
+        const h16x8 *src = db + (int64_t)min(tn, NT - 1) * NP * IA_WAVE + lane;
 #pragma unroll
-    for (int p = 0; p < NP; p++) a[p] = an[p];
-    t = tn;
-    msk = mn;
+        for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
+      }
+      asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
+      // 3. the needed pairs of tile t
+      k3p_pairs<KS, QT, 0>(a, ldsh + lane, msk, t, b1, b2, i1);
+      cnt += __popc(msk);
+      ntl++;
+#pragma unroll
+      for (int p = 0; p < NP; p++) a[p] = an[p];
+      t = tn;
+      msk = mn;
+    }
+  } else {
+    // the wave's k-th tile is t0w + tstep*k; lane j holds the box of tile k = 64*chunk + j
+    const int t0w = t;
+    const int K = t0w < NT ? (NT - t0w + tstep - 1) / tstep : 0;
+    auto rl = [](float v, int j) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j)); };
+    auto box_need = [&](int k) -> unsigned {
+      if ((k >> 6) != chunk) {  // wave-uniform: the next 64 boxes in one coalesced load
+        chunk = k >> 6;
+        const int tt = t0w + tstep * (64 * chunk + lane);
+        if (tt < NT) {
+          rlo = boxes[2 * tt];
+          rhi = boxes[2 * tt + 1];
+        }
+      }
+      const int j = k & 63;
+      const float4 blo = make_float4(rl(rlo.x, j), rl(rlo.y, j), rl(rlo.z, j), rl(rlo.w, j));
+      const float4 bhi = make_float4(rl(rhi.x, j), rl(rhi.y, j), rl(rhi.z, j), rl(rhi.w, j));
+      return need_box(blo, bhi);
+    };
+    auto next_k = [&](int k, unsigned &m) -> int {
+      for (; k < K; k++) {
+        m = box_need(k);
+        if (m) return k;
+      }
+      m = 0;
+      return K;
+    };
+    unsigned msk;
+    K3P_T(pt1);
+    K3P_T(px);
+    int k = next_k(0, msk);
+    K3P_T(py);
+    pneed += py - px;
+    if (k > 0 && k < K) {  // the speculative first tile is not needed: load the first needed one
+      const h16x8 *src = db + (int64_t)(t0w + tstep * k) * NP * IA_WAVE + lane;
+#pragma unroll
+      for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+    }
+    while (k < K) {
+      unsigned mn;
+      K3P_T(px);
+      const int kn = next_k(k + 1, mn);
+      K3P_T(py);
+      pneed += py - px;
+      if (kn < K) {  // wave-uniform; never a clamped dummy load: with every wave of the grid
+                     // re-reading one tile at its end, that tile's L2 channel serialised ~16 MiB
+        const h16x8 *src = db + (int64_t)(t0w + tstep * kn) * NP * IA_WAVE + lane;
+#pragma unroll
+        for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
+      }
+      asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
+      // 3. the needed pairs of tile t
+      k3p_pairs<KS, QT, 0>(a, ldsh + lane, msk, t0w + tstep * k, b1, b2, i1);
+      cnt += __popc(msk);
+      ntl++;
+#pragma unroll
+      for (int p = 0; p < NP; p++) a[p] = an[p];
+      k = kn;
+      msk = mn;
+    }
+    K3P_T(pt2);
   }
 #pragma unroll
   for (int q = 0; q < QT; q++) {  // tile + packed in-tile index -> DB position
@@ -434,7 +546,12 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
 
   // 4. merge the 2*NW subsets of each query (as K3h); records go to the original query slots
   __syncthreads();
-  if (lane == 0) wpairs[wave] = cnt;
+  unsigned long long ps1 = 0, ps2 = 0;
+  K3P_T(ps1);
+  if (lane == 0) {
+    wpairs[wave] = cnt;
+    wtiles[wave] = ntl;
+  }
   Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32], inside the query-fragment area
 #pragma unroll
   for (int q = 0; q < QT; q++) {
@@ -449,24 +566,66 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
     if (half == 0) red[(wave * QT + q) * IA_TILE + lane] = mrg;
   }
   __syncthreads();
+  K3P_T(ps2);
+  unsigned long long pw1 = 0, pw2 = 0, pw3 = 0;
   for (int x = threadIdx.x; x < NQ; x += WGT) {
     Top2 m = red[x];
 #pragma unroll
     for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
+    K3P_T(pw1);
     const int mq = order[s0 + x];
     if (mq < M) {
       const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
       const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
+#if IA_PROBE & 16
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+      K3P_T(pw2);
       rec[(int64_t)mq * nwg + wg] = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
       recT[(int64_t)mq * nwg + wg] = m.T;
     }
   }
+#if IA_PROBE & 16
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+  K3P_T(pw3);
   if (threadIdx.x == 0) {
-    unsigned long long s = 0;
+    unsigned long long s = 0, n = 0;
 #pragma unroll
-    for (int w = 0; w < NW; w++) s += wpairs[w];
-    atomicAdd(pairs, s);
+    for (int w = 0; w < NW; w++) {
+      s += wpairs[w];
+      n += wtiles[w];
+    }
+    if constexpr (V == 0) {
+      atomicAdd(pairs, s);
+      atomicAdd(tiles, n);
+    } else {  // the workgroup's own slots: launches are stream-ordered, so no atomics (512
+              // same-address device atomics per launch serialise far from the CU)
+      pairs[wg] += s;
+      tiles[wg] += n;
+    }
   }
+#if IA_PROBE & 16
+  if constexpr (V >= 1) {
+    K3P_T(pt3);
+    if (lane == 0 && M == Mpad - 10 && wg < 8) {  // 1024^2 plateau (M = 342), 8 sampled WGs
+      atomicAdd(&k3p_prof[0], pt1 - pt0);
+      atomicAdd(&k3p_prof[1], pneed);
+      atomicAdd(&k3p_prof[2], pt2 - pt1);
+      atomicAdd(&k3p_prof[3], pt3 - pt2);
+      atomicAdd(&k3p_prof[4], 1ull);
+      atomicAdd(&k3p_prof[5], (unsigned long long)ntl);
+      atomicAdd(&k3p_prof[6], (unsigned long long)cnt);
+      if (pw2 != 0) {
+        atomicAdd(&k3p_prof[7], pw1 - ps2);
+        atomicAdd(&k3p_prof[8], pw2 - pw1);
+        atomicAdd(&k3p_prof[9], pw3 - pw2);
+        atomicAdd(&k3p_prof[11], pt3 - pw3);
+        atomicAdd(&k3p_prof[10], 1ull);
+      }
+    }
+  }
+#endif
 }
 
 #if defined(IA_K3H_KS) && defined(IA_K3H_QT)
@@ -485,10 +644,448 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 }
 #endif
 
+// ------------------------------------------------------------------------------------------
+// K3p v3 (k3p_variant 3, the default where it applies: Mpad <= 512, <= 512 tiles per
+// workgroup).  Same pairs, same records semantics as V1, organised in phases so no phase waits
+// on another's memory latency:
+//   1. ONE global round: every query's pruning record (thread = query, registers), the step's
+//      unsorted split-f16 query fragments (coalesced, registers), the workgroup's tile boxes
+//      (to LDS) and each wave's speculative first DB tile
+//   2. rank sort by unique key (as V1); fragments and records scattered to their sorted LDS
+//      slots; query-tile boxes by 32-lane butterflies
+//   3. need masks of ALL the workgroup's tiles (wave v: tiles k = v mod NW), with the lane's
+//      per-pair query intervals held in registers; the needed tiles compacted into one list
+//      in tile order (ballot + mbcnt)
+//   4. list item j -> wave j mod NW (deterministic, balanced by tile count); the DB tiles of
+//      items j + NW and j + 2 NW are in flight while item j is contracted (nothing else
+//      between the loads: no need test left in the loop)
+//   5. per-query records exactly as V1
+// ------------------------------------------------------------------------------------------
+#define IA_K3P3_MAXQ 512   // queries per step (one per thread)
+#define IA_K3P3_MAXK 512   // DB tiles per workgroup
+template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false>
+__global__ void __launch_bounds__(NW * IA_WAVE, 1)
+k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
+           const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
+           float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
+           unsigned long long *__restrict__ tiles) {
+  constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
+  constexpr int NE = IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE / WGT;  // unsorted fragments per thread
+  static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
+  static_assert(WGT == IA_K3P3_MAXQ && WGT == IA_K3P3_MAXK, "one query / one tile per thread");
+  extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
+  float4 *qlo = reinterpret_cast<float4 *>(ldsh + QT * NP * IA_WAVE);  // [NQ]
+  float4 *qhi = qlo + NQ;                                               // [NQ]
+  float *qU = reinterpret_cast<float *>(qhi + NQ);                     // [NQ]
+  float4 *tlo = reinterpret_cast<float4 *>(qU + NQ);                   // [QT] query-tile boxes
+  float4 *thi = tlo + QT;                                               // [QT]
+  float *tU = reinterpret_cast<float *>(thi + QT);                     // [QT]
+  unsigned *skey = reinterpret_cast<unsigned *>(tU + ((QT + 3) & ~3));  // [Mpad]
+  int *order = reinterpret_cast<int *>(skey + Mpad);                    // [Mpad] sorted -> query
+  int *rankof = order + Mpad;                                           // [Mpad] query -> sorted
+  const int wg = blockIdx.x;
+  const int K = (NT - wg + nwg - 1) / nwg;  // tiles wg + nwg*k, k < K (host: nwg <= NT, K <= MAXK)
+  float4 *wbox = reinterpret_cast<float4 *>(rankof + Mpad);            // [2K] the WG's tile boxes
+  unsigned *kmask = reinterpret_cast<unsigned *>(wbox + 2 * K);        // [K] need mask per tile
+  int *items = reinterpret_cast<int *>(kmask + K);                     // [K] needed tiles, in order
+  __shared__ unsigned wpairs[NW], wtiles[NW];
+  __shared__ int wcnt[NW];
+  const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int s0 = qt0 * IA_TILE;
+  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+  K3P_T(ph[0]);
+
+  // ---- 1. one global round
+  h16x8 a[NP], an[NP], an2[NP];
+  {
+    const h16x8 *src = db + (int64_t)(wg + nwg * min(wave, K - 1)) * NP * IA_WAVE + lane;
+#pragma unroll
+    for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+  }
+  float4 mlo = make_float4(0.f, 0.f, 0.f, 0.f), mhi = mlo;
+  float mU = -INFINITY;
+  unsigned mkey = 0xFFFFFFFFu;
+  if (tid < Mpad) {
+    mlo = qinfo[3 * tid];
+    mhi = qinfo[3 * tid + 1];
+    const float4 u = qinfo[3 * tid + 2];
+    mU = u.x;
+    mkey = (__float_as_uint(u.y) & 0xFFFFF000u) | (unsigned)tid;  // unique (Mpad <= 4096)
+  }
+  const int ne = Mpad / IA_TILE * NP * IA_WAVE;
+  h16x8 qe[NE];
+#pragma unroll
+  for (int i = 0; i < NE; i++) {
+    const int e = tid + WGT * i;
+    if (e < ne) qe[i] = qf[e];
+  }
+  if (tid < K) {
+    const int t = wg + nwg * tid;
+    wbox[2 * tid] = boxes[2 * t];
+    wbox[2 * tid + 1] = boxes[2 * t + 1];
+  }
+  if (tid < Mpad) skey[tid] = mkey;
+  __syncthreads();
+  K3P_T(ph[1]);
+
+  // ---- 2. sort, scatter to sorted slots, query-tile boxes
+  __shared__ int kctr;  // DYN: next tile index to hand out
+  if (tid == 0) kctr = NW;
+  if (DYN && Mpad > 256) {  // (uniform) below 256 queries the rank count is cheaper
+    // bitonic network over the 512 threads' unique keys (padding threads: 0xFFFFFFFF, last):
+    // exchanges at distance < 64 are lane swaps, the 6 at distance >= 64 go through LDS (the
+    // query-fragment area, free until the scatter below)
+    unsigned *sx = reinterpret_cast<unsigned *>(ldsh);
+    unsigned v = mkey;
+#pragma unroll
+    for (int kb = 2; kb <= WGT; kb <<= 1) {
+#pragma unroll
+      for (int jb = kb >> 1; jb > 0; jb >>= 1) {
+        unsigned o;
+        if (jb >= IA_WAVE) {
+          sx[tid] = v;
+          __syncthreads();
+          o = sx[tid ^ jb];
+          __syncthreads();
+        } else {
+          o = (unsigned)__shfl_xor((int)v, jb, 64);
+        }
+        const bool keep_min = ((tid & kb) == 0) == ((tid & jb) == 0);
+        v = keep_min ? min(v, o) : max(v, o);
+      }
+    }
+    if (tid < Mpad) {
+      const int q = (int)(v & 0xFFFu);
+      order[tid] = q;
+      rankof[q] = tid;
+    }
+    __syncthreads();
+    if (tid < Mpad) {
+      const int x = rankof[tid] - s0;
+      if (x >= 0 && x < NQ) {
+        qlo[x] = mlo;
+        qhi[x] = mhi;
+        qU[x] = mU;
+      }
+    }
+  } else if (tid < Mpad) {
+    int rank = 0;
+    for (int j = 0; j < Mpad; j += 4) {
+      const uint4 kk = *reinterpret_cast<const uint4 *>(skey + j);
+      rank += (int)(kk.x < mkey) + (int)(kk.y < mkey) + (int)(kk.z < mkey) + (int)(kk.w < mkey);
+    }
+    order[rank] = tid;
+    rankof[tid] = rank;
+    const int x = rank - s0;
+    if (x >= 0 && x < NQ) {
+      qlo[x] = mlo;
+      qhi[x] = mhi;
+      qU[x] = mU;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < NE; i++) {
+    const int e = tid + WGT * i;
+    if (e < ne) {
+      const int L = e & 63, pq = e >> 6, tq = pq / NP, p = pq - tq * NP;
+      const int x = rankof[tq * IA_TILE + (L & 31)] - s0;
+      if (x >= 0 && x < NQ) ldsh[((x >> 5) * NP + p) * IA_WAVE + (L & 32) + (x & 31)] = qe[i];
+    }
+  }
+  {
+    const int j = 2 * wave + half, x = j * IA_TILE + (lane & 31);
+    float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    float u = -INFINITY;
+    if (j < QT && qU[x] != -INFINITY) {  // padding slots (U' = -inf) never widen a box
+      lo = qlo[x];
+      hi = qhi[x];
+      u = qU[x];
+    }
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      lo.x = fminf(lo.x, __shfl_xor(lo.x, o, 64));
+      lo.y = fminf(lo.y, __shfl_xor(lo.y, o, 64));
+      lo.z = fminf(lo.z, __shfl_xor(lo.z, o, 64));
+      lo.w = fminf(lo.w, __shfl_xor(lo.w, o, 64));
+      hi.x = fmaxf(hi.x, __shfl_xor(hi.x, o, 64));
+      hi.y = fmaxf(hi.y, __shfl_xor(hi.y, o, 64));
+      hi.z = fmaxf(hi.z, __shfl_xor(hi.z, o, 64));
+      hi.w = fmaxf(hi.w, __shfl_xor(hi.w, o, 64));
+      u = fmaxf(u, __shfl_xor(u, o, 64));
+    }
+    if ((lane & 31) == 0 && j < QT) {
+      tlo[j] = lo;
+      thi[j] = hi;
+      tU[j] = u;
+    }
+  }
+  __syncthreads();
+  K3P_T(ph[2]);
+
+  float b1[QT], b2[QT];
+  int i1[QT];  // tile of b1 (packed epilogue)
+#pragma unroll
+  for (int q = 0; q < QT; q++) {
+    b1[q] = FLT_MAX;
+    b2[q] = FLT_MAX;
+    i1[q] = 0x7fffffff;
+  }
+  unsigned cnt = 0, ntl = 0;
+  if constexpr (INTER) {
+    // ---- 3'/4'. need tests interleaved with the contraction: wave v walks tiles k = v mod NW;
+    // while tile k is contracted, the next needed tile's load is in flight and the need tests
+    // after it run on the VALU (two buffers in rotation)
+    const bool cl = lane < QT;
+    const float4 ctl = cl ? tlo[lane] : make_float4(0.f, 0.f, 0.f, 0.f), cth = cl ? thi[lane] : ctl;
+    const float ctu = cl ? tU[lane] : -INFINITY;
+    auto need_k = [&](int k) -> unsigned {
+      const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
+      const unsigned coarse = (unsigned)__ballot(cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
+      unsigned msk = 0;
+#pragma unroll
+      for (int pr = 0; pr < NPAIR; pr++) {
+        if ((coarse >> (2 * pr)) & 3u) {
+          const int jq = 2 * pr + half, x = jq * IA_TILE + (lane & 31);
+          bool nd = false;
+          if (jq < QT) nd = prune_lb(blo, bhi, qlo[x], qhi[x]) <= qU[x];
+          const unsigned long long b = __ballot(nd);
+          msk |= (((unsigned)b != 0u ? 1u : 0u) | ((unsigned)(b >> 32) != 0u ? 2u : 0u)) << (2 * pr);
+        }
+      }
+      return msk & coarse;
+    };
+    // DYN: tiles handed out through an LDS counter (balances the waves' pair counts; the
+    // records stay exact, only which subset holds which row varies)
+    auto grab = [&]() -> int {
+      int g = 0;
+      if (lane == 0) g = atomicAdd(&kctr, 1);
+      return __builtin_amdgcn_readfirstlane(g);
+    };
+    auto next_k = [&](int k, unsigned &m) -> int {
+      for (; k < K; k = DYN ? grab() : k + NW) {
+        m = need_k(k);
+        if (m) return k;
+      }
+      m = 0;
+      return K;
+    };
+    unsigned m;
+    int k = next_k(wave, m);
+    if (k < K && k != min(wave, K - 1)) {
+      const h16x8 *src = db + (int64_t)(wg + nwg * k) * NP * IA_WAVE + lane;
+#pragma unroll
+      for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+    }
+    auto step = [&](const h16x8(&cur)[NP], h16x8(&nxt)[NP]) {
+      unsigned mn;
+      const int kn = next_k(DYN ? grab() : k + NW, mn);
+      if (kn < K) {  // wave-uniform
+        const h16x8 *src = db + (int64_t)(wg + nwg * kn) * NP * IA_WAVE + lane;
+#pragma unroll
+        for (int p = 0; p < NP; p++) nxt[p] = src[p * IA_WAVE];
+      }
+      asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
+      k3p_pairs<KS, QT, 0>(cur, ldsh + lane, m, wg + nwg * k, b1, b2, i1);
+      cnt += __popc(m);
+      ntl++;
+      k = kn;
+      m = mn;
+    };
+    while (k < K) {
+      step(a, an);
+      if (k >= K) break;
+      step(an, a);
+    }
+  } else {
+  // ---- 3. need masks of the workgroup's tiles
+  {
+    float4 fl[NPAIR], fh[NPAIR];
+    float fu[NPAIR];
+#pragma unroll
+    for (int pr = 0; pr < NPAIR; pr++) {
+      const int j = 2 * pr + half, x = j * IA_TILE + (lane & 31);
+      fl[pr] = j < QT ? qlo[x] : make_float4(0.f, 0.f, 0.f, 0.f);
+      fh[pr] = j < QT ? qhi[x] : make_float4(0.f, 0.f, 0.f, 0.f);
+      fu[pr] = j < QT ? qU[x] : -INFINITY;
+    }
+    const bool cl = lane < QT;
+    const float4 ctl = cl ? tlo[lane] : make_float4(0.f, 0.f, 0.f, 0.f), cth = cl ? thi[lane] : ctl;
+    const float ctu = cl ? tU[lane] : -INFINITY;
+    for (int k = wave; k < K; k += NW) {
+      const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
+      const unsigned coarse = (unsigned)__ballot(cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
+      unsigned msk = 0;
+#pragma unroll
+      for (int pr = 0; pr < NPAIR; pr++) {
+        if ((coarse >> (2 * pr)) & 3u) {
+          const unsigned long long b = __ballot(prune_lb(blo, bhi, fl[pr], fh[pr]) <= fu[pr]);
+          msk |= (((unsigned)b != 0u ? 1u : 0u) | ((unsigned)(b >> 32) != 0u ? 2u : 0u)) << (2 * pr);
+        }
+      }
+      if (lane == 0) kmask[k] = msk & coarse;
+    }
+  }
+  __syncthreads();
+  int n = 0;  // needed tiles of the workgroup
+  {  // compaction in tile order (thread k = tile k)
+    const bool nd = tid < K && kmask[tid] != 0u;
+    const unsigned long long b = __ballot(nd);
+    const int pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
+    if (lane == 0) wcnt[wave] = __popcll(b);
+    __syncthreads();
+    int base = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      base += w < wave ? wcnt[w] : 0;
+      n += wcnt[w];
+    }
+    if (nd) items[base + pre] = tid;
+    __syncthreads();
+  }
+  K3P_T(ph[3]);
+
+  // ---- 4. contract the needed pairs: item j -> wave j mod NW, two tiles in flight
+  auto tile_of = [&](int j) { return wg + nwg * items[j]; };
+  int j = wave;
+  if (j < n) {
+    if (items[j] != min(wave, K - 1)) {  // the speculative tile is not this wave's first item
+      const h16x8 *src = db + (int64_t)tile_of(j) * NP * IA_WAVE + lane;
+#pragma unroll
+      for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+    }
+    if (NBUF == 3 && j + NW < n) {
+      const h16x8 *src = db + (int64_t)tile_of(j + NW) * NP * IA_WAVE + lane;
+#pragma unroll
+      for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
+    }
+  }
+  // three tile buffers in rotation (no register copies: a copy of a loaded register waits for
+  // its load, which would collapse the prefetch depth to zero)
+  constexpr int AHEAD = (NBUF - 1) * NW;  // items in flight ahead of the one contracted
+  auto step = [&](const h16x8(&cur)[NP], h16x8(&nx2)[NP], int jj) {
+    if (jj + AHEAD < n) {  // wave-uniform
+      const h16x8 *src = db + (int64_t)tile_of(jj + AHEAD) * NP * IA_WAVE + lane;
+#pragma unroll
+      for (int p = 0; p < NP; p++) nx2[p] = src[p * IA_WAVE];
+    }
+    asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
+    const unsigned msk = kmask[items[jj]];
+    k3p_pairs<KS, QT, 0>(cur, ldsh + lane, msk, tile_of(jj), b1, b2, i1);
+    cnt += __popc(msk);
+    ntl++;
+  };
+  if constexpr (NBUF == 3) {
+    for (; j < n; j += 3 * NW) {
+      step(a, an2, j);
+      if (j + NW >= n) break;
+      step(an, a, j + NW);
+      if (j + 2 * NW >= n) break;
+      step(an2, an, j + 2 * NW);
+    }
+  } else {
+    for (; j < n; j += 2 * NW) {
+      step(a, an, j);
+      if (j + NW >= n) break;
+      step(an, a, j + NW);
+    }
+  }
+  }  // !INTER
+  K3P_T(ph[4]);
+#pragma unroll
+  for (int q = 0; q < QT; q++) {  // tile + packed in-tile index -> DB position
+    const int r = (int)(__float_as_uint(b1[q]) & 15u);
+    i1[q] = b1[q] == FLT_MAX ? 0x7fffffff : i1[q] * IA_TILE + 4 * half + (r & 3) + 8 * (r >> 2);
+  }
+
+  // ---- 5. merge the 2*NW subsets of each query; records go to the original query slots
+  __syncthreads();
+  if (lane == 0) {
+    wpairs[wave] = cnt;
+    wtiles[wave] = ntl;
+  }
+  Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32], inside the query-fragment area
+#pragma unroll
+  for (int q = 0; q < QT; q++) {
+    Top2 mine = {b1[q], FLT_MAX, b2[q], i1[q], 0x7fffffff};
+    Top2 other;
+    other.v1 = __shfl_xor(b1[q], 32, 64);
+    other.i1 = __shfl_xor(i1[q], 32, 64);
+    other.T = __shfl_xor(b2[q], 32, 64);
+    other.v2 = FLT_MAX;
+    other.i2 = 0x7fffffff;
+    Top2 mrg = half == 0 ? top2_merge(mine, other) : top2_merge(other, mine);
+    if (half == 0) red[(wave * QT + q) * IA_TILE + lane] = mrg;
+  }
+  __syncthreads();
+  for (int x = tid; x < NQ; x += WGT) {
+    Top2 m = red[x];
+#pragma unroll
+    for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
+    const int mq = order[s0 + x];
+    if (mq < M) {
+      const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
+      const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
+      rec[(int64_t)mq * nwg + wg] = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
+      recT[(int64_t)mq * nwg + wg] = m.T;
+    }
+  }
+  if (tid == 0) {  // the workgroup's own counter slots (stream-ordered launches: no atomics)
+    unsigned long long sp = 0, st = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      sp += wpairs[w];
+      st += wtiles[w];
+    }
+    pairs[wg] += sp;
+    tiles[wg] += st;
+  }
+#if IA_PROBE & 16
+  K3P_T(ph[5]);
+  if (lane == 0 && M == Mpad - 10 && wg < 8) {
+    atomicAdd(&k3p_prof[0], ph[1] - ph[0]);
+    atomicAdd(&k3p_prof[1], ph[2] - ph[1]);
+    atomicAdd(&k3p_prof[2], ph[3] - ph[2]);
+    atomicAdd(&k3p_prof[3], ph[4] - ph[3]);
+    atomicAdd(&k3p_prof[7], ph[5] - ph[4]);
+    atomicAdd(&k3p_prof[4], 1ull);
+    atomicAdd(&k3p_prof[5], (unsigned long long)ntl);
+    atomicAdd(&k3p_prof[6], (unsigned long long)cnt);
+  }
+#endif
+}
+
+#if (IA_PROBE & 16) && defined(IA_K3H_KS) && defined(IA_K3H_QT) && IA_K3H_KS == 4 && IA_K3H_QT == 11
+void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau wave, to stderr
+  unsigned long long v[12];
+  if (hipMemcpyFromSymbol(v, HIP_SYMBOL(k3p_prof), sizeof(v)) != hipSuccess || v[4] == 0) return;
+  if (v[10])
+    fprintf(stderr, "K3P_PROBE write phase: merge=%.0f pos2row=%.0f stores=%.0f atomics=%.0f\n", (double)v[7] / v[10],
+            (double)v[8] / v[10], (double)v[9] / v[10], (double)v[11] / v[10]);
+  fprintf(stderr, "K3P_PROBE v3 phases if variant>=3: load=setup, sort+scatter=need, need=loop, loop=tail, tail=[7]\n");
+  fprintf(stderr, "K3P_PROBE [7]=%.0f\n", (double)v[7] / v[4]);
+  fprintf(stderr, "K3P_PROBE waves=%llu setup=%.0f need=%.0f loop=%.0f tail=%.0f tiles/wave=%.2f pairs/wave=%.2f (cycles/wave)\n",
+          v[4], (double)v[0] / v[4], (double)v[1] / v[4], (double)v[2] / v[4], (double)v[3] / v[4], (double)v[5] / v[4],
+          (double)v[6] / v[4]);
+  unsigned long long z[12] = {};
+  (void)hipMemcpyToSymbol(HIP_SYMBOL(k3p_prof), z, sizeof(z));
+}
+#endif
+
 #if defined(IA_K3H_KS) && defined(IA_K3H_QT)
 // pruned scan instance (1 channel only: KS = 4)
-k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)() {
-  if constexpr (IA_K3H_KS == 4) return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE>;
-  else return nullptr;
+k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
+  if constexpr (IA_K3H_KS == 4) {
+    if (variant == 0) return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 0>;
+    if (variant == 2) return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2>;
+    if (variant == 3) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 3, false>;
+    if (variant == 4) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, false>;
+    if (variant == 5) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true>;
+    if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
+    return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
+  } else {
+    return nullptr;
+  }
 }
 #endif

@@ -1684,7 +1684,7 @@ void ia_launch_k3h(int KS, int qt, const void *db, const void *qf, int n_tiles, 
 }
 
 // pruned split-f16 distance kernels (ia_k3h.hip k3h_prune, 1 channel)
-#define IA_K3P_DECL(qt) k3p_fn ia_k3p_get_4_##qt();
+#define IA_K3P_DECL(qt) k3p_fn ia_k3p_get_4_##qt(int);
 IA_K3P_DECL(1) IA_K3P_DECL(2) IA_K3P_DECL(3) IA_K3P_DECL(4) IA_K3P_DECL(5) IA_K3P_DECL(6) IA_K3P_DECL(7) IA_K3P_DECL(8)
 IA_K3P_DECL(9) IA_K3P_DECL(10) IA_K3P_DECL(11)
 size_t ia_k3p_lds(int qt, int Mpad) {
@@ -1694,17 +1694,20 @@ size_t ia_k3p_lds(int qt, int Mpad) {
 }
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
-                   hipStream_t st) {
-  typedef k3p_fn (*getter)();
+                   unsigned long long *tiles, int variant, hipStream_t st) {
+  typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
-  const k3p_fn fn = g4[qt - 1]();
-  const size_t lds = ia_k3p_lds(qt, Mpad);
-  static int attr_lds[16] = {};
-  if ((int)lds > attr_lds[qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
+  const int kmax = (NT + nwg - 1) / nwg;  // DB tiles per workgroup
+  if (variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // v3/v4 limits (ia_k3h.hip IA_K3P3_*)
+  const k3p_fn fn = g4[qt - 1](variant);
+  const size_t lds = ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
+  static int attr_lds[7][16] = {};
+  const int vi = variant < 0 || variant > 6 ? 1 : variant;
+  if ((int)lds > attr_lds[vi][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_lds[qt] = (int)lds;
+    attr_lds[vi][qt] = (int)lds;
   }
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WGH), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row, NT,
-                     qt0, M, Mpad, nwg, rec, recT, pairs);
+                     qt0, M, Mpad, nwg, rec, recT, pairs, tiles);
 }

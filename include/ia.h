@@ -63,6 +63,8 @@ typedef struct {
   int64_t pruned_levels;    /* levels run on the certified pruned scan (option "prune") */
   double dist_pairs;        /* (DB tile, query tile) pairs the distance kernel contracted */
   double dist_pairs_full;   /* pairs an unpruned scan contracts (dist_pairs / this = work left) */
+  double dist_tiles;        /* DB tiles the distance kernel loaded (summed over its launches) */
+  double dist_tiles_full;   /* DB tiles an unpruned scan loads (dist_tiles / this = DB bytes left) */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),

@@ -10,9 +10,10 @@ import ia_amd  # noqa: F401
 pytestmark = pytest.mark.gpu
 
 
-def _run(ctx, job, prune):
+def _run(ctx, job, prune, variant=6):
     from ia_amd import _native
     ctx.set_option('prune', prune)
+    ctx.set_option('k3p_variant', variant)
     Bp = [x.copy() for x in job.Bp_init]
     S, IM = {}, {}
     st = _native.Stats()
@@ -24,15 +25,18 @@ def _run(ctx, job, prune):
                 Bp[level], job.weights, job.kappa_factor(level), st)
     finally:
         ctx.set_option('prune', 1)
+        ctx.set_option('k3p_variant', 6)
     return Bp, S, IM, st
 
 
-@pytest.mark.parametrize('size,n_pruned', [(512, 1), (1024, 2)])
-def test_pruned_equals_unpruned(ctx, size, n_pruned):
+@pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 6), (1024, 2, 6), (1024, 2, 5), (1024, 2, 4),
+                                                      (1024, 2, 3), (1024, 2, 1), (512, 1, 0), (512, 1, 2)])
+def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
+    """variant = the pruned-scan kernel version (option k3p_variant): every one is exact"""
     from ia_amd import synth
     job = synth.make_job(size)
     Bp0, S0, IM0, st0 = _run(ctx, job, 0)
-    Bp1, S1, IM1, st1 = _run(ctx, job, 1)
+    Bp1, S1, IM1, st1 = _run(ctx, job, 1, variant)
     assert st0.pruned_levels == 0 and st1.pruned_levels == n_pruned
     for level in range(1, job.L):
         assert np.array_equal(S0[level], S1[level]), level
@@ -41,11 +45,15 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned):
     assert st1.bound_violations == 0 and st0.bound_violations == 0
     assert st1.dist_pairs < st1.dist_pairs_full
     assert st1.dist_pairs_full == st0.dist_pairs_full
-    print('size %d: pairs left %.3f, fallbacks %d -> %d' % (size, st1.dist_pairs / st1.dist_pairs_full,
-                                                            st0.fallbacks, st1.fallbacks))
+    assert st1.dist_tiles <= st1.dist_tiles_full and st1.dist_tiles_full == st0.dist_tiles_full
+    print('size %d: pairs left %.3f, DB tiles loaded %.3f, fallbacks %d -> %d'
+          % (size, st1.dist_pairs / st1.dist_pairs_full, st1.dist_tiles / st1.dist_tiles_full, st0.fallbacks,
+             st1.fallbacks))
 
 
 def test_prune_option_rejects_bad_values(ctx):
     from ia_amd import _native
     with pytest.raises(_native.IAError):
         ctx.set_option('prune', 2)
+    with pytest.raises(_native.IAError):
+        ctx.set_option('k3p_variant', 7)
