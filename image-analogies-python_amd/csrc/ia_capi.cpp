@@ -85,7 +85,7 @@ struct ia_ctx {
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
   int prune = 1;
   int matcher = IA_MATCH_F16X3;  // option "matcher"
-  int k3p_variant = 6;           // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
+  int k3p_variant = 7;           // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   // per-step K3 timing (optional)
   int time_dist = 0;
@@ -259,7 +259,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
   if (!std::strcmp(name, "k3p_variant")) {
-    if (value < 0 || value > 6) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..6");
+    if (value < 0 || value > 7) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..7");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -564,7 +564,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
           ia_launch_k3p(qt, c->db.p, c->qf.p, c->qinfo.as<float4>(), c->boxes.as<float4>(), g.pos2row, g.n_tiles, qt0, sd.M,
                         sd.Mpad, g.nwg, c->rec.as<float4>(), c->recT.as<float>(),
                         c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0), c->pairs.as<unsigned long long>() + 2 * IA_NWG_H,
-                        c->k3p_variant, c->st);
+                        c->k3p_variant, sd.t, c->st);
         else if (use_h)
           ia_launch_k3h(g.KS, qt, c->db.p, c->qf.p, ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0, ma.NT, c->rec.as<float4>(),
                         c->recT.as<float>(), c->k3_variant, c->st);

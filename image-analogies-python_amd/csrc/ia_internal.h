@@ -26,6 +26,20 @@
 #define IA_NORM_SCALE 256.0 // split-f16 DB stores |a'|^2 / 256 (query column D holds 256)
 #define IA_F16_MAXABS 64.0  // split-f16 matcher only when every image value is within +-64
 
+// Split-f16 DB tile in HBM (k_db_build_h): pieces p = 2s + part (part 0 = hi, 1 = lo) of
+// 64 lanes x h16x8 in v_mfma_f32_32x32x16_f16 operand order.  When the upper half of the last
+// k-step is pure padding (KS = 4: columns 56..63, D + 1 = 56), its two pieces store lanes 0..31
+// only: 7 KiB instead of 8 KiB per tile, a 224 MiB 1024^2 DB that stays resident in the 256 MB
+// memory-side cache across steps.  Upper-half lanes re-load the lower half's (finite) values:
+// the query's columns there are zero, so those products are exact zeros.
+template <int KS>
+struct TileFmt {
+  static constexpr bool CMP = KS == 4;
+  static constexpr int STRIDE = CMP ? (2 * KS - 2) * IA_WAVE + 2 * IA_TILE : 2 * KS * IA_WAVE;  // h16x8 per tile
+  __host__ __device__ static constexpr int off(int p, int L) {
+    return (CMP && p >= 2 * KS - 2) ? (2 * KS - 2) * IA_WAVE + (p - (2 * KS - 2)) * IA_TILE + (L & 31) : p * IA_WAVE + L;
+  }
+};
 // nearest-neighbour matcher of the distance scan (option "matcher")
 #define IA_MATCH_F32 0      // v_mfma_f32_32x32x2_f32 on fp32 operands
 #define IA_MATCH_F16X3 1    // v_mfma_f32_32x32x16_f16 x3 on hi/lo-split f16 operands

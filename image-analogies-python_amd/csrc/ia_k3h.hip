@@ -14,6 +14,13 @@
 #include "ia_top2.h"
 #include "ia_prune.h"
 
+template <int KS>
+__device__ __forceinline__ void ld_tile(h16x8 (&a)[2 * KS], const h16x8 *__restrict__ db, int64_t tile, int lane) {
+  const h16x8 *src = db + tile * TileFmt<KS>::STRIDE;
+#pragma unroll
+  for (int p = 0; p < 2 * KS; p++) a[p] = src[TileFmt<KS>::off(p, lane)];
+}
+
 #ifndef IA_PROBE
 #define IA_PROBE 0
 #endif
@@ -111,9 +118,7 @@ k3h_scan(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, int n_tiles
 
   h16x8 a[NP], an[NP];
   {  // first DB tile: requested before the query fill so both latencies overlap
-    const h16x8 *src = db + (int64_t)min(t, n_tiles - 1) * NP * IA_WAVE + lane;
-#pragma unroll
-    for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+    ld_tile<KS>(a, db, min(t, n_tiles - 1), lane);
   }
   const h16x8 *qsrc = qf + (int64_t)qt0 * NP * IA_WAVE;
   for (int i = threadIdx.x; i < QT * NP * IA_WAVE; i += WGT) ldsh[i] = qsrc[i];
@@ -129,9 +134,7 @@ k3h_scan(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, int n_tiles
   }
   for (; t < t_end; t += NW) {
     {  // prefetch the next tile of this wave (clamped: always issue, never branch per load)
-      const h16x8 *src = db + (int64_t)min(t + NW, n_tiles - 1) * NP * IA_WAVE + lane;
-#pragma unroll
-      for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
+      ld_tile<KS>(an, db, min(t + NW, n_tiles - 1), lane);
     }
     const int rbase = row0 + t * IA_TILE + 4 * half;
     asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
@@ -313,7 +316,7 @@ __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
           const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
           float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
-          unsigned long long *__restrict__ tiles) {
+          unsigned long long *__restrict__ tiles, int rev) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   static_assert(QT <= 32, "need masks are 32-bit");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
@@ -335,9 +338,7 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
 
   h16x8 a[NP], an[NP];
   {  // speculative first tile (usually needed), overlapping the query setup
-    const h16x8 *src = db + (int64_t)min(t, NT - 1) * NP * IA_WAVE + lane;
-#pragma unroll
-    for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+    ld_tile<KS>(a, db, min(t, NT - 1), lane);
   }
   float4 rlo = make_float4(0.f, 0.f, 0.f, 0.f), rhi = rlo;  // V >= 1: boxes of the wave's tiles
   int chunk = -1;
@@ -454,17 +455,13 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
     unsigned msk = t < NT ? need(t) : 0u;
     if (!msk && t < NT) {
       t = next_needed(t + tstep, msk);
-      const h16x8 *src = db + (int64_t)min(t, NT - 1) * NP * IA_WAVE + lane;
-#pragma unroll
-      for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+      ld_tile<KS>(a, db, min(t, NT - 1), lane);
     }
     while (t < NT) {
       unsigned mn;
       const int tn = next_needed(t + tstep, mn);
       {
-        const h16x8 *src = db + (int64_t)min(tn, NT - 1) * NP * IA_WAVE + lane;
-#pragma unroll
-        for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
+        ld_tile<KS>(an, db, min(tn, NT - 1), lane);
       }
       asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
       // 3. the needed pairs of tile t
@@ -510,9 +507,7 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
     K3P_T(py);
     pneed += py - px;
     if (k > 0 && k < K) {  // the speculative first tile is not needed: load the first needed one
-      const h16x8 *src = db + (int64_t)(t0w + tstep * k) * NP * IA_WAVE + lane;
-#pragma unroll
-      for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+      ld_tile<KS>(a, db, (t0w + tstep * k), lane);
     }
     while (k < K) {
       unsigned mn;
@@ -522,9 +517,7 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
       pneed += py - px;
       if (kn < K) {  // wave-uniform; never a clamped dummy load: with every wave of the grid
                      // re-reading one tile at its end, that tile's L2 channel serialised ~16 MiB
-        const h16x8 *src = db + (int64_t)(t0w + tstep * kn) * NP * IA_WAVE + lane;
-#pragma unroll
-        for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
+        ld_tile<KS>(an, db, (t0w + tstep * kn), lane);
       }
       asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
       // 3. the needed pairs of tile t
@@ -668,7 +661,7 @@ __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
            float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
-           unsigned long long *__restrict__ tiles) {
+           unsigned long long *__restrict__ tiles, int rev) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   constexpr int NE = IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE / WGT;  // unsorted fragments per thread
   static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
@@ -685,6 +678,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   int *rankof = order + Mpad;                                           // [Mpad] query -> sorted
   const int wg = blockIdx.x;
   const int K = (NT - wg + nwg - 1) / nwg;  // tiles wg + nwg*k, k < K (host: nwg <= NT, K <= MAXK)
+  // rev: this step walks the workgroup's tiles in reverse (alternate steps: the tiles read last
+  // by one step are read first by the next, while they are still in the memory-side cache)
+  auto tk = [&](int k) { return wg + nwg * (rev ? K - 1 - k : k); };
   float4 *wbox = reinterpret_cast<float4 *>(rankof + Mpad);            // [2K] the WG's tile boxes
   unsigned *kmask = reinterpret_cast<unsigned *>(wbox + 2 * K);        // [K] need mask per tile
   int *items = reinterpret_cast<int *>(kmask + K);                     // [K] needed tiles, in order
@@ -699,9 +695,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   // ---- 1. one global round
   h16x8 a[NP], an[NP], an2[NP];
   {
-    const h16x8 *src = db + (int64_t)(wg + nwg * min(wave, K - 1)) * NP * IA_WAVE + lane;
-#pragma unroll
-    for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+    ld_tile<KS>(a, db, tk(min(wave, K - 1)), lane);
   }
   float4 mlo = make_float4(0.f, 0.f, 0.f, 0.f), mhi = mlo;
   float mU = -INFINITY;
@@ -721,7 +715,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     if (e < ne) qe[i] = qf[e];
   }
   if (tid < K) {
-    const int t = wg + nwg * tid;
+    const int t = tk(tid);
     wbox[2 * tid] = boxes[2 * t];
     wbox[2 * tid + 1] = boxes[2 * t + 1];
   }
@@ -874,20 +868,16 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     unsigned m;
     int k = next_k(wave, m);
     if (k < K && k != min(wave, K - 1)) {
-      const h16x8 *src = db + (int64_t)(wg + nwg * k) * NP * IA_WAVE + lane;
-#pragma unroll
-      for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+      ld_tile<KS>(a, db, tk(k), lane);
     }
     auto step = [&](const h16x8(&cur)[NP], h16x8(&nxt)[NP]) {
       unsigned mn;
       const int kn = next_k(DYN ? grab() : k + NW, mn);
       if (kn < K) {  // wave-uniform
-        const h16x8 *src = db + (int64_t)(wg + nwg * kn) * NP * IA_WAVE + lane;
-#pragma unroll
-        for (int p = 0; p < NP; p++) nxt[p] = src[p * IA_WAVE];
+        ld_tile<KS>(nxt, db, tk(kn), lane);
       }
       asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-      k3p_pairs<KS, QT, 0>(cur, ldsh + lane, m, wg + nwg * k, b1, b2, i1);
+      k3p_pairs<KS, QT, 0>(cur, ldsh + lane, m, tk(k), b1, b2, i1);
       cnt += __popc(m);
       ntl++;
       k = kn;
@@ -947,18 +937,14 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   K3P_T(ph[3]);
 
   // ---- 4. contract the needed pairs: item j -> wave j mod NW, two tiles in flight
-  auto tile_of = [&](int j) { return wg + nwg * items[j]; };
+  auto tile_of = [&](int j) { return tk(items[j]); };
   int j = wave;
   if (j < n) {
     if (items[j] != min(wave, K - 1)) {  // the speculative tile is not this wave's first item
-      const h16x8 *src = db + (int64_t)tile_of(j) * NP * IA_WAVE + lane;
-#pragma unroll
-      for (int p = 0; p < NP; p++) a[p] = src[p * IA_WAVE];
+      ld_tile<KS>(a, db, tile_of(j), lane);
     }
     if (NBUF == 3 && j + NW < n) {
-      const h16x8 *src = db + (int64_t)tile_of(j + NW) * NP * IA_WAVE + lane;
-#pragma unroll
-      for (int p = 0; p < NP; p++) an[p] = src[p * IA_WAVE];
+      ld_tile<KS>(an, db, tile_of(j + NW), lane);
     }
   }
   // three tile buffers in rotation (no register copies: a copy of a loaded register waits for
@@ -966,9 +952,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   constexpr int AHEAD = (NBUF - 1) * NW;  // items in flight ahead of the one contracted
   auto step = [&](const h16x8(&cur)[NP], h16x8(&nx2)[NP], int jj) {
     if (jj + AHEAD < n) {  // wave-uniform
-      const h16x8 *src = db + (int64_t)tile_of(jj + AHEAD) * NP * IA_WAVE + lane;
-#pragma unroll
-      for (int p = 0; p < NP; p++) nx2[p] = src[p * IA_WAVE];
+      ld_tile<KS>(nx2, db, tile_of(jj + AHEAD), lane);
     }
     asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
     const unsigned msk = kmask[items[jj]];

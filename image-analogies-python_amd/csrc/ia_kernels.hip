@@ -577,9 +577,9 @@ __global__ void __launch_bounds__(IA_WG) k_db_build_h(LevelGeo g, Imgs A, const 
         vh[e] = hi;
         vl[e] = lo;
       }
-      if (inr) {
-        db[(ltile * NP + 2 * s) * IA_WAVE + h * IA_TILE + j] = vh;
-        db[(ltile * NP + 2 * s + 1) * IA_WAVE + h * IA_TILE + j] = vl;
+      if (inr && !(TileFmt<KS>::CMP && s == KS - 1 && h == 1)) {  // (compact: padding half not stored)
+        db[ltile * TileFmt<KS>::STRIDE + TileFmt<KS>::off(2 * s, h * IA_TILE + j)] = vh;
+        db[ltile * TileFmt<KS>::STRIDE + TileFmt<KS>::off(2 * s + 1, h * IA_TILE + j)] = vl;
       }
     }
   }
@@ -1694,11 +1694,13 @@ size_t ia_k3p_lds(int qt, int Mpad) {
 }
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
-                   unsigned long long *tiles, int variant, hipStream_t st) {
+                   unsigned long long *tiles, int variant, int step, hipStream_t st) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
   const int kmax = (NT + nwg - 1) / nwg;  // DB tiles per workgroup
+  const int rev = variant == 7 ? (step & 1) : 0;  // 7: variant 6 walking alternate steps in reverse
+  if (variant == 7) variant = 6;
   if (variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // v3/v4 limits (ia_k3h.hip IA_K3P3_*)
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t lds = ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
@@ -1709,5 +1711,5 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
     attr_lds[vi][qt] = (int)lds;
   }
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WGH), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row, NT,
-                     qt0, M, Mpad, nwg, rec, recT, pairs, tiles);
+                     qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev);
 }
