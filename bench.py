@@ -36,7 +36,7 @@ sys.path.insert(0, ROOT)
 METRIC = "B' pixels synthesized/sec, exact NN, 1024² A/A'/B, 1/2/4/8 GPUs; % MFMA peak"
 FP32_MFMA_PEAK = 157.3e12   # MI355X_MICROARCH.md: Peak FP32 (matrix), dense
 F16_MFMA_PEAK = 2.5e15      # MI355X_MICROARCH.md: BF16/F16 ~2.5 PF dense (same cycles for f16)
-HBM_PEAK = 8.0e12
+HBM_PEAK = 8.0e12           # MI355X_MICROARCH.md: HBM3E ~8 TB/s
 
 
 def log(*a):
@@ -121,8 +121,8 @@ def main():
     ap.add_argument('--time-stride', type=int, default=4, help='sample K3 timing every S-th wavefront step')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'k3_traffic.json'),
-                    help='per-launch HBM bytes of k3_dist from a rocprofv3 --pmc pass (optional)')
+    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'k3p_traffic.json'),
+                    help='per-launch HBM bytes of the dominant K3 kernel from a rocprofv3 --pmc pass (optional)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
@@ -199,15 +199,35 @@ def main():
     # MFMA flops the kernel issues per algorithmic flop: 3 f16 passes over 16*KS padded k
     # (split-f16) or 2*KH padded k (fp32); query-tile padding to 32 not included
     issued = 3.0 * 16 * {1: 4, 2: 7}.get(ch, 0) / D if f16 else (56 if ch == 1 else 112 if ch == 2 else 168) / D
-    roofline = {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': peak / 1e12, 'unit': 'TFLOP/s',
-                'frac': achieved / peak, 'traffic': traffic,
-                'mfma_issue_frac': achieved * issued / peak,
-                'kernel': (('k3h_prune (certified pruned scan; ' if st['pruned_levels'] else 'k3h_scan (') +
-                           '3 x v_mfma_f32_32x32x16_f16 on hi/lo-split operands, fused packed-index top-2)' if f16 else
-                           'k3_dist (v_mfma_f32_32x32x2_f32 distance scan + fused top-2)'),
-                'k3_us_per_launch': k3_ms_per_launch * 1e3, 'k3_launches_sampled': st['dist_launches_timed'],
-                'k3_share_of_step': st['dist_ms'] * (st['dist_flops'] / max(st['dist_flops_timed'], 1)) /
-                max(elapsed * 1e3, 1e-9)}
+    if st['prune_launches_timed'] > 0:
+        # the dominant kernel is the pruned scan (k3h_prune3), and it streams the DB tiles it
+        # needs: its roofline is HBM.  achieved = algorithmic bytes (DB tiles loaded x 7 KiB +
+        # tile boxes + queries + records) / device time of its timed launches
+        p_s = st['prune_ms_timed'] * 1e-3
+        p_bytes = st['prune_bytes_timed'] / st['prune_launches_timed']
+        p_gbs = st['prune_bytes_timed'] / p_s / 1e9
+        p_tf = st['prune_flops_timed'] / p_s / 1e12
+        roofline = {'bound': 'hbm', 'achieved': p_gbs, 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s',
+                    'frac': p_gbs * 1e9 / HBM_PEAK, 'traffic': traffic,
+                    'algorithmic_bytes_per_launch': p_bytes,
+                    'kernel': 'k3h_prune3 (certified pruned scan: PCA-box need tests, split-f16 '
+                              '3 x v_mfma_f32_32x32x16_f16, fused packed-index top-2)',
+                    'k3_us_per_launch': st['prune_ms_timed'] * 1e3 / st['prune_launches_timed'],
+                    'k3_launches_sampled': st['prune_launches_timed'],
+                    'mfma_achieved_tflops': p_tf, 'mfma_peak_tflops': peak / 1e12,
+                    'mfma_frac': p_tf * 1e12 / peak, 'mfma_issue_frac': p_tf * 1e12 * issued / peak,
+                    'all_k3_mfma_tflops': achieved / 1e12,
+                    'k3_share_of_step': st['dist_ms'] * (st['dist_flops'] / max(st['dist_flops_timed'], 1)) /
+                    max(elapsed * 1e3, 1e-9)}
+    else:
+        roofline = {'bound': 'mfma', 'achieved': achieved / 1e12, 'peak': peak / 1e12, 'unit': 'TFLOP/s',
+                    'frac': achieved / peak, 'traffic': traffic,
+                    'mfma_issue_frac': achieved * issued / peak,
+                    'kernel': ('k3h_scan (3 x v_mfma_f32_32x32x16_f16 on hi/lo-split operands, fused packed-index top-2)'
+                               if f16 else 'k3_dist (v_mfma_f32_32x32x2_f32 distance scan + fused top-2)'),
+                    'k3_us_per_launch': k3_ms_per_launch * 1e3, 'k3_launches_sampled': st['dist_launches_timed'],
+                    'k3_share_of_step': st['dist_ms'] * (st['dist_flops'] / max(st['dist_flops_timed'], 1)) /
+                    max(elapsed * 1e3, 1e-9)}
 
     out = {'metric': METRIC, 'value': value, 'unit': "B' px/s", 'n_gpus': world, 'steps': args.steps,
            'warmup': args.warmup, 'ms_per_step': elapsed * 1e3 / args.steps, 'higher_is_better': True,

@@ -38,7 +38,9 @@ class Stats(ctypes.Structure):
                 ('dist_flops_timed', ctypes.c_double), ('bound_violations', ctypes.c_int64),
                 ('f16_levels', ctypes.c_int64), ('pruned_levels', ctypes.c_int64),
                 ('dist_pairs', ctypes.c_double), ('dist_pairs_full', ctypes.c_double),
-                ('dist_tiles', ctypes.c_double), ('dist_tiles_full', ctypes.c_double)]
+                ('dist_tiles', ctypes.c_double), ('dist_tiles_full', ctypes.c_double),
+                ('prune_ms_timed', ctypes.c_double), ('prune_launches_timed', ctypes.c_int64),
+                ('prune_flops_timed', ctypes.c_double), ('prune_bytes_timed', ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

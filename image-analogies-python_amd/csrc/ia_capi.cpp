@@ -480,10 +480,11 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       (rc = c->rec.ensure((size_t)Mmax * std::max(g.nwg, 1) * 16)) ||
       (rc = c->recT.ensure((size_t)Mmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mmax * 16)) ||
       (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(4 * 8)) ||
-      (rc = c->pstat.ensure((size_t)NB * 4)) || (rc = c->pairs.ensure(3 * IA_NWG_H * 8)) ||
+      (rc = c->pstat.ensure((size_t)NB * 4)) || (rc = c->pairs.ensure(4 * IA_NWG_H * 8)) ||
       (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 : 16)))
     return rc;
-  HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 3 * IA_NWG_H * 8, c->st));  // [untimed pairs | timed pairs | tiles][wg]
+  // per-workgroup counters of the pruned scan: [pairs | pairs (timed steps) | tiles | tiles (timed)][wg]
+  HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 4 * IA_NWG_H * 8, c->st));
   HIP_TRY(hipMemsetAsync(c->Rbits.p, 0, 4, c->st));
   HIP_TRY(hipMemsetAsync(c->counters.p, 0, 4 * 8, c->st));
   HIP_TRY(hipMemsetAsync(c->pstat.p, 0, (size_t)NB * 4, c->st));
@@ -539,7 +540,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     for (size_t i = old; i < c->evs.size(); i++) hipEventCreate(&c->evs[i]);
   }
   int64_t dist_launches = 0, launches_timed = 0, n_rec = 0;
-  double dist_flops = 0., flops_timed = 0., pairs_full = 0., tiles_full = 0.;
+  double dist_flops = 0., flops_timed = 0., pairs_full = 0., tiles_full = 0., bytes_timed_fixed = 0.;
   for (int64_t t = 0; t < T; t++) {
     StepDesc sd;
     sd.t = (int)t;
@@ -563,7 +564,8 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
         if (prune)
           ia_launch_k3p(qt, c->db.p, c->qf.p, c->qinfo.as<float4>(), c->boxes.as<float4>(), g.pos2row, g.n_tiles, qt0, sd.M,
                         sd.Mpad, g.nwg, c->rec.as<float4>(), c->recT.as<float>(),
-                        c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0), c->pairs.as<unsigned long long>() + 2 * IA_NWG_H,
+                        c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
+                        c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
                         c->k3p_variant, sd.t, c->st);
         else if (use_h)
           ia_launch_k3h(g.KS, qt, c->db.p, c->qf.p, ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0, ma.NT, c->rec.as<float4>(),
@@ -580,6 +582,10 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
         if (timed) {
           flops_timed += fl;
           launches_timed++;
+          // algorithmic bytes of a pruned launch besides its DB tiles: tile boxes, query
+          // fragments and pruning records, K3 records written
+          bytes_timed_fixed += (double)g.n_tiles * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) +
+                               (double)mq * g.nwg * 20;
         }
         qt0 += qt;
       }
@@ -608,12 +614,12 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   if (prune) ia_k3p_probe_dump();
 #endif
   if (stats) {
-    unsigned long long ctr[4], prs[3];
+    unsigned long long ctr[4], prs[4];
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
     {  // per-workgroup counter slots (no same-address atomics in the distance kernel)
-      std::vector<unsigned long long> slots(3 * IA_NWG_H);
+      std::vector<unsigned long long> slots(4 * IA_NWG_H);
       HIP_TRY(hipMemcpy(slots.data(), c->pairs.p, slots.size() * 8, hipMemcpyDeviceToHost));
-      for (int j = 0; j < 3; j++) {
+      for (int j = 0; j < 4; j++) {
         prs[j] = 0;
         for (int w = 0; w < IA_NWG_H; w++) prs[j] += slots[j * IA_NWG_H + w];
       }
@@ -626,7 +632,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     stats->pruned_levels += prune ? 1 : 0;
     stats->dist_pairs += prune ? (double)(prs[0] + prs[1]) : pairs_full;
     stats->dist_pairs_full += pairs_full;
-    stats->dist_tiles += prune ? (double)prs[2] : tiles_full;
+    stats->dist_tiles += prune ? (double)(prs[2] + prs[3]) : tiles_full;
     stats->dist_tiles_full += tiles_full;
     float ms_db = 0.f, ms_syn = 0.f;
     hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
@@ -652,6 +658,12 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       stats->dist_ms += tot;
       stats->dist_launches_timed += launches_timed;
       stats->dist_flops_timed += flops_timed;
+      if (prune) {  // the pruned scan alone (bench roofline): time, MFMA flops, algorithmic bytes
+        stats->prune_ms_timed += tot;
+        stats->prune_launches_timed += launches_timed;
+        stats->prune_flops_timed += flops_timed;
+        stats->prune_bytes_timed += (double)prs[3] * ia_k3h_tile_bytes(g.KS) + bytes_timed_fixed;
+      }
     }
   }
   return IA_OK;

@@ -1584,6 +1584,7 @@ void ia_launch_merge_dense(const MergeArgs &ma, const double *pts, int d, const 
 }
 
 // ---- split-f16 matcher launchers -----------------------------------------------------------
+double ia_k3h_tile_bytes(int KS) { return KS == 4 ? 16.0 * TileFmt<4>::STRIDE : KS == 7 ? 16.0 * TileFmt<7>::STRIDE : 0.; }
 int ia_ks_for(int ch) { return ch == 1 ? 4 : ch == 2 ? 7 : 0; }  // 3 channels: fp32 matcher
 int ia_k3h_qtmax(int KS) { return KS == 4 ? 11 : 8; }
 // waves per workgroup of the K3h instance selected by (KS, qt, variant) (ia_k3h.hip getters)

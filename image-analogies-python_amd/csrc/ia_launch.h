@@ -27,6 +27,7 @@ void ia_launch_merge_dense(const MergeArgs &ma, const double *pts, int d, const 
                            double *dist, hipStream_t st);
 // split-f16 matcher (IA_MATCH_F16X3)
 int ia_ks_for(int ch);
+double ia_k3h_tile_bytes(int KS);  // HBM bytes of one split-f16 DB tile (TileFmt)
 int ia_k3h_qtmax(int KS);
 size_t ia_k3h_lds(int KS, int qt);
 void ia_launch_absmax(const double *const *p, const int64_t *n, unsigned *out, hipStream_t st);

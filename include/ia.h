@@ -65,6 +65,10 @@ typedef struct {
   double dist_pairs_full;   /* pairs an unpruned scan contracts (dist_pairs / this = work left) */
   double dist_tiles;        /* DB tiles the distance kernel loaded (summed over its launches) */
   double dist_tiles_full;   /* DB tiles an unpruned scan loads (dist_tiles / this = DB bytes left) */
+  double prune_ms_timed;    /* pruned-scan launches of the timed steps (option "time_dist"): device ms */
+  int64_t prune_launches_timed;
+  double prune_flops_timed; /* their MFMA flops (computed pairs x 2 D 32 32) */
+  double prune_bytes_timed; /* their algorithmic bytes (DB tiles loaded, boxes, queries, records) */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
