@@ -81,7 +81,7 @@ struct ia_ctx {
   DevBuf A, Ac, Ap, Apc, B, Bc, Bpc, Bp, S, IM, W;
   DevBuf db, db64, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, pstat, absmax;
   // certified pruned scan (option "prune"): per-level basis, sorted DB table, tile boxes
-  DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs;
+  DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs, ord;
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
   int prune = 1;
   int matcher = IA_MATCH_F16X3;  // option "matcher"
@@ -241,7 +241,7 @@ void ia_destroy(ia_ctx *c) {
   for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->B, &c->Bc, &c->Bpc, &c->Bp, &c->S, &c->IM, &c->W, &c->db, &c->db64,
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->pstat, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
-                    &c->boxes, &c->qinfo, &c->pairs})
+                    &c->boxes, &c->qinfo, &c->pairs, &c->ord})
     b->release();
   for (hipEvent_t e : c->evs) hipEventDestroy(e);
   hipEventDestroy(c->lv0);
@@ -259,7 +259,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
   if (!std::strcmp(name, "k3p_variant")) {
-    if (value < 0 || value > 7) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..7");
+    if (value < 0 || value > 8) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..8");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -480,7 +480,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       (rc = c->rec.ensure((size_t)Mmax * std::max(g.nwg, 1) * 16)) ||
       (rc = c->recT.ensure((size_t)Mmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mmax * 16)) ||
       (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(4 * 8)) ||
-      (rc = c->pstat.ensure((size_t)NB * 4)) || (rc = c->pairs.ensure(4 * IA_NWG_H * 8)) ||
+      (rc = c->pstat.ensure((size_t)NB * 4)) || (rc = c->pairs.ensure(4 * IA_NWG_H * 8)) || (rc = c->ord.ensure(2 * 4096 * 4)) ||
       (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 : 16)))
     return rc;
   // per-workgroup counters of the pruned scan: [pairs | pairs (timed steps) | tiles | tiles (timed)][wg]
@@ -541,11 +541,15 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   }
   int64_t dist_launches = 0, launches_timed = 0, n_rec = 0;
   double dist_flops = 0., flops_timed = 0., pairs_full = 0., tiles_full = 0., bytes_timed_fixed = 0.;
+  int ord_n = 0;  // pruned scan (k3p_variant 8): queries in the previous step's key order
   for (int64_t t = 0; t < T; t++) {
     StepDesc sd;
     sd.t = (int)t;
     ia_wavefront_step(g.bh, g.bw, t, &sd.r0, &sd.M);
-    if (sd.M <= 0) continue;  // levels narrower than 3 columns have empty steps
+    if (sd.M <= 0) {  // levels narrower than 3 columns have empty steps
+      ord_n = 0;
+      continue;
+    }
     sd.Mpad = (sd.M + IA_TILE - 1) / IA_TILE * IA_TILE;
     if (prune)
       ia_launch_gather_p(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
@@ -566,7 +570,8 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
                         sd.Mpad, g.nwg, c->rec.as<float4>(), c->recT.as<float>(),
                         c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                         c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
-                        c->k3p_variant, sd.t, c->st);
+                        c->k3p_variant, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
+                        c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), c->st);
         else if (use_h)
           ia_launch_k3h(g.KS, qt, c->db.p, c->qf.p, ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0, ma.NT, c->rec.as<float4>(),
                         c->recT.as<float>(), c->k3_variant, c->st);
@@ -590,6 +595,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
         qt0 += qt;
       }
       if (timed) hipEventRecord(c->evs[2 * n_rec++ + 1], c->st);
+      ord_n = prune && sd.Mpad <= 4096 ? sd.M : 0;
     }
     if (!sharded) {
       ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), dS, dIM, dBp, (const double *)dW, a->kappa_factor, true, c->st);

@@ -316,7 +316,8 @@ __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
           const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
           float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
-          unsigned long long *__restrict__ tiles, int rev) {
+          unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
+           int r0, int *__restrict__ ord_out) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   static_assert(QT <= 32, "need masks are 32-bit");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
@@ -656,12 +657,13 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // ------------------------------------------------------------------------------------------
 #define IA_K3P3_MAXQ 512   // queries per step (one per thread)
 #define IA_K3P3_MAXK 512   // DB tiles per workgroup
-template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false>
+template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
            float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
-           unsigned long long *__restrict__ tiles, int rev) {
+           unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
+           int r0, int *__restrict__ ord_out) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   constexpr int NE = IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE / WGT;  // unsorted fragments per thread
   static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
@@ -719,14 +721,67 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     wbox[2 * tid] = boxes[2 * t];
     wbox[2 * tid + 1] = boxes[2 * t + 1];
   }
-  if (tid < Mpad) skey[tid] = mkey;
+  if (tid < Mpad) {
+    skey[tid] = mkey;
+    rankof[tid] = -1;
+  }
+  const int prow = ORD && tid < n_in ? ord_in[tid] : -1;
   __syncthreads();
   K3P_T(ph[1]);
+  if (ORD && qt0 == 0 && wave == 0) {
+    // ORD: this step's exact key order, for the NEXT step (its queries are these pixels' right
+    // neighbours, whose features are close): workgroup w ranks queries w, w + nwg, ... and
+    // writes their rows at their ranks, so the grid writes the whole order once
+    for (int q = wg; q < M; q += nwg) {
+      const unsigned kq = skey[q];
+      int c = 0;
+      for (int j = lane; j < Mpad; j += IA_WAVE) c += (int)(skey[j] < kq);
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
+      if (lane == 0) ord_out[c] = r0 + q;
+    }
+  }
 
   // ---- 2. sort, scatter to sorted slots, query-tile boxes
   __shared__ int kctr;  // DYN: next tile index to hand out
   if (tid == 0) kctr = NW;
-  if (DYN && Mpad > 256) {  // (uniform) below 256 queries the rank count is cheaper
+  if (ORD && n_in > 0) {  // (uniform) the previous step's order: no sort on the critical path
+    // rows of the previous order still in this step keep their relative order; then the new
+    // rows, then padding, by index (any grouping is exact: it only steers the pruning)
+    const int pm = prow - r0;
+    const bool v1 = tid < n_in && pm >= 0 && pm < M;
+    unsigned long long b = __ballot(v1);
+    int pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
+    if (lane == 0) wcnt[wave] = __popcll(b);
+    __syncthreads();
+    int base = 0, nvalid = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) {
+      base += w < wave ? wcnt[w] : 0;
+      nvalid += wcnt[w];
+    }
+    if (v1) rankof[pm] = base + pre;
+    __syncthreads();
+    const bool un = tid < Mpad && rankof[tid] < 0;
+    b = __ballot(un);
+    pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
+    if (lane == 0) wcnt[wave] = __popcll(b);
+    __syncthreads();
+    base = nvalid;
+#pragma unroll
+    for (int w = 0; w < NW; w++) base += w < wave ? wcnt[w] : 0;
+    if (un) rankof[tid] = base + pre;
+    if (tid < Mpad) {
+      const int rk = rankof[tid];
+      order[rk] = tid;
+      const int x = rk - s0;
+      if (x >= 0 && x < NQ) {
+        qlo[x] = mlo;
+        qhi[x] = mhi;
+        qU[x] = mU;
+      }
+    }
+  } else if (DYN && Mpad > 256) {  // (uniform) below 256 queries the rank count is cheaper
     // bitonic network over the 512 threads' unique keys (padding threads: 0xFFFFFFFF, last):
     // exchanges at distance < 64 are lane swaps, the 6 at distance >= 64 go through LDS (the
     // query-fragment area, free until the scatter below)
@@ -828,6 +883,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   }
   unsigned cnt = 0, ntl = 0;
   if constexpr (INTER) {
+    K3P_T(ph[3]);
     // ---- 3'/4'. need tests interleaved with the contraction: wave v walks tiles k = v mod NW;
     // while tile k is contracted, the next needed tile's load is in flight and the need tests
     // after it run on the VALU (two buffers in rotation)
@@ -1067,6 +1123,7 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     if (variant == 4) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, false>;
     if (variant == 5) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true>;
     if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
+    if (variant == 8) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, true>;
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

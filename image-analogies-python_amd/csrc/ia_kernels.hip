@@ -1695,22 +1695,23 @@ size_t ia_k3p_lds(int qt, int Mpad) {
 }
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
-                   unsigned long long *tiles, int variant, int step, hipStream_t st) {
+                   unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
+                   hipStream_t st) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
   const int kmax = (NT + nwg - 1) / nwg;  // DB tiles per workgroup
-  const int rev = variant == 7 ? (step & 1) : 0;  // 7: variant 6 walking alternate steps in reverse
-  if (variant == 7) variant = 6;
+  const int rev = variant >= 7 ? (step & 1) : 0;  // 7, 8: alternate steps walk in reverse
+  if (variant == 7) variant = 6;  // 8: + the previous step's query order (no sort)
   if (variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // v3/v4 limits (ia_k3h.hip IA_K3P3_*)
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t lds = ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
-  static int attr_lds[7][16] = {};
-  const int vi = variant < 0 || variant > 6 ? 1 : variant;
+  static int attr_lds[9][16] = {};
+  const int vi = variant < 0 || variant > 8 ? 1 : variant;
   if ((int)lds > attr_lds[vi][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_lds[vi][qt] = (int)lds;
   }
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WGH), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row, NT,
-                     qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev);
+                     qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out);
 }

@@ -53,4 +53,5 @@ void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
 size_t ia_k3p_lds(int qt, int Mpad);
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
-                   unsigned long long *tiles, int variant, int step, hipStream_t st);
+                   unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
+                   hipStream_t st);

@@ -39,4 +39,5 @@ __device__ __forceinline__ Top2 top2_merge(Top2 a, const Top2 &b) {
 typedef void (*k3h_fn)(const h16x8 *, const h16x8 *, int, int, int, int, int, int, int, float4 *, float *);
 // pruned split-f16 distance kernel entry (ia_k3h.hip, k3h_prune)
 typedef void (*k3p_fn)(const h16x8 *, const h16x8 *, const float4 *, const float4 *, const int *, int, int, int, int, int,
-                       float4 *, float *, unsigned long long *, unsigned long long *, int);
+                       float4 *, float *, unsigned long long *, unsigned long long *, int, const int *, int, int,
+                       int *);
