@@ -259,7 +259,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
   if (!std::strcmp(name, "k3p_variant")) {
-    if (value < 0 || value > 8) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..8");
+    if (value < 0 || value > 10) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..10");
     c->k3p_variant = value;
     return IA_OK;
   }

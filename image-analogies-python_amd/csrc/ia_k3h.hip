@@ -272,6 +272,24 @@ __device__ __forceinline__ void k3p_epi1(const f32x16 &e, int t, float &b1, floa
 // query-tile pairs QP.. of one DB tile t; m2 = the pair's two need bits (wave-uniform).  A pair
 // with one needed tile runs one chain on it; its query state is selected with v_cndmask (never
 // a dynamically indexed register array, which would live in scratch)
+// software-pipelined alternative (PIPE): one chain per needed query tile, into accumulators
+// alternating by the tile's parity (static indices, no copies); the epilogue of tile q - 1 is
+// issued after the MFMAs of tile q, so the VALU work overlaps the matrix core
+template <int KS, int QT, int Q>
+__device__ __forceinline__ void k3p_pipe(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, int t, float (&b1)[QT],
+                                         float (&b2)[QT], int (&i1)[QT], f32x16 (&acc)[2]) {
+  if constexpr (Q <= QT) {
+    constexpr int NP = 2 * KS;
+    if constexpr (Q < QT) {
+      if ((msk >> Q) & 1u) acc[Q & 1] = k3p_chain<KS>(a, lq + Q * NP * IA_WAVE);
+    }
+    if constexpr (Q >= 1) {
+      if ((msk >> (Q - 1)) & 1u) k3p_epi1(acc[(Q - 1) & 1], t, b1[Q - 1], b2[Q - 1], i1[Q - 1]);
+    }
+    k3p_pipe<KS, QT, Q + 1>(a, lq, msk, t, b1, b2, i1, acc);
+  }
+}
+
 template <int KS, int QT, int QP>
 __device__ __forceinline__ void k3p_pairs(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, int t, float (&b1)[QT],
                                           float (&b2)[QT], int (&i1)[QT]) {
@@ -657,7 +675,7 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // ------------------------------------------------------------------------------------------
 #define IA_K3P3_MAXQ 512   // queries per step (one per thread)
 #define IA_K3P3_MAXK 512   // DB tiles per workgroup
-template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false>
+template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false, bool PIPE = false>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
@@ -714,7 +732,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
 #pragma unroll
   for (int i = 0; i < NE; i++) {
     const int e = tid + WGT * i;
-    if (e < ne) qe[i] = qf[e];
+    qe[i] = qf[e < ne ? e : 0];  // unconditional: equal vmcnt on every path
   }
   if (tid < K) {
     const int t = tk(tid);
@@ -923,17 +941,23 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     };
     unsigned m;
     int k = next_k(wave, m);
-    if (k < K && k != min(wave, K - 1)) {
-      ld_tile<KS>(a, db, tk(k), lane);
-    }
+    // (re)load the first needed tile unconditionally (usually the speculative one again: a
+    // cache hit), so the loop is entered with the same outstanding loads on every path
+    ld_tile<KS>(a, db, tk(k < K ? k : min(wave, K - 1)), lane);
     auto step = [&](const h16x8(&cur)[NP], h16x8(&nxt)[NP]) {
       unsigned mn;
       const int kn = next_k(DYN ? grab() : k + NW, mn);
-      if (kn < K) {  // wave-uniform
-        ld_tile<KS>(nxt, db, tk(kn), lane);
-      }
+      // always issue the 8 loads (past the last tile: the current tile again, an L2 hit): with a
+      // conditional prefetch the compiler's vmcnt at the join covers the no-load path, which
+      // makes the MFMAs below wait for the prefetch itself
+      ld_tile<KS>(nxt, db, tk(kn < K ? kn : k), lane);
       asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-      k3p_pairs<KS, QT, 0>(cur, ldsh + lane, m, tk(k), b1, b2, i1);
+      if constexpr (PIPE) {
+        f32x16 acc[2];
+        k3p_pipe<KS, QT, 0>(cur, ldsh + lane, m, tk(k), b1, b2, i1, acc);
+      } else {
+        k3p_pairs<KS, QT, 0>(cur, ldsh + lane, m, tk(k), b1, b2, i1);
+      }
       cnt += __popc(m);
       ntl++;
       k = kn;
@@ -1124,6 +1148,7 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     if (variant == 5) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true>;
     if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
     if (variant == 8) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, true>;
+    if (variant == 9) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, true>;
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

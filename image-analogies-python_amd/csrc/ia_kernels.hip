@@ -1701,13 +1701,14 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
   const int kmax = (NT + nwg - 1) / nwg;  // DB tiles per workgroup
-  const int rev = variant >= 7 ? (step & 1) : 0;  // 7, 8: alternate steps walk in reverse
+  const int rev = (variant == 7 || variant == 8 || variant == 10) ? (step & 1) : 0;  // alternate steps walk in reverse
   if (variant == 7) variant = 6;  // 8: + the previous step's query order (no sort)
+  if (variant == 10) variant = 9;  // 9: 6 + pipelined single chains; 10: 9 + reverse walks
   if (variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // v3/v4 limits (ia_k3h.hip IA_K3P3_*)
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t lds = ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
-  static int attr_lds[9][16] = {};
-  const int vi = variant < 0 || variant > 8 ? 1 : variant;
+  static int attr_lds[11][16] = {};
+  const int vi = variant < 0 || variant > 10 ? 1 : variant;
   if ((int)lds > attr_lds[vi][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_lds[vi][qt] = (int)lds;

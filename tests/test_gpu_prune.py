@@ -29,7 +29,7 @@ def _run(ctx, job, prune, variant=7):
     return Bp, S, IM, st
 
 
-@pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 8), (1024, 2, 8), (1024, 2, 6), (1024, 2, 7), (1024, 2, 5), (1024, 2, 4),
+@pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 10), (1024, 2, 10), (1024, 2, 9), (512, 1, 8), (1024, 2, 8), (1024, 2, 6), (1024, 2, 7), (1024, 2, 5), (1024, 2, 4),
                                                       (1024, 2, 3), (1024, 2, 1), (512, 1, 0), (512, 1, 2)])
 def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     """variant = the pruned-scan kernel version (option k3p_variant): every one is exact"""
@@ -56,4 +56,4 @@ def test_prune_option_rejects_bad_values(ctx):
     with pytest.raises(_native.IAError):
         ctx.set_option('prune', 2)
     with pytest.raises(_native.IAError):
-        ctx.set_option('k3p_variant', 9)
+        ctx.set_option('k3p_variant', 11)
