@@ -118,6 +118,8 @@ def main():
                     help='pruned-scan kernel version (ia_k3h.hip k3h_prune*): 0 = first version, 1 = boxes in '
                          'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
                          'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks')
+    ap.add_argument('--prune-min-rows', type=int, default=524288,
+                    help='smallest DB (rows) the pruned scan is used on (default: the 1024^2 level)')
     ap.add_argument('--time-stride', type=int, default=4, help='sample K3 timing every S-th wavefront step')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -150,6 +152,7 @@ def main():
     ctx.set_option('k3_variant', args.k3_variant)
     ctx.set_option('prune', args.prune)
     ctx.set_option('k3p_variant', args.k3p_variant)
+    ctx.set_option('prune_min_rows', args.prune_min_rows)
     if args.mode == 'shard' and world > 1:
         uid = [_native.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)

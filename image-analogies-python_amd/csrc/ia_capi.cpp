@@ -83,6 +83,7 @@ struct ia_ctx {
   // certified pruned scan (option "prune"): per-level basis, sorted DB table, tile boxes
   DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs, ord;
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
+  int64_t prune_min_rows = IA_PRUNE_MIN_ROWS;  // option "prune_min_rows": smallest DB that prunes
   int prune = 1;
   int matcher = IA_MATCH_F16X3;  // option "matcher"
   int k3p_variant = 7;           // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
@@ -266,6 +267,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "k3_variant")) {
     if (value < 0 || value > 3) return fail(IA_EINVAL, "ia_set_option: k3_variant must be 0..3 (2, 3: diagnostic builds)");
     c->k3_variant = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "prune_min_rows")) {
+    if (value < 1) return fail(IA_EINVAL, "ia_set_option: prune_min_rows must be >= 1");
+    c->prune_min_rows = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "prune")) {
@@ -468,7 +474,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   int64_t T, Mmax;
   ia_wavefront_shape(g.bh, g.bw, &T, &Mmax);
   const int64_t Mpad_max = (Mmax + IA_TILE - 1) / IA_TILE * IA_TILE;
-  const bool prune = c->prune && use_h && g.ch == 1 && !sharded && g.NA >= IA_PRUNE_MIN_ROWS && Mpad_max <= 4096;
+  const bool prune = c->prune && use_h && g.ch == 1 && !sharded && g.NA >= c->prune_min_rows && Mpad_max <= 4096;
   if (prune) g.nwg = std::min(IA_NWG_H, g.n_tiles);  // round-robin chunks: WG w owns tiles w + nwg*k
   const size_t db_row_bytes = use_h ? (size_t)16 * g.KS * 4 : (size_t)DP * 4;  // hi+lo f16 / fp32 per column
 

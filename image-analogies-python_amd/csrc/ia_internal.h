@@ -122,7 +122,8 @@ __host__ __device__ inline int64_t ia_pos_row_t(int64_t pos, int64_t NT, const i
 // certified pruning of the distance scan (ia_prune.hip): projection basis size, smallest DB
 // that prunes
 #define IA_NPC 4
-#define IA_PRUNE_MIN_ROWS 262144
+#define IA_PRUNE_MIN_ROWS 524288  // default of option "prune_min_rows": at 512^2 (262,144 rows) the
+                                  // unpruned scan + cheaper gather/merge is still faster
 
 // per-step wavefront description: pixels (r, t - 3r), r in [r0, r0 + M)
 struct StepDesc {

@@ -102,9 +102,11 @@ int ia_version(void);
  * measured device time and algorithmic flops (bench.py roofline).
  * "matcher" = IA_MATCH_F16X3 (default: split-f16 MFMA scan, 1 and 2 channels, image values
  * within +-64) or IA_MATCH_F32 (fp32 MFMA scan).  Both are certified exact: identical results.
- * "prune" = 1 (default) / 0: certified pruned scan on 1-channel split-f16 levels with >= 2^18
- * DB rows: (DB tile, query tile) pairs a projection bound proves farther than
- * the query's best coherence candidate are skipped.  Identical results either way. */
+ * "prune" = 1 (default) / 0: certified pruned scan on 1-channel split-f16 levels with at least
+ * "prune_min_rows" DB rows (default 2^19): (DB tile, query tile) pairs a
+ * projection bound proves farther than the query's best coherence candidate are skipped.
+ * "k3p_variant" = 0..10 (default 7): version of the pruned-scan kernel (ia_k3h.hip).
+ * Identical results for every setting. */
 #define IA_MATCH_F32 0
 #define IA_MATCH_F16X3 1
 int ia_set_option(ia_ctx *ctx, const char *name, int value);

@@ -14,6 +14,7 @@ def _run(ctx, job, prune, variant=7):
     from ia_amd import _native
     ctx.set_option('prune', prune)
     ctx.set_option('k3p_variant', variant)
+    ctx.set_option('prune_min_rows', 262144)  # prune the 512^2 level too (default: 1024^2 and up)
     Bp = [x.copy() for x in job.Bp_init]
     S, IM = {}, {}
     st = _native.Stats()
@@ -26,6 +27,7 @@ def _run(ctx, job, prune, variant=7):
     finally:
         ctx.set_option('prune', 1)
         ctx.set_option('k3p_variant', 7)
+        ctx.set_option('prune_min_rows', 524288)
     return Bp, S, IM, st
 
 
@@ -57,3 +59,5 @@ def test_prune_option_rejects_bad_values(ctx):
         ctx.set_option('prune', 2)
     with pytest.raises(_native.IAError):
         ctx.set_option('k3p_variant', 11)
+    with pytest.raises(_native.IAError):
+        ctx.set_option('prune_min_rows', 0)
