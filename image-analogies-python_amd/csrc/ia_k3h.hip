@@ -683,9 +683,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
            unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
            int r0, int *__restrict__ ord_out) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
-  constexpr int NE = IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE / WGT;  // unsorted fragments per thread
+  constexpr int NE = (IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE + WGT - 1) / WGT;  // unsorted fragments per thread
   static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
-  static_assert(WGT == IA_K3P3_MAXQ && WGT == IA_K3P3_MAXK, "one query / one tile per thread");
+  static_assert(WGT >= IA_K3P3_MAXQ && WGT >= IA_K3P3_MAXK, "one query / one tile per thread");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
   float4 *qlo = reinterpret_cast<float4 *>(ldsh + QT * NP * IA_WAVE);  // [NQ]
   float4 *qhi = qlo + NQ;                                               // [NQ]
@@ -800,13 +800,13 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       }
     }
   } else if (DYN && Mpad > 256) {  // (uniform) below 256 queries the rank count is cheaper
-    // bitonic network over the 512 threads' unique keys (padding threads: 0xFFFFFFFF, last):
+    // bitonic network over the first 512 threads' unique keys (padding: 0xFFFFFFFF, last):
     // exchanges at distance < 64 are lane swaps, the 6 at distance >= 64 go through LDS (the
     // query-fragment area, free until the scatter below)
     unsigned *sx = reinterpret_cast<unsigned *>(ldsh);
     unsigned v = mkey;
 #pragma unroll
-    for (int kb = 2; kb <= WGT; kb <<= 1) {
+    for (int kb = 2; kb <= IA_K3P3_MAXQ; kb <<= 1) {
 #pragma unroll
       for (int jb = kb >> 1; jb > 0; jb >>= 1) {
         unsigned o;
