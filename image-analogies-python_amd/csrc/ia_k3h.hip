@@ -132,7 +132,8 @@ k3h_scan(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, int n_tiles
     b2[q] = FLT_MAX;
     i1[q] = 0x7fffffff;
   }
-  for (; t < t_end; t += NW) {
+  // two tile buffers in rotation (a register copy `a = an` would wait for the prefetch)
+  auto body = [&](const h16x8(&a)[NP], h16x8(&an)[NP], int t) {
     {  // prefetch the next tile of this wave (clamped: always issue, never branch per load)
       ld_tile<KS>(an, db, min(t + NW, n_tiles - 1), lane);
     }
@@ -167,8 +168,11 @@ k3h_scan(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, int n_tiles
       }
     }
     if constexpr (PROBE == 0) k3h_epi2<QT, PK>(e0, e1, 2 * (NPAIR - 1), 2 * NPAIR - 1 < QT, rbase, t, b1, b2, i1);
-#pragma unroll
-    for (int p = 0; p < NP; p++) a[p] = an[p];
+  };
+  for (; t < t_end; t += 2 * NW) {
+    body(a, an, t);
+    if (t + NW >= t_end) break;
+    body(an, a, t + NW);
   }
   if constexpr (PK) {  // tile + packed in-tile index -> DB position
 #pragma unroll
