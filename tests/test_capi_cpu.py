@@ -96,3 +96,35 @@ def test_merge_winners_lowest_index_on_ties():
     do, ro = _native.merge_winners(d, r)
     assert list(do) == [0.9, 1.5, 3.0, 0.5]
     assert list(ro) == [11, 21, 29, 3]
+
+
+def test_ctypes_structs_match_the_c_header(tmp_path):
+    """ia_stats / ia_level_args as include/ia.h lays them out (gcc) == the ctypes mirrors in
+    _native.py: same size and the same offset for every field, so the Python side can never read
+    a shifted counter after a header change."""
+    import ctypes
+    import shutil
+    import subprocess
+    from ia_amd import _native
+    if shutil.which('gcc') is None:
+        pytest.skip('gcc not available')
+    structs = {'ia_stats': _native.Stats, 'ia_level_args': _native.LevelArgs}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "ia.h"', 'int main(void) {']
+    for cname, py in structs.items():
+        lines.append('printf("%s sizeof %%zu\\n", sizeof(%s));' % (cname, cname))
+        for f, _ in py._fields_:
+            lines.append('printf("%s %s %%zu\\n", offsetof(%s, %s));' % (cname, f, cname, f))
+    lines += ['return 0;', '}']
+    src = tmp_path / 'layout.c'
+    src.write_text('\n'.join(lines))
+    exe = tmp_path / 'layout'
+    inc = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'include')
+    subprocess.check_call(['gcc', '-std=c99', '-I', inc, str(src), '-o', str(exe)])
+    got = {}
+    for line in subprocess.check_output([str(exe)]).decode().splitlines():
+        s, f, v = line.split()
+        got[(s, f)] = int(v)
+    for cname, py in structs.items():
+        assert got[(cname, 'sizeof')] == ctypes.sizeof(py), cname
+        for f, _ in py._fields_:
+            assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
