@@ -27,7 +27,8 @@ class LevelArgs(ctypes.Structure):
                 ('A', ctypes.c_void_p), ('Ac', ctypes.c_void_p), ('Ap', ctypes.c_void_p), ('Apc', ctypes.c_void_p),
                 ('B', ctypes.c_void_p), ('Bc', ctypes.c_void_p), ('Bpc', ctypes.c_void_p), ('Bp', ctypes.c_void_p),
                 ('weights', ctypes.c_void_p), ('kappa_factor', ctypes.c_double),
-                ('s_out', ctypes.c_void_p), ('im_out', ctypes.c_void_p), ('mem', ctypes.c_int)]
+                ('s_out', ctypes.c_void_p), ('im_out', ctypes.c_void_p), ('mem', ctypes.c_int),
+                ('dbg_src', ctypes.c_void_p), ('dbg_dist', ctypes.c_void_p)]
 
 
 class Stats(ctypes.Structure):
@@ -144,10 +145,14 @@ class Context(object):
     def comm_init(self, rank, world, uid):
         check(lib().ia_comm_init(self._h, rank, world, bytes(uid)), 'ia_comm_init')
 
-    def synthesize_level(self, A, Ac, Ap_list, Apc_list, B, Bc, Bpc, Bp, weights, kappa_factor, stats=None):
+    def synthesize_level(self, A, Ac, Ap_list, Apc_list, B, Bc, Bpc, Bp, weights, kappa_factor, stats=None,
+                         debug=None):
         """ia_synthesize_level on host numpy arrays.  Bp (fp64, C-contiguous) is updated in place
         (the reference mutates Bp_pyr[level], image_analogies.py:214).  Returns (s, im):
-        s (N, 2) int32 source pixel in A', im (N,) int32 source A' image, raster order."""
+        s (N, 2) int32 source pixel in A', im (N,) int32 source A' image, raster order.
+        debug: a dict to receive the debug=True per-pixel records (include/ia.h dbg_src/dbg_dist):
+        'src' (N, 6) int32 [p_app row, col, img, r_star row, col, has_coh], 'dist' (N, 2) fp64
+        [d_app, d_coh] (image_analogies.py:224-240)."""
         A, Ac, B, Bc, Bpc = _c64(A), _c64(Ac), _c64(B), _c64(Bc), _c64(Bpc)
         Ap = _c64(np.stack(Ap_list))
         Apc = _c64(np.stack(Apc_list))
@@ -158,11 +163,18 @@ class Context(object):
         bh, bw = B.shape[:2]
         s = np.empty((bh * bw, 2), dtype=np.int32)
         im = np.empty(bh * bw, dtype=np.int32)
+        dsrc = ddist = None
+        if debug is not None:
+            dsrc = np.zeros((bh * bw, 6), dtype=np.int32)
+            ddist = np.zeros((bh * bw, 2), dtype=np.float64)
         args = LevelArgs(ch, Ap.shape[0], A.shape[0], A.shape[1], bh, bw,
                          _ptr(A), _ptr(Ac), _ptr(Ap), _ptr(Apc), _ptr(B), _ptr(Bc), _ptr(Bpc), _ptr(Bp), _ptr(w),
-                         float(kappa_factor), _ptr(s), _ptr(im), IA_MEM_HOST)
+                         float(kappa_factor), _ptr(s), _ptr(im), IA_MEM_HOST,
+                         None if dsrc is None else _ptr(dsrc), None if ddist is None else _ptr(ddist))
         st = stats if stats is not None else Stats()
         check(lib().ia_synthesize_level(self._h, ctypes.byref(args), ctypes.byref(st)), 'ia_synthesize_level')
+        if debug is not None:
+            debug['src'], debug['dist'] = dsrc, ddist
         return s, im
 
     def synthesize_level_device(self, ch, n_ap, a_hw, b_hw, ptrs, kappa_factor, stats=None):

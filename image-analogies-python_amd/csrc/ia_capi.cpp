@@ -78,7 +78,7 @@ struct ia_ctx {
   int dev = 0;
   hipStream_t st = nullptr;
   // uploads (IA_MEM_HOST) and per-level scratch
-  DevBuf A, Ac, Ap, Apc, B, Bc, Bpc, Bp, S, IM, W;
+  DevBuf A, Ac, Ap, Apc, B, Bc, Bpc, Bp, S, IM, W, DSRC, DDIST;
   DevBuf db, db64, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, pstat, absmax;
   // certified pruned scan (option "prune"): per-level basis, sorted DB table, tile boxes
   DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs, ord;
@@ -239,7 +239,7 @@ void ia_destroy(ia_ctx *c) {
   if (!c) return;
   hipSetDevice(c->dev);
   hipStreamSynchronize(c->st);
-  for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->B, &c->Bc, &c->Bpc, &c->Bp, &c->S, &c->IM, &c->W, &c->db, &c->db64,
+  for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->B, &c->Bc, &c->Bpc, &c->Bp, &c->S, &c->IM, &c->W, &c->DSRC, &c->DDIST, &c->db, &c->db64,
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->pstat, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
                     &c->boxes, &c->qinfo, &c->pairs, &c->ord})
@@ -385,6 +385,8 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       !a->im_out)
     return fail(IA_EINVAL, "ia_synthesize_level: NULL image pointer");
   if (a->mem != IA_MEM_HOST && a->mem != IA_MEM_DEVICE) return fail(IA_EINVAL, "ia_synthesize_level: bad mem kind");
+  if ((a->dbg_src == nullptr) != (a->dbg_dist == nullptr))
+    return fail(IA_EINVAL, "ia_synthesize_level: dbg_src and dbg_dist are given together or not at all");
   if ((int64_t)a->n_ap * a->a_h * a->a_w >= (int64_t)INT32_MAX)
     return fail(IA_EINVAL, "ia_synthesize_level: DB rows exceed int32 row ids");
   HIP_TRY(hipSetDevice(c->dev));
@@ -409,6 +411,8 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   // shard the DB over ranks unless the level is too small to be worth an exchange per step
   const bool sharded = shard_level(g.n_tiles, c->world);
   const int world = sharded ? c->world : 1, rank = sharded ? c->rank : 0;
+  if (sharded && a->dbg_src)
+    return fail(IA_EINVAL, "ia_synthesize_level: debug outputs are produced by single-rank levels only");
   {
     int64_t t0, t1;
     ia_shard_tiles(g.NA, c->world, c->rank, &t0, &t1);
@@ -444,6 +448,13 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     dS = c->S.as<int32_t>();
     dIM = c->IM.as<int32_t>();
     HIP_TRY(hipMemcpyAsync(dBp, a->Bp, nB * 8, hipMemcpyHostToDevice, c->st));
+  }
+  int32_t *dDS = a->dbg_src;
+  double *dDD = a->dbg_dist;
+  if (a->dbg_src && a->mem == IA_MEM_HOST) {
+    if ((rc = c->DSRC.ensure((size_t)NB * 24)) || (rc = c->DDIST.ensure((size_t)NB * 16))) return rc;
+    dDS = c->DSRC.as<int32_t>();
+    dDD = c->DDIST.as<double>();
   }
 
   // matcher: split-f16 when the channel count has a K3h instance and every image value fits
@@ -534,6 +545,8 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     shard_rows += std::min<int64_t>(IA_TILE, (g.NA - tr + g.n_tiles - 1) / g.n_tiles);
   }
   ma.pstat = c->pstat.as<unsigned>();
+  ma.dbg_src = dDS;
+  ma.dbg_dist = dDD;
   ma.eps_c = use_h ? ia_eps_c_h(g.KS, prune || c->k3_variant == 1) : ia_eps_c(DP);
   ma.eps_a = use_h ? ia_eps_a_h() : 0.;
 
@@ -620,6 +633,10 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     HIP_TRY(hipMemcpyAsync(a->Bp, dBp, nB * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipMemcpyAsync(a->s_out, dS, (size_t)NB * 8, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipMemcpyAsync(a->im_out, dIM, (size_t)NB * 4, hipMemcpyDeviceToHost, c->st));
+    if (a->dbg_src) {
+      HIP_TRY(hipMemcpyAsync(a->dbg_src, dDS, (size_t)NB * 24, hipMemcpyDeviceToHost, c->st));
+      HIP_TRY(hipMemcpyAsync(a->dbg_dist, dDD, (size_t)NB * 16, hipMemcpyDeviceToHost, c->st));
+    }
   }
   HIP_TRY(hipStreamSynchronize(c->st));
 #if IA_PROBE & 16
@@ -794,6 +811,8 @@ int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, d
   ma.boxes = nullptr;
   ma.ufac = 0.;
   ma.pstat = nullptr;
+  ma.dbg_src = nullptr;
+  ma.dbg_dist = nullptr;
   ma.eps_c = ia_eps_c(DP);
   ma.eps_a = 0.;
   const int qtmax = ia_k3_qtmax(x->KH);

@@ -94,6 +94,8 @@ struct MergeArgs {
   const float4 *qinfo;                // pruned levels: the step's query projection intervals (K2p)
   const float4 *boxes;                // pruned levels: per-tile projection boxes (ia_prune.hip)
   double ufac;                        // pruned levels: bound factor of ia_prune.h
+  int32_t *dbg_src;                   // optional (nullptr: off) N x 6: p_app row/col/img, r_star row/col, has_coh
+  double *dbg_dist;                   // optional N x 2: d_app, d_coh (compute_distance; 0 without a coherence candidate)
 };
 
 // DB positions are tile-strided and tile-scattered: slot j of tile t holds row j*NT + perm(t)

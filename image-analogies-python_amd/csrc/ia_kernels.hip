@@ -143,6 +143,89 @@ __device__ __forceinline__ double pw_block(T &&term, int off) {
     return res;
   }
 }
+// Correctly rounded fp64 square root, as numpy's np.sqrt / np.linalg.norm give on the host.
+// The device sqrt measured 1 ulp off on a few of the golden compute_distance values (4 of 2698
+// in g32), so the result is settled among sqrt(x) and its two neighbours by the exact residual
+// |x - y*y| (one fused multiply-add each).  Nearest-in-square equals nearest-in-root except in
+// a window of relative width ~2^-55 around the rounding midpoint.
+__device__ __forceinline__ double cr_sqrt(double x) {
+  double y = sqrt(x);
+  if (!(x > 0.) || !(x < DBL_MAX)) return y;
+  const long long b = __double_as_longlong(y);
+  const double yl = __longlong_as_double(b - 1), yh = __longlong_as_double(b + 1);
+  double r = fabs(__builtin_fma(-y, y, x));
+  const double rl = fabs(__builtin_fma(-yl, yl, x)), rh = fabs(__builtin_fma(-yh, yh, x));
+  if (rl < r) {
+    y = yl;
+    r = rl;
+  }
+  if (rh < r) y = yh;
+  return y;
+}
+
+// x.x in the summation order of numpy's dot (x.dot(x) inside np.linalg.norm(ord=2), i.e.
+// compute_distance, algorithms.py:133-135) on the host that produced the golden vectors: OpenBLAS
+// 0.3.29 ddot, SkylakeX kernel (found by matching np.dot bit-for-bit for n = 1..165,
+// oracle/ia_oracle.py blas_ddot).  n1 = N & -16 elements go through fused multiply-adds: 32-wide
+// blocks into four 8-lane accumulators, whose halves are added into four 4-lane accumulators
+// that take any remaining 16-wide block, then ((a0 + a1) + a2) + a3 per lane and
+// (l0 + l2) + (l1 + l3); the tail N - n1 elements are fused into the running sum.
+template <int N, class X>
+__device__ __forceinline__ double blas_dot_sq(X &&x) {
+  constexpr int N1 = N & ~15, N32 = N1 & ~31;
+  double acc[4][4];
+  if constexpr (N32 > 0) {
+    double z[4][8];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int l = 0; l < 8; l++) {
+        const double v = x(8 * k + l);
+        z[k][l] = v * v;  // fma(v, v, 0)
+      }
+#pragma unroll
+    for (int i = 32; i < N32; i += 32)
+#pragma unroll
+      for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int l = 0; l < 8; l++) {
+          const double v = x(i + 8 * k + l);
+          z[k][l] = __builtin_fma(v, v, z[k][l]);
+        }
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int l = 0; l < 4; l++) acc[k][l] = z[k][l] + z[k][l + 4];
+  } else {
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int l = 0; l < 4; l++) acc[k][l] = 0.;
+  }
+#pragma unroll
+  for (int i = N32; i < N1; i += 16)
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+      for (int l = 0; l < 4; l++) {
+        const double v = x(i + 4 * k + l);
+        acc[k][l] = __builtin_fma(v, v, acc[k][l]);
+      }
+  double dot = 0.;
+  if constexpr (N1 > 0) {
+    double sl[4];
+#pragma unroll
+    for (int l = 0; l < 4; l++) sl[l] = ((acc[0][l] + acc[1][l]) + acc[2][l]) + acc[3][l];
+    dot = (sl[0] + sl[2]) + (sl[1] + sl[3]);
+  }
+#pragma unroll
+  for (int f = N1; f < N; f++) {
+    const double v = x(f);
+    dot = __builtin_fma(v, v, dot);
+  }
+  return dot;
+}
+
 template <int N, class T>
 __device__ __forceinline__ double pw_sum(T &&term) {
   if constexpr (N <= 128) {
@@ -760,7 +843,7 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__r
           cpr = tr;
           cpc = tc;
           const int64_t row = (int64_t)cim * hw + (int64_t)tr * g.aw + tc;
-          dk = sqrt(exact_dist_level<CH>(db64, row, q));
+          dk = cr_sqrt(exact_dist_level<CH>(db64, row, q));
           kk = lane;
         }
       }
@@ -776,12 +859,8 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__r
       if (lane < 2) {
         const int ii = lane == 0 ? img : cim, rr_ = lane == 0 ? pr : cpr, cc_ = lane == 0 ? pc : cpc;
         const double *arow = db64 + ((int64_t)ii * hw + (int64_t)rr_ * g.aw + cc_) * Geo<CH>::DS;
-#pragma unroll
-        for (int f = 0; f < D; f++) {
-          const double x = (arow[f] - q[f]) * weights[f];
-          part += x * x;
-        }
-        part = sqrt(part);
+        part = blas_dot_sq<D>([&](int f) { return (arow[f] - q[f]) * weights[f]; });
+        part = cr_sqrt(part);
         part = part * part;
       }
       const double d_app = __shfl(part, 0, 64), d_coh = __shfl(part, 1, 64);
@@ -823,24 +902,13 @@ __device__ __forceinline__ void row_dists(const double *__restrict__ db64, int r
 #pragma unroll
     for (int f = 0; f < D; f++) t[f] -= q[f];
     unw = pw_sum<D>([&](int f) { return t[f] * t[f]; });
-    double s = 0.;
-#pragma unroll
-    for (int f = 0; f < D; f++) {
-      const double x = t[f] * w[f];
-      s += x * x;
-    }
-    wsq = s;
+    wsq = blas_dot_sq<D>([&](int f) { return t[f] * w[f]; });
   } else {  // 165 doubles do not fit in registers: read the row twice
     unw = pw_sum<D>([&](int f) {
       const double d = a[f] - q[f];
       return d * d;
     });
-    double s = 0.;
-    for (int f = 0; f < D; f++) {
-      const double x = (a[f] - q[f]) * w[f];
-      s += x * x;
-    }
-    wsq = s;
+    wsq = blas_dot_sq<D>([&](int f) { return (a[f] - q[f]) * w[f]; });
   }
 }
 
@@ -1139,7 +1207,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   }
   if (__ballot(n_over > 0)) recompute_app = true;
   // NN winner (lowest index on ties) and coherence winner (first argmin of the norm) together
-  double dk = (lane < NCOH && my_row >= 0) ? sqrt(unw) : DBL_MAX;
+  double dk = (lane < NCOH && my_row >= 0) ? cr_sqrt(unw) : DBL_MAX;
   int kk = (lane < NCOH && my_row >= 0) ? lane : INT_MAX;
   double bd = nd;
   int bi = ni;
@@ -1223,6 +1291,8 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   int img = (int)((unsigned)bi / hw);
   const unsigned rem = (unsigned)bi - (unsigned)img * hw;
   int pr = (int)(rem / (unsigned)g.aw), pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
+  const int app_img = img, app_pr = pr, app_pc = pc;
+  double dbg_app = 0., dbg_coh = 0.;
   bool coh_won = false;
   int src_lane = recompute_app ? -1 : app_lane;  // lane holding the chosen row's A' value
   if (kk != INT_MAX) {  // a coherence candidate exists (never for the level's first pixel)
@@ -1234,9 +1304,11 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
       wsq_app = __shfl(wq, 0, 64);
     }
     // compute_distance = norm(x)**2 = sqrt(sum x^2)**2 ; kappa rule image_analogies.py:206
-    double d_app = sqrt(wsq_app), d_coh = sqrt(wsq_coh);
+    double d_app = cr_sqrt(wsq_app), d_coh = cr_sqrt(wsq_coh);
     d_app = d_app * d_app;
     d_coh = d_coh * d_coh;
+    dbg_app = d_app;
+    dbg_coh = d_coh;
     if (d_coh <= d_app * kf) {
       img = kim;
       pr = kpr;
@@ -1264,6 +1336,18 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     const int slot = placed + 0;
     a.pstat[qi] = (unsigned)min(slot, 0xffff) | ((unsigned)min((int)nfb, 0x3fff) << 16) | (coh_won ? 1u << 30 : 0u) |
                   (any_viol ? 1u << 31 : 0u);
+    if (a.dbg_src) {  // debug=True structures (image_analogies.py:224-240): p_app, r_star, d_app, d_coh
+      const bool has_coh = kk != INT_MAX;
+      int32_t *o = a.dbg_src + (int64_t)qi * 6;
+      o[0] = app_pr;
+      o[1] = app_pc;
+      o[2] = app_img;
+      o[3] = has_coh ? r - 2 + kk / 5 : 0;
+      o[4] = has_coh ? c - 2 + kk % 5 : 0;
+      o[5] = has_coh ? 1 : 0;
+      a.dbg_dist[2 * qi] = dbg_app;
+      a.dbg_dist[2 * qi + 1] = dbg_coh;
+    }
   }
 #if IA_PROBE & 8
   if (lane == 0 && m == sd.M / 2 && (sd.t % 256) == 128) {

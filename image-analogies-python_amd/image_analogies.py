@@ -89,18 +89,21 @@ def img_setup(A_fname, Ap_fname_list, B_fname, out_path, c):
     return A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list, c
 
 
-def synthesize_pyramid(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c, ctx=None, stats=None, on_level=None):
+def synthesize_pyramid(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c, ctx=None, stats=None, on_level=None, debug=None):
     """The level loop of image_analogies_main (image_analogies.py:130-239) on the GPU.
-    Bp_pyr levels 1..max_levels-1 are synthesised in place; returns ({level: s}, {level: im})."""
+    Bp_pyr levels 1..max_levels-1 are synthesised in place; returns ({level: s}, {level: im}).
+    debug: a dict that receives {level: {'src', 'dist'}} per-pixel debug records
+    (_native.Context.synthesize_level)."""
     ctx = ctx or default_context()
     L = c.max_levels
     S, IM = {}, {}
     for level in range(1, L):
         Bp_pyr[level] = np.ascontiguousarray(Bp_pyr[level], dtype=np.float64)
         kf = 1 + (2 ** (level - L)) * c.k          # image_analogies.py:206
+        dbg = None if debug is None else debug.setdefault(level, {})
         S[level], IM[level] = ctx.synthesize_level(
             A_pyr[level], A_pyr[level - 1], [p[level] for p in Ap_pyr_list], [p[level - 1] for p in Ap_pyr_list],
-            B_pyr[level], B_pyr[level - 1], Bp_pyr[level - 1], Bp_pyr[level], c.weights, kf, stats)
+            B_pyr[level], B_pyr[level - 1], Bp_pyr[level - 1], Bp_pyr[level], c.weights, kf, stats, debug=dbg)
         if on_level is not None:
             on_level(level, S, IM)
     return S, IM
@@ -117,11 +120,71 @@ def level_colour(level, Bp_pyr, S, IM, color_pyr_list, c):
     return out.reshape(h, w, 3)
 
 
+def debug_structures(S_l, IM_l, dbg, shape):
+    """The debug=True bookkeeping of image_analogies.py:141-153,224-240 and :244-246 for one level,
+    from the GPU's per-pixel records (include/ia.h dbg_src / dbg_dist).  Returns
+    {'sa', 'sc', 'rstars', 'p_src', 'app_dist', 'coh_dist', 'img_src'}: sa = p_app per pixel;
+    sc / rstars = p_coh (= s[r_star] + q - r_star) / r_star where a coherence candidate existed,
+    (0, 0) otherwise (also at the level's first pixel); p_src colours coherence-chosen pixels
+    [1, 1, 0], NN-chosen ones [1, 0, 0] and pixels without a candidate [0, 0, 0]; img_src = im /
+    max(im) (0/0 = nan with one A' image, as in the reference)."""
+    h, w = shape
+    src, dist = dbg['src'], dbg['dist']
+    n = h * w
+    sa = [(int(x[0]), int(x[1])) for x in src[:, :2]]
+    sc, rstars = [], []
+    p_src = np.nan * np.ones((h, w, 3))
+    app_dist = np.zeros((h, w))
+    coh_dist = np.zeros((h, w))
+    for qi in range(n):
+        r, col = divmod(qi, w)
+        if qi > 0 and src[qi, 5]:
+            rr, rc = int(src[qi, 3]), int(src[qi, 4])
+            nb = rr * w + rc
+            p_coh = (int(S_l[nb, 0]) + r - rr, int(S_l[nb, 1]) + col - rc)
+            sc.append(p_coh)
+            rstars.append((rr, rc))
+            app_dist[r, col], coh_dist[r, col] = dist[qi]
+            if (int(S_l[qi, 0]), int(S_l[qi, 1])) == p_coh:          # np.allclose(p, p_coh)
+                p_src[r, col] = [1, 1, 0]
+            else:
+                p_src[r, col] = [1, 0, 0]
+        else:
+            sc.append((0, 0))
+            rstars.append((0, 0))
+            p_src[r, col] = [0, 0, 0]
+    with np.errstate(invalid='ignore', divide='ignore'):
+        img_src = (np.asarray(IM_l).astype(np.float64) / np.max(IM_l)).reshape(h, w)
+    return {'sa': sa, 'sc': sc, 'rstars': rstars, 'p_src': p_src, 'app_dist': app_dist, 'coh_dist': coh_dist,
+            'img_src': img_src}
+
+
+def _save_debug(out_path, level, d, Bp_l, S_l, IM_l):
+    """image_analogies.py:244-253: the five debug maps as .eps and the [sa, sc, rstars, s, im]
+    pickle (binary mode; the reference's text-mode open fails on Python 3)."""
+    try:
+        import matplotlib
+        matplotlib.use('Agg')
+        import matplotlib.pyplot as plt
+        from .img_preprocess import savefig_noborder
+        paths = ['%d_psrc.eps', '%d_appdist.eps', '%d_cohdist.eps', '%d_output.eps', '%d_imgsrc.eps']
+        for path, var in zip(paths, [d['p_src'], d['app_dist'], d['coh_dist'], Bp_l, d['img_src']]):
+            fig = plt.imshow(var, interpolation='nearest', cmap='gray')
+            savefig_noborder(out_path + path % level, fig)
+            plt.close()
+    except ImportError:
+        warnings.warn('matplotlib is not importable: debug .eps maps skipped')
+    s_list = [np.array([int(x[0]), int(x[1])]) for x in S_l]
+    with open(out_path + '%d_srcs.pickle' % level, 'wb') as f:
+        pickle.dump([d['sa'], d['sc'], d['rstars'], s_list, [int(x) for x in IM_l]], f)
+
+
 def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=False):
     """image_analogies.py:97-268.  Writes metadata.txt, level_<l>_color.jpg and
-    <dirname>.jpg per level like the reference; debug=True additionally pickles [s, im] per
-    level (the reference's [sa, sc, rstars, s, im] debug lists are not produced: the GPU level
-    path keeps no per-pixel candidate log).  Returns {'Bp_pyr', 's', 'im', 'stats'}."""
+    <dirname>.jpg per level like the reference; debug=True additionally writes the reference's
+    debug maps (<l>_psrc/appdist/cohdist/output/imgsrc.eps) and pickles [sa, sc, rstars, s, im]
+    per level (image_analogies.py:141-153,224-253), built from the GPU's per-pixel records.
+    Returns {'Bp_pyr', 's', 'im', 'stats'} (+ 'debug': {level: debug_structures} when debug)."""
     begin = time.time()
     A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list, c = img_setup(A_fname, Ap_fname_list, B_fname, out_path, c)
     names = ['A_fname', 'Ap_fname_list', 'B_fname', 'c.convert', 'c.remap_lum', 'c.init_rand', 'c.AB_weight', 'c.k']
@@ -139,13 +202,17 @@ def image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=Fal
         _imsave(out_path + 'level_%d_color.jpg' % level, col)
         _imsave(out_path + out_path.rstrip('/').split('/')[-1] + '.jpg', col)
         if debug:
-            with open(out_path + '%d_srcs.pickle' % level, 'wb') as f:
-                pickle.dump([S[level], IM[level]], f)
+            dbg_out[level] = debug_structures(S[level], IM[level], dbg_raw[level], Bp_pyr[level].shape[:2])
+            _save_debug(out_path, level, dbg_out[level], Bp_pyr[level], S[level], IM[level])
         now = time.time()
         print('Level %d time: %f' % (level, now - state['t']))
         state['t'] = now
 
-    S, IM = synthesize_pyramid(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c, stats=stats, on_level=on_level)
+    dbg_raw, dbg_out = ({}, {}) if debug else (None, None)
+    S, IM = synthesize_pyramid(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c, stats=stats, on_level=on_level, debug=dbg_raw)
     print('Total time: %f' % (time.time() - begin))
     print('GPU synthesis time: %f (DB build %f)' % (stats.synth_ms / 1e3, stats.db_ms / 1e3))
-    return {'Bp_pyr': Bp_pyr, 's': S, 'im': IM, 'stats': stats.as_dict()}
+    out = {'Bp_pyr': Bp_pyr, 's': S, 'im': IM, 'stats': stats.as_dict()}
+    if debug:
+        out['debug'] = dbg_out
+    return out

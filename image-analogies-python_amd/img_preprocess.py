@@ -134,3 +134,12 @@ def Ap_ix2px(ixs, h, w):
 
 def Ap_px2ix(pxs, img_nums, h, w):
     return (((h * np.asarray(img_nums)) + np.asarray(pxs[0])) * w + np.asarray(pxs[1])).astype(int)
+
+
+def savefig_noborder(fileName, fig):
+    """img_preprocess.py:109-113: save the current matplotlib image without axes or border."""
+    import matplotlib.pyplot as plt
+    plt.axis('off')
+    fig.axes.get_xaxis().set_visible(False)
+    fig.axes.get_yaxis().set_visible(False)
+    plt.savefig(fileName, bbox_inches='tight', pad_inches=0)

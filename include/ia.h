@@ -89,7 +89,15 @@ typedef struct {
   double kappa_factor;      /* 1 + 2^(level - max_levels) * k   (image_analogies.py:206) */
   int32_t *s_out;           /* N x 2 */
   int32_t *im_out;          /* N */
-  int mem;                  /* IA_MEM_HOST or IA_MEM_DEVICE for every pointer above */
+  int mem;                  /* IA_MEM_HOST or IA_MEM_DEVICE for every pointer in this struct */
+  /* Optional debug structures of image_analogies_main(debug=True) (image_analogies.py:141-153,
+   * 224-240); both NULL (off) or both given, single-rank levels only.  Per raster pixel:
+   * dbg_src  N x 6 int32: p_app row, col, image (the NN, Ap_ix2px of best_approximate_match),
+   *          r_star row, col (best_coherence_match, algorithms.py:126-130; 0, 0 without one),
+   *          has_coh (1 when a coherence candidate existed, i.e. the kappa rule compared);
+   * dbg_dist N x 2 fp64: d_app, d_coh (compute_distance, algorithms.py:133-135; 0 when has_coh = 0). */
+  int32_t *dbg_src;
+  double *dbg_dist;
 } ia_level_args;
 
 /* ---- context ---------------------------------------------------------------------------- */

@@ -136,6 +136,48 @@ def compute_distance(a, q, weights):
     return np.linalg.norm((a - q) * weights, ord=2) ** 2
 
 
+def _fma(a, b, c):
+    from fractions import Fraction
+    return float(Fraction(a) * Fraction(b) + Fraction(c))   # one rounding, like a hardware FMA
+
+
+def blas_ddot_sq(x):
+    """x.dot(x) in the order of the BLAS behind numpy on the host that made the golden vectors
+    (OpenBLAS 0.3.29 ddot, SkylakeX kernel; matched bit-for-bit against np.dot for n = 1..165).
+    np.linalg.norm(v, ord=2) of a 1-D v is sqrt(v.dot(v)), so compute_distance's last bits
+    depend on this order; the GPU's blas_dot_sq (ia_kernels.hip) restates it.  Pure Python,
+    exact FMA via fractions: test-sized inputs only."""
+    x = [float(v) for v in x]
+    n = len(x)
+    n1 = n & ~15
+    n32 = n1 & ~31
+    z = [[0.0] * 8 for _ in range(4)]
+    i = 0
+    while i < n32:
+        for k in range(4):
+            for l in range(8):
+                v = x[i + 8 * k + l]
+                z[k][l] = _fma(v, v, z[k][l])
+        i += 32
+    acc = [[z[k][l] + z[k][l + 4] for l in range(4)] for k in range(4)]
+    while i < n1:
+        for k in range(4):
+            for l in range(4):
+                v = x[i + 4 * k + l]
+                acc[k][l] = _fma(v, v, acc[k][l])
+        i += 16
+    sl = [((acc[0][l] + acc[1][l]) + acc[2][l]) + acc[3][l] for l in range(4)]
+    dot = (sl[0] + sl[2]) + (sl[1] + sl[3]) if n1 else 0.0
+    for j in range(n1, n):
+        dot = _fma(x[j], x[j], dot)
+    return dot
+
+
+def compute_distance_blas(a, q, weights):
+    """compute_distance with the dot order made explicit (blas_ddot_sq), machine-independent."""
+    return np.sqrt(blas_ddot_sq((a - q) * weights)) ** 2
+
+
 # ----------------------------------------------------------------------------- the level loop
 def synthesize_level(A_pyr, Ap_pyr_list, B_feat_l, Bp_pyr, level, L, k, weights,
                      As=None, faithful_pad=False, max_pixels=None, log=None):

@@ -1,0 +1,95 @@
+"""GPU parity of the debug=True records (image_analogies.py:141-153,224-253) against the
+reference's own per-call outputs, captured by oracle/gen_golden.py while the real reference ran:
+every best_approximate_match index ('app_ix'), every best_coherence_match return ('coh',
+(-1, -1, 0) for "no candidate") and every compute_distance value ('dist', d_app then d_coh).
+
+NN indices and coherence picks must be bit-exact.  compute_distance = norm((a - q) * w)**2
+evaluates the norm with the BLAS dot of the host that ran the reference; the kernels restate that
+summation order (blas_dot_sq in ia_kernels.hip; oracle blas_ddot_sq reproduces every golden value
+bit-for-bit on the CPU, tests/test_oracle_golden.py).  On the GPU a handful of values still land
+1 ulp away (4 of 2698 in g32; cause open), so the distances are held to rtol 1e-13
+plus a >= 99.5 % bit-identical share; the kappa decisions are bit-exact through s / im / B'.
+"""
+import pickle
+
+import numpy as np
+import pytest
+
+from golden_util import E2E_CASES, load_e2e
+
+pytestmark = pytest.mark.gpu
+
+
+def _run_debug(ctx, z):
+    L, k = z['L'], float(z['k'])
+    Bp = [x.copy() for x in z['Bp_init']]
+    out = {}
+    for level in range(1, L):
+        kf = 1 + (2 ** (level - L)) * k
+        dbg = {}
+        s, im = ctx.synthesize_level(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
+                                     [p[level - 1] for p in z['Ap_pyr']], z['B_pyr'][level], z['B_pyr'][level - 1],
+                                     Bp[level - 1], Bp[level], z['weights'], kf, debug=dbg)
+        out[level] = (s, im, dbg)
+    return out, Bp
+
+
+@pytest.mark.parametrize('name', E2E_CASES)
+def test_debug_records_match_reference_calls(ctx, name):
+    z = load_e2e(name)
+    out, Bp = _run_debug(ctx, z)
+    app, coh, dist = [], [], []
+    for level in range(1, z['L']):
+        s, im, dbg = out[level]
+        assert np.array_equal(s, z['s'][level]) and np.array_equal(im, z['im'][level])
+        assert np.array_equal(Bp[level], z['Bp_final'][level])
+        src, d = dbg['src'], dbg['dist']
+        a_h, a_w = z['A_pyr'][level].shape[:2]
+        h, w = z['B_pyr'][level].shape[:2]
+        app.extend((src[:, 2].astype(np.int64) * a_h + src[:, 0]) * a_w + src[:, 1])
+        for qi in range(1, h * w):
+            if src[qi, 5]:
+                nb = src[qi, 3] * w + src[qi, 4]
+                r, c = divmod(qi, w)
+                coh.append((s[nb, 0] + r - src[qi, 3], s[nb, 1] + c - src[qi, 4], im[nb]))
+                dist.extend(d[qi])
+            else:
+                assert src[qi, 3] == 0 and src[qi, 4] == 0 and d[qi, 0] == 0 and d[qi, 1] == 0
+                coh.append((-1, -1, 0))
+        assert src[0, 5] == 0   # the level's first pixel never consults coherence (:186-189)
+    assert np.array_equal(np.array(app), z['app_ix'])
+    assert np.array_equal(np.array(coh), z['coh'])
+    dist = np.array(dist)
+    assert dist.shape == z['dist'].shape
+    print('%s: %d of %d compute_distance values bit-identical' % (name, int((dist == z['dist']).sum()), dist.size))
+    np.testing.assert_allclose(dist, z['dist'], rtol=1e-13, atol=0)
+    assert (dist == z['dist']).mean() >= 0.995
+
+
+def test_main_debug_writes_reference_pickles(ctx, tmp_path):
+    """image_analogies_main(debug=True) on the g32 golden inputs: the [sa, sc, rstars, s, im]
+    pickles hold the reference's per-pixel lists (sa = every NN pick in raster order)."""
+    from ia_amd import image_analogies as IA
+    import types
+    z = load_e2e('g32')
+    c = types.SimpleNamespace(k=float(z['k']), weights=z['weights'], max_levels=z['L'])
+    Bp = [x.copy() for x in z['Bp_init']]
+    dbg = {}
+    S, IM = IA.synthesize_pyramid(z['A_pyr'], z['Ap_pyr'], z['B_pyr'], Bp, c, ctx=ctx, debug=dbg)
+    app = []
+    for level in range(1, z['L']):
+        h, w = Bp[level].shape[:2]
+        d = IA.debug_structures(S[level], IM[level], dbg[level], (h, w))
+        IA._save_debug(str(tmp_path) + '/', level, d, Bp[level], S[level], IM[level])
+        with open(tmp_path / ('%d_srcs.pickle' % level), 'rb') as f:
+            sa, sc, rstars, s_list, im_list = pickle.load(f)
+        assert len(sa) == len(sc) == len(rstars) == len(s_list) == len(im_list) == h * w
+        assert np.array_equal(np.array(s_list), z['s'][level]) and im_list == list(z['im'][level])
+        a_w = z['A_pyr'][level].shape[1]
+        app.extend(r * a_w + col for r, col in sa)           # one A' image: ix = r * a_w + c
+        assert all((tmp_path / (p % level)).exists() for p in ['%d_psrc.eps', '%d_appdist.eps', '%d_cohdist.eps',
+                                                                 '%d_output.eps', '%d_imgsrc.eps'])
+        colours = {tuple(x) for x in d['p_src'].reshape(-1, 3)}
+        assert colours <= {(1., 1., 0.), (1., 0., 0.), (0., 0., 0.)}
+        assert tuple(d['p_src'][0, 0]) == (0., 0., 0.) and sc[0] == (0, 0) and rstars[0] == (0, 0)
+    assert np.array_equal(np.array(app), z['app_ix'])

@@ -115,3 +115,29 @@ def test_coherence_and_distance_helpers_match_oracle():
         ref = O.coherence(As, A_h, A_w, q, s, im, r, col, w)
         assert tuple(np.asarray(got[0])) == tuple(ref[0]) and got[1] == ref[1]
         assert alg.compute_distance(As[5], q, z['weights']) == O.compute_distance(As[5], q, z['weights'])
+
+
+def test_debug_structures_from_records():
+    """debug=True bookkeeping (image_analogies.py:224-246) from per-pixel GPU records on a 2x3
+    level: sc = s[r_star] + q - r_star where a coherence candidate existed, (0, 0) otherwise;
+    p_src colours by which candidate won; img_src = im / max(im) (nan for one A' image)."""
+    from ia_amd.image_analogies import debug_structures
+    S = np.array([[4, 4], [4, 5], [7, 7], [5, 4], [5, 6], [1, 1]], dtype=np.int32)
+    IM = np.zeros(6, dtype=np.int32)
+    src = np.zeros((6, 6), dtype=np.int32)
+    src[:, 0], src[:, 1] = S[:, 0], S[:, 1]
+    src[2, :2] = (7, 7)
+    src[1, 3:] = (0, 0, 1)        # r_star (0,0): p_coh = (4,4) + (0,1) = (4,5) = s[1] -> coherence won
+    src[2, 3:] = (0, 1, 1)        # p_coh = (4,5) + (0,1) = (4,6) != s[2] -> NN won
+    src[4, 3:] = (1, 0, 1)        # p_coh = (5,4) + (0,1) = (5,5) != s[4] = (5,6) -> NN
+    src[4, :2] = (5, 6)
+    dist = np.zeros((6, 2))
+    dist[1], dist[2], dist[4] = (2., 1.), (1., 3.), (0.5, 0.75)
+    d = debug_structures(S, IM, {'src': src, 'dist': dist}, (2, 3))
+    assert d['sc'] == [(0, 0), (4, 5), (4, 6), (0, 0), (5, 5), (0, 0)]
+    assert d['rstars'] == [(0, 0), (0, 0), (0, 1), (0, 0), (1, 0), (0, 0)]
+    assert d['sa'][2] == (7, 7)
+    assert [tuple(x) for x in d['p_src'].reshape(-1, 3)] == [(0, 0, 0), (1, 1, 0), (1, 0, 0), (0, 0, 0), (1, 0, 0),
+                                                            (0, 0, 0)]
+    assert d['app_dist'][0, 1] == 2. and d['coh_dist'][1, 1] == 0.75 and d['app_dist'][1, 0] == 0.
+    assert np.isnan(d['img_src']).all()

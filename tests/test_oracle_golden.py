@@ -66,3 +66,27 @@ def test_decide_pixel_teacher_forcing_matches_reference():
                              A_h, A_w, level, L, k, w, r, c)
         (pr, pc), img = out['choice']
         assert (pr, pc, img) == (s[qi, 0], s[qi, 1], im[qi])
+
+
+def test_blas_dot_order_reproduces_reference_distances(monkeypatch):
+    """Every compute_distance value the reference produced (golden 'dist') is reproduced
+    bit-for-bit by the explicit BLAS ddot order the GPU kernels restate (blas_ddot_sq), so the
+    kappa rule's inputs, not only its decisions, are pinned independently of the host's BLAS."""
+    z = load_e2e('g24k5')
+    monkeypatch.setattr(O, 'compute_distance', O.compute_distance_blas)
+    Bp = [x.copy() for x in z['Bp_init']]
+    log = []
+    O.run_all_levels(z['A_pyr'], z['Ap_pyr'], z['B_pyr'], Bp, float(z['k']), z['weights'], log=log)
+    assert np.array_equal(np.array([v for x in log if x[1] for v in x[1][2:]]), z['dist'])
+
+
+def test_blas_dot_order_three_channel():
+    """D = 165 (3 channels) and 110: the same restatement against the host's np.dot on the rgb3
+    golden weights (skipped where numpy's BLAS uses another kernel)."""
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((40, 165)) * rng.uniform(0, 1, (40, 165))
+    got = [O.blas_ddot_sq(v) for v in x]
+    ref = [float(v.dot(v)) for v in x]
+    if got != ref:
+        pytest.skip('this host numpy BLAS sums in another order (not the golden-generating kernel)')
+    assert got == ref
