@@ -4,6 +4,7 @@ This is the only way the package reaches the GPU: there is no CPU fallback.  If 
 missing, or no gfx950 device is visible, every entry point raises IAError loudly.
 """
 import ctypes
+import math
 import os
 import threading
 
@@ -152,7 +153,7 @@ class Context(object):
         s (N, 2) int32 source pixel in A', im (N,) int32 source A' image, raster order.
         debug: a dict to receive the debug=True per-pixel records (include/ia.h dbg_src/dbg_dist):
         'src' (N, 6) int32 [p_app row, col, img, r_star row, col, has_coh], 'dist' (N, 2) fp64
-        [d_app, d_coh] (image_analogies.py:224-240)."""
+        [d_app, d_coh] (image_analogies.py:224-240), finished on the host as numpy does."""
         A, Ac, B, Bc, Bpc = _c64(A), _c64(Ac), _c64(B), _c64(Bc), _c64(Bpc)
         Ap = _c64(np.stack(Ap_list))
         Apc = _c64(np.stack(Apc_list))
@@ -174,6 +175,11 @@ class Context(object):
         st = stats if stats is not None else Stats()
         check(lib().ia_synthesize_level(self._h, ctypes.byref(args), ctypes.byref(st)), 'ia_synthesize_level')
         if debug is not None:
+            # compute_distance = norm(x) ** 2 on numpy scalars: sqrt, then libm pow(., 2), which
+            # can differ from sqrt(v) * sqrt(v) by 1 ulp; finish it here exactly like that
+            for qi in np.flatnonzero(dsrc[:, 5]):
+                ddist[qi, 0] = math.sqrt(ddist[qi, 0]) ** 2
+                ddist[qi, 1] = math.sqrt(ddist[qi, 1]) ** 2
             debug['src'], debug['dist'] = dsrc, ddist
         return s, im
 

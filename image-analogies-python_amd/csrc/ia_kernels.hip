@@ -1307,8 +1307,8 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     double d_app = cr_sqrt(wsq_app), d_coh = cr_sqrt(wsq_coh);
     d_app = d_app * d_app;
     d_coh = d_coh * d_coh;
-    dbg_app = d_app;
-    dbg_coh = d_coh;
+    dbg_app = wsq_app;  // the host finishes compute_distance as np.sqrt(v) ** 2 (libm pow)
+    dbg_coh = wsq_coh;
     if (d_coh <= d_app * kf) {
       img = kim;
       pr = kpr;

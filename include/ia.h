@@ -95,7 +95,10 @@ typedef struct {
    * dbg_src  N x 6 int32: p_app row, col, image (the NN, Ap_ix2px of best_approximate_match),
    *          r_star row, col (best_coherence_match, algorithms.py:126-130; 0, 0 without one),
    *          has_coh (1 when a coherence candidate existed, i.e. the kappa rule compared);
-   * dbg_dist N x 2 fp64: d_app, d_coh (compute_distance, algorithms.py:133-135; 0 when has_coh = 0). */
+   * dbg_dist N x 2 fp64: v_app, v_coh = x.dot(x) of compute_distance's x = (a - q) * w
+ *          (algorithms.py:133-135) in the golden host's BLAS order; 0 when has_coh = 0.
+ *          compute_distance itself is np.sqrt(v) ** 2 with libm's pow (numpy scalar power),
+ *          which is not always v's correctly rounded square root squared: the host applies it. */
   int32_t *dbg_src;
   double *dbg_dist;
 } ia_level_args;
