@@ -245,7 +245,7 @@ def main():
                                                  % ('split-f16 (hi/lo x3)' if f16 else 'fp32')},
            'roofline': roofline,
            'stats': {k: st[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
-                                        'synth_ms', 'bound_violations', 'f16_levels', 'pruned_levels',
+                                        'synth_ms', 'bound_violations', 'kappa_ambiguous', 'f16_levels', 'pruned_levels',
                                         'dist_pairs', 'dist_pairs_full', 'dist_tiles', 'dist_tiles_full')}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = cpu_baseline(job, args.cpu_seconds)

@@ -496,14 +496,14 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       (rc = c->qn2.ensure((size_t)Mpad_max * 8)) || (rc = c->qf.ensure((size_t)Mpad_max * db_row_bytes)) ||
       (rc = c->rec.ensure((size_t)Mmax * std::max(g.nwg, 1) * 16)) ||
       (rc = c->recT.ensure((size_t)Mmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mmax * 16)) ||
-      (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(4 * 8)) ||
+      (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(5 * 8)) ||
       (rc = c->pstat.ensure((size_t)NB * 4)) || (rc = c->pairs.ensure(4 * IA_NWG_H * 8)) || (rc = c->ord.ensure(2 * 4096 * 4)) ||
       (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 : 16)))
     return rc;
   // per-workgroup counters of the pruned scan: [pairs | pairs (timed steps) | tiles | tiles (timed)][wg]
   HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 4 * IA_NWG_H * 8, c->st));
   HIP_TRY(hipMemsetAsync(c->Rbits.p, 0, 4, c->st));
-  HIP_TRY(hipMemsetAsync(c->counters.p, 0, 4 * 8, c->st));
+  HIP_TRY(hipMemsetAsync(c->counters.p, 0, 5 * 8, c->st));
   HIP_TRY(hipMemsetAsync(c->pstat.p, 0, (size_t)NB * 4, c->st));
 
   Imgs Aim{(const double *)dAc, (const double *)dA, (const double *)dApc, (const double *)dAp,
@@ -643,7 +643,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   if (prune) ia_k3p_probe_dump();
 #endif
   if (stats) {
-    unsigned long long ctr[4], prs[4];
+    unsigned long long ctr[5], prs[4];
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
     {  // per-workgroup counter slots (no same-address atomics in the distance kernel)
       std::vector<unsigned long long> slots(4 * IA_NWG_H);
@@ -672,6 +672,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     stats->fallbacks += (int64_t)ctr[1];
     stats->coherence_wins += (int64_t)ctr[2];
     stats->bound_violations += (int64_t)ctr[3];
+    stats->kappa_ambiguous += (int64_t)ctr[4];
     stats->f16_levels += use_h ? 1 : 0;
     stats->db_ms += ms_db;
     stats->synth_ms += ms_syn;

@@ -84,7 +84,8 @@ struct MergeArgs {
   int NT;              // tiles of the whole DB: position p holds row ia_pos_row(p, NT)
   int NA;              // DB rows
   unsigned *pstat;                    // per-pixel stats word of the level (nullptr: none):
-                                      // bits 0-15 reranked, 16-29 fallbacks, 30 coherence won,
+                                      // bits 0-15 reranked, 16-28 fallbacks, 29 kappa decision
+                                      // ambiguous under libm pow, 30 coherence won,
                                       // 31 an MFMA value outside the certified error bound
   double eps_c;                       // relative error coefficient of the MFMA value
   double eps_a;                       // absolute (f16 subnormal) error coefficient

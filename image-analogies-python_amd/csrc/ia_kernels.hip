@@ -163,6 +163,26 @@ __device__ __forceinline__ double cr_sqrt(double x) {
   return y;
 }
 
+// compute_distance's final `** 2` is libm pow(y, 2.0) on a numpy scalar, K4 uses y * y.  They
+// differ only when the exact square lies next to a rounding midpoint (glibc pow is accurate to
+// ~0.52 ulp; measured: every difference has |y*y - hi| >= 0.986 half-ulp).  pow2_alt returns the
+// other value pow may give there (hi itself elsewhere) so K4 can flag a kappa decision that
+// would flip between the two (pstat bit 29, ia_stats.kappa_ambiguous).
+__device__ __forceinline__ double pow2_alt(double y, double hi) {
+  if (!(hi > 0.) || !(hi < DBL_MAX)) return hi;
+  const double lo = __builtin_fma(y, y, -hi);  // y*y = hi + lo exactly
+  const long long b = __double_as_longlong(hi);
+  const double half = 0.5 * (__longlong_as_double(b + 1) - hi);
+  if (fabs(lo) < 0.9 * half) return hi;
+  return __longlong_as_double(lo > 0. ? b + 1 : b - 1);
+}
+__device__ __forceinline__ bool kappa_ambiguous(double ya, double da, double yc, double dc, double kf) {
+  const double aa = pow2_alt(ya, da), ac = pow2_alt(yc, dc);
+  const bool dec = dc <= da * kf;
+  if (ya == yc) return (ac <= aa * kf) != dec;  // one value: pow rounds both the same way
+  return ((ac <= da * kf) != dec) || ((dc <= aa * kf) != dec) || ((ac <= aa * kf) != dec);
+}
+
 // x.x in the summation order of numpy's dot (x.dot(x) inside np.linalg.norm(ord=2), i.e.
 // compute_distance, algorithms.py:133-135) on the host that produced the golden vectors: OpenBLAS
 // 0.3.29 ddot, SkylakeX kernel (found by matching np.dot bit-for-bit for n = 1..165,
@@ -809,7 +829,7 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
   unsigned long long tot = nre;
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) tot += __shfl_xor(tot, o, 64);
-  *stat_out = (unsigned)min((unsigned long long)0xffff, tot) | ((unsigned)min((unsigned long long)0x3fff, nfb) << 16);
+  *stat_out = (unsigned)min((unsigned long long)0xffff, tot) | ((unsigned)min((unsigned long long)0x1fff, nfb) << 16);
   return Winner{bd, bi};
 }
 
@@ -827,7 +847,7 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__r
   int img = (int)((unsigned)app_ix / hw);
   const unsigned rem = (unsigned)app_ix - (unsigned)img * hw;
   int pr = (int)(rem / (unsigned)g.aw), pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
-  bool coh_won = false;
+  bool coh_won = false, kamb = false;
   if (qi > 0) {
     // best_coherence_match: candidates in product(rows, cols) order, first argmin of the norm
     double dk = DBL_MAX;
@@ -861,9 +881,10 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__r
         const double *arow = db64 + ((int64_t)ii * hw + (int64_t)rr_ * g.aw + cc_) * Geo<CH>::DS;
         part = blas_dot_sq<D>([&](int f) { return (arow[f] - q[f]) * weights[f]; });
         part = cr_sqrt(part);
-        part = part * part;
       }
-      const double d_app = __shfl(part, 0, 64), d_coh = __shfl(part, 1, 64);
+      const double y_app = __shfl(part, 0, 64), y_coh = __shfl(part, 1, 64);
+      const double d_app = y_app * y_app, d_coh = y_coh * y_coh;
+      kamb = kappa_ambiguous(y_app, d_app, y_coh, d_coh, kf);
       if (d_coh <= d_app * kf) {
         img = cim;
         pr = cpr;
@@ -877,7 +898,7 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__r
     s[2 * qi] = pr;
     s[2 * qi + 1] = pc;
     im[qi] = img;
-    if (pstat) pstat[qi] = stat | (coh_won ? 1u << 30 : 0u);
+    if (pstat) pstat[qi] = stat | (kamb ? 1u << 29 : 0u) | (coh_won ? 1u << 30 : 0u);
   }
 }
 
@@ -1293,6 +1314,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   int pr = (int)(rem / (unsigned)g.aw), pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
   const int app_img = img, app_pr = pr, app_pc = pc;
   double dbg_app = 0., dbg_coh = 0.;
+  bool kamb = false;
   bool coh_won = false;
   int src_lane = recompute_app ? -1 : app_lane;  // lane holding the chosen row's A' value
   if (kk != INT_MAX) {  // a coherence candidate exists (never for the level's first pixel)
@@ -1304,9 +1326,9 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
       wsq_app = __shfl(wq, 0, 64);
     }
     // compute_distance = norm(x)**2 = sqrt(sum x^2)**2 ; kappa rule image_analogies.py:206
-    double d_app = cr_sqrt(wsq_app), d_coh = cr_sqrt(wsq_coh);
-    d_app = d_app * d_app;
-    d_coh = d_coh * d_coh;
+    const double y_app = cr_sqrt(wsq_app), y_coh = cr_sqrt(wsq_coh);
+    const double d_app = y_app * y_app, d_coh = y_coh * y_coh;
+    kamb = kappa_ambiguous(y_app, d_app, y_coh, d_coh, kf);
     dbg_app = wsq_app;  // the host finishes compute_distance as np.sqrt(v) ** 2 (libm pow)
     dbg_coh = wsq_coh;
     if (d_coh <= d_app * kf) {
@@ -1334,7 +1356,8 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     // per-pixel stats word (no shared-counter atomics: hundreds of waves adding to one
     // address serialise at L2 and dominated this kernel); reduced once per level
     const int slot = placed + 0;
-    a.pstat[qi] = (unsigned)min(slot, 0xffff) | ((unsigned)min((int)nfb, 0x3fff) << 16) | (coh_won ? 1u << 30 : 0u) |
+    a.pstat[qi] = (unsigned)min(slot, 0xffff) | ((unsigned)min((int)nfb, 0x1fff) << 16) | (kamb ? 1u << 29 : 0u) |
+                  (coh_won ? 1u << 30 : 0u) |
                   (any_viol ? 1u << 31 : 0u);
     if (a.dbg_src) {  // debug=True structures (image_analogies.py:224-240): p_app, r_star, d_app, d_coh
       const bool has_coh = kk != INT_MAX;
@@ -1430,26 +1453,28 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
 // per-level statistics: sum the per-pixel stats words (one workgroup, fixed order)
 __global__ void __launch_bounds__(IA_WG) k_reduce_stats(const unsigned *__restrict__ pstat, int64_t n,
                                                          unsigned long long *__restrict__ counters) {
-  unsigned long long rr = 0, fb = 0, cw = 0, bv = 0;
+  unsigned long long rr = 0, fb = 0, cw = 0, bv = 0, ka = 0;
   for (int64_t i = threadIdx.x; i < n; i += IA_WG) {
     const unsigned v = pstat[i];
     rr += v & 0xffff;
-    fb += (v >> 16) & 0x3fff;
+    fb += (v >> 16) & 0x1fff;
+    ka += (v >> 29) & 1;
     cw += (v >> 30) & 1;
     bv += v >> 31;
   }
-  __shared__ unsigned long long red[4][IA_WG];
+  __shared__ unsigned long long red[5][IA_WG];
   red[0][threadIdx.x] = rr;
   red[1][threadIdx.x] = fb;
   red[2][threadIdx.x] = cw;
   red[3][threadIdx.x] = bv;
+  red[4][threadIdx.x] = ka;
   __syncthreads();
   for (int o = IA_WG / 2; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o)
-      for (int k = 0; k < 4; k++) red[k][threadIdx.x] += red[k][threadIdx.x + o];
+      for (int k = 0; k < 5; k++) red[k][threadIdx.x] += red[k][threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x < 4) counters[threadIdx.x] = red[threadIdx.x][0];
+  if (threadIdx.x < 5) counters[threadIdx.x] = red[threadIdx.x][0];
 }
 
 // ------------------------------------------------------------------------------------------

@@ -69,6 +69,10 @@ typedef struct {
   int64_t prune_launches_timed;
   double prune_flops_timed; /* their MFMA flops (computed pairs x 2 D 32 32) */
   double prune_bytes_timed; /* their algorithmic bytes (DB tiles loaded, boxes, queries, records) */
+  int64_t kappa_ambiguous;  /* pixels whose kappa decision (image_analogies.py:206) would flip if
+                             * compute_distance's `** 2` (libm pow on a numpy scalar) rounded a
+                             * near-midpoint square the other way than y * y does (audit; no
+                             * fixture has one) */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),

@@ -51,6 +51,7 @@ def test_level_path_matches_reference(ctx, matcher, name):
         assert np.array_equal(im, z['im'][level]), 'level %d image map differs' % level
         assert np.array_equal(Bp[level], z['Bp_final'][level]), 'level %d B\' differs' % level
     assert st.bound_violations == 0
+    assert st.kappa_ambiguous == 0
     ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]
     assert st.f16_levels == (z['L'] - 1 if (matcher == 'f16x3' and ch < 3) else 0)
 

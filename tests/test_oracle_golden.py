@@ -90,3 +90,25 @@ def test_blas_dot_order_three_channel():
     if got != ref:
         pytest.skip('this host numpy BLAS sums in another order (not the golden-generating kernel)')
     assert got == ref
+
+
+def test_libm_pow_square_differs_from_product_only_near_midpoints():
+    """compute_distance ends in `norm(...) ** 2` on a numpy scalar = libm pow(y, 2.0), which is
+    not always the correctly rounded y * y the kernels use.  K4's audit (pow2_alt in
+    ia_kernels.hip, ia_stats.kappa_ambiguous) assumes every difference lies where the exact
+    square is within 0.9 half-ulp of a rounding midpoint and equals the neighbour toward it:
+    checked here against this host's libm on random y."""
+    import math
+    from fractions import Fraction
+    rng = np.random.default_rng(11)
+    ys = rng.uniform(0, 1, 100000) * 10.0 ** rng.integers(-6, 3, 100000)
+    n_diff = 0
+    for y in ys.tolist():
+        p, h = y ** 2, y * y
+        lo = float(Fraction(y) * Fraction(y) - Fraction(h))
+        half = math.ulp(h) / 2
+        alt = h if abs(lo) < 0.9 * half else math.nextafter(h, math.inf if lo > 0 else 0.0)
+        assert p in (h, alt)
+        n_diff += p != h
+    assert n_diff > 0   # the effect is real (about 1 in 1000) ...
+    assert n_diff < 1000
