@@ -1454,7 +1454,7 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
 __global__ void __launch_bounds__(IA_WG) k_reduce_stats(const unsigned *__restrict__ pstat, int64_t n,
                                                          unsigned long long *__restrict__ counters) {
   unsigned long long rr = 0, fb = 0, cw = 0, bv = 0, ka = 0;
-  for (int64_t i = threadIdx.x; i < n; i += IA_WG) {
+  for (int64_t i = (int64_t)blockIdx.x * IA_WG + threadIdx.x; i < n; i += (int64_t)gridDim.x * IA_WG) {
     const unsigned v = pstat[i];
     rr += v & 0xffff;
     fb += (v >> 16) & 0x1fff;
@@ -1474,7 +1474,9 @@ __global__ void __launch_bounds__(IA_WG) k_reduce_stats(const unsigned *__restri
       for (int k = 0; k < 5; k++) red[k][threadIdx.x] += red[k][threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x < 5) counters[threadIdx.x] = red[threadIdx.x][0];
+  // integer sums: order-free, so one global atomic per counter and workgroup (counters are
+  // zeroed at the start of the level)
+  if (threadIdx.x < 5) atomicAdd(&counters[threadIdx.x], red[threadIdx.x][0]);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1670,7 +1672,8 @@ void ia_launch_db64_build(const LevelGeo &g, const Imgs &A, double *db64, hipStr
 int ia_db64_stride(int ch) { return ch == 1 ? Geo<1>::DS : ch == 2 ? Geo<2>::DS : Geo<3>::DS; }
 
 void ia_launch_reduce_stats(const unsigned *pstat, int64_t n, unsigned long long *counters, hipStream_t st) {
-  hipLaunchKernelGGL(k_reduce_stats, dim3(1), dim3(IA_WG), 0, st, pstat, n, counters);
+  const int64_t nwg = std::min<int64_t>(256, std::max<int64_t>(1, cdiv(n, (int64_t)IA_WG * 16)));
+  hipLaunchKernelGGL(k_reduce_stats, dim3((unsigned)nwg), dim3(IA_WG), 0, st, pstat, n, counters);
 }
 
 void ia_launch_dense_db(int KH, const double *pts, int64_t n, int d, int n_tiles, const double *mu, float4 *db,
