@@ -144,10 +144,11 @@ __device__ __forceinline__ double pw_block(T &&term, int off) {
   }
 }
 // Correctly rounded fp64 square root, as numpy's np.sqrt / np.linalg.norm give on the host.
-// The device sqrt measured 1 ulp off on a few of the golden compute_distance values (4 of 2698
-// in g32), so the result is settled among sqrt(x) and its two neighbours by the exact residual
-// |x - y*y| (one fused multiply-add each).  Nearest-in-square equals nearest-in-root except in
-// a window of relative width ~2^-55 around the rounding midpoint.
+// Insurance against a device sqrt expansion that is not correctly rounded (the 1-ulp golden
+// differences first blamed on it turned out to be libm pow, see pow2_alt): the result is
+// settled among sqrt(x) and its two neighbours by the exact residual |x - y*y| (one fused
+// multiply-add each).  Nearest-in-square equals nearest-in-root except in a window of relative
+// width ~2^-106 around the rounding midpoint.
 __device__ __forceinline__ double cr_sqrt(double x) {
   double y = sqrt(x);
   if (!(x > 0.) || !(x < DBL_MAX)) return y;
