@@ -111,11 +111,11 @@ def main():
     ap.add_argument('--matcher', default='f16x3', choices=['f16x3', 'f32'],
                     help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
     ap.add_argument('--k3-variant', type=int, default=1, choices=[0, 1],
-                    help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select')
+                    help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select (DIAG=1 builds)')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
     ap.add_argument('--k3p-variant', type=int, default=7, choices=list(range(11)),
-                    help='pruned-scan kernel version (ia_k3h.hip k3h_prune*): 0 = first version, 1 = boxes in '
+                    help='pruned-scan kernel version (ia_k3h.hip k3h_prune*; other than 7: DIAG=1 builds): 0 = first version, 1 = boxes in '
                          'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
                          'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks')
     ap.add_argument('--prune-min-rows', type=int, default=524288,
@@ -149,9 +149,11 @@ def main():
 
     ctx = _native.Context(local)
     ctx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
-    ctx.set_option('k3_variant', args.k3_variant)
+    if args.k3_variant != 1:
+        ctx.set_option('k3_variant', args.k3_variant)       # DIAG=1 builds only
     ctx.set_option('prune', args.prune)
-    ctx.set_option('k3p_variant', args.k3p_variant)
+    if args.k3p_variant != 7:
+        ctx.set_option('k3p_variant', args.k3p_variant)     # DIAG=1 builds only
     ctx.set_option('prune_min_rows', args.prune_min_rows)
     if args.mode == 'shard' and world > 1:
         uid = [_native.comm_unique_id() if rank == 0 else None]

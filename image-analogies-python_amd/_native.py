@@ -110,6 +110,34 @@ def _c64(a):
     return np.ascontiguousarray(a, dtype=np.float64)
 
 
+def check_level_shapes(A, Ac, Ap, Apc, B, Bc, Bpc, Bp, w):
+    """The C ABI derives every size from A's channel count and B's shape (include/ia.h
+    ia_level_args); check the rest here so a mismatched call raises instead of reading or
+    writing past a host buffer.  Ap / Apc are the stacked A' images.  Returns ch."""
+    if A.ndim not in (2, 3):
+        raise IAError('A must be (h, w) or (h, w, ch)')
+    ch = 1 if A.ndim == 2 else A.shape[2]
+    if not 1 <= ch <= 3:
+        raise IAError('images must have 1, 2 or 3 channels (got %d)' % ch)
+    half = lambda x: (-(-x.shape[0] // 2), -(-x.shape[1] // 2)) + x.shape[2:]
+    if B.ndim != A.ndim or B.shape[2:] != A.shape[2:]:
+        raise IAError('B must have the channel count of A: %s vs %s' % (B.shape, A.shape))
+    if Ap.ndim != A.ndim + 1 or Ap.shape[1:] != A.shape or Ap.shape[0] < 1:
+        raise IAError("every A' level must have A's shape %s (got %s)" % (A.shape, Ap.shape[1:]))
+    if Ac.shape != half(A):
+        raise IAError('Ac must be the coarser level of A, %s (got %s)' % (half(A), Ac.shape))
+    if Apc.shape != (Ap.shape[0],) + half(A):
+        raise IAError("every coarse A' level must be %s (got %s)" % (half(A), Apc.shape[1:]))
+    for name, x in (('Bc', Bc), ('Bpc', Bpc)):
+        if x.shape != half(B):
+            raise IAError('%s must be the coarser level of B, %s (got %s)' % (name, half(B), x.shape))
+    if Bp.shape != B.shape:
+        raise IAError("Bp must have B's shape %s (got %s)" % (B.shape, Bp.shape))
+    if w.shape != (55 * ch,):
+        raise IAError('weights must have 55 * ch = %d entries (3x3 / 5x5 windows; got %s)' % (55 * ch, w.shape))
+    return ch
+
+
 class Context(object):
     """One GPU (ia_ctx).  device: HIP ordinal (default: LOCAL_RANK or 0)."""
 
@@ -159,9 +187,9 @@ class Context(object):
         Ap = _c64(np.stack(Ap_list))
         Apc = _c64(np.stack(Apc_list))
         w = _c64(weights)
-        if not (Bp.dtype == np.float64 and Bp.flags.c_contiguous):
+        if not (isinstance(Bp, np.ndarray) and Bp.dtype == np.float64 and Bp.flags.c_contiguous):
             raise IAError('Bp must be a C-contiguous float64 array (updated in place)')
-        ch = 1 if A.ndim == 2 else A.shape[2]
+        ch = check_level_shapes(A, Ac, Ap, Apc, B, Bc, Bpc, Bp, w)
         bh, bw = B.shape[:2]
         s = np.empty((bh * bw, 2), dtype=np.int32)
         im = np.empty(bh * bw, dtype=np.int32)

@@ -259,16 +259,24 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     c->time_dist = value;
     return IA_OK;
   }
+#ifdef IA_K3H_DIAG  // DIAG=1 builds: every kernel version of DESIGN.md §4b's progression
   if (!std::strcmp(name, "k3p_variant")) {
     if (value < 0 || value > 10) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..10");
     c->k3p_variant = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "k3_variant")) {
-    if (value < 0 || value > 3) return fail(IA_EINVAL, "ia_set_option: k3_variant must be 0..3 (2, 3: diagnostic builds)");
+    if (value < 0 || value > 3) return fail(IA_EINVAL, "ia_set_option: k3_variant must be 0..3");
     c->k3_variant = value;
     return IA_OK;
   }
+#else  // product build: the default kernels only (7: pruned scan, 1: packed-index K3h)
+  if (!std::strcmp(name, "k3p_variant") || !std::strcmp(name, "k3_variant")) {
+    if (value != (name[2] == 'p' ? 7 : 1))
+      return fail(IA_EINVAL, std::string("ia_set_option: ") + name + " variants other than the default are in DIAG=1 builds only");
+    return IA_OK;
+  }
+#endif
   if (!std::strcmp(name, "prune_min_rows")) {
     if (value < 1) return fail(IA_EINVAL, "ia_set_option: prune_min_rows must be >= 1");
     c->prune_min_rows = value;

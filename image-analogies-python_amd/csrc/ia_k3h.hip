@@ -648,15 +648,18 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
 #define IA_K3H_CAT2(a, b, c) a##b##_##c
 #define IA_K3H_CAT(a, b, c) IA_K3H_CAT2(a, b, c)
 // variant (option "k3_variant"): 0 = compare/select epilogue, 1 = packed-index epilogue
+// The product library holds only the packed-index epilogue (variant 1); the compare/select
+// epilogue (0) and the probes (2, 3) are experiments, built with DIAG=1 only.
 k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
-  if (variant == 1) return k3h_scan<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, true>;
-#ifdef IA_K3H_DIAG  // diagnostic variants (plateau instance only)
-  if constexpr (IA_K3H_KS == 4 && IA_K3H_QT == 11) {
+#ifdef IA_K3H_DIAG
+  if (variant == 0) return k3h_scan<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, false>;
+  if constexpr (IA_K3H_KS == 4 && IA_K3H_QT == 11) {  // diagnostic variants (plateau instance only)
     if (variant == 2) return k3h_scan<IA_K3H_KS, IA_K3H_QT, 4, true>;
     if (variant == 3) return k3h_scan<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, true, 1>;
   }
 #endif
-  return k3h_scan<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, false>;
+  (void)variant;
+  return k3h_scan<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, true>;
 }
 #endif
 
@@ -1143,16 +1146,22 @@ void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau w
 
 #if defined(IA_K3H_KS) && defined(IA_K3H_QT)
 // pruned scan instance (1 channel only: KS = 4)
+// The product library holds the default pruned scan (variant 6 kernel; the launcher adds the
+// reverse walks of variant 7) and variant 1, the fallback for steps beyond v3+'s limits (more
+// than 512 queries or 512 tiles per workgroup).  The other versions of DESIGN.md §4b's
+// progression are built with DIAG=1 only.
 k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
   if constexpr (IA_K3H_KS == 4) {
+#ifdef IA_K3H_DIAG
     if (variant == 0) return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 0>;
     if (variant == 2) return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2>;
     if (variant == 3) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 3, false>;
     if (variant == 4) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, false>;
     if (variant == 5) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true>;
-    if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
     if (variant == 8) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, true>;
     if (variant == 9) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, true>;
+#endif
+    if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

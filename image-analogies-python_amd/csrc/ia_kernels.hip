@@ -1451,7 +1451,9 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
   finish_pixel<CH>(g, A, db64, r, sd.t - 3 * r, bi, q64 + (int64_t)m * Geo<CH>::D, s, im, Bp, weights, kf, pstat, prev);
 }
 
-// per-level statistics: sum the per-pixel stats words (one workgroup, fixed order)
+// per-level statistics: sum the per-pixel stats words.  Grid-stride loop over up to 256
+// workgroups; each workgroup reduces in LDS and adds its five integer sums with one u64
+// atomicAdd per counter (integer sums are order-free; counters are zeroed per level)
 __global__ void __launch_bounds__(IA_WG) k_reduce_stats(const unsigned *__restrict__ pstat, int64_t n,
                                                          unsigned long long *__restrict__ counters) {
   unsigned long long rr = 0, fb = 0, cw = 0, bv = 0, ka = 0;

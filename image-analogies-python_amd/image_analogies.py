@@ -36,6 +36,7 @@ def _imsave(path, img):
 
 def img_setup(A_fname, Ap_fname_list, B_fname, out_path, c):
     """image_analogies.py:17-94.  File names may also be numpy arrays."""
+    check_windows(c)
     os.makedirs(out_path, exist_ok=True)
     A_orig, B_orig = _imread(A_fname), _imread(B_fname)
     if A_orig.ndim != B_orig.ndim:
@@ -89,14 +90,28 @@ def img_setup(A_fname, Ap_fname_list, B_fname, out_path, c):
     return A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, color_pyr_list, c
 
 
+def check_windows(c):
+    """The kernels hard-code the reference's 3x3 coarse / 5x5 fine windows (config.py:15-16;
+    feature width 55 * ch): refuse other sizes loudly instead of misreading the weight vector."""
+    n_sm, n_lg = getattr(c, 'n_sm', 3), getattr(c, 'n_lg', 5)
+    if (n_sm, n_lg) != (3, 5) or int(getattr(c, 'n_half', 12)) != 12:
+        raise ValueError('only n_sm = 3, n_lg = 5, n_half = 12 are supported (the reference defaults; '
+                         'got n_sm = %r, n_lg = %r, n_half = %r)' % (n_sm, n_lg, getattr(c, 'n_half', None)))
+
+
 def synthesize_pyramid(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c, ctx=None, stats=None, on_level=None, debug=None):
     """The level loop of image_analogies_main (image_analogies.py:130-239) on the GPU.
     Bp_pyr levels 1..max_levels-1 are synthesised in place; returns ({level: s}, {level: im}).
     debug: a dict that receives {level: {'src', 'dist'}} per-pixel debug records
-    (_native.Context.synthesize_level)."""
+    (_native.Context.synthesize_level).
+    Warns when a kappa decision sat where libm's pow (the reference's `** 2`) could round the
+    other way than the kernel's y * y (ia_stats.kappa_ambiguous; 0 on every fixture)."""
+    check_windows(c)
     ctx = ctx or default_context()
     L = c.max_levels
     S, IM = {}, {}
+    stats = stats if stats is not None else _native.Stats()
+    amb0 = stats.kappa_ambiguous
     for level in range(1, L):
         Bp_pyr[level] = np.ascontiguousarray(Bp_pyr[level], dtype=np.float64)
         kf = 1 + (2 ** (level - L)) * c.k          # image_analogies.py:206
@@ -106,6 +121,9 @@ def synthesize_pyramid(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c, ctx=None, stats=Non
             B_pyr[level], B_pyr[level - 1], Bp_pyr[level - 1], Bp_pyr[level], c.weights, kf, stats, debug=dbg)
         if on_level is not None:
             on_level(level, S, IM)
+    if stats.kappa_ambiguous > amb0:
+        warnings.warn('%d kappa decisions were within libm pow rounding of the threshold: those pixels may '
+                      'differ from the reference (ia_stats.kappa_ambiguous)' % (stats.kappa_ambiguous - amb0))
     return S, IM
 
 

@@ -120,7 +120,8 @@ int ia_version(void);
  * "prune" = 1 (default) / 0: certified pruned scan on 1-channel split-f16 levels with at least
  * "prune_min_rows" DB rows (default 2^19): (DB tile, query tile) pairs a
  * projection bound proves farther than the query's best coherence candidate are skipped.
- * "k3p_variant" = 0..10 (default 7): version of the pruned-scan kernel (ia_k3h.hip).
+ * "k3p_variant" / "k3_variant": kernel versions of DESIGN.md §4b; the product build accepts
+ * only the defaults (7 / 1), DIAG=1 builds every version.
  * Identical results for every setting. */
 #define IA_MATCH_F32 0
 #define IA_MATCH_F16X3 1

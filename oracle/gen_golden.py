@@ -21,7 +21,9 @@ Recipe:
      - plt.imread returns in-memory arrays; plt.imsave captures the colour output.
   3. state is captured by wrapping functions in the `image_analogies` module namespace.
 
-Run:  /opt/conda/bin/python3.9 oracle/gen_golden.py   (takes ~1-2 min)
+Run:  /opt/conda/bin/python3.9 oracle/gen_golden.py            (base fixtures, ~1-2 min)
+      /opt/conda/bin/python3.9 oracle/gen_golden.py cfg1 g128 ties128 k25 g256
+                                        (round-2 larger e2e cases, one by one; g256 ~10-15 min)
 """
 import os
 import shutil
@@ -124,7 +126,9 @@ def blocky(h, w, seed, ch=None):
 
 # ----------------------------------------------------------------------------- end to end
 def run_case(mods, name, A, Ap_list, B, convert=False, remap=False, init_rand=True,
-             AB_weight=1, k=0.5, seed=3):
+             AB_weight=1, k=0.5, seed=3, lean=False):
+    """lean: larger cases keep the fixture small: int32 index arrays, no colour pyramid when it
+    equals the A' pyramid (convert=False), colour output of the finest level only."""
     config, img_preprocess, algorithms, ia = mods
     import matplotlib.pyplot as plt
     imgs = {'A': A, 'B': B}
@@ -186,17 +190,20 @@ def run_case(mods, name, A, Ap_list, B, convert=False, remap=False, init_rand=Tr
     ia.best_coherence_match, ia.compute_distance = orig_bcm, orig_cd
 
     L = config.max_levels
+    ity = np.int32 if lean else np.int64
     out = {'A': A, 'B': B, 'Ap': np.stack(Ap_list), 'L': L, 'convert': convert, 'remap': remap,
            'init_rand': init_rand, 'AB_weight': AB_weight, 'k': k, 'seed': seed,
-           'weights': config.weights, 'app_ix': np.array(cap['app'], dtype=np.int64),
-           'coh': np.array(cap['coh'], dtype=np.int64).reshape(-1, 3),
-           'dist': np.array(cap['dist'], dtype=np.float64)}
+           'weights': config.weights, 'app_ix': np.array(cap['app'], dtype=ity),
+           'coh': np.array(cap['coh'], dtype=ity).reshape(-1, 3),
+           'dist': np.array(cap['dist'], dtype=np.float64), 'lean': lean}
     for l in range(len(cap['A_pyr'])):
         out['A_%d' % l] = cap['A_pyr'][l]
     for j, p in enumerate(cap['Ap_pyr']):
         for l in range(len(p)):
             out['Ap%d_%d' % (j, l)] = p[l]
     for j, p in enumerate(cap['color_pyr']):
+        if lean and not convert:
+            break   # identical to the A' pyramid
         for l in range(len(p)):
             out['color%d_%d' % (j, l)] = p[l]
     for l in range(len(cap['B_pyr'])):
@@ -205,21 +212,47 @@ def run_case(mods, name, A, Ap_list, B, convert=False, remap=False, init_rand=Tr
         out['Bp_%d' % l] = cap['Bp_live'][l]
     # s / im per level in level order (dict preserves insertion order)
     for l, (s, im) in zip(range(1, L), cap['s'].values()):
-        out['s_%d' % l] = np.array([np.asarray(p, dtype=np.int64) for p in s]).reshape(-1, 2)
-        out['im_%d' % l] = np.array(im, dtype=np.int64)
+        out['s_%d' % l] = np.array([np.asarray(p, dtype=np.int64) for p in s]).reshape(-1, 2).astype(ity)
+        out['im_%d' % l] = np.array(im, dtype=ity)
     for f, x in colour.items():
-        if f.startswith('level_'):
+        if f.startswith('level_') and (not lean or int(f.split('_')[1]) == L - 1):
             out['out_' + f.split('_')[1]] = x
     np.savez_compressed(os.path.join(OUT, 'e2e_%s.npz' % name), **out)
     print('case %-10s L=%d levels, %d px synthesised' % (name, L, len(cap['app'])))
 
 
+def big_cases(mods, names):
+    """Round-2 fixtures at the sizes the pruned scan and cfg1 need (VERDICT r1 'do this' 1):
+    cfg1 = the shore-crop stand-in of BASELINE config 1 (117x180 RGB -> YIQ luminance, k = 0.5,
+    seeds 1/2/3); g128 / g256 = the bench generator at 128^2 / 256^2; ties128 =
+    piecewise-constant 128^2 (exact duplicate DB rows at a size where every level can prune);
+    k25 = 96^2 with kappa 25 (cfg4's high-kappa coherence)."""
+    todo = {
+        'cfg1': lambda: run_case(mods, 'cfg1', smooth(117, 180, 2, 1, ch=3), [filt(smooth(117, 180, 2, 1, ch=3))],
+                                 smooth(117, 180, 2, 2, ch=3), convert=True, k=0.5, seed=3, lean=True),
+        'g128': lambda: run_case(mods, 'g128', smooth(128, 128, 2, 1), [filt(smooth(128, 128, 2, 1))],
+                                 smooth(128, 128, 2, 2), seed=3, lean=True),
+        'ties128': lambda: run_case(mods, 'ties128', blocky(128, 128, 16), [1 - blocky(128, 128, 16)],
+                                    blocky(128, 128, 17), seed=5, lean=True),
+        'k25': lambda: run_case(mods, 'k25', smooth(96, 96, 2, 18), [filt(smooth(96, 96, 2, 18))],
+                                smooth(96, 96, 2, 19), k=25.0, seed=6, lean=True),
+        'g256': lambda: run_case(mods, 'g256', smooth(256, 256, 2, 1), [filt(smooth(256, 256, 2, 1))],
+                                 smooth(256, 256, 2, 2), seed=3, lean=True),
+    }
+    for n in names:
+        todo[n]()
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     tmp = tempfile.mkdtemp()
+    want = sys.argv[1:] or ['base']
     try:
         mods = load_reference(tmp)
         config, img_preprocess, algorithms, ia = mods
+        big_cases(mods, [n for n in want if n != 'base'])
+        if 'base' not in want:
+            return
 
         # G1 weights (config.py:68-79)
         np.savez(os.path.join(OUT, 'weights.npz'),

@@ -5,6 +5,11 @@ import numpy as np
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden')
 E2E_CASES = ['g32', 'g24k5', 'rect', 'g64', 'yiq', 'remap', 'rgb3', 'multiap', 'noinit', 'ties']
+# round-2 reference runs at larger sizes (oracle/gen_golden.py big_cases; 'lean' fixtures):
+# cfg1 = BASELINE config 1's 117x180 YIQ stand-in, g128 / g256 = the bench generator,
+# ties128 = piecewise-constant (duplicate DB rows), k25 = kappa 25
+BIG_CASES = [c for c in ['cfg1', 'g128', 'ties128', 'k25', 'g256']
+             if os.path.exists(os.path.join(GOLDEN, 'e2e_%s.npz' % c))]
 
 
 def load_e2e(name):
@@ -19,6 +24,8 @@ def load_e2e(name):
     d['B_pyr'] = [z['B_%d' % l] for l in range(nB)]
     d['Bp_init'] = [z['Bp0_%d' % l] for l in range(nB)]
     d['Bp_final'] = [z['Bp_%d' % l] for l in range(nB)]
-    d['s'] = {l: z['s_%d' % l] for l in range(1, L)}
-    d['im'] = {l: z['im_%d' % l] for l in range(1, L)}
+    d['s'] = {l: z['s_%d' % l].astype(np.int64) for l in range(1, L)}
+    d['im'] = {l: z['im_%d' % l].astype(np.int64) for l in range(1, L)}
+    d['app_ix'] = z['app_ix'].astype(np.int64)
+    d['coh'] = z['coh'].astype(np.int64)
     return d

@@ -128,3 +128,39 @@ def test_ctypes_structs_match_the_c_header(tmp_path):
         assert got[(cname, 'sizeof')] == ctypes.sizeof(py), cname
         for f, _ in py._fields_:
             assert got[(cname, f)] == getattr(py, f).offset, (cname, f)
+
+
+def test_level_shape_contract_raises_before_the_abi():
+    """every size the C ABI derives (weights = 55 * ch, B' = B's shape, coarse levels
+    = ceil halves, A' = A's shape, B's channel count = A's) is checked on the host first."""
+    import numpy as np
+    import ia_amd  # noqa: F401
+    from ia_amd import _native
+    A, Ac = np.zeros((9, 7)), np.zeros((5, 4))
+    B, Bc = np.zeros((6, 8)), np.zeros((3, 4))
+    Ap, Apc = np.zeros((1, 9, 7)), np.zeros((1, 5, 4))
+    w = np.zeros(55)
+    assert _native.check_level_shapes(A, Ac, Ap, Apc, B, Bc, Bc, B.copy(), w) == 1
+    bad = [
+        (A, Ac, Ap, Apc, B, Bc, Bc, B.copy(), np.zeros(31)),            # n_lg = 3 weight vector
+        (A, Ac, Ap, Apc, B, Bc, Bc, np.zeros((6, 7)), w),               # B' shape
+        (A, np.zeros((4, 4)), Ap, Apc, B, Bc, Bc, B.copy(), w),         # coarse A
+        (A, Ac, np.zeros((1, 9, 6)), Apc, B, Bc, Bc, B.copy(), w),      # A' shape
+        (A, Ac, Ap, Apc, B, np.zeros((3, 3)), Bc, B.copy(), w),         # coarse B
+        (A, Ac, Ap, Apc, B, Bc, np.zeros((2, 4)), B.copy(), w),         # coarse B'
+        (A, Ac, Ap, Apc, np.zeros((6, 8, 3)), np.zeros((3, 4, 3)), np.zeros((3, 4, 3)),
+         np.zeros((6, 8, 3)), np.zeros(165)),                           # channels of B != A
+    ]
+    for args in bad:
+        with pytest.raises(_native.IAError):
+            _native.check_level_shapes(*args)
+
+
+def test_window_sizes_other_than_the_reference_are_refused():
+    import types
+    import ia_amd  # noqa: F401
+    from ia_amd.image_analogies import check_windows
+    check_windows(types.SimpleNamespace(n_sm=3, n_lg=5, n_half=12))
+    for bad in (dict(n_sm=3, n_lg=3, n_half=4), dict(n_sm=5, n_lg=5, n_half=12)):
+        with pytest.raises(ValueError):
+            check_windows(types.SimpleNamespace(**bad))

@@ -14,29 +14,47 @@ import pickle
 import numpy as np
 import pytest
 
-from golden_util import E2E_CASES, load_e2e
+from golden_util import BIG_CASES, E2E_CASES, load_e2e
 
 pytestmark = pytest.mark.gpu
 
 
-def _run_debug(ctx, z):
+def _run_debug(ctx, z, prune_all=False):
+    """prune_all: option prune_min_rows = 1, so every 1-channel level goes through the certified
+    pruned scan (K2p -> K3p) instead of only DB levels of >= 2^19 rows."""
+    from ia_amd import _native
     L, k = z['L'], float(z['k'])
     Bp = [x.copy() for x in z['Bp_init']]
     out = {}
-    for level in range(1, L):
-        kf = 1 + (2 ** (level - L)) * k
-        dbg = {}
-        s, im = ctx.synthesize_level(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
-                                     [p[level - 1] for p in z['Ap_pyr']], z['B_pyr'][level], z['B_pyr'][level - 1],
-                                     Bp[level - 1], Bp[level], z['weights'], kf, debug=dbg)
-        out[level] = (s, im, dbg)
-    return out, Bp
+    st = _native.Stats()
+    if prune_all:
+        ctx.set_option('prune_min_rows', 1)
+    try:
+        for level in range(1, L):
+            kf = 1 + (2 ** (level - L)) * k
+            dbg = {}
+            s, im = ctx.synthesize_level(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
+                                         [p[level - 1] for p in z['Ap_pyr']], z['B_pyr'][level],
+                                         z['B_pyr'][level - 1], Bp[level - 1], Bp[level], z['weights'], kf, st,
+                                         debug=dbg)
+            out[level] = (s, im, dbg)
+    finally:
+        ctx.set_option('prune_min_rows', 524288)
+    return out, Bp, st
 
 
-@pytest.mark.parametrize('name', E2E_CASES)
-def test_debug_records_match_reference_calls(ctx, name):
+@pytest.mark.parametrize('prune_all', [False, True], ids=['default', 'pruned'])
+@pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
+def test_debug_records_match_reference_calls(ctx, name, prune_all):
+    """Every NN pick, coherence pick and compute_distance value of the reference run.  With
+    prune_all, the pruned scan K3p decides every 1-channel level (the bench's
+    dominant kernel checked directly against the reference's own per-pixel picks)."""
     z = load_e2e(name)
-    out, Bp = _run_debug(ctx, z)
+    out, Bp, st = _run_debug(ctx, z, prune_all)
+    ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]
+    if prune_all:
+        assert st.pruned_levels == (z['L'] - 1 if ch == 1 else 0)
+    assert st.bound_violations == 0 and st.kappa_ambiguous == 0
     app, coh, dist = [], [], []
     for level in range(1, z['L']):
         s, im, dbg = out[level]

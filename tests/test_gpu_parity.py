@@ -1,7 +1,8 @@
 """GPU parity: the HIP path (through the C ABI) against the reference's own outputs.
 
 Golden end-to-end fixtures (tests/golden/e2e_*.npz) were produced by running the real reference
-(oracle/gen_golden.py).  Fed the same pyramids, B' initialisation and weights, the GPU level
+(oracle/gen_golden.py): the round-1 cases up to 64x64 and the round-2 cases cfg1 (BASELINE
+config 1's 117x180 YIQ stand-in), g128, g256, ties128 and k25 (kappa 25).  Fed the same pyramids, B' initialisation and weights, the GPU level
 path must reproduce every level's source map s, image map im and final B' BIT-EXACTLY: the NN
 is exact (certified MFMA + fp64 rerank in numpy's summation order), coherence distances are
 bit-identical, and the kappa test's weighted distances follow the golden host's BLAS dot order
@@ -10,21 +11,19 @@ bit-identical, and the kappa test's weighted distances follow the golden host's 
 import numpy as np
 import pytest
 
-from golden_util import E2E_CASES, load_e2e
+from golden_util import BIG_CASES, E2E_CASES, load_e2e
 
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=['f16x3', 'f16x3-cmpsel', 'f32'])
+@pytest.fixture(params=['f16x3', 'f32'])
 def matcher(request, ctx):
-    """Every certified matcher (split-f16 MFMA with the packed-index or the compare/select K3
-    epilogue, fp32 MFMA) must give the reference's decisions."""
+    """Every certified matcher (split-f16 MFMA with the packed-index K3 epilogue, fp32 MFMA)
+    must give the reference's decisions."""
     from ia_amd import _native
     ctx.set_option('matcher', _native.IA_MATCH_F32 if request.param == 'f32' else _native.IA_MATCH_F16X3)
-    ctx.set_option('k3_variant', 0 if request.param == 'f16x3-cmpsel' else 1)
-    yield request.param.split('-')[0]
+    yield request.param
     ctx.set_option('matcher', _native.IA_MATCH_F16X3)
-    ctx.set_option('k3_variant', 1)
 
 
 def _run_levels(ctx, z, Bp, A_pyr=None, Ap_pyr=None, B_pyr=None):
@@ -41,7 +40,7 @@ def _run_levels(ctx, z, Bp, A_pyr=None, Ap_pyr=None, B_pyr=None):
     return out, st
 
 
-@pytest.mark.parametrize('name', E2E_CASES)
+@pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
 def test_level_path_matches_reference(ctx, matcher, name):
     z = load_e2e(name)
     Bp = [x.copy() for x in z['Bp_init']]

@@ -10,10 +10,22 @@ import ia_amd  # noqa: F401
 pytestmark = pytest.mark.gpu
 
 
+def _diag_build(ctx):
+    """True when libia was built with DIAG=1 (every kernel version selectable)."""
+    from ia_amd import _native
+    try:
+        ctx.set_option('k3p_variant', 6)
+    except _native.IAError:
+        return False
+    ctx.set_option('k3p_variant', 7)
+    return True
+
+
 def _run(ctx, job, prune, variant=7):
     from ia_amd import _native
     ctx.set_option('prune', prune)
-    ctx.set_option('k3p_variant', variant)
+    if variant != 7:
+        ctx.set_option('k3p_variant', variant)
     ctx.set_option('prune_min_rows', 262144)  # prune the 512^2 level too (default: 1024^2 and up)
     Bp = [x.copy() for x in job.Bp_init]
     S, IM = {}, {}
@@ -31,11 +43,15 @@ def _run(ctx, job, prune, variant=7):
     return Bp, S, IM, st
 
 
-@pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 10), (1024, 2, 10), (1024, 2, 9), (512, 1, 8), (1024, 2, 8), (1024, 2, 6), (1024, 2, 7), (1024, 2, 5), (1024, 2, 4),
-                                                      (1024, 2, 3), (1024, 2, 1), (512, 1, 0), (512, 1, 2)])
+@pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 7), (1024, 2, 7), (512, 1, 10), (1024, 2, 9), (512, 1, 8),
+                                                      (1024, 2, 6), (1024, 2, 5), (1024, 2, 4), (1024, 2, 3),
+                                                      (1024, 2, 1), (512, 1, 0), (512, 1, 2)])
 def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
-    """variant = the pruned-scan kernel version (option k3p_variant): every one is exact"""
+    """variant = the pruned-scan kernel version (option k3p_variant; the product build holds the
+    default 7 and the fallback 1 only, DIAG=1 builds the rest): every one is exact"""
     from ia_amd import synth
+    if variant != 7 and not _diag_build(ctx):
+        pytest.skip('kernel version %d is built with DIAG=1 only' % variant)
     job = synth.make_job(size)
     Bp0, S0, IM0, st0 = _run(ctx, job, 0)
     Bp1, S1, IM1, st1 = _run(ctx, job, 1, variant)
@@ -59,5 +75,8 @@ def test_prune_option_rejects_bad_values(ctx):
         ctx.set_option('prune', 2)
     with pytest.raises(_native.IAError):
         ctx.set_option('k3p_variant', 11)
+    if not _diag_build(ctx):
+        with pytest.raises(_native.IAError):
+            ctx.set_option('k3p_variant', 6)
     with pytest.raises(_native.IAError):
         ctx.set_option('prune_min_rows', 0)
