@@ -63,6 +63,10 @@ EXPORTS = {
     'ia_index_query': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                       ctypes.c_void_p]),
     'ia_index_destroy': (None, [ctypes.c_void_p]),
+    'ia_coherence_batch': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                          ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
     'ia_k3_microbench': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_double)]),
     'ia_merge_winners': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
@@ -244,6 +248,26 @@ class ExactIndex(object):
         dist = np.empty(q.shape[0], dtype=np.float64)
         check(lib().ia_index_query(self._h, _ptr(q), q.shape[0], _ptr(idx), _ptr(dist)), 'ia_index_query')
         return idx, dist
+
+    def coherence(self, q, px, s, im, A_hw, Bp_w, pad=2):
+        """ia_coherence_batch: best_coherence_match (algorithms.py:92-130) of every pixel px[i]
+        (row, col) with query feature q[i], against this index's rows (As).  s (n, 2) / im (n)
+        must cover every causal neighbour of the batch.  Returns (p (nq, 2), img (nq,),
+        r_star (nq, 2)) as int32; p = (-1, -1), img 0, r_star (0, 0) where there is no candidate."""
+        q = _c64(np.atleast_2d(q))
+        px = np.ascontiguousarray(np.atleast_2d(px), dtype=np.int32)
+        s = np.ascontiguousarray(np.asarray(s).reshape(-1, 2), dtype=np.int32)
+        im = np.ascontiguousarray(np.asarray(im).reshape(-1), dtype=np.int32)
+        if q.shape[1] != self.d or px.shape != (q.shape[0], 2) or len(im) != len(s):
+            raise IAError('ExactIndex.coherence: q (nq, %d), px (nq, 2) and len(s) == len(im) expected' % self.d)
+        nq = q.shape[0]
+        p = np.empty((nq, 2), dtype=np.int32)
+        img = np.empty(nq, dtype=np.int32)
+        rs = np.empty((nq, 2), dtype=np.int32)
+        check(lib().ia_coherence_batch(self._h, _ptr(q), nq, _ptr(px), _ptr(s), _ptr(im), len(s), int(A_hw[0]),
+                                       int(A_hw[1]), int(Bp_w), int(pad), _ptr(p), _ptr(img), _ptr(rs)),
+              'ia_coherence_batch')
+        return p, img, rs
 
     def close(self):
         if self._h:

@@ -9,10 +9,13 @@ Hot-path functions run on the GPU:
   * image_analogies_main does not call the per-pixel functions at all: the whole level (DB
     build, wavefront, NN, coherence, kappa rule, writeback) is one ia_synthesize_level call.
 
-compute_feature_array, extract_pixel_feature, best_coherence_match and compute_distance are
-kept as the reference's per-pixel/array helpers (host numpy over the caller's arrays) for code
-written against that API; the level path computes the same quantities on the GPU (K1/K2/K4 in
-csrc/ia_kernels.hip).
+  * best_coherence_match: libia's ia_coherence_batch (one wave per pixel) against the rows of
+    the index create_index built for that level (As[level] carries it, IndexedRows);
+    best_coherence_match_batch answers many pixels in one call.
+
+compute_feature_array, extract_pixel_feature and compute_distance are kept as the reference's
+per-pixel/array helpers (host numpy over the caller's arrays) for code written against that API;
+the level path computes the same quantities on the GPU (K1/K2/K4 in csrc/ia_kernels.hip).
 """
 import numpy as np
 
@@ -92,6 +95,28 @@ class GpuFLANN(object):
             self._index = None
 
 
+class IndexedRows(np.ndarray):
+    """The As[level] array of create_index (algorithms.py:63-67) with the GPU index built over it
+    attached (`.index`, an _native.ExactIndex), so best_coherence_match finds the device copy of
+    the rows instead of uploading them per call.  Behaves as the plain ndarray otherwise."""
+
+    def __new__(cls, rows, index):
+        obj = np.asarray(rows).view(cls)
+        obj.index = index
+        return obj
+
+    def __array_finalize__(self, obj):
+        self.index = getattr(obj, 'index', None)
+
+
+def _rows_index(As):
+    idx = getattr(As, 'index', None)
+    if idx is not None and idx._h and As.shape == (idx.n, idx.d):
+        return idx
+    # rows without an attached index (e.g. a caller-built As): one GPU upload for this call
+    return _native.ExactIndex(default_context(), np.asarray(As))
+
+
 def create_index(A_pyr, Ap_pyr_list, c):
     """Per-level DB of [A full feature | A'_i half feature] rows stacked over the A' images and
     its (GPU) index (algorithms.py:50-70).  Returns (flann, flann_params, As, As_size)."""
@@ -106,6 +131,7 @@ def create_index(A_pyr, Ap_pyr_list, c):
         As[level] = np.vstack([np.hstack([A_feat[level], f[level]]) for f in Ap_feats])
         As_size[level] = As[level].shape
         flann_params[level] = flann[level].build_index(As[level], algorithm='kdtree')
+        As[level] = IndexedRows(As[level], flann[level]._index)
     return flann, flann_params, As, As_size
 
 
@@ -129,28 +155,24 @@ def extract_pixel_feature(padded_pair, px, c, full_feat):
 
 
 def best_coherence_match(As, A_hw, BBp_feat, s, im, px, Bp_w, c):
-    """Coherence candidate of pixel px (algorithms.py:92-130): over the already synthesised
-    pixels r of the causal L-shaped window (rows px-2..px, cols px-2..px+2, raster-earlier),
-    candidate p = s(r) + (px - r) in image im(r) if inside A; first argmin of the unweighted
-    L2 distance.  Returns (p, img, r*) or ((-1, -1), 0, (0, 0))."""
-    A_h, A_w = A_hw
-    row, col = int(px[0]), int(px[1])
-    here = row * Bp_w + col
-    cand_rows, out = [], []
-    for rr in range(max(0, row - int(c.pad_lg)), row + 1):
-        for rc in range(max(0, col - int(c.pad_lg)), min(Bp_w, col + int(c.pad_lg) + 1)):
-            ri = rr * Bp_w + rc
-            if ri >= here:
-                continue
-            pr = np.asarray(s[ri]) + np.array([row - rr, col - rc])
-            if 0 <= pr[0] < A_h and 0 <= pr[1] < A_w:
-                cand_rows.append(Ap_px2ix(pr, im[ri], A_h, A_w))
-                out.append((pr, im[ri], np.array([rr, rc])))
-    if not out:
+    """Coherence candidate of pixel px (algorithms.py:92-130), on the GPU (ia_coherence_batch):
+    over the already synthesised pixels r of the causal L-shaped window (rows px-2..px, cols
+    px-2..px+2, raster-earlier), candidate p = s(r) + (px - r) in image im(r) if inside A; first
+    argmin of the unweighted L2 distance.  Returns (p, img, r*) or ((-1, -1), 0, (0, 0)).
+    s / im are the level's lists so far (raster order), as the reference keeps them."""
+    p, img, rs = best_coherence_match_batch(As, A_hw, np.atleast_2d(BBp_feat), s, im, np.array([px]), Bp_w, c)
+    if p[0, 0] < 0:
         return (-1, -1), 0, (0, 0)
-    diff = As[np.array(cand_rows)] - BBp_feat
-    best = int(np.argmin(np.sqrt(np.add.reduce(diff * diff, axis=1))))
-    return out[best]
+    return p[0].astype(np.int64), int(img[0]), rs[0].astype(np.int64)
+
+
+def best_coherence_match_batch(As, A_hw, BBp_feats, s, im, pxs, Bp_w, c):
+    """best_coherence_match for many pixels in one GPU call (e.g. one wavefront step: every
+    causal neighbour of every pixel must already be in s / im).  Returns int32 arrays
+    p (n, 2), img (n,), r_star (n, 2); p = (-1, -1) where there is no candidate."""
+    s = np.asarray(s, dtype=np.int32).reshape(-1, 2)
+    im = np.asarray(im, dtype=np.int32).reshape(-1)
+    return _rows_index(As).coherence(BBp_feats, pxs, s, im, A_hw, Bp_w, int(c.pad_lg))
 
 
 def compute_distance(AAp_p, BBp_q, weights):

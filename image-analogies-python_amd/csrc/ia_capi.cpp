@@ -102,6 +102,7 @@ struct ia_index {
   int64_t n = 0;
   int d = 0, KH = 0, n_tiles = 0, tpw = 0, nwg = 0;
   DevBuf pts, db, mu, Rbits, q, q64, qn2, qf, rec, recT, idx, dist, counters;
+  DevBuf cpx, cs, cim, cout;  // ia_coherence_batch staging
 };
 
 namespace {
@@ -847,12 +848,49 @@ int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, d
   return IA_OK;
 }
 
+int ia_coherence_batch(ia_index *x, const double *q, int64_t nq, const int32_t *px, const int32_t *s, const int32_t *im,
+                       int64_t n_s, int a_h, int a_w, int bp_w, int pad, int32_t *p_out, int32_t *img_out, int32_t *rstar_out) {
+  if (!x || nq < 0 || n_s < 0 || a_h < 1 || a_w < 1 || bp_w < 1 || pad < 0 || (pad + 1) * (2 * pad + 1) > 64)
+    return fail(IA_EINVAL, "ia_coherence_batch: bad arguments (pad must be 0..4)");
+  if (nq == 0) return IA_OK;
+  if (!q || !px || !p_out || !img_out || !rstar_out || (n_s > 0 && (!s || !im)))
+    return fail(IA_EINVAL, "ia_coherence_batch: NULL buffer");
+  ia_ctx *c = x->ctx;
+  HIP_TRY(hipSetDevice(c->dev));
+  int rc;
+  if ((rc = x->q.ensure((size_t)nq * x->d * 8)) || (rc = x->cpx.ensure((size_t)nq * 8)) ||
+      (rc = x->cs.ensure((size_t)std::max<int64_t>(n_s, 1) * 8)) || (rc = x->cim.ensure((size_t)std::max<int64_t>(n_s, 1) * 4)) ||
+      (rc = x->cout.ensure((size_t)nq * 20 + 16)))
+    return rc;
+  int32_t *dp = x->cout.as<int32_t>(), *di = dp + 2 * nq, *dr = di + nq;
+  unsigned *derr = reinterpret_cast<unsigned *>(dr + 2 * nq);
+  HIP_TRY(hipMemcpyAsync(x->q.p, q, (size_t)nq * x->d * 8, hipMemcpyHostToDevice, c->st));
+  HIP_TRY(hipMemcpyAsync(x->cpx.p, px, (size_t)nq * 8, hipMemcpyHostToDevice, c->st));
+  if (n_s > 0) {
+    HIP_TRY(hipMemcpyAsync(x->cs.p, s, (size_t)n_s * 8, hipMemcpyHostToDevice, c->st));
+    HIP_TRY(hipMemcpyAsync(x->cim.p, im, (size_t)n_s * 4, hipMemcpyHostToDevice, c->st));
+  }
+  HIP_TRY(hipMemsetAsync(derr, 0, 4, c->st));
+  ia_launch_coherence_batch(x->pts.as<double>(), x->n, x->d, x->q.as<double>(), nq, x->cpx.as<int32_t>(), x->cs.as<int32_t>(),
+                            x->cim.as<int32_t>(), n_s, a_h, a_w, bp_w, pad, dp, di, dr, derr, c->st);
+  HIP_TRY(hipGetLastError());
+  unsigned err = 0;
+  HIP_TRY(hipMemcpyAsync(p_out, dp, (size_t)nq * 8, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(hipMemcpyAsync(img_out, di, (size_t)nq * 4, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(hipMemcpyAsync(rstar_out, dr, (size_t)nq * 8, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(hipMemcpyAsync(&err, derr, 4, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(hipStreamSynchronize(c->st));
+  if (err & 1u) return fail(IA_EINVAL, "ia_coherence_batch: a causal neighbour lies beyond the n_s entries of s / im");
+  if (err & 2u) return fail(IA_EINVAL, "ia_coherence_batch: a coherence candidate's DB row lies beyond the index");
+  return IA_OK;
+}
+
 void ia_index_destroy(ia_index *x) {
   if (!x) return;
   hipSetDevice(x->ctx->dev);
   hipStreamSynchronize(x->ctx->st);
   for (DevBuf *b : {&x->pts, &x->db, &x->mu, &x->Rbits, &x->q, &x->q64, &x->qn2, &x->qf, &x->rec, &x->recT, &x->idx,
-                    &x->dist, &x->counters})
+                    &x->dist, &x->counters, &x->cpx, &x->cs, &x->cim, &x->cout})
     b->release();
   delete x;
 }

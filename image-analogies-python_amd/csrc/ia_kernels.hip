@@ -1563,6 +1563,74 @@ __global__ void __launch_bounds__(IA_WG) k_merge_dense(MergeArgs ma, const doubl
   }
 }
 
+// best_coherence_match (algorithms.py:92-130) for a batch of B' pixels against an index's rows,
+// one wave per pixel.  Lane j < (pad+1)(2 pad+1) is the window cell (row - pad + j / (2 pad+1),
+// col - pad + j % (2 pad+1)), i.e. product(rows, cols) order (:101-104); a cell is a candidate
+// when it is inside the level, raster-earlier (:107) and its shifted source s[r] + (q - r) lies
+// inside A (:116).  Distance = sqrt of numpy's pairwise sum of squares (norm(..., axis=1),
+// :126), first argmin.  err bit 0: an s index beyond n_s; bit 1: a DB row beyond the index.
+__global__ void __launch_bounds__(IA_WG) k_coherence_batch(const double *__restrict__ pts, int64_t n, int d,
+                                                            const double *__restrict__ q, int64_t nq,
+                                                            const int32_t *__restrict__ px, const int32_t *__restrict__ s,
+                                                            const int32_t *__restrict__ im, int64_t n_s, int a_h, int a_w,
+                                                            int bp_w, int pad, int32_t *__restrict__ p_out,
+                                                            int32_t *__restrict__ img_out, int32_t *__restrict__ r_out,
+                                                            unsigned *__restrict__ err) {
+  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
+  if (m >= nq) return;
+  const int row = px[2 * m], col = px[2 * m + 1], wd = 2 * pad + 1;
+  const int rr = row - pad + lane / wd, rc = col - pad + lane % wd;
+  const int64_t here = (int64_t)row * bp_w + col, ri = (int64_t)rr * bp_w + rc;
+  bool ok = lane < (pad + 1) * wd && rr >= 0 && rc >= 0 && rc < bp_w && ri < here;
+  int pr0 = 0, pr1 = 0, img = 0;
+  int64_t dbrow = 0;
+  unsigned e = 0;
+  if (ok && ri >= n_s) {
+    e |= 1u;
+    ok = false;
+  }
+  if (ok) {
+    pr0 = s[2 * ri] + row - rr;
+    pr1 = s[2 * ri + 1] + col - rc;
+    img = im[ri];
+    ok = pr0 >= 0 && pr0 < a_h && pr1 >= 0 && pr1 < a_w;
+    dbrow = ((int64_t)img * a_h + pr0) * a_w + pr1;
+    if (ok && (dbrow < 0 || dbrow >= n)) {
+      e |= 2u;
+      ok = false;
+    }
+  }
+  double dist = INFINITY;
+  int64_t key = ok ? lane : 64;
+  if (ok) {
+    const double *a = pts + dbrow * d, *qm = q + (int64_t)m * d;
+    dist = cr_sqrt(pw_sum_rt([&](int f) {
+      const double x = a[f] - qm[f];
+      return x * x;
+    }, d));
+  }
+  if (e) atomicOr(err, e);
+  wave_min_di(dist, key);  // first argmin (lowest window cell) among the candidates
+  if (key >= 64) {
+    if (lane == 0) {
+      p_out[2 * m] = -1;
+      p_out[2 * m + 1] = -1;
+      img_out[m] = 0;
+      r_out[2 * m] = 0;
+      r_out[2 * m + 1] = 0;
+    }
+    return;
+  }
+  if (lane == (int)key) {  // s[r*] + q - r*, im[r*], r*
+    p_out[2 * m] = pr0;
+    p_out[2 * m + 1] = pr1;
+    img_out[m] = img;
+    r_out[2 * m] = rr;
+    r_out[2 * m + 1] = rc;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // host-side launchers (called from ia_capi.cpp)
 // ------------------------------------------------------------------------------------------
@@ -1696,6 +1764,12 @@ void ia_launch_dense_query(int KH, const double *q, int64_t nq, int d, int Mpad,
 void ia_launch_merge_dense(const MergeArgs &ma, const double *pts, int d, const double *q, int64_t nq, int64_t *idx,
                            double *dist, hipStream_t st) {
   hipLaunchKernelGGL(k_merge_dense, dim3(cdiv(nq, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, ma, pts, d, q, nq, idx, dist);
+}
+void ia_launch_coherence_batch(const double *pts, int64_t n, int d, const double *q, int64_t nq, const int32_t *px,
+                               const int32_t *s, const int32_t *im, int64_t n_s, int a_h, int a_w, int bp_w, int pad,
+                               int32_t *p_out, int32_t *img_out, int32_t *r_out, unsigned *err, hipStream_t st) {
+  hipLaunchKernelGGL(k_coherence_batch, dim3(cdiv(nq, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, pts, n, d, q, nq, px, s, im, n_s,
+                     a_h, a_w, bp_w, pad, p_out, img_out, r_out, err);
 }
 
 // ---- split-f16 matcher launchers -----------------------------------------------------------

@@ -25,6 +25,9 @@ void ia_launch_dense_query(int KH, const double *q, int64_t nq, int d, int Mpad,
                            hipStream_t st);
 void ia_launch_merge_dense(const MergeArgs &ma, const double *pts, int d, const double *q, int64_t nq, int64_t *idx,
                            double *dist, hipStream_t st);
+void ia_launch_coherence_batch(const double *pts, int64_t n, int d, const double *q, int64_t nq, const int32_t *px,
+                               const int32_t *s, const int32_t *im, int64_t n_s, int a_h, int a_w, int bp_w, int pad,
+                               int32_t *p_out, int32_t *img_out, int32_t *r_out, unsigned *err, hipStream_t st);
 // split-f16 matcher (IA_MATCH_F16X3)
 int ia_ks_for(int ch);
 double ia_k3h_tile_bytes(int KS);  // HBM bytes of one split-f16 DB tile (TileFmt)

@@ -144,6 +144,20 @@ int ia_index_build(ia_ctx *ctx, const double *pts, int64_t n, int d, ia_index **
  * lowest index on ties.  q is nq x d fp64; idx_out (nq) int64, dist_out (nq) fp64 (may be NULL). */
 int ia_index_query(ia_index *index, const double *q, int64_t nq, int64_t *idx_out, double *dist_out);
 void ia_index_destroy(ia_index *index);
+/* best_coherence_match (algorithms.py:92-130) for nq B' pixels against the index's rows (the
+ * As of create_index, algorithms.py:63-67), one call per batch instead of one per pixel.
+ * q: nq x d fp64 query features (BBp_feat); px: nq x 2 int32 (row, col) of each pixel in the
+ * B' level of width bp_w; s (n_s x 2 int32) / im (n_s) the raster-order source map of that
+ * level, which must hold every causal neighbour of every pixel of the batch (s[r], im[r] for
+ * the raster-earlier r in rows row-pad..row, cols col-pad..col+pad); a_h, a_w: A's level
+ * shape (DB row = Ap_px2ix(p, im, a_h, a_w), img_preprocess.py:104-106); pad = c.pad_lg (2).
+ * Out per pixel: p_out (row, col) = s[r*] + px - r*, img_out = im[r*], rstar_out = r*; or
+ * (-1, -1), 0, (0, 0) without a candidate.  Candidates are ranked by sqrt of numpy's pairwise
+ * sum of squares, first argmin (np.argmin of norm(..., axis=1)).  IA_EINVAL when a neighbour
+ * index reaches beyond n_s or a candidate row beyond the index (an IndexError there). */
+int ia_coherence_batch(ia_index *index, const double *q, int64_t nq, const int32_t *px,
+                       const int32_t *s, const int32_t *im, int64_t n_s, int a_h, int a_w,
+                       int bp_w, int pad, int32_t *p_out, int32_t *img_out, int32_t *rstar_out);
 
 /* ---- kernel tuning ------------------------------------------------------------------------- */
 /* Time the split-f16 distance scan (K3h, current "k3_variant") alone: n_rows random DB rows

@@ -20,6 +20,12 @@ Recipe:
        (img_preprocess.py:56; the Py2-era skimage treated ndim==3 as multichannel).
      - plt.imread returns in-memory arrays; plt.imsave captures the colour output.
   3. state is captured by wrapping functions in the `image_analogies` module namespace.
+  4. compute_distance's last bits depend on the ddot kernel OpenBLAS (DYNAMIC_ARCH) picks for
+     the host CPU.  Containers whose CPUID OpenBLAS does not recognise fall back to the generic
+     'Prescott' kernel, a different summation order than the SkylakeX kernel the round-1
+     fixtures were made with.  OPENBLAS_CORETYPE=SkylakeX is therefore set before numpy loads,
+     and _check_blas_order() refuses to write fixtures unless np.dot matches the order
+     oracle/ia_oracle.py blas_ddot_sq (and the kernels' blas_dot_sq) restate.
 
 Run:  /opt/conda/bin/python3.9 oracle/gen_golden.py            (base fixtures, ~1-2 min)
       /opt/conda/bin/python3.9 oracle/gen_golden.py cfg1 g128 ties128 k25 g256
@@ -32,11 +38,24 @@ import sys
 import tempfile
 import types
 
-import numpy as np
+os.environ.setdefault('OPENBLAS_CORETYPE', 'SkylakeX')   # before numpy loads OpenBLAS (step 4)
+import numpy as np  # noqa: E402
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, '..', 'tests', 'golden')
 REF = '/root/reference'
+
+
+def _check_blas_order():
+    sys.path.insert(0, os.path.join(HERE, '..'))
+    from oracle.ia_oracle import blas_ddot_sq
+    rs = np.random.RandomState(0)
+    for n in list(range(1, 60)) + [110, 165]:
+        for _ in range(8):
+            x = rs.rand(n) * 1e-2
+            if np.dot(x, x) != blas_ddot_sq(x):
+                raise SystemExit('gen_golden: np.dot(x, x) (n=%d) does not follow the SkylakeX ddot order; '
+                                 'OPENBLAS_CORETYPE=%s' % (n, os.environ.get('OPENBLAS_CORETYPE')))
 
 
 # ----------------------------------------------------------------------------- shims
@@ -244,6 +263,7 @@ def big_cases(mods, names):
 
 
 def main():
+    _check_blas_order()
     os.makedirs(OUT, exist_ok=True)
     tmp = tempfile.mkdtemp()
     want = sys.argv[1:] or ['base']

@@ -53,30 +53,53 @@ def test_teacher_forced_256(ctx, size, levels, n):
     job = synth.make_job(size)
     Bp, S, IM, st = _run_job(ctx, job)
     assert st.pixels == job.pixels
+    _invariants(job, Bp, S, IM)
     for level in levels:
         npx, mism = _teacher_force(job, Bp, S, IM, level, n, seed=level)
         assert all(near for _, near, _, _ in mism), mism
         assert len(mism) <= max(1, npx // 100), mism
 
 
-def test_teacher_forced_1024_finest_level(ctx):
-    """cfg3 (BASELINE metric config): the full 10-level 1024^2 job, 40 sampled finest-level pixels."""
-    from ia_amd import synth
-    job = synth.make_job(1024)
-    Bp, S, IM, st = _run_job(ctx, job)
-    L = job.L
-    # size-independent invariants on every level: sources inside A, B' values copied from A'
-    for level in range(1, L):
+def _invariants(job, Bp, S, IM):
+    """size-independent invariants on every level: sources inside A, B' values copied from A'"""
+    for level in range(1, job.L):
         s, im = S[level], IM[level]
         A_h, A_w = job.A_pyr[level].shape[:2]
         assert (s[:, 0] >= 0).all() and (s[:, 0] < A_h).all() and (s[:, 1] >= 0).all() and (s[:, 1] < A_w).all()
         assert (im == 0).all()
         assert np.array_equal(Bp[level].ravel(), job.Ap_pyr_list[0][level][s[:, 0], s[:, 1]])
-    npx, mism = _teacher_force(job, Bp, S, IM, L - 1, 40, seed=1)
-    assert all(near for _, near, _, _ in mism), mism
-    assert len(mism) <= 1, mism
+
+
+def test_teacher_forced_cfg2(ctx):
+    """BASELINE config 2 (512^2, n_levels=5: the kappa factor uses L = 5): every synthesised level
+    teacher-forced on 100 sampled pixels."""
+    from ia_amd import synth
+    job = synth.make_job(**synth.CONFIGS['cfg2'][0])
+    assert job.L == 5 and job.B_pyr[-1].shape == (512, 512)
+    Bp, S, IM, st = _run_job(ctx, job)
+    assert st.pixels == job.pixels and st.bound_violations == 0
+    _invariants(job, Bp, S, IM)
+    for level in range(1, job.L):
+        npx, mism = _teacher_force(job, Bp, S, IM, level, 100, seed=10 + level)
+        assert all(near for _, near, _, _ in mism), (level, mism)
+        assert len(mism) <= max(1, npx // 100), (level, mism)
+
+
+def test_teacher_forced_1024_levels_5_to_9(ctx):
+    """cfg3 (BASELINE metric config): the full 10-level 1024^2 job (pruned scan on the 1024^2
+    level), 100 sampled pixels teacher-forced on each of levels 5..9 (64^2 .. 1024^2)."""
+    from ia_amd import synth
+    job = synth.make_job(1024)
+    Bp, S, IM, st = _run_job(ctx, job)
+    L = job.L
+    _invariants(job, Bp, S, IM)
+    for level in range(5, L):
+        npx, mism = _teacher_force(job, Bp, S, IM, level, 100, seed=level)
+        assert all(near for _, near, _, _ in mism), (level, mism)
+        assert len(mism) <= max(1, npx // 100), (level, mism)
     assert st.fallbacks < 0.01 * st.pixels
     assert st.bound_violations == 0 and st.f16_levels == L - 1   # default matcher: split-f16
+    assert st.pruned_levels == 1
 
 
 def test_driver_end_to_end_matches_oracle(tmp_path):
