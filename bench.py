@@ -72,11 +72,11 @@ class DeviceJob(object):
                                         ptrs, self.job.kappa_factor(l), stats)
 
 
-def cpu_baseline(job, seconds):
+def cpu_per_pixel(job, seconds):
     """Reference loop (oracle restatement: per-pixel np.pad + exact fp64 numpy NN, 1 thread)
     timed on bounded raster samples of the three finest levels; coarser levels are priced by
     scaling the smallest sampled level's per-pixel cost with the DB size (the per-pixel cost is
-    a full DB scan + a full-level pad, position independent)."""
+    a full DB scan + a full-level pad, position independent).  Returns ({level: s/px}, sample)."""
     from oracle import ia_oracle as O
     L = job.L
     lv = [l for l in range(L - 1, 0, -1)][:3]
@@ -87,18 +87,43 @@ def cpu_baseline(job, seconds):
         t2 = O.time_sample(job.A_pyr, job.Ap_pyr_list, job.B_pyr, job.Bp_init, l, L, job.k, job.weights, 2)
         n = int(max(2, min(n_b, budget / max(t2, 1e-9))))
         per_px[l] = O.time_sample(job.A_pyr, job.Ap_pyr_list, job.B_pyr, job.Bp_init, l, L, job.k, job.weights, n)
-        sample.append('%d px of level %d (%dx%d)' % (n, l, job.B_pyr[l].shape[0], job.B_pyr[l].shape[1]))
+        sample.append('%d px of level %d (%dx%d B, %dx%d A)' % (n, l, job.B_pyr[l].shape[0], job.B_pyr[l].shape[1],
+                                                                 job.A_pyr[l].shape[0], job.A_pyr[l].shape[1]))
     lmin = min(lv)
     na_min = np.prod(job.A_pyr[lmin].shape[:2])
-    total = 0.
     for l in range(1, L):
-        n_b = np.prod(job.B_pyr[l].shape[:2])
-        t = per_px[l] if l in per_px else per_px[lmin] * np.prod(job.A_pyr[l].shape[:2]) / na_min
-        total += n_b * t
+        if l not in per_px:
+            per_px[l] = per_px[lmin] * np.prod(job.A_pyr[l].shape[:2]) / na_min
+    return per_px, sample
+
+
+def cpu_baseline(job, seconds):
+    per_px, sample = cpu_per_pixel(job, seconds)
+    total = sum(np.prod(job.B_pyr[l].shape[:2]) * per_px[l] for l in range(1, job.L))
     return {'value': job.pixels / total, 'unit': "B' px/s", 'cores': 1, 'kind': 'port',
             'sample': 'oracle/ia_oracle.py reference-loop restatement (per-pixel pad, exact fp64 NN), '
                       'timed on ' + ', '.join(sample) + '; coarser levels scaled by DB size; '
                       'extrapolated whole-job time %.0f s' % total}
+
+
+def cpu_baseline_sweep(sw, seconds):
+    """cfg5: per-pixel costs of each resolution from the deepest job, summed over every job's
+    levels (the reference runs the jobs one after the other, multi_script.py:19-32)."""
+    from ia_amd import synth
+    deep = int(np.argmax(sw.L))
+    off = sw.offset(deep)
+    job = synth.Job(sw.A_pyr[off:], [p[off:] for p in sw.Ap_pyr_list], sw.B_pyr[off:], sw.Bp_init[deep],
+                    sw.jobs[deep].k, sw.weights)
+    per_px, sample = cpu_per_pixel(job, seconds)
+    total = 0.
+    for j in range(len(sw.jobs)):
+        for l in range(1, sw.L[j]):
+            f = sw.offset(j) + l
+            total += np.prod(sw.B_pyr[f].shape[:2]) * per_px[f - off]
+    return {'value': sw.pixels() / total, 'unit': "B' px/s", 'cores': 1, 'kind': 'port',
+            'sample': 'oracle/ia_oracle.py reference-loop restatement, timed on ' + ', '.join(sample) +
+                      ' of the deepest job; every job of the sweep priced per level; extrapolated sweep time '
+                      '%.0f s' % total}
 
 
 def main():
@@ -106,7 +131,12 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=3)
     ap.add_argument('--warmup', type=int, default=1)
-    ap.add_argument('--config', default='cfg3', help='synthetic workload (ia_amd.synth.CONFIGS)')
+    ap.add_argument('--config', default='cfg3', help='synthetic workload (ia_amd.synth.CONFIGS): cfg3 (default), '
+                    'cfg2, cfg4 (2048^2 B vs 1024^2 A, kappa 25) or cfg5 (64-job sweep)')
+    ap.add_argument('--sequential', action='store_true',
+                    help='cfg5: run the sweep one job at a time (the reference\'s order) instead of batching the '
+                         'jobs that share a GPU')
+    ap.add_argument('--max-batch', type=int, default=16, help='cfg5: jobs per batched level call')
     ap.add_argument('--mode', default='replicas', choices=['replicas', 'shard'])
     ap.add_argument('--matcher', default='f16x3', choices=['f16x3', 'f32'],
                     help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
@@ -143,9 +173,26 @@ def main():
 
     kw, desc = synth.CONFIGS[args.config]
     t0 = time.time()
-    job = synth.make_job(**kw)
-    log('[bench] rank %d: job %s built in %.1fs: L=%d, %d B\' px/step, %.3e NN flops/step'
-        % (rank, args.config, time.time() - t0, job.L, job.pixels, job.flops()))
+    sw = None
+    if args.config == 'cfg5':
+        from ia_amd import sweep
+        n = kw['size']
+        A = synth.smooth(n, n, 2, 1)
+        sw = sweep.Sweep(A, [synth.filt(A)], synth.smooth(n, n, 2, 2), sweep.cfg5_jobs())
+        mine = [j for j in range(len(sw.jobs)) if j % world == rank]
+        deep = int(np.argmax(sw.L))
+        job = synth.Job(sw.A_pyr, sw.Ap_pyr_list, sw.B_pyr, sw.Bp_init[deep], sw.jobs[deep].k, sw.weights)
+        job_pixels = sw.pixels()
+        job_flops = sum(2.0 * 55 * np.prod(sw.A_pyr[sw.offset(j) + l].shape[:2]) *
+                        np.prod(sw.B_pyr[sw.offset(j) + l].shape[:2]) for j in range(len(sw.jobs))
+                        for l in range(1, sw.L[j]))
+        log('[bench] rank %d: sweep of %d jobs (%d on this rank) built in %.1fs: %d B\' px/step'
+            % (rank, len(sw.jobs), len(mine), time.time() - t0, job_pixels))
+    else:
+        job = synth.make_job(**kw)
+        job_pixels, job_flops = job.pixels, job.flops()
+        log('[bench] rank %d: job %s built in %.1fs: L=%d, %d B\' px/step, %.3e NN flops/step'
+            % (rank, args.config, time.time() - t0, job.L, job.pixels, job.flops()))
 
     ctx = _native.Context(local)
     ctx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
@@ -159,10 +206,17 @@ def main():
         uid = [_native.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(rank, world, uid[0])
-    dj = DeviceJob(job, torch, dev)
+    if sw is not None:
+        from ia_amd import sweep
+        dsw = sweep.DeviceSweep(sw, mine, torch, dev)
+        run = lambda st: dsw.run(ctx, st, batched=not args.sequential, max_batch=args.max_batch)
+        dj = dsw
+    else:
+        dj = DeviceJob(job, torch, dev)
+        run = lambda st: dj.run(ctx, torch, st)
 
     for _ in range(args.warmup):
-        dj.run(ctx, torch, _native.Stats())
+        run(_native.Stats())
     if args.time_stride > 0:
         ctx.set_option('time_dist', args.time_stride)
     stats = _native.Stats()
@@ -171,7 +225,7 @@ def main():
         dist.barrier()
     t_start = time.perf_counter()
     for _ in range(args.steps):
-        dj.run(ctx, torch, stats)
+        run(stats)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -182,8 +236,8 @@ def main():
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    jobs = world if (args.mode == 'replicas') else 1
-    pixels = job.pixels * args.steps * jobs
+    jobs = world if (args.mode == 'replicas' and sw is None) else 1   # cfg5: the ranks split one sweep
+    pixels = job_pixels * args.steps * jobs
     value = pixels / elapsed
     st = stats.as_dict()
     log('[bench] rank %d stats: %s' % (rank, json.dumps(st)))
@@ -238,19 +292,22 @@ def main():
     # nothing pruned) per second, against the fp32 MFMA dense peak.  The timed kernel does not
     # do that work (certified pruning skips most (DB tile, query tile) pairs), so this is an
     # "equivalent" rate and may exceed the peak; pairs_frac is the share actually contracted.
-    fp32_equiv = job.flops() * args.steps * jobs / elapsed
+    fp32_equiv = job_flops * args.steps * jobs / elapsed
     roofline['fp32_mfma_equiv_tflops'] = fp32_equiv / 1e12
     roofline['fp32_mfma_equiv_frac'] = fp32_equiv / FP32_MFMA_PEAK
     roofline['pairs_frac'] = st['dist_pairs'] / max(st['dist_pairs_full'], 1.)
     out = {'metric': METRIC, 'value': value, 'unit': "B' px/s", 'n_gpus': world, 'steps': args.steps,
            'warmup': args.warmup, 'ms_per_step': elapsed * 1e3 / args.steps, 'higher_is_better': True,
-           'scaling': 'weak' if args.mode == 'replicas' else 'strong', 'vs_baseline': None,
+           'scaling': 'strong' if (args.mode == 'shard' or sw is not None) else 'weak', 'vs_baseline': None,
            'dtype': 'f16x3' if f16 else 'f32',
            'data': 'synthetic', 'config': {'workload': '%s: %s' % (args.config, desc),
-                                           'a_shape': list(job.A_pyr[-1].shape), 'pyramid_levels': job.L,
-                                           'px_per_step': job.pixels, 'nn_flops_per_step': job.flops(),
-                                           'mode': args.mode, 'parallelism': ('replicas%d' if args.mode == 'replicas'
-                                                                              else 'dbshard%d') % world,
+                                           'a_shape': list(job.A_pyr[-1].shape), 'b_shape': list(job.B_pyr[-1].shape),
+                                           'pyramid_levels': job.L,
+                                           'px_per_step': job_pixels, 'nn_flops_per_step': job_flops,
+                                           'mode': 'sweep' if sw is not None else args.mode,
+                                           'parallelism': (('jobs%d' % world) if sw is not None else
+                                                           ('replicas%d' if args.mode == 'replicas' else 'dbshard%d')
+                                                           % world),
                                            'nn': 'exact: %s MFMA candidates + certified fp64 rerank'
                                                  % ('split-f16 (hi/lo x3)' if f16 else 'fp32'),
                                            'precision': ('f16x3 = every operand split into f16 hi + lo, 3 MFMA '
@@ -263,13 +320,17 @@ def main():
                                                             'synthesis) from device-resident pyramids to device '
                                                             "completion of B'/s/im; the D2H copy of B'/s/im (about "
                                                             '%.0f MB, <1%% of the step) is excluded'
-                                                            % (job.pixels * 20 / 1e6))},
+                                                            % (job_pixels * 20 / 1e6))},
            'roofline': roofline,
            'stats': {k: st[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
                                         'synth_ms', 'bound_violations', 'kappa_ambiguous', 'f16_levels', 'pruned_levels',
                                         'dist_pairs', 'dist_pairs_full', 'dist_tiles', 'dist_tiles_full')}}
+    if sw is not None:
+        out['config']['sweep'] = {'jobs': len(sw.jobs), 'batched': not args.sequential, 'max_batch': args.max_batch,
+                                  'kappas': sorted({j.k for j in sw.jobs}), 'depths': sorted(set(sw.L))}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = cpu_baseline(job, args.cpu_seconds)
+        out['cpu_baseline'] = (cpu_baseline_sweep(sw, args.cpu_seconds) if sw is not None
+                               else cpu_baseline(job, args.cpu_seconds))
     if rank == 0:
         print(json.dumps(out), flush=True)
     ctx.close()

@@ -58,6 +58,8 @@ EXPORTS = {
     'ia_comm_unique_id': (ctypes.c_int, [ctypes.c_char_p]),
     'ia_comm_init': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
     'ia_synthesize_level': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LevelArgs), ctypes.POINTER(Stats)]),
+    'ia_synthesize_levels': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LevelArgs), ctypes.c_int,
+                                            ctypes.POINTER(Stats)]),
     'ia_index_build': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_void_p)]),
     'ia_index_query': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
@@ -187,44 +189,71 @@ class Context(object):
         debug: a dict to receive the debug=True per-pixel records (include/ia.h dbg_src/dbg_dist):
         'src' (N, 6) int32 [p_app row, col, img, r_star row, col, has_coh], 'dist' (N, 2) fp64
         [d_app, d_coh] (image_analogies.py:224-240), finished on the host as numpy does."""
-        A, Ac, B, Bc, Bpc = _c64(A), _c64(Ac), _c64(B), _c64(Bc), _c64(Bpc)
+        job = dict(B=B, Bc=Bc, Bpc=Bpc, Bp=Bp, weights=weights, kappa_factor=kappa_factor, debug=debug)
+        return self.synthesize_levels(A, Ac, Ap_list, Apc_list, [job], stats)[0]
+
+    def synthesize_levels(self, A, Ac, Ap_list, Apc_list, jobs, stats=None):
+        """ia_synthesize_levels: one level of several jobs that share the A side (A, A' levels l and
+        l-1), e.g. a kappa / pyramid-depth sweep (multi_script.py).  jobs: list of dicts with
+        B, Bc, Bpc, Bp (updated in place), weights, kappa_factor and optionally debug (a dict, see
+        synthesize_level).  One DB, one distance scan per wavefront step for all jobs.  Returns
+        [(s, im)] per job, each identical to a separate synthesize_level call."""
+        if not 1 <= len(jobs) <= 32:
+            raise IAError('synthesize_levels: 1..32 jobs per call (got %d)' % len(jobs))
+        A, Ac = _c64(A), _c64(Ac)
         Ap = _c64(np.stack(Ap_list))
         Apc = _c64(np.stack(Apc_list))
-        w = _c64(weights)
-        if not (isinstance(Bp, np.ndarray) and Bp.dtype == np.float64 and Bp.flags.c_contiguous):
-            raise IAError('Bp must be a C-contiguous float64 array (updated in place)')
-        ch = check_level_shapes(A, Ac, Ap, Apc, B, Bc, Bpc, Bp, w)
-        bh, bw = B.shape[:2]
-        s = np.empty((bh * bw, 2), dtype=np.int32)
-        im = np.empty(bh * bw, dtype=np.int32)
-        dsrc = ddist = None
-        if debug is not None:
-            dsrc = np.zeros((bh * bw, 6), dtype=np.int32)
-            ddist = np.zeros((bh * bw, 2), dtype=np.float64)
-        args = LevelArgs(ch, Ap.shape[0], A.shape[0], A.shape[1], bh, bw,
-                         _ptr(A), _ptr(Ac), _ptr(Ap), _ptr(Apc), _ptr(B), _ptr(Bc), _ptr(Bpc), _ptr(Bp), _ptr(w),
-                         float(kappa_factor), _ptr(s), _ptr(im), IA_MEM_HOST,
-                         None if dsrc is None else _ptr(dsrc), None if ddist is None else _ptr(ddist))
+        keep, args, outs = [], [], []
+        for jb in jobs:
+            B, Bc, Bpc, Bp, w = _c64(jb['B']), _c64(jb['Bc']), _c64(jb['Bpc']), jb['Bp'], _c64(jb['weights'])
+            if not (isinstance(Bp, np.ndarray) and Bp.dtype == np.float64 and Bp.flags.c_contiguous):
+                raise IAError('Bp must be a C-contiguous float64 array (updated in place)')
+            ch = check_level_shapes(A, Ac, Ap, Apc, B, Bc, Bpc, Bp, w)
+            bh, bw = B.shape[:2]
+            s = np.empty((bh * bw, 2), dtype=np.int32)
+            im = np.empty(bh * bw, dtype=np.int32)
+            dsrc = ddist = None
+            if jb.get('debug') is not None:
+                dsrc = np.zeros((bh * bw, 6), dtype=np.int32)
+                ddist = np.zeros((bh * bw, 2), dtype=np.float64)
+            args.append(LevelArgs(ch, Ap.shape[0], A.shape[0], A.shape[1], bh, bw,
+                                  _ptr(A), _ptr(Ac), _ptr(Ap), _ptr(Apc), _ptr(B), _ptr(Bc), _ptr(Bpc), _ptr(Bp),
+                                  _ptr(w), float(jb['kappa_factor']), _ptr(s), _ptr(im), IA_MEM_HOST,
+                                  None if dsrc is None else _ptr(dsrc), None if ddist is None else _ptr(ddist)))
+            keep.append((B, Bc, Bpc, w))
+            outs.append((s, im, dsrc, ddist, jb.get('debug')))
+        arr = (LevelArgs * len(args))(*args)
         st = stats if stats is not None else Stats()
-        check(lib().ia_synthesize_level(self._h, ctypes.byref(args), ctypes.byref(st)), 'ia_synthesize_level')
-        if debug is not None:
-            # compute_distance = norm(x) ** 2 on numpy scalars: sqrt, then libm pow(., 2), which
-            # can differ from sqrt(v) * sqrt(v) by 1 ulp; finish it here exactly like that
-            for qi in np.flatnonzero(dsrc[:, 5]):
-                ddist[qi, 0] = math.sqrt(ddist[qi, 0]) ** 2
-                ddist[qi, 1] = math.sqrt(ddist[qi, 1]) ** 2
-            debug['src'], debug['dist'] = dsrc, ddist
-        return s, im
+        check(lib().ia_synthesize_levels(self._h, arr, len(args), ctypes.byref(st)), 'ia_synthesize_levels')
+        res = []
+        for s, im, dsrc, ddist, debug in outs:
+            if debug is not None:
+                # compute_distance = norm(x) ** 2 on numpy scalars: sqrt, then libm pow(., 2), which
+                # can differ from sqrt(v) * sqrt(v) by 1 ulp; finish it here exactly like that
+                for qi in np.flatnonzero(dsrc[:, 5]):
+                    ddist[qi, 0] = math.sqrt(ddist[qi, 0]) ** 2
+                    ddist[qi, 1] = math.sqrt(ddist[qi, 1]) ** 2
+                debug['src'], debug['dist'] = dsrc, ddist
+            res.append((s, im))
+        return res
 
     def synthesize_level_device(self, ch, n_ap, a_hw, b_hw, ptrs, kappa_factor, stats=None):
         """Same on device pointers (IA_MEM_DEVICE): ptrs = dict of int addresses for
         A, Ac, Ap, Apc, B, Bc, Bpc, Bp, weights, s_out, im_out (e.g. torch tensor data_ptr())."""
-        p = {k: ctypes.c_void_p(int(v)) for k, v in ptrs.items()}
-        args = LevelArgs(ch, n_ap, a_hw[0], a_hw[1], b_hw[0], b_hw[1], p['A'], p['Ac'], p['Ap'], p['Apc'],
-                         p['B'], p['Bc'], p['Bpc'], p['Bp'], p['weights'], float(kappa_factor),
-                         p['s_out'], p['im_out'], IA_MEM_DEVICE)
+        return self.synthesize_levels_device(ch, n_ap, a_hw, b_hw, [ptrs], [kappa_factor], stats)
+
+    def synthesize_levels_device(self, ch, n_ap, a_hw, b_hw, ptr_list, kappa_factors, stats=None):
+        """ia_synthesize_levels on device pointers: one ptrs dict per job (the A-side addresses
+        must be equal in all of them), one kappa factor per job."""
+        args = []
+        for ptrs, kf in zip(ptr_list, kappa_factors):
+            p = {k: ctypes.c_void_p(int(v)) for k, v in ptrs.items()}
+            args.append(LevelArgs(ch, n_ap, a_hw[0], a_hw[1], b_hw[0], b_hw[1], p['A'], p['Ac'], p['Ap'], p['Apc'],
+                                  p['B'], p['Bc'], p['Bpc'], p['Bp'], p['weights'], float(kf),
+                                  p['s_out'], p['im_out'], IA_MEM_DEVICE))
+        arr = (LevelArgs * len(args))(*args)
         st = stats if stats is not None else Stats()
-        check(lib().ia_synthesize_level(self._h, ctypes.byref(args), ctypes.byref(st)), 'ia_synthesize_level')
+        check(lib().ia_synthesize_levels(self._h, arr, len(args), ctypes.byref(st)), 'ia_synthesize_levels')
         return st
 
 

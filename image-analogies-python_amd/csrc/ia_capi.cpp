@@ -65,6 +65,13 @@ struct DevBuf {
   }
 };
 
+struct JobBufs {
+  DevBuf B, Bc, Bpc, Bp, S, IM, W, DSRC, DDIST, pstat;
+  void release() {
+    for (DevBuf *b : {&B, &Bc, &Bpc, &Bp, &S, &IM, &W, &DSRC, &DDIST, &pstat}) b->release();
+  }
+};
+
 int kh_for(int d_plus_norm) {  // smallest instantiated K3 width that holds d + norm column
   if (d_plus_norm <= 56) return 28;
   if (d_plus_norm <= 112) return 56;
@@ -78,8 +85,10 @@ struct ia_ctx {
   int dev = 0;
   hipStream_t st = nullptr;
   // uploads (IA_MEM_HOST) and per-level scratch
-  DevBuf A, Ac, Ap, Apc, B, Bc, Bpc, Bp, S, IM, W, DSRC, DDIST;
-  DevBuf db, db64, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, pstat, absmax;
+  DevBuf A, Ac, Ap, Apc;
+  std::vector<JobBufs> jb;  // per job of a batch: B-side uploads / outputs, stats words
+  DevBuf jobs;              // device JobPtrs[n_jobs]
+  DevBuf db, db64, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, absmax;
   // certified pruned scan (option "prune"): per-level basis, sorted DB table, tile boxes
   DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs, ord;
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
@@ -240,8 +249,9 @@ void ia_destroy(ia_ctx *c) {
   if (!c) return;
   hipSetDevice(c->dev);
   hipStreamSynchronize(c->st);
-  for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->B, &c->Bc, &c->Bpc, &c->Bp, &c->S, &c->IM, &c->W, &c->DSRC, &c->DDIST, &c->db, &c->db64,
-                    &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->pstat, &c->absmax,
+  for (JobBufs &b : c->jb) b.release();
+  for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->jobs, &c->db, &c->db64,
+                    &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
                     &c->boxes, &c->qinfo, &c->pairs, &c->ord})
     b->release();
@@ -385,8 +395,7 @@ static int stage(ia_ctx *c, DevBuf &buf, const void *src, size_t bytes, int mem,
   return IA_OK;
 }
 
-int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
-  if (!c || !a) return fail(IA_EINVAL, "ia_synthesize_level: NULL argument");
+static int check_level_args(const ia_level_args *a) {
   if (a->ch < 1 || a->ch > 3) return fail(IA_EINVAL, "ia_synthesize_level: ch must be 1, 2 or 3");
   if (a->n_ap < 1 || a->a_h < 1 || a->a_w < 1 || a->b_h < 1 || a->b_w < 1)
     return fail(IA_EINVAL, "ia_synthesize_level: empty image or no A' image");
@@ -398,7 +407,28 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     return fail(IA_EINVAL, "ia_synthesize_level: dbg_src and dbg_dist are given together or not at all");
   if ((int64_t)a->n_ap * a->a_h * a->a_w >= (int64_t)INT32_MAX)
     return fail(IA_EINVAL, "ia_synthesize_level: DB rows exceed int32 row ids");
+  return IA_OK;
+}
+
+int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) { return ia_synthesize_levels(c, a, 1, stats); }
+
+int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_stats *stats) {
+  if (!c || !args) return fail(IA_EINVAL, "ia_synthesize_level: NULL argument");
+  if (n_jobs < 1 || n_jobs > IA_MAX_JOBS)
+    return fail(IA_EINVAL, "ia_synthesize_levels: n_jobs must be 1.." + std::to_string(IA_MAX_JOBS));
+  const ia_level_args *a = &args[0];
+  int rc;
+  for (int j = 0; j < n_jobs; j++) {
+    const ia_level_args *x = &args[j];
+    if ((rc = check_level_args(x))) return rc;
+    if (x->ch != a->ch || x->n_ap != a->n_ap || x->a_h != a->a_h || x->a_w != a->a_w || x->b_h != a->b_h ||
+        x->b_w != a->b_w || x->mem != a->mem)
+      return fail(IA_EINVAL, "ia_synthesize_levels: every job of a batch has the same shapes, channels and mem kind");
+    if (x->A != a->A || x->Ac != a->Ac || x->Ap != a->Ap || x->Apc != a->Apc)
+      return fail(IA_EINVAL, "ia_synthesize_levels: every job of a batch shares the A side (same A / A' buffers)");
+  }
   HIP_TRY(hipSetDevice(c->dev));
+  const int J = n_jobs;
 
   LevelGeo g;
   g.pos2row = nullptr;
@@ -419,9 +449,11 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   g.n_tiles = (int)((g.NA + IA_TILE - 1) / IA_TILE);
   // shard the DB over ranks unless the level is too small to be worth an exchange per step
   const bool sharded = shard_level(g.n_tiles, c->world);
-  const int world = sharded ? c->world : 1, rank = sharded ? c->rank : 0;
-  if (sharded && a->dbg_src)
-    return fail(IA_EINVAL, "ia_synthesize_level: debug outputs are produced by single-rank levels only");
+  const int world = sharded ? c->world : 1;
+  if (sharded && J > 1) return fail(IA_EINVAL, "ia_synthesize_levels: sharded levels take one job per call");
+  for (int j = 0; j < J; j++)
+    if (sharded && args[j].dbg_src)
+      return fail(IA_EINVAL, "ia_synthesize_level: debug outputs are produced by single-rank levels only");
   {
     int64_t t0, t1;
     ia_shard_tiles(g.NA, c->world, c->rank, &t0, &t1);
@@ -435,36 +467,54 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   const size_t nA = (size_t)g.ah * g.aw * g.ch, nAc = (size_t)g.ahc * g.awc * g.ch;
   const size_t nB = (size_t)g.bh * g.bw * g.ch, nBc = (size_t)g.bhc * g.bwc * g.ch;
   const int64_t NB = (int64_t)g.bh * g.bw;
-  const void *dA, *dAc, *dAp, *dApc, *dB, *dBc, *dBpc, *dW;
-  int rc;
+  const void *dA, *dAc, *dAp, *dApc;
   if ((rc = stage(c, c->A, a->A, nA * 8, a->mem, &dA)) || (rc = stage(c, c->Ac, a->Ac, nAc * 8, a->mem, &dAc)) ||
       (rc = stage(c, c->Ap, a->Ap, nA * g.n_ap * 8, a->mem, &dAp)) ||
-      (rc = stage(c, c->Apc, a->Apc, nAc * g.n_ap * 8, a->mem, &dApc)) ||
-      (rc = stage(c, c->B, a->B, nB * 8, a->mem, &dB)) || (rc = stage(c, c->Bc, a->Bc, nBc * 8, a->mem, &dBc)) ||
-      (rc = stage(c, c->Bpc, a->Bpc, nBc * 8, a->mem, &dBpc)) ||
-      (rc = stage(c, c->W, a->weights, (size_t)g.D * 8, a->mem, &dW)))
+      (rc = stage(c, c->Apc, a->Apc, nAc * g.n_ap * 8, a->mem, &dApc)))
     return rc;
-  double *dBp;
-  int32_t *dS, *dIM;
-  if (a->mem == IA_MEM_DEVICE) {
-    dBp = a->Bp;
-    dS = a->s_out;
-    dIM = a->im_out;
-  } else {
-    if ((rc = c->Bp.ensure(nB * 8)) || (rc = c->S.ensure((size_t)NB * 8)) || (rc = c->IM.ensure((size_t)NB * 4)))
+  // the B side of every job (host buffers: one staging set per job)
+  if ((int)c->jb.size() < J) c->jb.resize(J);
+  std::vector<JobPtrs> jp(J);
+  for (int j = 0; j < J; j++) {
+    const ia_level_args *x = &args[j];
+    JobBufs &b = c->jb[j];
+    const void *dB, *dBc, *dBpc, *dW;
+    if ((rc = stage(c, b.B, x->B, nB * 8, x->mem, &dB)) || (rc = stage(c, b.Bc, x->Bc, nBc * 8, x->mem, &dBc)) ||
+        (rc = stage(c, b.Bpc, x->Bpc, nBc * 8, x->mem, &dBpc)) || (rc = stage(c, b.W, x->weights, (size_t)g.D * 8, x->mem, &dW)) ||
+        (rc = b.pstat.ensure((size_t)NB * 4)))
       return rc;
-    dBp = c->Bp.as<double>();
-    dS = c->S.as<int32_t>();
-    dIM = c->IM.as<int32_t>();
-    HIP_TRY(hipMemcpyAsync(dBp, a->Bp, nB * 8, hipMemcpyHostToDevice, c->st));
+    JobPtrs &p = jp[j];
+    p.Bc = (const double *)dBc;
+    p.B = (const double *)dB;
+    p.Bpc = (const double *)dBpc;
+    p.weights = (const double *)dW;
+    p.kf = x->kappa_factor;
+    p.pstat = b.pstat.as<unsigned>();
+    if (x->mem == IA_MEM_DEVICE) {
+      p.Bp = x->Bp;
+      p.s = x->s_out;
+      p.im = x->im_out;
+      p.dbg_src = x->dbg_src;
+      p.dbg_dist = x->dbg_dist;
+    } else {
+      if ((rc = b.Bp.ensure(nB * 8)) || (rc = b.S.ensure((size_t)NB * 8)) || (rc = b.IM.ensure((size_t)NB * 4))) return rc;
+      p.Bp = b.Bp.as<double>();
+      p.s = b.S.as<int32_t>();
+      p.im = b.IM.as<int32_t>();
+      HIP_TRY(hipMemcpyAsync(p.Bp, x->Bp, nB * 8, hipMemcpyHostToDevice, c->st));
+      p.dbg_src = nullptr;
+      p.dbg_dist = nullptr;
+      if (x->dbg_src) {
+        if ((rc = b.DSRC.ensure((size_t)NB * 24)) || (rc = b.DDIST.ensure((size_t)NB * 16))) return rc;
+        p.dbg_src = b.DSRC.as<int32_t>();
+        p.dbg_dist = b.DDIST.as<double>();
+      }
+    }
+    HIP_TRY(hipMemsetAsync(p.pstat, 0, (size_t)NB * 4, c->st));
   }
-  int32_t *dDS = a->dbg_src;
-  double *dDD = a->dbg_dist;
-  if (a->dbg_src && a->mem == IA_MEM_HOST) {
-    if ((rc = c->DSRC.ensure((size_t)NB * 24)) || (rc = c->DDIST.ensure((size_t)NB * 16))) return rc;
-    dDS = c->DSRC.as<int32_t>();
-    dDD = c->DDIST.as<double>();
-  }
+  if ((rc = c->jobs.ensure(sizeof(JobPtrs) * J))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->jobs.p, jp.data(), sizeof(JobPtrs) * J, hipMemcpyHostToDevice, c->st));
+  const JobPtrs *djobs = c->jobs.as<JobPtrs>();
 
   // matcher: split-f16 when the channel count has a K3h instance and every image value fits
   // (IA_F16_MAXABS, one 4-byte read-back per level); otherwise the fp32 MFMA scan
@@ -472,11 +522,14 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   if (c->matcher == IA_MATCH_F16X3 && ia_ks_for(g.ch) > 0) {
     if ((rc = c->absmax.ensure(4))) return rc;
     HIP_TRY(hipMemsetAsync(c->absmax.p, 0, 4, c->st));
-    const double *arrs[8] = {(const double *)dA, (const double *)dAc, (const double *)dAp, (const double *)dApc,
-                             (const double *)dB, (const double *)dBc, (const double *)dBpc, dBp};
-    const int64_t ns8[8] = {(int64_t)nA, (int64_t)nAc, (int64_t)(nA * g.n_ap), (int64_t)(nAc * g.n_ap),
-                            (int64_t)nB, (int64_t)nBc, (int64_t)nBc, (int64_t)nB};
-    ia_launch_absmax(arrs, ns8, c->absmax.as<unsigned>(), c->st);
+    for (int j = 0; j < J; j++) {
+      const double *arrs[8] = {j ? nullptr : (const double *)dA, j ? nullptr : (const double *)dAc,
+                               j ? nullptr : (const double *)dAp, j ? nullptr : (const double *)dApc,
+                               jp[j].B, jp[j].Bc, jp[j].Bpc, jp[j].Bp};
+      const int64_t ns8[8] = {(int64_t)nA, (int64_t)nAc, (int64_t)(nA * g.n_ap), (int64_t)(nAc * g.n_ap),
+                              (int64_t)nB, (int64_t)nBc, (int64_t)nBc, (int64_t)nB};
+      ia_launch_absmax(arrs, ns8, c->absmax.as<unsigned>(), c->st);
+    }
     unsigned mbits = 0;
     HIP_TRY(hipMemcpyAsync(&mbits, c->absmax.p, 4, hipMemcpyDeviceToHost, c->st));
     HIP_TRY(hipStreamSynchronize(c->st));
@@ -493,7 +546,8 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   // one workgroup's LDS)
   int64_t T, Mmax;
   ia_wavefront_shape(g.bh, g.bw, &T, &Mmax);
-  const int64_t Mpad_max = (Mmax + IA_TILE - 1) / IA_TILE * IA_TILE;
+  const int64_t Mtmax = Mmax * J;  // queries of the widest step over all jobs
+  const int64_t Mpad_max = (Mtmax + IA_TILE - 1) / IA_TILE * IA_TILE;
   const bool prune = c->prune && use_h && g.ch == 1 && !sharded && g.NA >= c->prune_min_rows && Mpad_max <= 4096;
   if (prune) g.nwg = std::min(IA_NWG_H, g.n_tiles);  // round-robin chunks: WG w owns tiles w + nwg*k
   const size_t db_row_bytes = use_h ? (size_t)16 * g.KS * 4 : (size_t)DP * 4;  // hi+lo f16 / fp32 per column
@@ -503,21 +557,20 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       (rc = c->db64.ensure((size_t)g.NA * ia_db64_stride(g.ch) * 8)) ||
       (rc = c->Rbits.ensure(4)) || (rc = c->q64.ensure((size_t)Mpad_max * g.D * 8)) ||
       (rc = c->qn2.ensure((size_t)Mpad_max * 8)) || (rc = c->qf.ensure((size_t)Mpad_max * db_row_bytes)) ||
-      (rc = c->rec.ensure((size_t)Mmax * std::max(g.nwg, 1) * 16)) ||
-      (rc = c->recT.ensure((size_t)Mmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mmax * 16)) ||
-      (rc = c->allwin.ensure((size_t)Mmax * 16 * world)) || (rc = c->counters.ensure(5 * 8)) ||
-      (rc = c->pstat.ensure((size_t)NB * 4)) || (rc = c->pairs.ensure(4 * IA_NWG_H * 8)) || (rc = c->ord.ensure(2 * 4096 * 4)) ||
+      (rc = c->rec.ensure((size_t)Mtmax * std::max(g.nwg, 1) * 16)) ||
+      (rc = c->recT.ensure((size_t)Mtmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mtmax * 16)) ||
+      (rc = c->allwin.ensure((size_t)Mtmax * 16 * world)) || (rc = c->counters.ensure(5 * 8)) ||
+      (rc = c->pairs.ensure(4 * IA_NWG_H * 8)) || (rc = c->ord.ensure(2 * 4096 * 4)) ||
       (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 : 16)))
     return rc;
   // per-workgroup counters of the pruned scan: [pairs | pairs (timed steps) | tiles | tiles (timed)][wg]
   HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 4 * IA_NWG_H * 8, c->st));
   HIP_TRY(hipMemsetAsync(c->Rbits.p, 0, 4, c->st));
   HIP_TRY(hipMemsetAsync(c->counters.p, 0, 5 * 8, c->st));
-  HIP_TRY(hipMemsetAsync(c->pstat.p, 0, (size_t)NB * 4, c->st));
 
   Imgs Aim{(const double *)dAc, (const double *)dA, (const double *)dApc, (const double *)dAp,
            g.ah, g.aw, g.ahc, g.awc, (int64_t)nA, (int64_t)nAc};
-  Imgs Bim{(const double *)dBc, (const double *)dB, (const double *)dBpc, dBp, g.bh, g.bw, g.bhc, g.bwc, 0, 0};
+  Imgs Bim{nullptr, nullptr, nullptr, nullptr, g.bh, g.bw, g.bhc, g.bwc, 0, 0};  // images per job (JobPtrs)
 
   HIP_TRY(hipEventRecord(c->lv0, c->st));
   ia_launch_means(g.ch, Aim, g.n_ap, c->mu.as<double>(), c->st);
@@ -553,9 +606,6 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     const int64_t tr = ia_tile_perm(t, g.n_tiles);
     shard_rows += std::min<int64_t>(IA_TILE, (g.NA - tr + g.n_tiles - 1) / g.n_tiles);
   }
-  ma.pstat = c->pstat.as<unsigned>();
-  ma.dbg_src = dDS;
-  ma.dbg_dist = dDD;
   ma.eps_c = use_h ? ia_eps_c_h(g.KS, prune || c->k3_variant == 1) : ia_eps_c(DP);
   ma.eps_a = use_h ? ia_eps_a_h() : 0.;
 
@@ -573,19 +623,22 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
   for (int64_t t = 0; t < T; t++) {
     StepDesc sd;
     sd.t = (int)t;
+    sd.J = J;
     ia_wavefront_step(g.bh, g.bw, t, &sd.r0, &sd.M);
     if (sd.M <= 0) {  // levels narrower than 3 columns have empty steps
       ord_n = 0;
       continue;
     }
-    sd.Mpad = (sd.M + IA_TILE - 1) / IA_TILE * IA_TILE;
+    const int Mt = J * sd.M;  // queries of this step over all jobs
+    sd.Mpad = (Mt + IA_TILE - 1) / IA_TILE * IA_TILE;
     if (prune)
-      ia_launch_gather_p(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
-                         c->db64.as<double>(), dS, dIM, c->pr_basis.as<double>(), ufac, c->qinfo.as<float4>(), c->st);
+      ia_launch_gather_p(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
+                         c->db64.as<double>(), c->pr_basis.as<double>(), ufac, c->qinfo.as<float4>(), c->st);
     else if (use_h)
-      ia_launch_gather_h(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p, c->st);
+      ia_launch_gather_h(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p, c->st);
     else
-      ia_launch_gather(g, sd, Bim, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(), c->st);
+      ia_launch_gather(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(),
+                       c->st);
     if (ns > 0) {
       const int qtt = sd.Mpad / IA_TILE, nqb = (qtt + qtmax - 1) / qtmax;
       const bool timed = stride && t % stride == 0;
@@ -594,19 +647,19 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       for (int b = 0; b < nqb; b++) {
         const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
         if (prune)
-          ia_launch_k3p(qt, c->db.p, c->qf.p, c->qinfo.as<float4>(), c->boxes.as<float4>(), g.pos2row, g.n_tiles, qt0, sd.M,
+          ia_launch_k3p(qt, c->db.p, c->qf.p, c->qinfo.as<float4>(), c->boxes.as<float4>(), g.pos2row, g.n_tiles, qt0, Mt,
                         sd.Mpad, g.nwg, c->rec.as<float4>(), c->recT.as<float>(),
                         c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                         c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
                         c->k3p_variant, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
                         c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), c->st);
         else if (use_h)
-          ia_launch_k3h(g.KS, qt, c->db.p, c->qf.p, ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0, ma.NT, c->rec.as<float4>(),
+          ia_launch_k3h(g.KS, qt, c->db.p, c->qf.p, ns, g.tiles_per_wg, qt0, Mt, g.nwg, ma.pos0, ma.NT, c->rec.as<float4>(),
                         c->recT.as<float>(), c->k3_variant, c->st);
         else
-          ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, sd.M, g.nwg, ma.pos0,
+          ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, Mt, g.nwg, ma.pos0,
                        ma.NT, c->rec.as<float4>(), c->recT.as<float>(), c->st);
-        const int mq = std::min(sd.M, (qt0 + qt) * IA_TILE) - qt0 * IA_TILE;
+        const int mq = std::min(Mt, (qt0 + qt) * IA_TILE) - qt0 * IA_TILE;
         const double fl = prune ? 0. : 2.0 * g.D * (double)shard_rows * std::max(mq, 0);  // pruned: pair counters
         dist_flops += fl;
         pairs_full += (double)ns * qt;
@@ -623,28 +676,30 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
         qt0 += qt;
       }
       if (timed) hipEventRecord(c->evs[2 * n_rec++ + 1], c->st);
-      ord_n = prune && sd.Mpad <= 4096 ? sd.M : 0;
+      ord_n = prune && J == 1 && sd.Mpad <= 4096 ? sd.M : 0;
     }
     if (!sharded) {
-      ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), dS, dIM, dBp, (const double *)dW, a->kappa_factor, true, c->st);
+      ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), djobs, true, c->st);
     } else {
-      ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), dS, dIM, dBp, (const double *)dW, a->kappa_factor, false,
-                      c->st);
+      ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), djobs, false, c->st);
       NCCL_TRY(ncclAllGather(c->win.p, c->allwin.p, (size_t)sd.M * sizeof(Winner), ncclUint8, c->comm, c->st));
-      ia_launch_finish(g, sd, Aim, c->db64.as<double>(), c->q64.as<double>(), c->allwin.as<Winner>(), world, sd.M, dS, dIM, dBp,
-                       (const double *)dW, a->kappa_factor, c->pstat.as<unsigned>(), c->st);
+      ia_launch_finish(g, sd, Aim, c->db64.as<double>(), c->q64.as<double>(), c->allwin.as<Winner>(), world, sd.M, djobs,
+                       c->st);
     }
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->lv2, c->st));
-  if (stats) ia_launch_reduce_stats(c->pstat.as<unsigned>(), NB, c->counters.as<unsigned long long>(), c->st);
-  if (a->mem == IA_MEM_HOST) {
-    HIP_TRY(hipMemcpyAsync(a->Bp, dBp, nB * 8, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(hipMemcpyAsync(a->s_out, dS, (size_t)NB * 8, hipMemcpyDeviceToHost, c->st));
-    HIP_TRY(hipMemcpyAsync(a->im_out, dIM, (size_t)NB * 4, hipMemcpyDeviceToHost, c->st));
-    if (a->dbg_src) {
-      HIP_TRY(hipMemcpyAsync(a->dbg_src, dDS, (size_t)NB * 24, hipMemcpyDeviceToHost, c->st));
-      HIP_TRY(hipMemcpyAsync(a->dbg_dist, dDD, (size_t)NB * 16, hipMemcpyDeviceToHost, c->st));
+  if (stats)
+    for (int j = 0; j < J; j++) ia_launch_reduce_stats(jp[j].pstat, NB, c->counters.as<unsigned long long>(), c->st);
+  for (int j = 0; j < J; j++) {
+    const ia_level_args *x = &args[j];
+    if (x->mem != IA_MEM_HOST) continue;
+    HIP_TRY(hipMemcpyAsync(x->Bp, jp[j].Bp, nB * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipMemcpyAsync(x->s_out, jp[j].s, (size_t)NB * 8, hipMemcpyDeviceToHost, c->st));
+    HIP_TRY(hipMemcpyAsync(x->im_out, jp[j].im, (size_t)NB * 4, hipMemcpyDeviceToHost, c->st));
+    if (x->dbg_src) {
+      HIP_TRY(hipMemcpyAsync(x->dbg_src, jp[j].dbg_src, (size_t)NB * 24, hipMemcpyDeviceToHost, c->st));
+      HIP_TRY(hipMemcpyAsync(x->dbg_dist, jp[j].dbg_dist, (size_t)NB * 16, hipMemcpyDeviceToHost, c->st));
     }
   }
   HIP_TRY(hipStreamSynchronize(c->st));
@@ -667,7 +722,7 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
       dist_flops = pair_flops * (double)(prs[0] + prs[1]);
       flops_timed = pair_flops * (double)prs[1];
     }
-    stats->pruned_levels += prune ? 1 : 0;
+    stats->pruned_levels += prune ? J : 0;
     stats->dist_pairs += prune ? (double)(prs[0] + prs[1]) : pairs_full;
     stats->dist_pairs_full += pairs_full;
     stats->dist_tiles += prune ? (double)(prs[2] + prs[3]) : tiles_full;
@@ -675,14 +730,14 @@ int ia_synthesize_level(ia_ctx *c, const ia_level_args *a, ia_stats *stats) {
     float ms_db = 0.f, ms_syn = 0.f;
     hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
     hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);
-    stats->pixels += NB;
+    stats->pixels += NB * J;
     stats->steps += T;
     stats->reranked += (int64_t)ctr[0];
     stats->fallbacks += (int64_t)ctr[1];
     stats->coherence_wins += (int64_t)ctr[2];
     stats->bound_violations += (int64_t)ctr[3];
     stats->kappa_ambiguous += (int64_t)ctr[4];
-    stats->f16_levels += use_h ? 1 : 0;
+    stats->f16_levels += use_h ? J : 0;
     stats->db_ms += ms_db;
     stats->synth_ms += ms_syn;
     stats->dist_launches += dist_launches;
@@ -820,9 +875,6 @@ int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, d
   ma.qinfo = nullptr;
   ma.boxes = nullptr;
   ma.ufac = 0.;
-  ma.pstat = nullptr;
-  ma.dbg_src = nullptr;
-  ma.dbg_dist = nullptr;
   ma.eps_c = ia_eps_c(DP);
   ma.eps_a = 0.;
   const int qtmax = ia_k3_qtmax(x->KH);

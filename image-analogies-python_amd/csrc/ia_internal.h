@@ -83,11 +83,11 @@ struct MergeArgs {
   int pos0, pos_end;   // this rank's DB positions [tile0*32, tile1*32)
   int NT;              // tiles of the whole DB: position p holds row ia_pos_row(p, NT)
   int NA;              // DB rows
-  unsigned *pstat;                    // per-pixel stats word of the level (nullptr: none):
-                                      // bits 0-15 reranked, 16-28 fallbacks, 29 kappa decision
-                                      // ambiguous under libm pow, 30 coherence won,
-                                      // 31 an MFMA value outside the certified error bound
-  double eps_c;                       // relative error coefficient of the MFMA value
+                                      // (per-pixel stats words, JobPtrs::pstat: bits 0-15
+                                      // reranked, 16-28 fallbacks, 29 kappa decision ambiguous
+                                      // under libm pow, 30 coherence won, 31 an MFMA value
+                                      // outside the certified error bound)
+  double eps_c;                      // relative error coefficient of the MFMA value
   double eps_a;                       // absolute (f16 subnormal) error coefficient
   const int *pos2row;                 // position -> row table (pruned levels) or nullptr
   int rr;                             // 1: workgroup w's chunk is tiles {w, w + nwg, ...} (pruned
@@ -95,8 +95,6 @@ struct MergeArgs {
   const float4 *qinfo;                // pruned levels: the step's query projection intervals (K2p)
   const float4 *boxes;                // pruned levels: per-tile projection boxes (ia_prune.hip)
   double ufac;                        // pruned levels: bound factor of ia_prune.h
-  int32_t *dbg_src;                   // optional (nullptr: off) N x 6: p_app row/col/img, r_star row/col, has_coh
-  double *dbg_dist;                   // optional N x 2: d_app, d_coh (compute_distance; 0 without a coherence candidate)
 };
 
 // DB positions are tile-strided and tile-scattered: slot j of tile t holds row j*NT + perm(t)
@@ -128,10 +126,37 @@ __host__ __device__ inline int64_t ia_pos_row_t(int64_t pos, int64_t NT, const i
 #define IA_PRUNE_MIN_ROWS 524288  // default of option "prune_min_rows": at 512^2 (262,144 rows) the
                                   // unpruned scan + cheaper gather/merge is still faster
 
-// per-step wavefront description: pixels (r, t - 3r), r in [r0, r0 + M)
+// per-step wavefront description: pixels (r, t - 3r), r in [r0, r0 + M), of each of J jobs.
+// Query m of the step (0 <= m < J*M) is job m / M, row r0 + m % M; Mpad = J*M rounded up to
+// whole query tiles of 32.
 struct StepDesc {
-  int t, r0, M, Mpad;
+  int t, r0, M, Mpad, J;
 };
+
+// One synthesis job of a batched level (ia_synthesize_levels): its B side.  Every job of a
+// batch shares the level's A side (one DB) and the B level shape, so the wavefront steps align.
+#define IA_MAX_JOBS 32
+struct JobPtrs {
+  const double *Bc, *B, *Bpc;  // B level l-1, l and B' level l-1 (complete)
+  double *Bp;                  // B' level l: in init, out synthesised
+  int32_t *s, *im;             // source maps (written)
+  unsigned *pstat;             // per-pixel stats words of the level
+  int32_t *dbg_src;            // optional debug records (include/ia.h), nullptr: off
+  double *dbg_dist;
+  const double *weights;       // compute_distance weights
+  double kf;                   // kappa factor 1 + 2^(level - L) k
+};
+struct QPix {
+  int job, r, c, qi;           // job, pixel (r, c) and its raster index in the B level
+};
+__host__ __device__ inline QPix ia_qpix(const StepDesc &sd, int bw, int m) {
+  QPix p;
+  p.job = m / sd.M;
+  p.r = sd.r0 + (m - p.job * sd.M);
+  p.c = sd.t - 3 * p.r;
+  p.qi = p.r * bw + p.c;
+  return p;
+}
 
 // single-rank certified winner of one query
 struct Winner {

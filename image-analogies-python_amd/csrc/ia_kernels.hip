@@ -109,6 +109,15 @@ __device__ __forceinline__ double feat(const Imgs &I, int f, int r, int c, int i
   }
 }
 
+// the B side of job jp as the four images its query rows read (B-side FeatDesc parts)
+__device__ __forceinline__ Imgs job_imgs(Imgs B, const JobPtrs &jp) {
+  B.p0 = jp.Bc;
+  B.p1 = jp.B;
+  B.p2 = jp.Bpc;
+  B.p3 = jp.Bp;
+  return B;
+}
+
 template <int CH>
 __device__ __forceinline__ int feat_part(int f) {
   return f < 9 * CH ? 0 : f < 34 * CH ? 1 : f < 43 * CH ? 2 : 3;
@@ -427,18 +436,21 @@ __device__ __forceinline__ void put_qfrag(float *qf, int m, int f, float v) {
 }
 
 template <int CH>
-__global__ void __launch_bounds__(IA_WG) k_gather_query(LevelGeo g, StepDesc sd, Imgs B, const double *__restrict__ mu_part,
+__global__ void __launch_bounds__(IA_WG) k_gather_query(LevelGeo g, StepDesc sd, Imgs B, const JobPtrs *__restrict__ jobs,
+                                                         const double *__restrict__ mu_part,
                                                          double *__restrict__ q64, double *__restrict__ qn2,
                                                          float *__restrict__ qf) {
   using G = Geo<CH>;
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
   if (m >= sd.Mpad) return;
-  if (m >= sd.M) {
+  if (m >= sd.J * sd.M) {
     for (int f = lane; f < G::DP; f += IA_WAVE) put_qfrag<CH>(qf, m, f, 0.f);
     return;
   }
-  const int r = sd.r0 + m, c = sd.t - 3 * r;
+  const QPix px = ia_qpix(sd, g.bw, m);
+  B = job_imgs(B, jobs[px.job]);
+  const int r = px.r, c = px.c;
   double ss = 0.;
   for (int f = lane; f < G::DP; f += IA_WAVE) {
     if (f < G::D) {
@@ -705,7 +717,7 @@ __device__ __forceinline__ void put_qh(_Float16 *qf, int m, int f, double v) {
 }
 
 template <int CH, int KS>
-__global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc sd, Imgs B,
+__global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc sd, Imgs B, const JobPtrs *__restrict__ jobs,
                                                            const double *__restrict__ mu_part,
                                                            double *__restrict__ q64, double *__restrict__ qn2,
                                                            _Float16 *__restrict__ qf) {
@@ -713,11 +725,13 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc s
   const int lane = threadIdx.x & 63;
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
   if (m >= sd.Mpad) return;
-  if (m >= sd.M) {
+  if (m >= sd.J * sd.M) {
     for (int f = lane; f < KD; f += IA_WAVE) put_qh<KS>(qf, m, f, 0.);
     return;
   }
-  const int r = sd.r0 + m, c = sd.t - 3 * r;
+  const QPix px = ia_qpix(sd, g.bw, m);
+  B = job_imgs(B, jobs[px.job]);
+  const int r = px.r, c = px.c;
   double ss = 0.;
   for (int f = lane; f < KD; f += IA_WAVE) {
     if (f < D) {
@@ -1020,10 +1034,10 @@ __device__ __forceinline__ double wave_sum_d_x(double v) {  // fixed butterfly o
 //                           Morton key of the projection (sort order of the query tiles)
 // ------------------------------------------------------------------------------------------
 template <int KS>
-__global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc sd, Imgs B, const double *__restrict__ mu_part,
+__global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc sd, Imgs B, const JobPtrs *__restrict__ jobs,
+                                                          const double *__restrict__ mu_part,
                                                           double *__restrict__ q64, double *__restrict__ qn2,
                                                           _Float16 *__restrict__ qf, const double *__restrict__ db64,
-                                                          const int32_t *__restrict__ s, const int32_t *__restrict__ im,
                                                           const double *__restrict__ basis, double ufac,
                                                           float4 *__restrict__ qinfo) {
   constexpr int D = 55, KD = 16 * KS;
@@ -1032,7 +1046,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + wv;
   if (m >= sd.Mpad) return;
-  if (m >= sd.M) {
+  if (m >= sd.J * sd.M) {
     if (lane < KD) put_qh<KS>(qf, m, lane, 0.);
     if (lane == 0) {
       qinfo[3 * m] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1041,7 +1055,11 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
     }
     return;
   }
-  const int r = sd.r0 + m, c = sd.t - 3 * r, qi = r * g.bw + c;
+  const QPix px = ia_qpix(sd, g.bw, m);
+  const JobPtrs &jp = jobs[px.job];
+  B = job_imgs(B, jp);
+  const int32_t *__restrict__ s = jp.s, *__restrict__ im = jp.im;
+  const int r = px.r, c = px.c, qi = px.qi;
   // coherence candidate of this lane (lanes 0..14, product(rows, cols) order as merge_fused)
   int crow = -1;
   if (qi > 0 && lane < 15) {
@@ -1099,8 +1117,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
 // Wave reductions use DPP / permlane exchanges (no LDS round trips).
 template <int CH>
 __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &a,
-                                            int m, int32_t *__restrict__ s, int32_t *__restrict__ im,
-                                            double *__restrict__ Bp, const double *__restrict__ weights, double kf,
+                                            int m, const JobPtrs &jp, const QPix &px,
                                             double *qs, double *ws, int *cand_row, float *cand_v) {
 #if IA_PROBE & 8
   unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -1109,7 +1126,11 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   constexpr int RPL = IA_WG_TARGET / IA_WAVE;
   constexpr int NCOH = 15, NRR = IA_WAVE - NCOH;  // lanes for coherence / rerank candidates
   const int lane = threadIdx.x & 63;
-  const int r = sd.r0 + m, c = sd.t - 3 * r, qi = r * g.bw + c;
+  const int r = px.r, c = px.c, qi = px.qi;
+  int32_t *__restrict__ s = jp.s, *__restrict__ im = jp.im;
+  double *__restrict__ Bp = jp.Bp;
+  const double *__restrict__ weights = jp.weights;
+  const double kf = jp.kf;
   const double *q = a.q64 + (int64_t)m * Geo<CH>::D;
   const float4 *rr = a.rec + (int64_t)m * a.nwg;
   const float *rT = a.recT + (int64_t)m * a.nwg;
@@ -1357,20 +1378,20 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     // per-pixel stats word (no shared-counter atomics: hundreds of waves adding to one
     // address serialise at L2 and dominated this kernel); reduced once per level
     const int slot = placed + 0;
-    a.pstat[qi] = (unsigned)min(slot, 0xffff) | ((unsigned)min((int)nfb, 0x1fff) << 16) | (kamb ? 1u << 29 : 0u) |
+    jp.pstat[qi] = (unsigned)min(slot, 0xffff) | ((unsigned)min((int)nfb, 0x1fff) << 16) | (kamb ? 1u << 29 : 0u) |
                   (coh_won ? 1u << 30 : 0u) |
                   (any_viol ? 1u << 31 : 0u);
-    if (a.dbg_src) {  // debug=True structures (image_analogies.py:224-240): p_app, r_star, d_app, d_coh
+    if (jp.dbg_src) {  // debug=True structures (image_analogies.py:224-240): p_app, r_star, d_app, d_coh
       const bool has_coh = kk != INT_MAX;
-      int32_t *o = a.dbg_src + (int64_t)qi * 6;
+      int32_t *o = jp.dbg_src + (int64_t)qi * 6;
       o[0] = app_pr;
       o[1] = app_pc;
       o[2] = app_img;
       o[3] = has_coh ? r - 2 + kk / 5 : 0;
       o[4] = has_coh ? c - 2 + kk % 5 : 0;
       o[5] = has_coh ? 1 : 0;
-      a.dbg_dist[2 * qi] = dbg_app;
-      a.dbg_dist[2 * qi + 1] = dbg_coh;
+      jp.dbg_dist[2 * qi] = dbg_app;
+      jp.dbg_dist[2 * qi + 1] = dbg_coh;
     }
   }
 #if IA_PROBE & 8
@@ -1386,18 +1407,18 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
 
 template <int CH, bool FUSED>
 __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, Winner *__restrict__ win,
-                                                        int32_t *__restrict__ s, int32_t *__restrict__ im,
-                                                        double *__restrict__ Bp, const double *__restrict__ weights,
-                                                        double kf) {
+                                                        const JobPtrs *__restrict__ jobs) {
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
-  if (m >= sd.M) return;
+  if (m >= sd.J * sd.M) return;
+  const QPix px = ia_qpix(sd, g.bw, m);
+  const JobPtrs &jp = jobs[px.job];
 #if (IA_PROBE & 3) == 0
   if constexpr (FUSED) {
     __shared__ double qsh[IA_WG / IA_WAVE][Geo<CH>::DS], wsh[IA_WG / IA_WAVE][Geo<CH>::DS];
     __shared__ int crsh[IA_WG / IA_WAVE][IA_WAVE];
     __shared__ float cvsh[IA_WG / IA_WAVE][IA_WAVE];
     const int wv = threadIdx.x >> 6;
-    merge_fused<CH>(g, sd, A, ma, m, s, im, Bp, weights, kf, qsh[wv], wsh[wv], crsh[wv], cvsh[wv]);
+    merge_fused<CH>(g, sd, A, ma, m, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv]);
     return;
   }
 #endif
@@ -1410,21 +1431,18 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
 #endif
 #if IA_PROBE & 2  // diagnostic build only: no coherence / kappa
   if ((threadIdx.x & 63) == 0) {
-    const int r = sd.r0 + m, qi = r * g.bw + sd.t - 3 * r;
-    s[2 * qi] = (int)(wn.idx / g.aw) % g.ah;
-    s[2 * qi + 1] = (int)(wn.idx % g.aw);
-    im[qi] = 0;
+    jp.s[2 * px.qi] = (int)(wn.idx / g.aw) % g.ah;
+    jp.s[2 * px.qi + 1] = (int)(wn.idx % g.aw);
+    jp.im[px.qi] = 0;
   }
   return;
 #endif
   if constexpr (FUSED) {
-    const int r = sd.r0 + m;
-    finish_pixel<CH>(g, A, ma.db64, r, sd.t - 3 * r, wn.idx, q, s, im, Bp, weights, kf, ma.pstat, stat);
+    finish_pixel<CH>(g, A, ma.db64, px.r, px.c, wn.idx, q, jp.s, jp.im, jp.Bp, jp.weights, jp.kf, jp.pstat, stat);
   } else {
     if ((threadIdx.x & 63) == 0) {
       win[m] = wn;
-      const int r = sd.r0 + m;
-      if (ma.pstat) ma.pstat[r * g.bw + sd.t - 3 * r] = stat;  // finish adds the coherence bit
+      if (jp.pstat) jp.pstat[px.qi] = stat;  // finish adds the coherence bit
     }
   }
 }
@@ -1434,21 +1452,20 @@ template <int CH>
 __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd, Imgs A, const double *__restrict__ db64,
                                                          const double *__restrict__ q64,
                                                          const Winner *__restrict__ allwin, int world, int Mstride,
-                                                         int32_t *__restrict__ s, int32_t *__restrict__ im,
-                                                         double *__restrict__ Bp, const double *__restrict__ weights,
-                                                         double kf, unsigned *pstat) {
+                                                         const JobPtrs *__restrict__ jobs) {
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
-  if (m >= sd.M) return;
+  if (m >= sd.J * sd.M) return;
   double bd = DBL_MAX;
   int64_t bi = INT64_MAX;
   for (int k = 0; k < world; k++) {  // same order on every rank -> identical replicas
     const Winner w = allwin[(int64_t)k * Mstride + m];
     if (w.d < bd || (w.d == bd && w.idx < bi)) { bd = w.d; bi = w.idx; }
   }
-  const int r = sd.r0 + m;
-  const int qi = r * g.bw + sd.t - 3 * r;
-  const unsigned prev = pstat ? pstat[qi] : 0u;
-  finish_pixel<CH>(g, A, db64, r, sd.t - 3 * r, bi, q64 + (int64_t)m * Geo<CH>::D, s, im, Bp, weights, kf, pstat, prev);
+  const QPix px = ia_qpix(sd, g.bw, m);
+  const JobPtrs &jp = jobs[px.job];
+  const unsigned prev = jp.pstat ? jp.pstat[px.qi] : 0u;
+  finish_pixel<CH>(g, A, db64, px.r, px.c, bi, q64 + (int64_t)m * Geo<CH>::D, jp.s, jp.im, jp.Bp, jp.weights, jp.kf,
+                   jp.pstat, prev);
 }
 
 // per-level statistics: sum the per-pixel stats words.  Grid-stride loop over up to 256
@@ -1660,16 +1677,16 @@ void ia_launch_db_build(const LevelGeo &g, const Imgs &A, const double *mu, floa
 }
 
 template <int CH>
-static void launch_gather_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64,
-                            double *qn2, float *qf, hipStream_t st) {
-  hipLaunchKernelGGL(k_gather_query<CH>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, mu, q64,
+static void launch_gather_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu,
+                            double *q64, double *qn2, float *qf, hipStream_t st) {
+  hipLaunchKernelGGL(k_gather_query<CH>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs, mu, q64,
                      qn2, qf);
 }
-void ia_launch_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64, double *qn2,
-                      float *qf, hipStream_t st) {
-  if (g.ch == 1) launch_gather_t<1>(g, sd, B, mu, q64, qn2, qf, st);
-  else if (g.ch == 2) launch_gather_t<2>(g, sd, B, mu, q64, qn2, qf, st);
-  else launch_gather_t<3>(g, sd, B, mu, q64, qn2, qf, st);
+void ia_launch_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu, double *q64,
+                      double *qn2, float *qf, hipStream_t st) {
+  if (g.ch == 1) launch_gather_t<1>(g, sd, B, jobs, mu, q64, qn2, qf, st);
+  else if (g.ch == 2) launch_gather_t<2>(g, sd, B, jobs, mu, q64, qn2, qf, st);
+  else launch_gather_t<3>(g, sd, B, jobs, mu, q64, qn2, qf, st);
 }
 
 // K3 dispatch table: QT query tiles per launch (1..QTMAX(KH))
@@ -1701,33 +1718,31 @@ void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tile
 
 template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
-                           int32_t *s, int32_t *im, double *Bp, const double *w, double kf, bool fused, hipStream_t st) {
-  dim3 grid(cdiv(sd.M, IA_WG / IA_WAVE));
+                           const JobPtrs *jobs, bool fused, hipStream_t st) {
+  dim3 grid(cdiv(sd.J * sd.M, IA_WG / IA_WAVE));
   if (fused)
-    hipLaunchKernelGGL((k_merge_level<CH, true>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, s, im, Bp, w, kf);
+    hipLaunchKernelGGL((k_merge_level<CH, true>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
   else
-    hipLaunchKernelGGL((k_merge_level<CH, false>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, s, im, Bp, w, kf);
+    hipLaunchKernelGGL((k_merge_level<CH, false>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
 }
-void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win, int32_t *s,
-                     int32_t *im, double *Bp, const double *w, double kf, bool fused, hipStream_t st) {
-  if (g.ch == 1) launch_merge_t<1>(g, sd, A, ma, win, s, im, Bp, w, kf, fused, st);
-  else if (g.ch == 2) launch_merge_t<2>(g, sd, A, ma, win, s, im, Bp, w, kf, fused, st);
-  else launch_merge_t<3>(g, sd, A, ma, win, s, im, Bp, w, kf, fused, st);
+void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
+                     const JobPtrs *jobs, bool fused, hipStream_t st) {
+  if (g.ch == 1) launch_merge_t<1>(g, sd, A, ma, win, jobs, fused, st);
+  else if (g.ch == 2) launch_merge_t<2>(g, sd, A, ma, win, jobs, fused, st);
+  else launch_merge_t<3>(g, sd, A, ma, win, jobs, fused, st);
 }
 
 template <int CH>
 static void launch_finish_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
-                            const Winner *allwin, int world, int Mstride, int32_t *s, int32_t *im, double *Bp,
-                            const double *w, double kf, unsigned *ctr, hipStream_t st) {
-  hipLaunchKernelGGL(k_finish_level<CH>, dim3(cdiv(sd.M, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, A, db64, q64, allwin,
-                     world, Mstride, s, im, Bp, w, kf, ctr);
+                            const Winner *allwin, int world, int Mstride, const JobPtrs *jobs, hipStream_t st) {
+  hipLaunchKernelGGL(k_finish_level<CH>, dim3(cdiv(sd.J * sd.M, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, A, db64, q64,
+                     allwin, world, Mstride, jobs);
 }
 void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
-                      const Winner *allwin, int world, int Mstride, int32_t *s, int32_t *im, double *Bp, const double *w,
-                      double kf, unsigned *ctr, hipStream_t st) {
-  if (g.ch == 1) launch_finish_t<1>(g, sd, A, db64, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
-  else if (g.ch == 2) launch_finish_t<2>(g, sd, A, db64, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
-  else launch_finish_t<3>(g, sd, A, db64, q64, allwin, world, Mstride, s, im, Bp, w, kf, ctr, st);
+                      const Winner *allwin, int world, int Mstride, const JobPtrs *jobs, hipStream_t st) {
+  if (g.ch == 1) launch_finish_t<1>(g, sd, A, db64, q64, allwin, world, Mstride, jobs, st);
+  else if (g.ch == 2) launch_finish_t<2>(g, sd, A, db64, q64, allwin, world, Mstride, jobs, st);
+  else launch_finish_t<3>(g, sd, A, db64, q64, allwin, world, Mstride, jobs, st);
 }
 
 template <int CH>
@@ -1826,22 +1841,22 @@ void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *mu, vo
 }
 
 template <int CH, int KS>
-static void launch_gather_h_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64,
-                              double *qn2, void *qf, hipStream_t st) {
-  hipLaunchKernelGGL((k_gather_query_h<CH, KS>), dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, mu,
-                     q64, qn2, (_Float16 *)qf);
+static void launch_gather_h_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu,
+                              double *q64, double *qn2, void *qf, hipStream_t st) {
+  hipLaunchKernelGGL((k_gather_query_h<CH, KS>), dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs,
+                     mu, q64, qn2, (_Float16 *)qf);
 }
-void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64, double *qn2,
-                        void *qf, hipStream_t st) {
-  if (g.ch == 1) launch_gather_h_t<1, 4>(g, sd, B, mu, q64, qn2, qf, st);
-  else launch_gather_h_t<2, 7>(g, sd, B, mu, q64, qn2, qf, st);
+void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu,
+                        double *q64, double *qn2, void *qf, hipStream_t st) {
+  if (g.ch == 1) launch_gather_h_t<1, 4>(g, sd, B, jobs, mu, q64, qn2, qf, st);
+  else launch_gather_h_t<2, 7>(g, sd, B, jobs, mu, q64, qn2, qf, st);
 }
 
-void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const double *mu, double *q64, double *qn2,
-                        void *qf, const double *db64, const int32_t *s, const int32_t *im, const double *basis, double ufac,
+void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu,
+                        double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
                         float4 *qinfo, hipStream_t st) {
-  hipLaunchKernelGGL(k_gather_query_p<4>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, mu, q64, qn2,
-                     (_Float16 *)qf, db64, s, im, basis, ufac, qinfo);
+  hipLaunchKernelGGL(k_gather_query_p<4>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs, mu, q64,
+                     qn2, (_Float16 *)qf, db64, basis, ufac, qinfo);
 }
 
 // split-f16 distance kernels live in ia_k3h.hip, compiled once per (KS, QT) instance

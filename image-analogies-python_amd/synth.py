@@ -56,9 +56,12 @@ class Job(object):
                          for l in range(1, self.L)))
 
 
-def make_job(size=1024, b_size=None, n_levels=None, k=0.5, seed_a=1, seed_b=2, seed_bp=3):
+def make_job(size=1024, b_size=None, n_levels=None, k=0.5, seed_a=1, seed_b=2, seed_bp=3, level_align='coarse'):
     """A/A'/B synthetic job.  size: A (and default B) side; n_levels caps the pyramid depth
-    (cfg2 uses 5); the pyramid rule otherwise is the reference's (min_size = n_sm = 3)."""
+    (cfg2 uses 5); the pyramid rule otherwise is the reference's (min_size = n_sm = 3).
+    level_align: 'coarse' = the reference's alignment of unequal pyramids (coarsest levels
+    paired, B's extra fine levels dropped, image_analogies.py:82-86); 'fine' = B's finest level
+    paired with A's finest (B level k + d <-> A level k; config.level_align, cfg4)."""
     ah, aw = (size, size) if np.isscalar(size) else size
     b_size = (ah, aw) if b_size is None else b_size
     bh, bw = (b_size, b_size) if np.isscalar(b_size) else b_size
@@ -68,6 +71,8 @@ def make_job(size=1024, b_size=None, n_levels=None, k=0.5, seed_a=1, seed_b=2, s
     A_pyr = compute_gaussian_pyramid(A, _config.n_sm, n_levels)
     Ap_pyr = compute_gaussian_pyramid(Ap, _config.n_sm, n_levels)
     B_pyr = compute_gaussian_pyramid(B, _config.n_sm, n_levels)
+    if level_align == 'fine' and len(B_pyr) > len(A_pyr):
+        B_pyr = B_pyr[len(B_pyr) - len(A_pyr):]
     L = min(len(A_pyr), len(B_pyr))
     A_pyr, Ap_pyr, B_pyr = A_pyr[:L], Ap_pyr[:L], B_pyr[:L]
     Bp = initialize_Bp(B_pyr, init_rand=True, seed=seed_bp)
@@ -80,5 +85,10 @@ CONFIGS = {
     'cfg1': (dict(size=(117, 180)), "shore-crop stand-in 117x180 (CPU reference path config)"),
     'cfg2': (dict(size=512, n_levels=5), "512x512 synthetic A/A'/B, 5-level pyramid, 1 GPU"),
     'cfg3': (dict(size=1024), "1024x1024 synthetic A/A'/B, full 10-level pyramid"),
+    'cfg4': (dict(size=1024, b_size=2048, k=25.0, level_align='fine'),
+             "2048x2048 B against 1024x1024 A/A' (Freud-crop-style filter), kappa 25, B's finest level paired "
+             "with A's (level_align='fine')"),
+    'cfg5': (dict(size=512), "multi_script-style sweep: 64 jobs, kappa {0.5,1,2,5,10,15,20,25} x pyramid "
+                             "depth 2..9 on 512x512 A/A'/B, job j on GPU j mod N, jobs sharing a GPU batched"),
     'small': (dict(size=128), "128x128 smoke size"),
 }

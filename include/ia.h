@@ -136,6 +136,15 @@ int ia_comm_init(ia_ctx *ctx, int rank, int world, const unsigned char id[128]);
 
 /* ---- fast path: one level ----------------------------------------------------------------- */
 int ia_synthesize_level(ia_ctx *ctx, const ia_level_args *args, ia_stats *stats);
+/* The same level for n_jobs independent jobs at once (multi_script.py's parameter sweeps,
+ * multi_script.py:13-32: kappa / pyramid depth change, the A side does not).  args[0..n_jobs)
+ * must share the A side (identical A, Ac, Ap, Apc pointers: one feature DB is built) and every
+ * shape, channel count and mem kind; B, Bc, Bpc, Bp, weights, kappa_factor, outputs and debug
+ * buffers are per job.  Every wavefront step gathers the queries of all jobs and runs ONE
+ * distance scan over the DB for them (the DB is streamed once per step, not once per job), then
+ * each job's coherence / kappa / writeback.  Results are those of n_jobs separate
+ * ia_synthesize_level calls, bit for bit.  1 <= n_jobs <= 32; single-rank levels only. */
+int ia_synthesize_levels(ia_ctx *ctx, const ia_level_args *args, int n_jobs, ia_stats *stats);
 
 /* ---- FLANN-compatible exact index (algorithms.py:56,69,74) -------------------------------- */
 /* build_index(pts): pts is n x d fp64 (row-major), d <= 167. */

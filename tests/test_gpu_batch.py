@@ -1,0 +1,121 @@
+"""Batched levels (ia_synthesize_levels) and parameter sweeps (ia_amd.sweep, BASELINE config 5,
+multi_script.py:13-32): several jobs sharing the A side step through one wavefront together -
+one gather, one distance scan and one merge per step for all of them - and every job's B', s
+and im must be bit-identical to running it alone (and, for the golden job, to the reference)."""
+import numpy as np
+import pytest
+
+from golden_util import load_e2e
+
+pytestmark = pytest.mark.gpu
+
+
+def _jobs_g32(z, kappas=(0.5, 5.0, 25.0, 1.0)):
+    """the golden g32 job (k = 0.5, the reference's B' init) + variants: other kappas and B' inits"""
+    from ia_amd.img_preprocess import initialize_Bp
+    out = []
+    for n, k in enumerate(kappas):
+        Bp = [x.copy() for x in z['Bp_init']] if n == 0 else initialize_Bp(z['B_pyr'], True, seed=100 + n)
+        out.append((k, Bp))
+    return out
+
+
+def _run(ctx, z, jobs, batched):
+    from ia_amd import _native
+    L = z['L']
+    S, IM = [dict() for _ in jobs], [dict() for _ in jobs]
+    st = _native.Stats()
+    for level in range(1, L):
+        specs = [dict(B=z['B_pyr'][level], Bc=z['B_pyr'][level - 1], Bpc=Bp[level - 1], Bp=Bp[level],
+                      weights=z['weights'], kappa_factor=1 + 2.0 ** (level - L) * k) for k, Bp in jobs]
+        if batched:
+            res = ctx.synthesize_levels(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
+                                        [p[level - 1] for p in z['Ap_pyr']], specs, st)
+        else:
+            res = [ctx.synthesize_levels(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
+                                         [p[level - 1] for p in z['Ap_pyr']], [sp], st)[0] for sp in specs]
+        for j, (s, im) in enumerate(res):
+            S[j][level], IM[j][level] = s, im
+    return S, IM, st
+
+
+@pytest.mark.parametrize('mode', ['default', 'pruned', 'f32'])
+@pytest.mark.parametrize('name', ['g32', 'multiap', 'ties'])
+def test_batched_levels_match_separate_and_reference(ctx, name, mode):
+    from ia_amd import _native
+    z = load_e2e(name)
+    if mode == 'pruned':
+        ctx.set_option('prune_min_rows', 1)
+    if mode == 'f32':
+        ctx.set_option('matcher', _native.IA_MATCH_F32)
+    try:
+        jb = _jobs_g32(z)
+        js = [(k, [x.copy() for x in Bp]) for k, Bp in jb]
+        Sb, IMb, stb = _run(ctx, z, jb, True)
+        Ss, IMs, sts = _run(ctx, z, js, False)
+    finally:
+        ctx.set_option('prune_min_rows', 524288)
+        ctx.set_option('matcher', _native.IA_MATCH_F16X3)
+    for j in range(len(jb)):
+        for level in range(1, z['L']):
+            assert np.array_equal(Sb[j][level], Ss[j][level]) and np.array_equal(IMb[j][level], IMs[j][level])
+            assert np.array_equal(jb[j][1][level], js[j][1][level])
+    for level in range(1, z['L']):   # job 0 is the reference's own run
+        assert np.array_equal(Sb[0][level], z['s'][level]) and np.array_equal(IMb[0][level], z['im'][level])
+        assert np.array_equal(jb[0][1][level], z['Bp_final'][level])
+    assert stb.pixels == sts.pixels and stb.coherence_wins == sts.coherence_wins
+    assert stb.bound_violations == 0 and stb.kappa_ambiguous == 0
+    if mode == 'pruned':
+        assert stb.pruned_levels == len(jb) * (z['L'] - 1)
+
+
+def test_batched_512_pruned_wide_step(ctx):
+    """3 jobs on a 512^2 level with the pruned scan forced: 513 queries per step in one scan (the
+    separate runs sort 171 per step) - a different kernel path, the same decisions."""
+    from ia_amd import synth
+    job = synth.make_job(512, n_levels=3)
+    ctx.set_option('prune_min_rows', 1)
+    try:
+        z = {'L': job.L, 'A_pyr': job.A_pyr, 'Ap_pyr': job.Ap_pyr_list, 'B_pyr': job.B_pyr, 'weights': job.weights,
+             'Bp_init': job.Bp_init}
+        jb = _jobs_g32(z, kappas=(0.5, 5.0, 25.0))
+        js = [(k, [x.copy() for x in Bp]) for k, Bp in jb]
+        Sb, IMb, stb = _run(ctx, z, jb, True)
+        Ss, IMs, sts = _run(ctx, z, js, False)
+    finally:
+        ctx.set_option('prune_min_rows', 524288)
+    for j in range(len(jb)):
+        for level in range(1, job.L):
+            assert np.array_equal(Sb[j][level], Ss[j][level]) and np.array_equal(IMb[j][level], IMs[j][level])
+            assert np.array_equal(jb[j][1][level], js[j][1][level])
+    assert stb.pruned_levels == 3 * (job.L - 1) and stb.bound_violations == 0
+
+
+def test_sweep_batched_equals_sequential_and_oracle(ctx):
+    """A 6-job mini sweep (kappa x pyramid depth, multi_script-style) on 96x96 images: batched ==
+    one job at a time, and one job against the oracle's restatement of the reference loop."""
+    from ia_amd import sweep, synth
+    from oracle import ia_oracle as O
+    A = synth.smooth(96, 96, 2, 1)
+    Ap = synth.filt(A)
+    B = synth.smooth(96, 96, 2, 2)
+    jobs = [sweep.SweepJob(k, n, seed=3 + i) for i, (k, n) in enumerate([(0.5, 3), (5, 3), (25, 3), (0.5, 5),
+                                                                          (5, 5), (2, None)])]
+    sw = sweep.Sweep(A, [Ap], B, jobs)
+    rb = sw.run(ctx, batched=True)
+    rs = sw.run(ctx, batched=False)
+    for j in range(len(jobs)):
+        Bpb, Sb, IMb = rb[j]
+        Bps, Ss, IMs = rs[j]
+        assert sorted(Sb) == list(range(1, sw.L[j]))
+        for level in Sb:
+            assert np.array_equal(Sb[level], Ss[level]) and np.array_equal(IMb[level], IMs[level])
+            assert np.array_equal(Bpb[level], Bps[level])
+    j = 4   # k = 5, 5 levels
+    off = sw.offset(j)
+    Bp = [x.copy() for x in sw.Bp_init[j]]
+    S, IM = O.run_all_levels(sw.A_pyr[off:], [p[off:] for p in sw.Ap_pyr_list], sw.B_pyr[off:], Bp, jobs[j].k,
+                             sw.weights)
+    for level in range(1, sw.L[j]):
+        assert np.array_equal(rb[j][1][level], S[level]) and np.array_equal(rb[j][2][level], IM[level])
+        assert np.array_equal(rb[j][0][level], Bp[level])
