@@ -144,12 +144,15 @@ def main():
                     help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select (DIAG=1 builds)')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
-    ap.add_argument('--k3p-variant', type=int, default=7, choices=list(range(11)),
+    ap.add_argument('--k3p-variant', type=int, default=7, choices=list(range(12)),
                     help='pruned-scan kernel version (ia_k3h.hip k3h_prune*; other than 7: DIAG=1 builds): 0 = first version, 1 = boxes in '
                          'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
                          'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks')
     ap.add_argument('--prune-min-rows', type=int, default=524288,
                     help='smallest DB (rows) the pruned scan is used on (default: the 1024^2 level)')
+    ap.add_argument('--shard-emulate', type=int, default=1,
+                    help='run every large level as a W-way DB shard on this one GPU (the multi-rank kernels '
+                         'without the all-gather: per-shard scans and winners, then the finish); for the cost model')
     ap.add_argument('--time-stride', type=int, default=4, help='sample K3 timing every S-th wavefront step')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
@@ -202,6 +205,8 @@ def main():
     if args.k3p_variant != 7:
         ctx.set_option('k3p_variant', args.k3p_variant)     # DIAG=1 builds only
     ctx.set_option('prune_min_rows', args.prune_min_rows)
+    if args.shard_emulate > 1:
+        ctx.set_option('shard_emulate', args.shard_emulate)
     if args.mode == 'shard' and world > 1:
         uid = [_native.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
@@ -305,6 +310,7 @@ def main():
                                            'pyramid_levels': job.L,
                                            'px_per_step': job_pixels, 'nn_flops_per_step': job_flops,
                                            'mode': 'sweep' if sw is not None else args.mode,
+                                           'shard_emulate': args.shard_emulate,
                                            'parallelism': (('jobs%d' % world) if sw is not None else
                                                            ('replicas%d' if args.mode == 'replicas' else 'dbshard%d')
                                                            % world),

@@ -91,9 +91,11 @@ struct ia_ctx {
   DevBuf db, db64, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, absmax;
   // certified pruned scan (option "prune"): per-level basis, sorted DB table, tile boxes
   DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs, ord;
+  DevBuf qs_order, qs_info, qs_frag, qs_tbox;  // presorted queries of a step (k3p_variant 11, K2s)
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
   int64_t prune_min_rows = IA_PRUNE_MIN_ROWS;  // option "prune_min_rows": smallest DB that prunes
   int prune = 1;
+  int shard_emulate = 1;         // option "shard_emulate": W > 1 runs a W-way DB shard on this device
   int matcher = IA_MATCH_F16X3;  // option "matcher"
   int k3p_variant = 7;           // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
@@ -162,7 +164,7 @@ void jacobi_eig(int n, std::vector<double> &A, std::vector<double> &V, std::vect
 // the centred fp64 DB (sampled) -> top IA_NPC eigenvectors (host Jacobi) -> projections and
 // Morton keys of every row -> radix sort -> position -> row table + per-tile projection boxes.
 // Sets g.pos2row; *ufac = the U' factor of ia_prune.h.  One host sync (the covariance).
-int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, double *ufac) {
+int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac) {
   constexpr int D = 55, NPAIR = D * (D + 1) / 2, NWG_COV = 256;
   const int64_t NA = g.NA, NT = g.n_tiles;
   const int64_t stride = std::max<int64_t>(1, NA / 65536), nsamp = (NA + stride - 1) / stride;
@@ -209,7 +211,7 @@ int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, double *ufac) {
   ia_launch_proj_keys(c->db64.as<double>(), NA, mu, c->pr_basis.as<double>(), c->pr_proj.as<double>(), keys, rows, c->st);
   if (ia_sort_pairs(c->pr_tmp.p, sort_bytes, keys, keys + NA, rows, rows + NA, NA, c->st) != 0)
     return fail(IA_EHIP, "prepare_prune: radix sort failed");
-  ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, c->pos2row.as<int>(), c->boxes.as<float>(), c->st);
+  ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, W, c->pos2row.as<int>(), c->boxes.as<float>(), c->st);
   HIP_TRY(hipGetLastError());
   g.pos2row = c->pos2row.as<int>();
   return IA_OK;
@@ -253,7 +255,7 @@ void ia_destroy(ia_ctx *c) {
   for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->jobs, &c->db, &c->db64,
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
-                    &c->boxes, &c->qinfo, &c->pairs, &c->ord})
+                    &c->boxes, &c->qinfo, &c->pairs, &c->ord, &c->qs_order, &c->qs_info, &c->qs_frag, &c->qs_tbox})
     b->release();
   for (hipEvent_t e : c->evs) hipEventDestroy(e);
   hipEventDestroy(c->lv0);
@@ -272,7 +274,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   }
 #ifdef IA_K3H_DIAG  // DIAG=1 builds: every kernel version of DESIGN.md §4b's progression
   if (!std::strcmp(name, "k3p_variant")) {
-    if (value < 0 || value > 10) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..10");
+    if (value < 0 || value > 11) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..11");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -282,15 +284,25 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
 #else  // product build: the default kernels only (7: pruned scan, 1: packed-index K3h)
-  if (!std::strcmp(name, "k3p_variant") || !std::strcmp(name, "k3_variant")) {
-    if (value != (name[2] == 'p' ? 7 : 1))
-      return fail(IA_EINVAL, std::string("ia_set_option: ") + name + " variants other than the default are in DIAG=1 builds only");
+  if (!std::strcmp(name, "k3p_variant")) {  // 7: in-kernel sort up to 512 queries, presorted above; 11: always presorted
+    if (value != 7 && value != 11)
+      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7 or 11 (other versions are in DIAG=1 builds only)");
+    c->k3p_variant = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "k3_variant")) {
+    if (value != 1) return fail(IA_EINVAL, "ia_set_option: k3_variant other than 1 is in DIAG=1 builds only");
     return IA_OK;
   }
 #endif
   if (!std::strcmp(name, "prune_min_rows")) {
     if (value < 1) return fail(IA_EINVAL, "ia_set_option: prune_min_rows must be >= 1");
     c->prune_min_rows = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "shard_emulate")) {
+    if (value < 1 || value > 64) return fail(IA_EINVAL, "ia_set_option: shard_emulate must be 1..64");
+    c->shard_emulate = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "prune")) {
@@ -447,22 +459,23 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   g.bwc = (a->b_w + 1) / 2;
   g.NA = (int64_t)g.n_ap * g.ah * g.aw;
   g.n_tiles = (int)((g.NA + IA_TILE - 1) / IA_TILE);
-  // shard the DB over ranks unless the level is too small to be worth an exchange per step
+  // DB shards: over the ranks of ia_comm_init (world > 1), or emulated on this device (option
+  // "shard_emulate" = W: the W shards' scans and per-shard certified winners run here one after
+  // the other, then the multi-rank finish; no RCCL).  Levels under 64 tiles per shard replicate.
   const bool sharded = shard_level(g.n_tiles, c->world);
-  const int world = sharded ? c->world : 1;
-  if (sharded && J > 1) return fail(IA_EINVAL, "ia_synthesize_levels: sharded levels take one job per call");
+  const bool emulated = !sharded && c->world == 1 && c->shard_emulate > 1 && shard_level(g.n_tiles, c->shard_emulate);
+  const int Wsh = sharded ? c->world : emulated ? c->shard_emulate : 1;  // shards of this level
+  const bool multi = Wsh > 1;
+  if (multi && J > 1) return fail(IA_EINVAL, "ia_synthesize_levels: sharded levels take one job per call");
   for (int j = 0; j < J; j++)
-    if (sharded && args[j].dbg_src)
+    if (multi && args[j].dbg_src)
       return fail(IA_EINVAL, "ia_synthesize_level: debug outputs are produced by single-rank levels only");
   {
-    int64_t t0, t1;
+    int64_t t0, t1;  // this rank's contiguous DB tiles (unpruned sharded levels hold only those)
     ia_shard_tiles(g.NA, c->world, c->rank, &t0, &t1);
     g.tile0 = (int)t0;
     g.tile1 = (int)t1;
   }
-  const int ns = g.tile1 - g.tile0;
-  g.tiles_per_wg = std::max(4, (ns + IA_WG_TARGET - 1) / IA_WG_TARGET);
-  g.nwg = (ns + g.tiles_per_wg - 1) / g.tiles_per_wg;
 
   const size_t nA = (size_t)g.ah * g.aw * g.ch, nAc = (size_t)g.ahc * g.awc * g.ch;
   const size_t nB = (size_t)g.bh * g.bw * g.ch, nBc = (size_t)g.bhc * g.bwc * g.ch;
@@ -514,7 +527,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   }
   if ((rc = c->jobs.ensure(sizeof(JobPtrs) * J))) return rc;
   HIP_TRY(hipMemcpyAsync(c->jobs.p, jp.data(), sizeof(JobPtrs) * J, hipMemcpyHostToDevice, c->st));
-  const JobPtrs *djobs = c->jobs.as<JobPtrs>();
+  const JobSet djobs{jp[0], c->jobs.as<JobPtrs>()};
 
   // matcher: split-f16 when the channel count has a K3h instance and every image value fits
   // (IA_F16_MAXABS, one 4-byte read-back per level); otherwise the fp32 MFMA scan
@@ -538,30 +551,71 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     use_h = mx <= IA_F16_MAXABS;
   }
   g.KS = use_h ? ia_ks_for(g.ch) : 0;
-  if (use_h) {
-    g.tiles_per_wg = std::max(IA_WGH / IA_WAVE, (ns + IA_NWG_H - 1) / IA_NWG_H);
-    g.nwg = (ns + g.tiles_per_wg - 1) / g.tiles_per_wg;
-  }
-  // certified pruned scan (1 channel, single rank, large DBs; every query of a step sorted in
-  // one workgroup's LDS)
+  // certified pruned scan (1 channel, large DBs; every query of a step sorted in one
+  // workgroup's LDS)
   int64_t T, Mmax;
   ia_wavefront_shape(g.bh, g.bw, &T, &Mmax);
   const int64_t Mtmax = Mmax * J;  // queries of the widest step over all jobs
   const int64_t Mpad_max = (Mtmax + IA_TILE - 1) / IA_TILE * IA_TILE;
-  const bool prune = c->prune && use_h && g.ch == 1 && !sharded && g.NA >= c->prune_min_rows && Mpad_max <= 4096;
-  if (prune) g.nwg = std::min(IA_NWG_H, g.n_tiles);  // round-robin chunks: WG w owns tiles w + nwg*k
+  const bool prune = c->prune && use_h && g.ch == 1 && g.NA >= c->prune_min_rows && Mpad_max <= 4096;
+  // Pruned levels: every rank holds the whole Morton-sorted DB, its tiles stored shard by shard
+  // (ia_internal.h ia_shard_morton_tile: shard r = Morton tiles r, r + W, ...), and scans its own
+  // contiguous storage range.  Unpruned levels: contiguous tile ranges (ia_shard_tiles).
+  if (prune) {
+    g.tile0 = 0;
+    g.tile1 = g.n_tiles;
+  }
+  const int ns = g.tile1 - g.tile0;  // DB tiles this process holds
+  struct Shard {
+    int t0, t1, nwg, tpw;  // storage tiles [t0, t1) of the level's DB, scan decomposition
+  };
+  auto decomp = [&](int t0, int t1) {
+    Shard d{t0, t1, 0, 0};
+    const int n = t1 - t0;
+    if (prune) d.nwg = std::min(IA_NWG_H, n);  // round-robin chunks: WG w owns tiles w + nwg*k
+    else {
+      d.tpw = use_h ? std::max(IA_WGH / IA_WAVE, (n + IA_NWG_H - 1) / IA_NWG_H) : std::max(4, (n + IA_WG_TARGET - 1) / IA_WG_TARGET);
+      d.nwg = (n + d.tpw - 1) / d.tpw;
+    }
+    return d;
+  };
+  std::vector<Shard> shards;  // the shards this process scans
+  if (!multi) {
+    shards.push_back(decomp(g.tile0, g.tile1));
+  } else {
+    for (int r = sharded ? c->rank : 0; r < (sharded ? c->rank + 1 : Wsh); r++) {
+      if (prune) {
+        const int t0 = (int)ia_shard_off(g.n_tiles, Wsh, r), t1 = (int)ia_shard_off(g.n_tiles, Wsh, r + 1);
+        shards.push_back(decomp(t0, t1));
+      } else {
+        int64_t t0, t1;
+        ia_shard_tiles(g.NA, Wsh, r, &t0, &t1);
+        shards.push_back(decomp((int)t0, (int)t1));
+      }
+    }
+  }
+  int nwg_max = 1;
+  for (const Shard &x : shards) nwg_max = std::max(nwg_max, x.nwg);
+  g.nwg = shards[0].nwg;
+  g.tiles_per_wg = shards[0].tpw;
+  const size_t rec_stride = (size_t)Mtmax * nwg_max;  // records of one shard's scan
   const size_t db_row_bytes = use_h ? (size_t)16 * g.KS * 4 : (size_t)DP * 4;  // hi+lo f16 / fp32 per column
+  const size_t tile_bytes = use_h ? (size_t)ia_k3h_tile_bytes(g.KS) : (size_t)IA_TILE * DP * 4;  // one stored DB tile
 
   // per-level scratch
   if ((rc = c->db.ensure((size_t)std::max(ns, 1) * IA_TILE * db_row_bytes)) || (rc = c->mu.ensure(4 * g.ch * 8)) ||
       (rc = c->db64.ensure((size_t)g.NA * ia_db64_stride(g.ch) * 8)) ||
       (rc = c->Rbits.ensure(4)) || (rc = c->q64.ensure((size_t)Mpad_max * g.D * 8)) ||
       (rc = c->qn2.ensure((size_t)Mpad_max * 8)) || (rc = c->qf.ensure((size_t)Mpad_max * db_row_bytes)) ||
-      (rc = c->rec.ensure((size_t)Mtmax * std::max(g.nwg, 1) * 16)) ||
-      (rc = c->recT.ensure((size_t)Mtmax * std::max(g.nwg, 1) * 4)) || (rc = c->win.ensure((size_t)Mtmax * 16)) ||
-      (rc = c->allwin.ensure((size_t)Mtmax * 16 * world)) || (rc = c->counters.ensure(5 * 8)) ||
+      (rc = c->rec.ensure(rec_stride * shards.size() * 16)) || (rc = c->recT.ensure(rec_stride * shards.size() * 4)) ||
+      (rc = c->win.ensure((size_t)Mtmax * 16)) || (rc = c->allwin.ensure((size_t)Mtmax * 16 * Wsh)) ||
+      (rc = c->counters.ensure(5 * 8)) ||
       (rc = c->pairs.ensure(4 * IA_NWG_H * 8)) || (rc = c->ord.ensure(2 * 4096 * 4)) ||
       (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 : 16)))
+    return rc;
+  if (prune && ((rc = c->qs_order.ensure((size_t)Mpad_max * 4)) || (rc = c->qs_info.ensure((size_t)Mpad_max * 3 * 16)) ||
+                (rc = c->qs_frag.ensure((size_t)Mpad_max * db_row_bytes)) ||
+                (rc = c->qs_tbox.ensure((size_t)Mpad_max / IA_TILE * 3 * 16))))
     return rc;
   // per-workgroup counters of the pruned scan: [pairs | pairs (timed steps) | tiles | tiles (timed)][wg]
   HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 4 * IA_NWG_H * 8, c->st));
@@ -576,7 +630,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   ia_launch_means(g.ch, Aim, g.n_ap, c->mu.as<double>(), c->st);
   ia_launch_db64_build(g, Aim, c->db64.as<double>(), c->st);  // every row: coherence reads any row
   double ufac = 0.;
-  if (prune && (rc = prepare_prune(c, g, c->mu.as<double>(), &ufac))) return rc;  // sets g.pos2row
+  if (prune && (rc = prepare_prune(c, g, c->mu.as<double>(), Wsh, &ufac))) return rc;  // sets g.pos2row
   if (ns > 0) {
     if (use_h) ia_launch_db_build_h(g, Aim, c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
     else ia_launch_db_build(g, Aim, c->mu.as<double>(), c->db.as<float4>(), c->Rbits.as<unsigned>(), c->st);
@@ -601,13 +655,30 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   ma.qinfo = prune ? c->qinfo.as<float4>() : nullptr;
   ma.boxes = prune ? c->boxes.as<float4>() : nullptr;
   ma.ufac = ufac;
-  int64_t shard_rows = 0;  // real DB rows in this shard's tiles (strided layout)
-  for (int t = g.tile0; t < g.tile1; t++) {
-    const int64_t tr = ia_tile_perm(t, g.n_tiles);
-    shard_rows += std::min<int64_t>(IA_TILE, (g.NA - tr + g.n_tiles - 1) / g.n_tiles);
-  }
   ma.eps_c = use_h ? ia_eps_c_h(g.KS, prune || c->k3_variant == 1) : ia_eps_c(DP);
   ma.eps_a = use_h ? ia_eps_a_h() : 0.;
+  // per shard: its records, decomposition, DB positions (and table / boxes of a pruned level)
+  std::vector<MergeArgs> mas(shards.size(), ma);
+  std::vector<int64_t> shard_rows(shards.size(), 0);  // real DB rows in each shard (unpruned flops)
+  for (size_t i = 0; i < shards.size(); i++) {
+    const Shard &x = shards[i];
+    MergeArgs &m = mas[i];
+    m.rec = c->rec.as<float4>() + i * rec_stride;
+    m.recT = c->recT.as<float>() + i * rec_stride;
+    m.nwg = x.nwg;
+    m.tpw = x.tpw;
+    m.pos0 = x.t0 * IA_TILE;
+    m.pos_end = x.t1 * IA_TILE;
+    if (prune) {
+      m.pos2row = g.pos2row + (size_t)x.t0 * IA_TILE;
+      m.boxes = c->boxes.as<float4>() + 2 * (size_t)x.t0;
+      m.NT = x.t1 - x.t0;
+    }
+    for (int t = x.t0; t < x.t1 && !prune; t++) {
+      const int64_t tr = ia_tile_perm(t, g.n_tiles);
+      shard_rows[i] += std::min<int64_t>(IA_TILE, (g.NA - tr + g.n_tiles - 1) / g.n_tiles);
+    }
+  }
 
   const int qtmax = use_h ? ia_k3h_qtmax(g.KS) : ia_k3_qtmax(g.KH);
   const int stride = c->time_dist > 0 ? c->time_dist : 0;
@@ -639,51 +710,71 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     else
       ia_launch_gather(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(),
                        c->st);
+    // pruned scan: queries sorted once per step (K2s) when the step is wider than the in-kernel
+    // sort of v6/v7 (512) or variant 11 is selected
+    const int k3v = prune && (c->k3p_variant == 11 || sd.Mpad > 512) ? 11 : c->k3p_variant;
+    if (prune && k3v == 11)
+      ia_launch_query_sort(c->qinfo.as<float4>(), c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
+                           c->qs_frag.p, c->qs_tbox.as<float4>(), c->st);
     if (ns > 0) {
       const int qtt = sd.Mpad / IA_TILE, nqb = (qtt + qtmax - 1) / qtmax;
       const bool timed = stride && t % stride == 0;
       if (timed) hipEventRecord(c->evs[2 * n_rec], c->st);
-      int qt0 = 0;
-      for (int b = 0; b < nqb; b++) {
-        const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
-        if (prune)
-          ia_launch_k3p(qt, c->db.p, c->qf.p, c->qinfo.as<float4>(), c->boxes.as<float4>(), g.pos2row, g.n_tiles, qt0, Mt,
-                        sd.Mpad, g.nwg, c->rec.as<float4>(), c->recT.as<float>(),
-                        c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
-                        c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
-                        c->k3p_variant, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
-                        c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), c->st);
-        else if (use_h)
-          ia_launch_k3h(g.KS, qt, c->db.p, c->qf.p, ns, g.tiles_per_wg, qt0, Mt, g.nwg, ma.pos0, ma.NT, c->rec.as<float4>(),
-                        c->recT.as<float>(), c->k3_variant, c->st);
-        else
-          ia_launch_k3(g.KH, qt, c->db.as<float4>(), c->qf.as<float4>(), ns, g.tiles_per_wg, qt0, Mt, g.nwg, ma.pos0,
-                       ma.NT, c->rec.as<float4>(), c->recT.as<float>(), c->st);
-        const int mq = std::min(Mt, (qt0 + qt) * IA_TILE) - qt0 * IA_TILE;
-        const double fl = prune ? 0. : 2.0 * g.D * (double)shard_rows * std::max(mq, 0);  // pruned: pair counters
-        dist_flops += fl;
-        pairs_full += (double)ns * qt;
-        tiles_full += (double)ns;
-        dist_launches++;
-        if (timed) {
-          flops_timed += fl;
-          launches_timed++;
-          // algorithmic bytes of a pruned launch besides its DB tiles: tile boxes, query
-          // fragments and pruning records, K3 records written
-          bytes_timed_fixed += (double)g.n_tiles * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) +
-                               (double)mq * g.nwg * 20;
+      for (size_t i = 0; i < shards.size(); i++) {
+        const Shard &x = shards[i];
+        const MergeArgs &m = mas[i];
+        const int n = x.t1 - x.t0;
+        const char *dbp = (const char *)c->db.p + (size_t)(x.t0 - g.tile0) * tile_bytes;
+        int qt0 = 0;
+        for (int b = 0; b < nqb; b++) {
+          const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
+          if (prune && k3v == 11)
+            ia_launch_k3p(qt, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
+                          (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
+                          c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, 11, sd.t,
+                          c->qs_order.as<int>(), 0, sd.r0, nullptr, c->qs_tbox.as<float4>(), c->st);
+          else if (prune)
+            ia_launch_k3p(qt, dbp, c->qf.p, c->qinfo.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
+                          (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
+                          c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
+                          c->k3p_variant, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
+                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, c->st);
+          else if (use_h)
+            ia_launch_k3h(g.KS, qt, dbp, c->qf.p, n, x.tpw, qt0, Mt, x.nwg, m.pos0, g.n_tiles, (float4 *)m.rec,
+                          (float *)m.recT, c->k3_variant, c->st);
+          else
+            ia_launch_k3(g.KH, qt, (const float4 *)dbp, c->qf.as<float4>(), n, x.tpw, qt0, Mt, x.nwg, m.pos0, g.n_tiles,
+                         (float4 *)m.rec, (float *)m.recT, c->st);
+          const int mq = std::min(Mt, (qt0 + qt) * IA_TILE) - qt0 * IA_TILE;
+          const double fl = prune ? 0. : 2.0 * g.D * (double)shard_rows[i] * std::max(mq, 0);  // pruned: pair counters
+          dist_flops += fl;
+          pairs_full += (double)n * qt;
+          tiles_full += (double)n;
+          dist_launches++;
+          if (timed) {
+            flops_timed += fl;
+            launches_timed++;
+            // algorithmic bytes of a pruned launch besides its DB tiles: tile boxes, query
+            // fragments and pruning records, K3 records written
+            bytes_timed_fixed += (double)n * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) + (double)mq * x.nwg * 20;
+          }
+          qt0 += qt;
         }
-        qt0 += qt;
       }
       if (timed) hipEventRecord(c->evs[2 * n_rec++ + 1], c->st);
-      ord_n = prune && J == 1 && sd.Mpad <= 4096 ? sd.M : 0;
+      ord_n = prune && J == 1 && !multi && sd.Mpad <= 4096 ? sd.M : 0;
     }
-    if (!sharded) {
-      ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), djobs, true, c->st);
+    if (!multi) {
+      ia_launch_merge(g, sd, Aim, mas[0], c->win.as<Winner>(), djobs, true, c->st);
     } else {
-      ia_launch_merge(g, sd, Aim, ma, c->win.as<Winner>(), djobs, false, c->st);
-      NCCL_TRY(ncclAllGather(c->win.p, c->allwin.p, (size_t)sd.M * sizeof(Winner), ncclUint8, c->comm, c->st));
-      ia_launch_finish(g, sd, Aim, c->db64.as<double>(), c->q64.as<double>(), c->allwin.as<Winner>(), world, sd.M, djobs,
+      // certified per-shard winners, then the global winner (smallest exact distance, lowest row)
+      // and coherence / kappa / writeback, identical on every rank
+      for (size_t i = 0; i < shards.size(); i++)
+        ia_launch_merge(g, sd, Aim, mas[i], (sharded ? c->win.as<Winner>() : c->allwin.as<Winner>() + i * sd.M), djobs,
+                        false, c->st);
+      if (sharded)
+        NCCL_TRY(ncclAllGather(c->win.p, c->allwin.p, (size_t)sd.M * sizeof(Winner), ncclUint8, c->comm, c->st));
+      ia_launch_finish(g, sd, Aim, c->db64.as<double>(), c->q64.as<double>(), c->allwin.as<Winner>(), Wsh, sd.M, djobs,
                        c->st);
     }
   }

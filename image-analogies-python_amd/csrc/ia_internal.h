@@ -120,6 +120,23 @@ __host__ __device__ inline int64_t ia_pos_row_t(int64_t pos, int64_t NT, const i
   return tab ? (int64_t)tab[pos] : ia_pos_row(pos, NT);
 }
 
+// Pruned levels sharded over W ranks (ia_prune.hip k_make_table): Morton tile m belongs to
+// shard m mod W; storage tile ts of shard r (storage range [off_r, off_r + NT_r), NT_r =
+// ceil((NT - r) / W), off_r = r q + min(r, NT mod W), q = NT / W) holds Morton tile r + W k.
+__host__ __device__ inline int64_t ia_shard_morton_tile(int64_t ts, int64_t NT, int W) {
+  const int64_t q = NT / W, rem = NT % W;
+  int64_t r, k;
+  if (ts < rem * (q + 1)) {
+    r = ts / (q + 1);
+    k = ts - r * (q + 1);
+  } else {
+    r = rem + (ts - rem * (q + 1)) / q;
+    k = ts - rem * (q + 1) - (r - rem) * q;
+  }
+  return r + (int64_t)W * k;
+}
+inline int64_t ia_shard_off(int64_t NT, int W, int r) { return r * (NT / W) + (r < NT % W ? r : NT % W); }
+
 // certified pruning of the distance scan (ia_prune.hip): projection basis size, smallest DB
 // that prunes
 #define IA_NPC 4
@@ -145,6 +162,13 @@ struct JobPtrs {
   double *dbg_dist;
   const double *weights;       // compute_distance weights
   double kf;                   // kappa factor 1 + 2^(level - L) k
+};
+// the jobs of a launch: job 0 travels in the kernel arguments (a single job - the common case -
+// costs no extra dependent load), the others in a device array
+struct JobSet {
+  JobPtrs j0;
+  const JobPtrs *rest;  // device JobPtrs[n_jobs] (entry 0 unused by kernels)
+  __device__ __forceinline__ JobPtrs get(int job) const { return job == 0 ? j0 : rest[job]; }
 };
 struct QPix {
   int job, r, c, qi;           // job, pixel (r, c) and its raster index in the B level

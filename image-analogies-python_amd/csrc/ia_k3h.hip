@@ -339,7 +339,7 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
           const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
           float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
           unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
-           int r0, int *__restrict__ ord_out) {
+           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   static_assert(QT <= 32, "need masks are 32-bit");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
@@ -682,15 +682,20 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // ------------------------------------------------------------------------------------------
 #define IA_K3P3_MAXQ 512   // queries per step (one per thread)
 #define IA_K3P3_MAXK 512   // DB tiles per workgroup
-template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false, bool PIPE = false>
+// PRE (k3p_variant 11, any Mpad <= 4096): the step's queries were sorted once by k_query_sort
+// (ia_prune.hip): qf / qinfo hold them in sorted order (fragments; lo, hi, (U', key) per slot),
+// ord_in maps a sorted slot to its query and tbox holds the sorted query tiles' boxes, so phase
+// 1 loads only this launch's slice and phase 2 (sort, scatter, tile boxes) is skipped.
+template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false, bool PIPE = false,
+          bool PRE = false>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
            float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
            unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
-           int r0, int *__restrict__ ord_out) {
+           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
-  constexpr int NE = (IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE + WGT - 1) / WGT;  // unsorted fragments per thread
+  constexpr int NE = PRE ? 1 : (IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE + WGT - 1) / WGT;  // unsorted fragments per thread
   static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
   static_assert(WGT >= IA_K3P3_MAXQ && WGT >= IA_K3P3_MAXK, "one query / one tile per thread");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
@@ -700,15 +705,15 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   float4 *tlo = reinterpret_cast<float4 *>(qU + NQ);                   // [QT] query-tile boxes
   float4 *thi = tlo + QT;                                               // [QT]
   float *tU = reinterpret_cast<float *>(thi + QT);                     // [QT]
-  unsigned *skey = reinterpret_cast<unsigned *>(tU + ((QT + 3) & ~3));  // [Mpad]
-  int *order = reinterpret_cast<int *>(skey + Mpad);                    // [Mpad] sorted -> query
-  int *rankof = order + Mpad;                                           // [Mpad] query -> sorted
+  unsigned *skey = reinterpret_cast<unsigned *>(tU + ((QT + 3) & ~3));  // [Mpad]   (PRE: [NQ] slice order)
+  int *order = reinterpret_cast<int *>(skey + (PRE ? NQ : Mpad));       // [Mpad] sorted -> query
+  int *rankof = order + (PRE ? 0 : Mpad);                               // [Mpad] query -> sorted
   const int wg = blockIdx.x;
   const int K = (NT - wg + nwg - 1) / nwg;  // tiles wg + nwg*k, k < K (host: nwg <= NT, K <= MAXK)
   // rev: this step walks the workgroup's tiles in reverse (alternate steps: the tiles read last
   // by one step are read first by the next, while they are still in the memory-side cache)
   auto tk = [&](int k) { return wg + nwg * (rev ? K - 1 - k : k); };
-  float4 *wbox = reinterpret_cast<float4 *>(rankof + Mpad);            // [2K] the WG's tile boxes
+  float4 *wbox = reinterpret_cast<float4 *>(rankof + (PRE ? 0 : Mpad));  // [2K] the WG's tile boxes
   unsigned *kmask = reinterpret_cast<unsigned *>(wbox + 2 * K);        // [K] need mask per tile
   int *items = reinterpret_cast<int *>(kmask + K);                     // [K] needed tiles, in order
   __shared__ unsigned wpairs[NW], wtiles[NW];
@@ -724,10 +729,37 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   {
     ld_tile<KS>(a, db, tk(min(wave, K - 1)), lane);
   }
+  if constexpr (PRE) {
+    // this launch's slice of the presorted queries, straight into LDS
+    const h16x8 *qs = qf + (int64_t)qt0 * NP * IA_WAVE;
+    for (int e = tid; e < QT * NP * IA_WAVE; e += WGT) ldsh[e] = qs[e];
+    for (int x = tid; x < NQ; x += WGT) {
+      const int sl = s0 + x;
+      const bool ok = sl < Mpad;
+      qlo[x] = ok ? qinfo[3 * sl] : make_float4(0.f, 0.f, 0.f, 0.f);
+      qhi[x] = ok ? qinfo[3 * sl + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+      qU[x] = ok ? qinfo[3 * sl + 2].x : -INFINITY;
+      skey[x] = ok ? ord_in[sl] : 0x7fffffff;  // slot -> query of this slice
+    }
+    if (tid < QT) {
+      tlo[tid] = tbox[3 * (qt0 + tid)];
+      thi[tid] = tbox[3 * (qt0 + tid) + 1];
+      tU[tid] = tbox[3 * (qt0 + tid) + 2].x;
+    }
+    if (tid < K) {
+      const int t = tk(tid);
+      wbox[2 * tid] = boxes[2 * t];
+      wbox[2 * tid + 1] = boxes[2 * t + 1];
+    }
+  }
+  __shared__ int kctr;  // DYN: next tile index to hand out
+  if (tid == 0) kctr = NW;
+  if constexpr (PRE) __syncthreads();
+  if constexpr (!PRE) {
   float4 mlo = make_float4(0.f, 0.f, 0.f, 0.f), mhi = mlo;
   float mU = -INFINITY;
   unsigned mkey = 0xFFFFFFFFu;
-  if (tid < Mpad) {
+  if (!PRE && tid < Mpad) {
     mlo = qinfo[3 * tid];
     mhi = qinfo[3 * tid + 1];
     const float4 u = qinfo[3 * tid + 2];
@@ -768,8 +800,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   }
 
   // ---- 2. sort, scatter to sorted slots, query-tile boxes
-  __shared__ int kctr;  // DYN: next tile index to hand out
-  if (tid == 0) kctr = NW;
   if (ORD && n_in > 0) {  // (uniform) the previous step's order: no sort on the critical path
     // rows of the previous order still in this step keep their relative order; then the new
     // rows, then padding, by index (any grouping is exact: it only steers the pruning)
@@ -896,6 +926,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
   }
   __syncthreads();
+  }  // !PRE
   K3P_T(ph[2]);
 
   float b1[QT], b2[QT];
@@ -1094,7 +1125,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     Top2 m = red[x];
 #pragma unroll
     for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
-    const int mq = order[s0 + x];
+    const int mq = PRE ? (int)skey[x] : order[s0 + x];
     if (mq < M) {
       const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
       const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
@@ -1162,6 +1193,7 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     if (variant == 9) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, true>;
 #endif
     if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
+    if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true>;
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

@@ -436,7 +436,7 @@ __device__ __forceinline__ void put_qfrag(float *qf, int m, int f, float v) {
 }
 
 template <int CH>
-__global__ void __launch_bounds__(IA_WG) k_gather_query(LevelGeo g, StepDesc sd, Imgs B, const JobPtrs *__restrict__ jobs,
+__global__ void __launch_bounds__(IA_WG) k_gather_query(LevelGeo g, StepDesc sd, Imgs B, JobSet jobs,
                                                          const double *__restrict__ mu_part,
                                                          double *__restrict__ q64, double *__restrict__ qn2,
                                                          float *__restrict__ qf) {
@@ -449,7 +449,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query(LevelGeo g, StepDesc sd,
     return;
   }
   const QPix px = ia_qpix(sd, g.bw, m);
-  B = job_imgs(B, jobs[px.job]);
+  B = job_imgs(B, jobs.get(px.job));
   const int r = px.r, c = px.c;
   double ss = 0.;
   for (int f = lane; f < G::DP; f += IA_WAVE) {
@@ -717,7 +717,7 @@ __device__ __forceinline__ void put_qh(_Float16 *qf, int m, int f, double v) {
 }
 
 template <int CH, int KS>
-__global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc sd, Imgs B, const JobPtrs *__restrict__ jobs,
+__global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc sd, Imgs B, JobSet jobs,
                                                            const double *__restrict__ mu_part,
                                                            double *__restrict__ q64, double *__restrict__ qn2,
                                                            _Float16 *__restrict__ qf) {
@@ -730,7 +730,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc s
     return;
   }
   const QPix px = ia_qpix(sd, g.bw, m);
-  B = job_imgs(B, jobs[px.job]);
+  B = job_imgs(B, jobs.get(px.job));
   const int r = px.r, c = px.c;
   double ss = 0.;
   for (int f = lane; f < KD; f += IA_WAVE) {
@@ -813,6 +813,13 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
     }
   }
   wave_min_di(bd, bi);
+  if (a.rr && bd == DBL_MAX) {
+    // a shard of the pruned scan that contracted no pair for this query: none of its tiles
+    // passed the bound U' (K3p computes every pair a query needs), so none of its rows can be
+    // the exact NN or tie it.  No winner from this shard.
+    *stat_out = 0u;
+    return Winner{DBL_MAX, INT64_MAX};
+  }
 
   // certification: every unlisted row of chunk w has MFMA value >= T_w, hence true distance
   // >= T_w + |q'|^2 - eps.  Chunks with T_w <= theta may hide a row that beats or ties bd.
@@ -826,15 +833,41 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
       const int j = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
       const int wgid = base + j;
-      const int64_t p0 = (int64_t)a.pos0 + (int64_t)wgid * a.tpw * IA_TILE;
-      const int64_t p1 = min((int64_t)a.pos_end, p0 + (int64_t)a.tpw * IA_TILE);
       double cd = DBL_MAX;
       int64_t ci = INT64_MAX;
-      for (int64_t p = p0 + lane; p < p1; p += IA_WAVE) {
-        const int64_t i = ia_pos_row(p, a.NT);
-        if (i >= a.NA) continue;
-        const double d = dist(i);
-        if (d < cd || (d == cd && i < ci)) { cd = d; ci = i; }
+      if (a.rr) {
+        // pruned scan (a shard of it): chunk = tiles wgid, wgid + nwg, ...  Rows that can
+        // displace or tie the winner have exact distance <= bd, and the global NN is <= U (the
+        // query's coherence candidate), so only tiles whose projection bound passes
+        // min(bd * ufac, U') are rescanned.  A shard none of whose tiles passed U' in K3p holds
+        // no such row: nothing is rescanned and it reports no winner (d = DBL_MAX).
+        const float4 ql = a.qinfo[3 * m], qh = a.qinfo[3 * m + 1];
+        const float ub = fminf(round_up_f(bd * a.ufac), a.qinfo[3 * m + 2].x);
+        for (int64_t tb = 0; wgid + (int64_t)a.nwg * tb < a.NT; tb += IA_WAVE) {
+          const int64_t t = wgid + (int64_t)a.nwg * (tb + lane);
+          const bool nd = t < a.NT && prune_lb(a.boxes[2 * t], a.boxes[2 * t + 1], ql, qh) <= ub;
+          unsigned long long nm = __ballot(nd);
+          while (nm) {
+            const int jt = __ffsll((long long)nm) - 1;
+            nm &= nm - 1;
+            if (lane < IA_TILE) {
+              const int64_t i = a.pos2row[(wgid + (int64_t)a.nwg * (tb + jt)) * IA_TILE + lane];
+              if (i < a.NA) {
+                const double d = dist(i);
+                if (d < cd || (d == cd && i < ci)) { cd = d; ci = i; }
+              }
+            }
+          }
+        }
+      } else {
+        const int64_t p0 = (int64_t)a.pos0 + (int64_t)wgid * a.tpw * IA_TILE;
+        const int64_t p1 = min((int64_t)a.pos_end, p0 + (int64_t)a.tpw * IA_TILE);
+        for (int64_t p = p0 + lane; p < p1; p += IA_WAVE) {
+          const int64_t i = ia_pos_row(p, a.NT);
+          if (i >= a.NA) continue;
+          const double d = dist(i);
+          if (d < cd || (d == cd && i < ci)) { cd = d; ci = i; }
+        }
       }
       wave_min_di(cd, ci);
       if (cd < bd || (cd == bd && ci < bi)) { bd = cd; bi = ci; }
@@ -1034,7 +1067,7 @@ __device__ __forceinline__ double wave_sum_d_x(double v) {  // fixed butterfly o
 //                           Morton key of the projection (sort order of the query tiles)
 // ------------------------------------------------------------------------------------------
 template <int KS>
-__global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc sd, Imgs B, const JobPtrs *__restrict__ jobs,
+__global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc sd, Imgs B, JobSet jobs,
                                                           const double *__restrict__ mu_part,
                                                           double *__restrict__ q64, double *__restrict__ qn2,
                                                           _Float16 *__restrict__ qf, const double *__restrict__ db64,
@@ -1056,7 +1089,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
     return;
   }
   const QPix px = ia_qpix(sd, g.bw, m);
-  const JobPtrs &jp = jobs[px.job];
+  const JobPtrs jp = jobs.get(px.job);
   B = job_imgs(B, jp);
   const int32_t *__restrict__ s = jp.s, *__restrict__ im = jp.im;
   const int r = px.r, c = px.c, qi = px.qi;
@@ -1407,11 +1440,11 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
 
 template <int CH, bool FUSED>
 __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, Winner *__restrict__ win,
-                                                        const JobPtrs *__restrict__ jobs) {
+                                                        JobSet jobs) {
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
   if (m >= sd.J * sd.M) return;
   const QPix px = ia_qpix(sd, g.bw, m);
-  const JobPtrs &jp = jobs[px.job];
+  const JobPtrs jp = jobs.get(px.job);
 #if (IA_PROBE & 3) == 0
   if constexpr (FUSED) {
     __shared__ double qsh[IA_WG / IA_WAVE][Geo<CH>::DS], wsh[IA_WG / IA_WAVE][Geo<CH>::DS];
@@ -1452,7 +1485,7 @@ template <int CH>
 __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd, Imgs A, const double *__restrict__ db64,
                                                          const double *__restrict__ q64,
                                                          const Winner *__restrict__ allwin, int world, int Mstride,
-                                                         const JobPtrs *__restrict__ jobs) {
+                                                         JobSet jobs) {
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
   if (m >= sd.J * sd.M) return;
   double bd = DBL_MAX;
@@ -1462,7 +1495,7 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
     if (w.d < bd || (w.d == bd && w.idx < bi)) { bd = w.d; bi = w.idx; }
   }
   const QPix px = ia_qpix(sd, g.bw, m);
-  const JobPtrs &jp = jobs[px.job];
+  const JobPtrs jp = jobs.get(px.job);
   const unsigned prev = jp.pstat ? jp.pstat[px.qi] : 0u;
   finish_pixel<CH>(g, A, db64, px.r, px.c, bi, q64 + (int64_t)m * Geo<CH>::D, jp.s, jp.im, jp.Bp, jp.weights, jp.kf,
                    jp.pstat, prev);
@@ -1677,12 +1710,12 @@ void ia_launch_db_build(const LevelGeo &g, const Imgs &A, const double *mu, floa
 }
 
 template <int CH>
-static void launch_gather_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu,
+static void launch_gather_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                             double *q64, double *qn2, float *qf, hipStream_t st) {
   hipLaunchKernelGGL(k_gather_query<CH>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs, mu, q64,
                      qn2, qf);
 }
-void ia_launch_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu, double *q64,
+void ia_launch_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu, double *q64,
                       double *qn2, float *qf, hipStream_t st) {
   if (g.ch == 1) launch_gather_t<1>(g, sd, B, jobs, mu, q64, qn2, qf, st);
   else if (g.ch == 2) launch_gather_t<2>(g, sd, B, jobs, mu, q64, qn2, qf, st);
@@ -1718,7 +1751,7 @@ void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tile
 
 template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
-                           const JobPtrs *jobs, bool fused, hipStream_t st) {
+                           const JobSet &jobs, bool fused, hipStream_t st) {
   dim3 grid(cdiv(sd.J * sd.M, IA_WG / IA_WAVE));
   if (fused)
     hipLaunchKernelGGL((k_merge_level<CH, true>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
@@ -1726,7 +1759,7 @@ static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A,
     hipLaunchKernelGGL((k_merge_level<CH, false>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
 }
 void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
-                     const JobPtrs *jobs, bool fused, hipStream_t st) {
+                     const JobSet &jobs, bool fused, hipStream_t st) {
   if (g.ch == 1) launch_merge_t<1>(g, sd, A, ma, win, jobs, fused, st);
   else if (g.ch == 2) launch_merge_t<2>(g, sd, A, ma, win, jobs, fused, st);
   else launch_merge_t<3>(g, sd, A, ma, win, jobs, fused, st);
@@ -1734,12 +1767,12 @@ void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const
 
 template <int CH>
 static void launch_finish_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
-                            const Winner *allwin, int world, int Mstride, const JobPtrs *jobs, hipStream_t st) {
+                            const Winner *allwin, int world, int Mstride, const JobSet &jobs, hipStream_t st) {
   hipLaunchKernelGGL(k_finish_level<CH>, dim3(cdiv(sd.J * sd.M, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, A, db64, q64,
                      allwin, world, Mstride, jobs);
 }
 void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
-                      const Winner *allwin, int world, int Mstride, const JobPtrs *jobs, hipStream_t st) {
+                      const Winner *allwin, int world, int Mstride, const JobSet &jobs, hipStream_t st) {
   if (g.ch == 1) launch_finish_t<1>(g, sd, A, db64, q64, allwin, world, Mstride, jobs, st);
   else if (g.ch == 2) launch_finish_t<2>(g, sd, A, db64, q64, allwin, world, Mstride, jobs, st);
   else launch_finish_t<3>(g, sd, A, db64, q64, allwin, world, Mstride, jobs, st);
@@ -1841,18 +1874,18 @@ void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *mu, vo
 }
 
 template <int CH, int KS>
-static void launch_gather_h_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu,
+static void launch_gather_h_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                               double *q64, double *qn2, void *qf, hipStream_t st) {
   hipLaunchKernelGGL((k_gather_query_h<CH, KS>), dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs,
                      mu, q64, qn2, (_Float16 *)qf);
 }
-void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu,
+void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, hipStream_t st) {
   if (g.ch == 1) launch_gather_h_t<1, 4>(g, sd, B, jobs, mu, q64, qn2, qf, st);
   else launch_gather_h_t<2, 7>(g, sd, B, jobs, mu, q64, qn2, qf, st);
 }
 
-void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu,
+void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
                         float4 *qinfo, hipStream_t st) {
   hipLaunchKernelGGL(k_gather_query_p<4>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs, mu, q64,
@@ -1900,23 +1933,27 @@ size_t ia_k3p_lds(int qt, int Mpad) {
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
-                   hipStream_t st) {
+                   const float4 *tbox, hipStream_t st) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
   const int kmax = (NT + nwg - 1) / nwg;  // DB tiles per workgroup
-  const int rev = (variant == 7 || variant == 8 || variant == 10) ? (step & 1) : 0;  // alternate steps walk in reverse
+  const int rev = (variant == 7 || variant == 8 || variant == 10 || variant == 11) ? (step & 1) : 0;  // alternate steps walk in reverse
   if (variant == 7) variant = 6;  // 8: + the previous step's query order (no sort)
   if (variant == 10) variant = 9;  // 9: 6 + pipelined single chains; 10: 9 + reverse walks
-  if (variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // v3/v4 limits (ia_k3h.hip IA_K3P3_*)
+  if (variant != 11 && variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // v3/v4 limits (ia_k3h.hip IA_K3P3_*)
+  if (variant == 11 && kmax > 512) variant = 1;  // (never with presorted queries: the caller only uses 11 below)
   const k3p_fn fn = g4[qt - 1](variant);
-  const size_t lds = ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
-  static int attr_lds[11][16] = {};
-  const int vi = variant < 0 || variant > 10 ? 1 : variant;
+  const size_t NQ = (size_t)qt * IA_TILE;
+  const size_t lds = variant == 11 ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 +
+                                         NQ * 4 + (size_t)kmax * 40
+                                   : ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
+  static int attr_lds[12][16] = {};
+  const int vi = variant < 0 || variant > 11 ? 1 : variant;
   if ((int)lds > attr_lds[vi][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_lds[vi][qt] = (int)lds;
   }
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WGH), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row, NT,
-                     qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out);
+                     qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox);
 }

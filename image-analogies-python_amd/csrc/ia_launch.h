@@ -6,15 +6,15 @@
 
 void ia_launch_means(int ch, const Imgs &A, int n_ap, double *mu, hipStream_t st);
 void ia_launch_db_build(const LevelGeo &g, const Imgs &A, const double *mu, float4 *db, unsigned *Rbits, hipStream_t st);
-void ia_launch_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu, double *q64,
+void ia_launch_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu, double *q64,
                       double *qn2, float *qf, hipStream_t st);
 int ia_k3_qtmax(int KH);
 void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tiles, int tpw, int qt0, int M, int nwg,
                   int row0, int NT, float4 *rec, float *recT, hipStream_t st);
 void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
-                     const JobPtrs *jobs, bool fused, hipStream_t st);
+                     const JobSet &jobs, bool fused, hipStream_t st);
 void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
-                      const Winner *allwin, int world, int Mstride, const JobPtrs *jobs, hipStream_t st);
+                      const Winner *allwin, int world, int Mstride, const JobSet &jobs, hipStream_t st);
 void ia_launch_db64_build(const LevelGeo &g, const Imgs &A, double *db64, hipStream_t st);
 int ia_db64_stride(int ch);
 void ia_launch_reduce_stats(const unsigned *pstat, int64_t n, unsigned long long *counters, hipStream_t st);
@@ -34,7 +34,7 @@ int ia_k3h_qtmax(int KS);
 size_t ia_k3h_lds(int KS, int qt);
 void ia_launch_absmax(const double *const *p, const int64_t *n, unsigned *out, hipStream_t st);
 void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *mu, void *db, unsigned *Rbits, hipStream_t st);
-void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu,
+void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, hipStream_t st);
 void ia_launch_k3h(int KS, int qt, const void *db, const void *qf, int n_tiles, int tpw, int qt0, int M, int nwg, int row0,
                    int NT, float4 *rec, float *recT, int variant, hipStream_t st);
@@ -47,13 +47,15 @@ void ia_launch_proj_keys(const double *db64, int64_t NA, const double *mu_part, 
 size_t ia_sort_temp_bytes(int64_t n);
 int ia_sort_pairs(void *temp, size_t temp_bytes, const unsigned *keys_in, unsigned *keys_out, const int *vals_in,
                   int *vals_out, int64_t n, hipStream_t st);
-void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int *pos2row, float *boxes,
-                           hipStream_t st);
-void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs *jobs, const double *mu,
+void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int W, int *pos2row,
+                           float *boxes, hipStream_t st);
+void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
                         float4 *qinfo, hipStream_t st);
+void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS, int *order, float4 *sq, void *qfs,
+                          float4 *tbox, hipStream_t st);
 size_t ia_k3p_lds(int qt, int Mpad);
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
-                   hipStream_t st);
+                   const float4 *tbox, hipStream_t st);

@@ -22,6 +22,7 @@
 #include "ia_internal.h"
 #include "ia_launch.h"
 #include "ia_prune.h"
+#include "ia_top2.h"
 
 #define PR_WG 256
 #define PR_COV_ROWS 16  // rows staged in LDS per covariance pass
@@ -119,13 +120,19 @@ __global__ void __launch_bounds__(PR_WG) k_proj_keys(const double *__restrict__ 
 // 8 * (k >> 3) + 4 * (k & 1): consecutive sorted rows alternate between the lane halves of the
 // MFMA output (half = (slot >> 2) & 1), i.e. between K3 subsets.  Positions past NA map to
 // rows >= NA (padding: never a candidate).
-__global__ void __launch_bounds__(PR_WG) k_make_table(const int *__restrict__ sorted_rows, int64_t NA, int n_tiles,
+// Shards (W > 1, DB sharded over W ranks): Morton tile m belongs to shard m mod W, and the
+// storage order groups each shard's tiles contiguously (shard r: storage tiles [off_r, off_r +
+// NT_r), NT_r = ceil((NT - r) / W), local tile k = Morton tile r + W k).  Every shard thus
+// covers the whole feature space evenly (balanced pruned work) and is a contiguous range of
+// the DB, the table and the boxes.
+__global__ void __launch_bounds__(PR_WG) k_make_table(const int *__restrict__ sorted_rows, int64_t NA, int n_tiles, int W,
                                                       int *__restrict__ pos2row) {
   const int64_t p = (int64_t)blockIdx.x * PR_WG + threadIdx.x;
   if (p >= (int64_t)n_tiles * IA_TILE) return;
   const int j = (int)(p & 31);
   const int k = (((j & 3) << 1) | ((j >> 2) & 1) | ((j >> 3) << 3));
-  const int64_t s = (p & ~(int64_t)31) + k;
+  const int64_t tm = W > 1 ? ia_shard_morton_tile(p >> 5, n_tiles, W) : (p >> 5);
+  const int64_t s = tm * IA_TILE + k;
   pos2row[p] = s < NA ? sorted_rows[s] : (int)s;
 }
 
@@ -158,7 +165,90 @@ __global__ void __launch_bounds__(PR_WG) k_tile_boxes(const int *__restrict__ po
   }
 }
 
+// K2s: one sort of a wavefront step's queries for the pruned scan (k3p_variant 11).  One
+// workgroup: unique keys (the Morton key's top 20 bits above the 12-bit query index; padding
+// slots and unused sort slots last) sorted by a bitonic network in LDS; then the step's
+// pruning records and split-f16 fragments are written in sorted order, with each sorted query
+// tile's box (min lo, max hi, max U' over its real queries), so every K3p launch loads just its
+// slice.  Any Mpad <= 4096 (the in-kernel sort of K3p v6/v7 is limited to 512).
+#define QS_WG 1024
+__global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__ qinfo, const h16x8 *__restrict__ qf,
+                                                      int Mpad, int NS, int NP, int *__restrict__ order,
+                                                      float4 *__restrict__ sq, h16x8 *__restrict__ qfs,
+                                                      float4 *__restrict__ tbox) {
+  __shared__ unsigned key[4096];
+  const int tid = threadIdx.x;
+  for (int i = tid; i < NS; i += QS_WG)
+    key[i] = i < Mpad ? ((__float_as_uint(qinfo[3 * i + 2].y) & 0xFFFFF000u) | (unsigned)i) : 0xFFFFFFFFu;
+  __syncthreads();
+  for (int k = 2; k <= NS; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < NS / 2; i += QS_WG) {
+        const int lo = 2 * i - (i & (j - 1)), hi = lo + j;
+        const unsigned a = key[lo], b = key[hi];
+        const bool up = (lo & k) == 0;
+        if ((a > b) == up) {
+          key[lo] = b;
+          key[hi] = a;
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int x = tid; x < Mpad; x += QS_WG) {
+    const int q = (int)(key[x] & 0xFFFu);
+    order[x] = q;
+    sq[3 * x] = qinfo[3 * q];
+    sq[3 * x + 1] = qinfo[3 * q + 1];
+    sq[3 * x + 2] = qinfo[3 * q + 2];
+  }
+  // fragments: sorted slot x of tile xt, piece p, lane L (k-half L >> 5, row L & 31)
+  const int ne = Mpad / IA_TILE * NP * IA_WAVE;
+  for (int e = tid; e < ne; e += QS_WG) {
+    const int L = e & 63, pq = e >> 6, xt = pq / NP, p = pq - xt * NP;
+    const int q = (int)(key[xt * IA_TILE + (L & 31)] & 0xFFFu);
+    qfs[e] = qf[((q >> 5) * NP + p) * IA_WAVE + (L & 32) + (q & 31)];
+  }
+  // sorted query-tile boxes: one 32-lane half-wave per tile
+  const int nt = Mpad / IA_TILE, lane = tid & 63;
+  for (int t = tid >> 5; t < nt; t += QS_WG / 32) {
+    const int q = (int)(key[t * IA_TILE + (lane & 31)] & 0xFFFu);
+    const float4 u = qinfo[3 * q + 2];
+    float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    float um = -INFINITY;
+    if (u.x != -INFINITY) {  // padding slots (U' = -inf) never widen a box
+      lo = qinfo[3 * q];
+      hi = qinfo[3 * q + 1];
+      um = u.x;
+    }
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      lo.x = fminf(lo.x, __shfl_xor(lo.x, o, 64));
+      lo.y = fminf(lo.y, __shfl_xor(lo.y, o, 64));
+      lo.z = fminf(lo.z, __shfl_xor(lo.z, o, 64));
+      lo.w = fminf(lo.w, __shfl_xor(lo.w, o, 64));
+      hi.x = fmaxf(hi.x, __shfl_xor(hi.x, o, 64));
+      hi.y = fmaxf(hi.y, __shfl_xor(hi.y, o, 64));
+      hi.z = fmaxf(hi.z, __shfl_xor(hi.z, o, 64));
+      hi.w = fmaxf(hi.w, __shfl_xor(hi.w, o, 64));
+      um = fmaxf(um, __shfl_xor(um, o, 64));
+    }
+    if ((lane & 31) == 0) {
+      tbox[3 * t] = lo;
+      tbox[3 * t + 1] = hi;
+      tbox[3 * t + 2] = make_float4(um, 0.f, 0.f, 0.f);
+    }
+  }
+}
+
 // ---- host launchers ---------------------------------------------------------------------------
+void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS, int *order, float4 *sq, void *qfs,
+                          float4 *tbox, hipStream_t st) {
+  int NS = 32;
+  while (NS < Mpad) NS <<= 1;
+  hipLaunchKernelGGL(k_query_sort, dim3(1), dim3(QS_WG), 0, st, qinfo, (const h16x8 *)qf, Mpad, NS, 2 * KS, order, sq,
+                     (h16x8 *)qfs, tbox);
+}
 static inline unsigned pr_cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
 void ia_launch_cov(const double *db64, int64_t NA, int64_t stride, int nwg, const double *mu_part, double *part,
@@ -184,9 +274,9 @@ int ia_sort_pairs(void *temp, size_t temp_bytes, const unsigned *keys_in, unsign
   return (int)hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (int)n, 0, 32, st);
 }
 
-void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int *pos2row, float *boxes,
-                           hipStream_t st) {
+void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int W, int *pos2row,
+                           float *boxes, hipStream_t st) {
   hipLaunchKernelGGL(k_make_table, dim3(pr_cdiv((int64_t)n_tiles * IA_TILE, PR_WG)), dim3(PR_WG), 0, st, sorted_rows, NA,
-                     n_tiles, pos2row);
+                     n_tiles, W, pos2row);
   hipLaunchKernelGGL(k_tile_boxes, dim3(pr_cdiv(n_tiles, PR_WG)), dim3(PR_WG), 0, st, pos2row, proj, NA, n_tiles, boxes);
 }

@@ -121,3 +121,37 @@ def test_driver_end_to_end_matches_oracle(tmp_path):
     psnr = np.inf if mse == 0 else 10 * np.log10(1.0 / mse)
     assert psnr >= 50, psnr
     assert (tmp_path / 'out' / 'level_4_color.jpg').exists() and (tmp_path / 'out' / 'metadata.txt').exists()
+
+
+def test_fine_alignment_small_matches_oracle(ctx):
+    """level_align='fine' (config.level_align, cfg4's pairing): B 96x96 against A 48x48, B's finest
+    level paired with A's finest.  Every level bit-exact against the oracle's restatement of the
+    reference loop run on the same aligned pyramids (the loop itself is alignment-agnostic)."""
+    from ia_amd import synth
+    job = synth.make_job(48, b_size=96, k=25.0, level_align='fine')
+    assert job.B_pyr[-1].shape == (96, 96) and job.A_pyr[-1].shape == (48, 48)
+    for l in range(job.L):
+        assert job.B_pyr[l].shape[0] == 2 * job.A_pyr[l].shape[0]
+    Bp, S, IM, st = _run_job(ctx, job)
+    Bp_o = [x.copy() for x in job.Bp_init]
+    So, IMo = O.run_all_levels(job.A_pyr, job.Ap_pyr_list, job.B_pyr, Bp_o, job.k, job.weights)
+    for level in range(1, job.L):
+        assert np.array_equal(S[level], So[level]) and np.array_equal(IM[level], IMo[level])
+        assert np.array_equal(Bp[level], Bp_o[level])
+    assert st.bound_violations == 0 and st.kappa_ambiguous == 0
+
+
+def test_teacher_forced_cfg4(ctx):
+    """BASELINE config 4: B 2048^2 against A 1024^2, kappa 25, level_align='fine' (683 queries per
+    step on the 2048^2 level, pruned scan on its 1024^2 DB).  Invariants on every level, 60
+    sampled pixels teacher-forced on each of the two finest levels."""
+    from ia_amd import synth
+    job = synth.make_job(**synth.CONFIGS['cfg4'][0])
+    assert job.B_pyr[-1].shape == (2048, 2048) and job.A_pyr[-1].shape == (1024, 1024) and job.k == 25.0
+    Bp, S, IM, st = _run_job(ctx, job)
+    _invariants(job, Bp, S, IM)
+    for level in (job.L - 2, job.L - 1):
+        npx, mism = _teacher_force(job, Bp, S, IM, level, 60, seed=40 + level)
+        assert all(near for _, near, _, _ in mism), (level, mism)
+        assert len(mism) <= max(1, npx // 100), (level, mism)
+    assert st.bound_violations == 0 and st.pruned_levels == 1

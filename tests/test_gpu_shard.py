@@ -1,0 +1,68 @@
+"""The sharded device path on one GPU (option "shard_emulate" = W): the A DB
+of every level with >= 64 W tiles is split into W shards; each shard's distance scan and
+certified per-shard winner (k_merge_level<FUSED=false>) run in turn, then the multi-rank finish
+(k_finish_level: global winner = smallest exact distance, lowest row; coherence, kappa,
+writeback) - everything the RCCL path runs except the all-gather itself.  Pruned levels keep
+pruning under sharding (shard r = Morton tiles r, r + W, ..., stored contiguously).  Results must
+be bit-identical to the reference (golden runs) and to unsharded runs (1024^2)."""
+import numpy as np
+import pytest
+
+from golden_util import BIG_CASES, load_e2e
+
+pytestmark = pytest.mark.gpu
+
+
+def _run(ctx, z, W, prune_all):
+    from ia_amd import _native
+    L, k = z['L'], float(z['k'])
+    Bp = [x.copy() for x in z['Bp_init']]
+    st = _native.Stats()
+    out = {}
+    ctx.set_option('shard_emulate', W)
+    if prune_all:
+        ctx.set_option('prune_min_rows', 1)
+    try:
+        for level in range(1, L):
+            out[level] = ctx.synthesize_level(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
+                                              [p[level - 1] for p in z['Ap_pyr']], z['B_pyr'][level],
+                                              z['B_pyr'][level - 1], Bp[level - 1], Bp[level], z['weights'],
+                                              1 + 2.0 ** (level - L) * k, st)
+    finally:
+        ctx.set_option('shard_emulate', 1)
+        ctx.set_option('prune_min_rows', 524288)
+    return out, Bp, st
+
+
+@pytest.mark.parametrize('prune_all', [False, True], ids=['unpruned', 'pruned'])
+@pytest.mark.parametrize('W', [2, 4, 8])
+@pytest.mark.parametrize('name', ['g64', 'ties128'] + [c for c in ('g128', 'g256') if c in BIG_CASES])
+def test_emulated_shards_match_reference(ctx, name, W, prune_all):
+    z = load_e2e(name)
+    out, Bp, st = _run(ctx, z, W, prune_all)
+    for level, (s, im) in out.items():
+        assert np.array_equal(s, z['s'][level]) and np.array_equal(im, z['im'][level]), level
+        assert np.array_equal(Bp[level], z['Bp_final'][level]), level
+    assert st.bound_violations == 0 and st.kappa_ambiguous == 0
+
+
+@pytest.mark.parametrize('W', [4, 8])
+def test_emulated_shards_1024_match_unsharded(ctx, W):
+    """cfg3 (pruned 1024^2 level, unpruned 512^2 level): W-way sharded == unsharded, every level."""
+    from ia_amd import synth
+    job = synth.make_job(1024)
+    z = {'L': job.L, 'k': job.k, 'A_pyr': job.A_pyr, 'Ap_pyr': job.Ap_pyr_list, 'B_pyr': job.B_pyr,
+         'Bp_init': job.Bp_init, 'weights': job.weights}
+    ref, Bp_ref, _ = _run(ctx, z, 1, False)
+    out, Bp, st = _run(ctx, z, W, False)
+    for level in range(1, job.L):
+        assert np.array_equal(out[level][0], ref[level][0]) and np.array_equal(out[level][1], ref[level][1]), level
+        assert np.array_equal(Bp[level], Bp_ref[level]), level
+    assert st.pruned_levels == 1 and st.bound_violations == 0
+
+
+def test_shard_emulate_option_bounds(ctx):
+    from ia_amd import _native
+    for bad in (0, 65):
+        with pytest.raises(_native.IAError):
+            ctx.set_option('shard_emulate', bad)
