@@ -150,6 +150,9 @@ def main():
                          'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks')
     ap.add_argument('--prune-min-rows', type=int, default=524288,
                     help='smallest DB (rows) the pruned scan is used on (default: the 1024^2 level)')
+    ap.add_argument('--row-source', type=int, default=0, choices=[0, 1],
+                    help='exact rows of the rerank / coherence / pruning bound: 0 = fp64 row DB, 1 = gathered from '
+                         'the A-side images (identical results)')
     ap.add_argument('--shard-emulate', type=int, default=1,
                     help='run every large level as a W-way DB shard on this one GPU (the multi-rank kernels '
                          'without the all-gather: per-shard scans and winners, then the finish); for the cost model')
@@ -205,6 +208,8 @@ def main():
     if args.k3p_variant != 7:
         ctx.set_option('k3p_variant', args.k3p_variant)     # DIAG=1 builds only
     ctx.set_option('prune_min_rows', args.prune_min_rows)
+    if args.row_source:
+        ctx.set_option('row_source', args.row_source)
     if args.shard_emulate > 1:
         ctx.set_option('shard_emulate', args.shard_emulate)
     if args.mode == 'shard' and world > 1:
@@ -310,7 +315,7 @@ def main():
                                            'pyramid_levels': job.L,
                                            'px_per_step': job_pixels, 'nn_flops_per_step': job_flops,
                                            'mode': 'sweep' if sw is not None else args.mode,
-                                           'shard_emulate': args.shard_emulate,
+                                           'shard_emulate': args.shard_emulate, 'row_source': args.row_source,
                                            'parallelism': (('jobs%d' % world) if sw is not None else
                                                            ('replicas%d' if args.mode == 'replicas' else 'dbshard%d')
                                                            % world),

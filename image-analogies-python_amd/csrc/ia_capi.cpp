@@ -95,6 +95,7 @@ struct ia_ctx {
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
   int64_t prune_min_rows = IA_PRUNE_MIN_ROWS;  // option "prune_min_rows": smallest DB that prunes
   int prune = 1;
+  int row_source = 0;            // option "row_source": exact rows from 0 = the fp64 row DB, 1 = the A images
   int shard_emulate = 1;         // option "shard_emulate": W > 1 runs a W-way DB shard on this device
   int matcher = IA_MATCH_F16X3;  // option "matcher"
   int k3p_variant = 7;           // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
@@ -298,6 +299,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "prune_min_rows")) {
     if (value < 1) return fail(IA_EINVAL, "ia_set_option: prune_min_rows must be >= 1");
     c->prune_min_rows = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "row_source")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: row_source must be 0 (row DB) or 1 (images)");
+    c->row_source = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "shard_emulate")) {
@@ -655,6 +661,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   ma.qinfo = prune ? c->qinfo.as<float4>() : nullptr;
   ma.boxes = prune ? c->boxes.as<float4>() : nullptr;
   ma.ufac = ufac;
+  ma.img_rows = (c->row_source == 1 && g.ch == 1) ? 1 : 0;
   ma.eps_c = use_h ? ia_eps_c_h(g.KS, prune || c->k3_variant == 1) : ia_eps_c(DP);
   ma.eps_a = use_h ? ia_eps_a_h() : 0.;
   // per shard: its records, decomposition, DB positions (and table / boxes of a pruned level)
@@ -704,7 +711,8 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     sd.Mpad = (Mt + IA_TILE - 1) / IA_TILE * IA_TILE;
     if (prune)
       ia_launch_gather_p(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
-                         c->db64.as<double>(), c->pr_basis.as<double>(), ufac, c->qinfo.as<float4>(), c->st);
+                         c->db64.as<double>(), c->pr_basis.as<double>(), ufac, c->qinfo.as<float4>(), Aim, ma.img_rows,
+                         c->st);
     else if (use_h)
       ia_launch_gather_h(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p, c->st);
     else
@@ -966,6 +974,7 @@ int ia_index_query(ia_index *x, const double *q, int64_t nq, int64_t *idx_out, d
   ma.qinfo = nullptr;
   ma.boxes = nullptr;
   ma.ufac = 0.;
+  ma.img_rows = 0;
   ma.eps_c = ia_eps_c(DP);
   ma.eps_a = 0.;
   const int qtmax = ia_k3_qtmax(x->KH);

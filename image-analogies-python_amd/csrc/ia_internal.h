@@ -95,6 +95,7 @@ struct MergeArgs {
   const float4 *qinfo;                // pruned levels: the step's query projection intervals (K2p)
   const float4 *boxes;                // pruned levels: per-tile projection boxes (ia_prune.hip)
   double ufac;                        // pruned levels: bound factor of ia_prune.h
+  int img_rows;                       // 1: exact rows gathered from the A-side images (1 channel)
 };
 
 // DB positions are tile-strided and tile-scattered: slot j of tile t holds row j*NT + perm(t)

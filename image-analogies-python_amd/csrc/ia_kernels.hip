@@ -751,10 +751,36 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc s
 // ------------------------------------------------------------------------------------------
 // K4: exact rerank + certification (+ coherence, kappa rule, writeback) — one wave / query
 // ------------------------------------------------------------------------------------------
+// The 55 exact features of DB row `row` (1 channel) read straight from the A-side pyramid images
+// (option "row_source" = 1) instead of the fp64 row DB: row = img*h*w + r*w + c holds
+// [A coarse 3x3 | A fine 5x5 | A'_img coarse 3x3 | A'_img fine, first 12] (algorithms.py:36-41,
+// 63-67), the windows symmetric-padded (ia_reflect).  20 MB of images at 1024^2 instead of a
+// 470 MB row DB: the rows stay cache resident and the memory-side cache is left to the MFMA DB.
+__device__ __forceinline__ void row_from_imgs(const Imgs &A, int64_t row, double (&t)[56]) {
+  const unsigned hw = (unsigned)A.h * (unsigned)A.w;
+  const int img = (int)((unsigned)row / hw);
+  const unsigned rem = (unsigned)row - (unsigned)img * hw;
+  const int r = (int)(rem / (unsigned)A.w), c = (int)(rem - (unsigned)r * (unsigned)A.w);
+  const Px P = make_px<1>(A, r, c);
+#pragma unroll
+  for (int f = 0; f < 55; f++) t[f] = featp<1>(A, P, f, img);
+  t[55] = 0.;
+}
 // exact DB-row distance of row `row` (level path): ((a - q)**2).sum() in numpy order, the row
-// read from the fp64 DB (K1b)
+// read from the fp64 DB (K1b) or, with Ai (1 channel), from the images
 template <int CH>
-__device__ __forceinline__ double exact_dist_level(const double *__restrict__ db64, int64_t row, const double *q) {
+__device__ __forceinline__ double exact_dist_level(const double *__restrict__ db64, int64_t row, const double *q,
+                                                   const Imgs *Ai = nullptr) {
+  if constexpr (CH == 1) {
+    if (Ai) {
+      double t[56];
+      row_from_imgs(*Ai, row, t);
+      return pw_sum<55>([&](int f) {
+        const double d = t[f] - q[f];
+        return d * d;
+      });
+    }
+  }
   const double *a = db64 + row * Geo<CH>::DS;
   return pw_sum<Geo<CH>::D>([&](int f) {
     const double d = a[f] - q[f];
@@ -956,17 +982,21 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__r
 //   wsq = sum(((a - q) * w)**2) sequentially (compute_distance before its sqrt / square)
 template <int CH>
 __device__ __forceinline__ void row_dists(const double *__restrict__ db64, int row, const double *q, const double *w,
-                                          double &unw, double &wsq) {
+                                          double &unw, double &wsq, const Imgs *Ai = nullptr) {
   constexpr int D = Geo<CH>::D, DS = Geo<CH>::DS;
   const double *a = db64 + (int64_t)row * DS;
   if constexpr (CH == 1) {
-    const double2 *a2 = reinterpret_cast<const double2 *>(a);
     double t[D + 1];
+    if (Ai) {
+      row_from_imgs(*Ai, row, t);
+    } else {
+      const double2 *a2 = reinterpret_cast<const double2 *>(a);
 #pragma unroll
-    for (int k = 0; k < (D + 1) / 2; k++) {  // all 28 loads issued before any use
-      const double2 v = a2[k];
-      t[2 * k] = v.x;
-      t[2 * k + 1] = v.y;
+      for (int k = 0; k < (D + 1) / 2; k++) {  // all 28 loads issued before any use
+        const double2 v = a2[k];
+        t[2 * k] = v.x;
+        t[2 * k + 1] = v.y;
+      }
     }
 #pragma unroll
     for (int f = 0; f < D; f++) t[f] -= q[f];
@@ -1072,7 +1102,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
                                                           double *__restrict__ q64, double *__restrict__ qn2,
                                                           _Float16 *__restrict__ qf, const double *__restrict__ db64,
                                                           const double *__restrict__ basis, double ufac,
-                                                          float4 *__restrict__ qinfo) {
+                                                          float4 *__restrict__ qinfo, Imgs A, int img_rows) {
   constexpr int D = 55, KD = 16 * KS;
   static_assert(KD <= IA_WAVE, "one feature per lane");
   __shared__ double qsh[IA_WG / IA_WAVE][Geo<1>::DS];
@@ -1126,7 +1156,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
   for (int i = 0; i < IA_NPC; i++) p[i] = wave_sum_d_x(p[i]);
   __builtin_amdgcn_wave_barrier();  // qsh written by this wave's lanes, read below
   double u = DBL_MAX;
-  if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh[wv]);
+  if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh[wv], img_rows ? &A : nullptr);
   u = wave_min_d_x(u);
   if (lane == 0) {
     qn2[m] = ss;
@@ -1253,7 +1283,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     const double *src = A.p3 + img * A.img_stride_f + (int64_t)((unsigned)my_row - img * hw) * CH;
 #pragma unroll
     for (int k = 0; k < CH; k++) av[k] = src[k];
-    row_dists<CH>(a.db64, my_row, qs, ws, unw, wsq);
+    row_dists<CH>(a.db64, my_row, qs, ws, unw, wsq, a.img_rows ? &A : nullptr);
   }
   // bound audit: the exact distance of every reranked candidate must lie within eps of its
   // MFMA value + |q'|^2 (a violation would void the certification; counted, never expected)
@@ -1274,7 +1304,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     const int row = lowest_cand<RPL>(cmask, i1, i2, v1, v2, v);
     cmask &= cmask - 1;
     double u, wq;
-    row_dists<CH>(a.db64, row, qs, ws, u, wq);
+    row_dists<CH>(a.db64, row, qs, ws, u, wq, a.img_rows ? &A : nullptr);
     if (u < nd || (u == nd && row < ni)) {
       nd = u;
       ni = row;
@@ -1335,7 +1365,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
             if (j >= 0) {
               const int64_t i = a.pos2row[(wgid + (int64_t)a.nwg * (tb + j)) * IA_TILE + (lane & 31)];
               if (i < a.NA) {
-                const double d = exact_dist_level<CH>(a.db64, i, qs);
+                const double d = exact_dist_level<CH>(a.db64, i, qs, a.img_rows ? &A : nullptr);
                 if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
               }
             }
@@ -1347,7 +1377,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
         for (int64_t p = p0 + lane; p < p1; p += IA_WAVE) {
           const int64_t i = ia_pos_row_t(p, a.NT, a.pos2row);
           if (i >= a.NA) continue;
-          const double d = exact_dist_level<CH>(a.db64, i, qs);
+          const double d = exact_dist_level<CH>(a.db64, i, qs, a.img_rows ? &A : nullptr);
           if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
         }
       }
@@ -1377,7 +1407,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     const double wsq_coh = __shfl(wsq, kk, 64);
     if (recompute_app) {
       double u, wq = 0.;
-      if (lane == 0) row_dists<CH>(a.db64, bi, qs, ws, u, wq);
+      if (lane == 0) row_dists<CH>(a.db64, bi, qs, ws, u, wq, a.img_rows ? &A : nullptr);
       wsq_app = __shfl(wq, 0, 64);
     }
     // compute_distance = norm(x)**2 = sqrt(sum x^2)**2 ; kappa rule image_analogies.py:206
@@ -1460,7 +1490,9 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
   const Winner wn{0., (int64_t)__float_as_int(ma.rec[(int64_t)m * ma.nwg].y)};
 #else
   unsigned stat = 0;
-  const Winner wn = certified_winner(ma, m, [&](int64_t row) { return exact_dist_level<CH>(ma.db64, row, q); }, &stat);
+  const Winner wn = certified_winner(ma, m, [&](int64_t row) {
+    return exact_dist_level<CH>(ma.db64, row, q, ma.img_rows ? &A : nullptr);
+  }, &stat);
 #endif
 #if IA_PROBE & 2  // diagnostic build only: no coherence / kappa
   if ((threadIdx.x & 63) == 0) {
@@ -1887,9 +1919,9 @@ void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
 
 void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
-                        float4 *qinfo, hipStream_t st) {
+                        float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st) {
   hipLaunchKernelGGL(k_gather_query_p<4>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs, mu, q64,
-                     qn2, (_Float16 *)qf, db64, basis, ufac, qinfo);
+                     qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A, img_rows);
 }
 
 // split-f16 distance kernels live in ia_k3h.hip, compiled once per (KS, QT) instance

@@ -51,7 +51,7 @@ void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t N
                            float *boxes, hipStream_t st);
 void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
-                        float4 *qinfo, hipStream_t st);
+                        float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st);
 void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS, int *order, float4 *sq, void *qfs,
                           float4 *tbox, hipStream_t st);
 size_t ia_k3p_lds(int qt, int Mpad);

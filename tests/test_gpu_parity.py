@@ -40,8 +40,16 @@ def _run_levels(ctx, z, Bp, A_pyr=None, Ap_pyr=None, B_pyr=None):
     return out, st
 
 
+@pytest.fixture(params=[0, 1], ids=['rowdb', 'rowimg'])
+def row_source(request, ctx):
+    """exact rows of the rerank / coherence / bound from the fp64 row DB or the A-side images"""
+    ctx.set_option('row_source', request.param)
+    yield request.param
+    ctx.set_option('row_source', 0)
+
+
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
-def test_level_path_matches_reference(ctx, matcher, name):
+def test_level_path_matches_reference(ctx, matcher, row_source, name):
     z = load_e2e(name)
     Bp = [x.copy() for x in z['Bp_init']]
     out, st = _run_levels(ctx, z, Bp)
