@@ -79,6 +79,9 @@ EXPORTS = {
                                          ctypes.POINTER(ctypes.c_int)]),
     'ia_shard_tiles': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
                                       ctypes.POINTER(ctypes.c_int64)]),
+    'ia_shard_tiles_pruned': (ctypes.c_int, [ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                             ctypes.POINTER(ctypes.c_int64), ctypes.POINTER(ctypes.c_int64)]),
+    'ia_shard_morton_tile': (ctypes.c_int64, [ctypes.c_int64, ctypes.c_int64, ctypes.c_int]),
 }
 
 _lib = None
@@ -339,6 +342,17 @@ def shard_tiles(n_rows, world, rank):
     a, b = ctypes.c_int64(), ctypes.c_int64()
     check(lib().ia_shard_tiles(n_rows, world, rank, ctypes.byref(a), ctypes.byref(b)), 'ia_shard_tiles')
     return a.value, b.value
+
+
+def shard_tiles_pruned(n_rows, world, rank):
+    """Storage tiles [t0, t1) of `rank` on a pruned level (Morton tiles rank, rank + world, ...)."""
+    a, b = ctypes.c_int64(), ctypes.c_int64()
+    check(lib().ia_shard_tiles_pruned(n_rows, world, rank, ctypes.byref(a), ctypes.byref(b)), 'ia_shard_tiles_pruned')
+    return a.value, b.value
+
+
+def shard_morton_tile(storage_tile, n_tiles, world):
+    return lib().ia_shard_morton_tile(storage_tile, n_tiles, world)
 
 
 TILE_MUL = 2654435761  # IA_TILE_MUL of ia_internal.h

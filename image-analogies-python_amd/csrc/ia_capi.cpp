@@ -378,6 +378,25 @@ int ia_shard_tiles(int64_t n_rows, int world, int rank, int64_t *tile0, int64_t 
   return IA_OK;
 }
 
+int ia_shard_tiles_pruned(int64_t n_rows, int world, int rank, int64_t *tile0, int64_t *tile1) {
+  if (n_rows < 1 || world < 1 || rank < 0 || rank >= world || !tile0 || !tile1)
+    return fail(IA_EINVAL, "ia_shard_tiles_pruned: bad args");
+  const int64_t n_tiles = (n_rows + IA_TILE - 1) / IA_TILE;
+  if (!shard_level(n_tiles, world)) {
+    *tile0 = 0;
+    *tile1 = n_tiles;
+    return IA_OK;
+  }
+  *tile0 = ia_shard_off(n_tiles, world, rank);
+  *tile1 = ia_shard_off(n_tiles, world, rank + 1);
+  return IA_OK;
+}
+
+int64_t ia_shard_morton_tile(int64_t storage_tile, int64_t n_tiles, int world) {
+  if (world < 1 || n_tiles < 1 || storage_tile < 0 || storage_tile >= n_tiles) return -1;
+  return world > 1 ? ia_shard_morton_tile_(storage_tile, n_tiles, world) : storage_tile;
+}
+
 int ia_merge_winners(const double *dist, const int64_t *row, int world, int64_t nq, double *dist_out,
                      int64_t *row_out) {
   if (!dist || !row || !dist_out || !row_out || world < 1 || nq < 0) return fail(IA_EINVAL, "ia_merge_winners: bad args");

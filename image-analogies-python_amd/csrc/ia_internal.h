@@ -124,7 +124,7 @@ __host__ __device__ inline int64_t ia_pos_row_t(int64_t pos, int64_t NT, const i
 // Pruned levels sharded over W ranks (ia_prune.hip k_make_table): Morton tile m belongs to
 // shard m mod W; storage tile ts of shard r (storage range [off_r, off_r + NT_r), NT_r =
 // ceil((NT - r) / W), off_r = r q + min(r, NT mod W), q = NT / W) holds Morton tile r + W k.
-__host__ __device__ inline int64_t ia_shard_morton_tile(int64_t ts, int64_t NT, int W) {
+__host__ __device__ inline int64_t ia_shard_morton_tile_(int64_t ts, int64_t NT, int W) {
   const int64_t q = NT / W, rem = NT % W;
   int64_t r, k;
   if (ts < rem * (q + 1)) {

@@ -238,8 +238,11 @@ __device__ __forceinline__ f32x16 k3p_chain(const h16x8 (&a)[2 * KS], const h16x
 #pragma unroll
   for (int s = 0; s < KS; s++) {
     const h16x8 xh = qb[(2 * s) * IA_WAVE], xl = qb[(2 * s + 1) * IA_WAVE];
+#if !(IA_PROBE & 32)  // PROBE=32 (timing only, results invalid): one f16 product per 16 k, the
+                      // cost of a single-pass f16/bf16 prefilter
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], xh, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], xl, c, 0, 0, 0);
+#endif
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], xh, c, 0, 0, 0);
   }
   return c;
@@ -254,10 +257,12 @@ __device__ __forceinline__ void k3p_chain2(const h16x8 (&a)[2 * KS], const h16x8
   for (int s = 0; s < KS; s++) {
     const h16x8 x0h = qb0[(2 * s) * IA_WAVE], x0l = qb0[(2 * s + 1) * IA_WAVE];
     const h16x8 x1h = qb1[(2 * s) * IA_WAVE], x1l = qb1[(2 * s + 1) * IA_WAVE];
+#if !(IA_PROBE & 32)
     c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x0h, c0, 0, 0, 0);
     c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x1h, c1, 0, 0, 0);
     c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0l, c0, 0, 0, 0);
     c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1l, c1, 0, 0, 0);
+#endif
     c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0h, c0, 0, 0, 0);
     c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1h, c1, 0, 0, 0);
   }

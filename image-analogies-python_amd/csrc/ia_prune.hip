@@ -131,7 +131,7 @@ __global__ void __launch_bounds__(PR_WG) k_make_table(const int *__restrict__ so
   if (p >= (int64_t)n_tiles * IA_TILE) return;
   const int j = (int)(p & 31);
   const int k = (((j & 3) << 1) | ((j >> 2) & 1) | ((j >> 3) << 3));
-  const int64_t tm = W > 1 ? ia_shard_morton_tile(p >> 5, n_tiles, W) : (p >> 5);
+  const int64_t tm = W > 1 ? ia_shard_morton_tile_(p >> 5, n_tiles, W) : (p >> 5);
   const int64_t s = tm * IA_TILE + k;
   pos2row[p] = s < NA ? sorted_rows[s] : (int)s;
 }

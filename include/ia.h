@@ -121,7 +121,14 @@ int ia_version(void);
  * "prune_min_rows" DB rows (default 2^19): (DB tile, query tile) pairs a
  * projection bound proves farther than the query's best coherence candidate are skipped.
  * "k3p_variant" / "k3_variant": kernel versions of DESIGN.md §4b; the product build accepts
- * only the defaults (7 / 1), DIAG=1 builds every version.
+ * k3p_variant 7 (default: the pruned scan sorts a step's queries itself up to 512 of them, a
+ * step wider than that is sorted once by k_query_sort) or 11 (always presorted) and
+ * k3_variant 1; DIAG=1 builds every version.
+ * "row_source" = 0 (default: exact rows of the rerank / coherence / pruning bound from the fp64
+ * row DB) or 1 (gathered from the A-side pyramid images, 1 channel).
+ * "shard_emulate" = W (1 = off): on a single-rank context, every level with >= 64 W DB tiles
+ * runs as a W-way DB shard on this device (per-shard scans and certified winners, then the
+ * multi-rank finish; no RCCL): the sharded code path, testable on one GPU.
  * Identical results for every setting. */
 #define IA_MATCH_F32 0
 #define IA_MATCH_F16X3 1
@@ -189,6 +196,12 @@ int ia_wavefront_step(int h, int w, int64_t t, int *r0, int *M);
  * pixels sit in far-apart tiles).  Tiles are split contiguously over ranks; levels under
  * 64*world tiles are not sharded (every rank owns every tile). */
 int ia_shard_tiles(int64_t n_rows, int world, int rank, int64_t *tile0, int64_t *tile1);
+/* Pruned levels (certified pruned scan) shard differently: every rank holds the whole
+ * Morton-sorted DB, stored shard by shard; shard r = Morton tiles r, r + world, r + 2 world, ...
+ * (each covers the whole feature space: balanced pruned work), stored as storage tiles
+ * [tile0, tile1).  ia_shard_morton_tile gives the Morton tile of a storage tile. */
+int ia_shard_tiles_pruned(int64_t n_rows, int world, int rank, int64_t *tile0, int64_t *tile1);
+int64_t ia_shard_morton_tile(int64_t storage_tile, int64_t n_tiles, int world);
 
 #ifdef __cplusplus
 }

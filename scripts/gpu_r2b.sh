@@ -18,5 +18,8 @@ for W in 2 4 8; do
   timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/shard$W -o run -- python3 -u bench.py --steps 1 --warmup 1 --no-cpu-baseline --shard-emulate $W > gpurun_out/bench_shard$W.json 2> gpurun_out/bench_shard$W.err || { echo "shard $W failed"; tail -20 gpurun_out/bench_shard$W.err; exit 1; }
   python3 tools/trace_breakdown.py gpurun_out/shard$W/run_kernel_trace.csv 1 > gpurun_out/breakdown_shard$W.txt 2>&1 || true
 done
-for f in cfg3 cfg3_v11 cfg3_row1 cfg3_row1_v11 cfg4 cfg5 shard2 shard4 shard8; do echo "$f $(cut -c1-200 gpurun_out/bench_$f.json)"; done
+# timing-only diagnostic: K3p with one f16 product per 16 k instead of three (a single-pass
+# prefilter's MFMA cost); its decisions are not certified, only the kernel time is read
+IA_LIBIA=image-analogies-python_amd/libia_probe32.so timeout -k 10 300 python -u bench.py --no-cpu-baseline --steps 1 --warmup 1 > gpurun_out/bench_probe32.json 2> gpurun_out/bench_probe32.err || echo "probe32 failed (diagnostic only)"
+for f in cfg3 cfg3_v11 cfg3_row1 cfg3_row1_v11 cfg4 cfg5 shard2 shard4 shard8 probe32; do echo "$f $(cut -c1-200 gpurun_out/bench_$f.json)"; done
 echo ALL-OK
