@@ -1096,13 +1096,13 @@ __device__ __forceinline__ double wave_sum_d_x(double v) {  // fixed butterfly o
 //                           shifted source pixels, all final at this wavefront step), the
 //                           Morton key of the projection (sort order of the query tiles)
 // ------------------------------------------------------------------------------------------
-template <int KS>
+template <int KS, bool IMG>
 __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc sd, Imgs B, JobSet jobs,
                                                           const double *__restrict__ mu_part,
                                                           double *__restrict__ q64, double *__restrict__ qn2,
                                                           _Float16 *__restrict__ qf, const double *__restrict__ db64,
                                                           const double *__restrict__ basis, double ufac,
-                                                          float4 *__restrict__ qinfo, Imgs A, int img_rows) {
+                                                          float4 *__restrict__ qinfo, Imgs A) {
   constexpr int D = 55, KD = 16 * KS;
   static_assert(KD <= IA_WAVE, "one feature per lane");
   __shared__ double qsh[IA_WG / IA_WAVE][Geo<1>::DS];
@@ -1156,7 +1156,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
   for (int i = 0; i < IA_NPC; i++) p[i] = wave_sum_d_x(p[i]);
   __builtin_amdgcn_wave_barrier();  // qsh written by this wave's lanes, read below
   double u = DBL_MAX;
-  if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh[wv], img_rows ? &A : nullptr);
+  if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh[wv], IMG ? &A : nullptr);
   u = wave_min_d_x(u);
   if (lane == 0) {
     qn2[m] = ss;
@@ -1178,7 +1178,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
 // the weighted one (kappa rule) and its row's A' value (the B' write) from the same round.
 // Candidates beyond the 49 rerank lanes (rare) are evaluated by the lanes that listed them.
 // Wave reductions use DPP / permlane exchanges (no LDS round trips).
-template <int CH>
+template <int CH, bool IMG>
 __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &a,
                                             int m, const JobPtrs &jp, const QPix &px,
                                             double *qs, double *ws, int *cand_row, float *cand_v) {
@@ -1283,7 +1283,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     const double *src = A.p3 + img * A.img_stride_f + (int64_t)((unsigned)my_row - img * hw) * CH;
 #pragma unroll
     for (int k = 0; k < CH; k++) av[k] = src[k];
-    row_dists<CH>(a.db64, my_row, qs, ws, unw, wsq, a.img_rows ? &A : nullptr);
+    row_dists<CH>(a.db64, my_row, qs, ws, unw, wsq, IMG ? &A : nullptr);
   }
   // bound audit: the exact distance of every reranked candidate must lie within eps of its
   // MFMA value + |q'|^2 (a violation would void the certification; counted, never expected)
@@ -1304,7 +1304,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     const int row = lowest_cand<RPL>(cmask, i1, i2, v1, v2, v);
     cmask &= cmask - 1;
     double u, wq;
-    row_dists<CH>(a.db64, row, qs, ws, u, wq, a.img_rows ? &A : nullptr);
+    row_dists<CH>(a.db64, row, qs, ws, u, wq, IMG ? &A : nullptr);
     if (u < nd || (u == nd && row < ni)) {
       nd = u;
       ni = row;
@@ -1365,7 +1365,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
             if (j >= 0) {
               const int64_t i = a.pos2row[(wgid + (int64_t)a.nwg * (tb + j)) * IA_TILE + (lane & 31)];
               if (i < a.NA) {
-                const double d = exact_dist_level<CH>(a.db64, i, qs, a.img_rows ? &A : nullptr);
+                const double d = exact_dist_level<CH>(a.db64, i, qs, IMG ? &A : nullptr);
                 if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
               }
             }
@@ -1377,7 +1377,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
         for (int64_t p = p0 + lane; p < p1; p += IA_WAVE) {
           const int64_t i = ia_pos_row_t(p, a.NT, a.pos2row);
           if (i >= a.NA) continue;
-          const double d = exact_dist_level<CH>(a.db64, i, qs, a.img_rows ? &A : nullptr);
+          const double d = exact_dist_level<CH>(a.db64, i, qs, IMG ? &A : nullptr);
           if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
         }
       }
@@ -1407,7 +1407,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     const double wsq_coh = __shfl(wsq, kk, 64);
     if (recompute_app) {
       double u, wq = 0.;
-      if (lane == 0) row_dists<CH>(a.db64, bi, qs, ws, u, wq, a.img_rows ? &A : nullptr);
+      if (lane == 0) row_dists<CH>(a.db64, bi, qs, ws, u, wq, IMG ? &A : nullptr);
       wsq_app = __shfl(wq, 0, 64);
     }
     // compute_distance = norm(x)**2 = sqrt(sum x^2)**2 ; kappa rule image_analogies.py:206
@@ -1468,7 +1468,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
 #endif
 }
 
-template <int CH, bool FUSED>
+template <int CH, bool FUSED, bool IMG = false>
 __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, Winner *__restrict__ win,
                                                         JobSet jobs) {
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
@@ -1481,7 +1481,7 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
     __shared__ int crsh[IA_WG / IA_WAVE][IA_WAVE];
     __shared__ float cvsh[IA_WG / IA_WAVE][IA_WAVE];
     const int wv = threadIdx.x >> 6;
-    merge_fused<CH>(g, sd, A, ma, m, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv]);
+    merge_fused<CH, IMG>(g, sd, A, ma, m, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv]);
     return;
   }
 #endif
@@ -1491,7 +1491,7 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
 #else
   unsigned stat = 0;
   const Winner wn = certified_winner(ma, m, [&](int64_t row) {
-    return exact_dist_level<CH>(ma.db64, row, q, ma.img_rows ? &A : nullptr);
+    return exact_dist_level<CH>(ma.db64, row, q, IMG ? &A : nullptr);
   }, &stat);
 #endif
 #if IA_PROBE & 2  // diagnostic build only: no coherence / kappa
@@ -1785,6 +1785,15 @@ template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
                            const JobSet &jobs, bool fused, hipStream_t st) {
   dim3 grid(cdiv(sd.J * sd.M, IA_WG / IA_WAVE));
+  if constexpr (CH == 1) {  // row_source = 1 (exact rows from the images): 1 channel only
+    if (ma.img_rows) {
+      if (fused)
+        hipLaunchKernelGGL((k_merge_level<CH, true, true>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
+      else
+        hipLaunchKernelGGL((k_merge_level<CH, false, true>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
+      return;
+    }
+  }
   if (fused)
     hipLaunchKernelGGL((k_merge_level<CH, true>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
   else
@@ -1920,8 +1929,12 @@ void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
 void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
                         float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st) {
-  hipLaunchKernelGGL(k_gather_query_p<4>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs, mu, q64,
-                     qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A, img_rows);
+  if (img_rows)
+    hipLaunchKernelGGL((k_gather_query_p<4, true>), dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs,
+                       mu, q64, qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A);
+  else
+    hipLaunchKernelGGL((k_gather_query_p<4, false>), dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs,
+                       mu, q64, qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A);
 }
 
 // split-f16 distance kernels live in ia_k3h.hip, compiled once per (KS, QT) instance
