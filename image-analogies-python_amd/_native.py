@@ -69,6 +69,10 @@ EXPORTS = {
                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                           ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                                           ctypes.c_void_p]),
+    'ia_gaussian_pyramid': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    'ia_color_matrix': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
+                                       ctypes.c_void_p, ctypes.c_int]),
     'ia_k3_microbench': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
                                         ctypes.POINTER(ctypes.c_double)]),
     'ia_merge_winners': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
@@ -174,6 +178,38 @@ class Context(object):
 
     def set_option(self, name, value):
         check(lib().ia_set_option(self._h, name.encode(), int(value)), 'ia_set_option')
+
+    def gaussian_pyramid(self, img, n_reduce, weights7):
+        """ia_gaussian_pyramid on a host array: the n_reduce successive pyramid_reduce levels of
+        img (finest first), as a list of arrays."""
+        img = _c64(img)
+        h, w = img.shape[:2]
+        ch = 1 if img.ndim == 2 else img.shape[2]
+        shapes, hh, ww = [], h, w
+        for _ in range(n_reduce):
+            hh, ww = (hh + 1) // 2, (ww + 1) // 2
+            shapes.append((hh, ww) + img.shape[2:])
+        out = np.empty(sum(int(np.prod(x)) for x in shapes) or 1, dtype=np.float64)
+        w7 = _c64(weights7)
+        check(lib().ia_gaussian_pyramid(self._h, _ptr(img), h, w, ch, n_reduce, _ptr(w7), _ptr(out), IA_MEM_HOST),
+              'ia_gaussian_pyramid')
+        res, off = [], 0
+        for shp in shapes:
+            n = int(np.prod(shp))
+            res.append(out[off:off + n].reshape(shp))
+            off += n
+        return res
+
+    def color_matrix(self, img, M):
+        """ia_color_matrix: np.einsum('ij,klj->kli', M, img) for an (h, w, 3) host array."""
+        img = _c64(img)
+        if img.ndim != 3 or img.shape[2] != 3:
+            raise IAError('color_matrix: (h, w, 3) image expected')
+        out = np.empty_like(img)
+        M = _c64(M)
+        check(lib().ia_color_matrix(self._h, _ptr(img), img.shape[0] * img.shape[1], _ptr(M), _ptr(out), IA_MEM_HOST),
+              'ia_color_matrix')
+        return out
 
     def k3_microbench(self, n_rows, M, reps=20):
         """Mean device microseconds of one split-f16 distance-scan launch (random operands)."""

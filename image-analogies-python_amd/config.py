@@ -34,6 +34,7 @@ n_levels = None      # pyramid depth override (BASELINE cfg2: 5 levels); None = 
 level_align = 'coarse'  # 'coarse' = reference (image_analogies.py:82-86), 'fine' = B level k+1 <-> A level k
 seed = None          # np.random seed for initialize_Bp (reference: unseeded global RNG)
 device = None        # HIP device ordinal (None: LOCAL_RANK or 0)
+gpu_preprocess = True  # Gaussian pyramids + YIQ matrices on the GPU (bit-identical to the host code)
 
 
 def setup_vars(img):

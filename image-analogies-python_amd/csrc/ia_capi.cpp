@@ -92,6 +92,7 @@ struct ia_ctx {
   // certified pruned scan (option "prune"): per-level basis, sorted DB table, tile boxes
   DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs, ord;
   DevBuf qs_order, qs_info, qs_frag, qs_tbox;  // presorted queries of a step (k3p_variant 11, K2s)
+  DevBuf py_in, py_tmp, py_sm, py_mm, py_out;  // GPU preprocessing (ia_gaussian_pyramid, ia_color_matrix)
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
   int64_t prune_min_rows = IA_PRUNE_MIN_ROWS;  // option "prune_min_rows": smallest DB that prunes
   int prune = 1;
@@ -256,7 +257,8 @@ void ia_destroy(ia_ctx *c) {
   for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->jobs, &c->db, &c->db64,
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
-                    &c->boxes, &c->qinfo, &c->pairs, &c->ord, &c->qs_order, &c->qs_info, &c->qs_frag, &c->qs_tbox})
+                    &c->boxes, &c->qinfo, &c->pairs, &c->ord, &c->qs_order, &c->qs_info, &c->qs_frag, &c->qs_tbox,
+                    &c->py_in, &c->py_tmp, &c->py_sm, &c->py_mm, &c->py_out})
     b->release();
   for (hipEvent_t e : c->evs) hipEventDestroy(e);
   hipEventDestroy(c->lv0);
@@ -878,6 +880,76 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       }
     }
   }
+  return IA_OK;
+}
+
+// ------------------------------------------------------------------------------------------
+// GPU preprocessing: Gaussian pyramid reductions and 3x3 colour matrices
+// ------------------------------------------------------------------------------------------
+int ia_gaussian_pyramid(ia_ctx *c, const double *img, int h, int w, int ch, int n_reduce, const double *weights7,
+                        double *out, int mem) {
+  if (!c || !img || !weights7 || (n_reduce > 0 && !out) || h < 1 || w < 1 || ch < 1 || ch > 4 || n_reduce < 0)
+    return fail(IA_EINVAL, "ia_gaussian_pyramid: bad arguments");
+  if (mem != IA_MEM_HOST && mem != IA_MEM_DEVICE) return fail(IA_EINVAL, "ia_gaussian_pyramid: bad mem kind");
+  if (n_reduce == 0) return IA_OK;
+  HIP_TRY(hipSetDevice(c->dev));
+  const size_t n0 = (size_t)h * w * ch;
+  size_t tot = 0;  // doubles of all reduced levels
+  {
+    int hh = h, ww = w;
+    for (int k = 0; k < n_reduce; k++) {
+      hh = (hh + 1) / 2;
+      ww = (ww + 1) / 2;
+      tot += (size_t)hh * ww * ch;
+    }
+  }
+  int rc;
+  if ((rc = c->py_in.ensure(n0 * 8)) || (rc = c->py_tmp.ensure(n0 * 8)) || (rc = c->py_sm.ensure(n0 * 8)) ||
+      (rc = c->py_mm.ensure(2 * 256 * 8)) || (rc = c->py_out.ensure(std::max<size_t>(tot, 1) * 8)))
+    return rc;
+  const double *din = img;
+  if (mem == IA_MEM_HOST) {
+    HIP_TRY(hipMemcpyAsync(c->py_in.p, img, n0 * 8, hipMemcpyHostToDevice, c->st));
+    din = c->py_in.as<double>();
+  }
+  double *dout = mem == IA_MEM_DEVICE ? out : c->py_out.as<double>();
+  int hh = h, ww = w;
+  const double *src = din;
+  double *dst = dout;
+  for (int k = 0; k < n_reduce; k++) {
+    ia_launch_pyramid_reduce(src, dst, c->py_tmp.as<double>(), c->py_sm.as<double>(), c->py_mm.as<double>(), hh, ww, ch,
+                             weights7, c->st);
+    src = dst;
+    hh = (hh + 1) / 2;
+    ww = (ww + 1) / 2;
+    dst += (size_t)hh * ww * ch;
+  }
+  HIP_TRY(hipGetLastError());
+  if (mem == IA_MEM_HOST) HIP_TRY(hipMemcpyAsync(out, dout, tot * 8, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(hipStreamSynchronize(c->st));
+  return IA_OK;
+}
+
+int ia_color_matrix(ia_ctx *c, const double *in, int64_t npx, const double *M9, double *out, int mem) {
+  if (!c || !in || !M9 || !out || npx < 0) return fail(IA_EINVAL, "ia_color_matrix: bad arguments");
+  if (mem != IA_MEM_HOST && mem != IA_MEM_DEVICE) return fail(IA_EINVAL, "ia_color_matrix: bad mem kind");
+  if (npx == 0) return IA_OK;
+  HIP_TRY(hipSetDevice(c->dev));
+  int rc;
+  if ((rc = c->py_mm.ensure(2 * 256 * 8))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->py_mm.p, M9, 9 * 8, hipMemcpyHostToDevice, c->st));
+  const double *din = in;
+  double *dout = out;
+  if (mem == IA_MEM_HOST) {
+    if ((rc = c->py_in.ensure((size_t)npx * 24)) || (rc = c->py_out.ensure((size_t)npx * 24))) return rc;
+    HIP_TRY(hipMemcpyAsync(c->py_in.p, in, (size_t)npx * 24, hipMemcpyHostToDevice, c->st));
+    din = c->py_in.as<double>();
+    dout = c->py_out.as<double>();
+  }
+  ia_launch_color3(din, dout, npx, c->py_mm.as<double>(), c->st);
+  HIP_TRY(hipGetLastError());
+  if (mem == IA_MEM_HOST) HIP_TRY(hipMemcpyAsync(out, dout, (size_t)npx * 24, hipMemcpyDeviceToHost, c->st));
+  HIP_TRY(hipStreamSynchronize(c->st));
   return IA_OK;
 }
 

@@ -2,8 +2,10 @@
 img_setup(A_fname, Ap_fname_list, B_fname, out_path, c) and
 image_analogies_main(A_fname, Ap_fname_list, B_fname, out_path, c, debug=False).
 
-Setup (image reading, scaling, YIQ, remap, compression, pyramids, B' initialisation) is host
-numpy as in the reference.  The per-level loop (image_analogies.py:130-239) is one
+Setup (image reading, scaling, YIQ, remap, compression, pyramids, B' initialisation) follows
+the reference; the Gaussian pyramids and the YIQ matrices run on the GPU (ia_gaussian_pyramid,
+ia_color_matrix: bit-identical to the host restatement) unless config.gpu_preprocess is False.
+The per-level loop (image_analogies.py:130-239) is one
 ia_synthesize_level call per level on the GPU: create_index's DB for the level, the skewed
 wavefront over B', exact NN, coherence, the kappa rule and the B'/s/im writeback.  There is no
 CPU path.
@@ -49,28 +51,29 @@ def img_setup(A_fname, Ap_fname_list, B_fname, out_path, c):
     scale = lambda x: 255. if np.max(x) > 1.0 else 1.0
     sA, sB, sAp = scale(A_orig), scale(B_orig), scale(Ap_orig_list[-1][0])
 
+    gpu = default_context() if getattr(c, 'gpu_preprocess', True) else None
     if c.convert:
-        A = convert_to_YIQ(A_orig / sA)[:, :, 0]
-        B_yiq = convert_to_YIQ(B_orig / sB)
+        A = convert_to_YIQ(A_orig / sA, gpu)[:, :, 0]
+        B_yiq = convert_to_YIQ(B_orig / sB, gpu)
         B = B_yiq[:, :, 0]
-        Ap_list = [convert_to_YIQ(x / sAp)[:, :, 0] for x in Ap_orig_list]
+        Ap_list = [convert_to_YIQ(x / sAp, gpu)[:, :, 0] for x in Ap_orig_list]
     else:
         A, B = A_orig / sA, B_orig / sB
         Ap_list = [x / sAp for x in Ap_orig_list]
     if c.remap_lum:
         A, Ap_list = remap_luminance(A, Ap_list, B)
     if not c.init_rand:
-        B_orig_pyr = compute_gaussian_pyramid(B, c.n_sm, c.n_levels)
+        B_orig_pyr = compute_gaussian_pyramid(B, c.n_sm, c.n_levels, gpu)
     A, B = compress_values(A, B, c.AB_weight)
     c.num_ch, c.padding_sm, c.padding_lg, c.weights = setup_vars(A)
 
-    A_pyr = compute_gaussian_pyramid(A, c.n_sm, c.n_levels)
-    B_pyr = compute_gaussian_pyramid(B, c.n_sm, c.n_levels)
-    Ap_pyr_list = [compute_gaussian_pyramid(x, c.n_sm, c.n_levels) for x in Ap_list]
+    A_pyr = compute_gaussian_pyramid(A, c.n_sm, c.n_levels, gpu)
+    B_pyr = compute_gaussian_pyramid(B, c.n_sm, c.n_levels, gpu)
+    Ap_pyr_list = [compute_gaussian_pyramid(x, c.n_sm, c.n_levels, gpu) for x in Ap_list]
     if c.convert:
-        color_pyr_list = [compute_gaussian_pyramid(B_yiq, c.n_sm, c.n_levels)]
+        color_pyr_list = [compute_gaussian_pyramid(B_yiq, c.n_sm, c.n_levels, gpu)]
     else:
-        color_pyr_list = [compute_gaussian_pyramid(x, c.n_sm, c.n_levels) for x in Ap_list]
+        color_pyr_list = [compute_gaussian_pyramid(x, c.n_sm, c.n_levels, gpu) for x in Ap_list]
 
     if len(A_pyr) != len(B_pyr):
         c.max_levels = min(len(A_pyr), len(B_pyr))
@@ -130,7 +133,8 @@ def synthesize_pyramid(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, c, ctx=None, stats=Non
 def level_colour(level, Bp_pyr, S, IM, color_pyr_list, c):
     """Colour output of a level (image_analogies.py:216-217, 255-258)."""
     if c.convert:
-        return np.clip(convert_to_RGB(np.dstack([Bp_pyr[level], color_pyr_list[0][level][:, :, 1:]])), 0, 1)
+        gpu = default_context() if getattr(c, 'gpu_preprocess', True) else None
+        return np.clip(convert_to_RGB(np.dstack([Bp_pyr[level], color_pyr_list[0][level][:, :, 1:]]), gpu), 0, 1)
     h, w = Bp_pyr[level].shape[:2]
     src = np.stack([p[level] for p in color_pyr_list])[IM[level], S[level][:, 0], S[level][:, 1]]
     out = np.empty((h * w, 3))

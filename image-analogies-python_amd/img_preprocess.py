@@ -15,15 +15,20 @@ _YIQ2RGB = np.array([[1., 0.956, 0.621],
                      [1., -1.105, 1.702]])
 
 
-def convert_to_YIQ(img):
-    """img_preprocess.py:6-13 (input must already be on the 0..1 scale)."""
+def convert_to_YIQ(img, ctx=None):
+    """img_preprocess.py:6-13 (input must already be on the 0..1 scale).  ctx: a libia Context
+    to run the matrix on the GPU (ia_color_matrix, bit-identical to numpy's einsum)."""
     if not 0 <= np.max(img) <= 1:
         raise ValueError('convert_to_YIQ expects an image scaled to [0, 1]')
+    if ctx is not None:
+        return ctx.color_matrix(img, _RGB2YIQ)
     return np.einsum('ij,klj->kli', _RGB2YIQ, img)
 
 
-def convert_to_RGB(img):
-    """img_preprocess.py:16-22."""
+def convert_to_RGB(img, ctx=None):
+    """img_preprocess.py:16-22 (ctx: on the GPU, as convert_to_YIQ)."""
+    if ctx is not None:
+        return ctx.color_matrix(img, _YIQ2RGB)
     return np.einsum('ij,klj->kli', _YIQ2RGB, img)
 
 
@@ -73,10 +78,22 @@ def _pyramid_reduce(img):
     return _bilinear_downsize(smooth, -(-img.shape[0] // 2), -(-img.shape[1] // 2))
 
 
-def compute_gaussian_pyramid(img, min_size, n_levels=None):
+def gaussian_weights():
+    """scipy.ndimage.gaussian_filter's 7-tap kernel for sigma = 2/3, truncate 4 (its
+    _gaussian_kernel1d restated: exp(-0.5 / sigma^2 x^2) normalised by its sum)."""
+    sigma = 2 * 2 / 6.0
+    radius = int(4.0 * sigma + 0.5)
+    x = np.arange(-radius, radius + 1)
+    phi = np.exp(-0.5 / (sigma * sigma) * x ** 2)
+    return phi / phi.sum()
+
+
+def compute_gaussian_pyramid(img, min_size, n_levels=None, ctx=None):
     """Coarsest-first Gaussian pyramid (img_preprocess.py:47-63).  The number of reductions is
     the number of halvings until min(h, w) <= min_size; (h, w, 3) images are reduced per channel
-    (SURVEY §7 hard part 6).  n_levels (extension) caps the pyramid at that many images."""
+    (SURVEY §7 hard part 6).  n_levels (extension) caps the pyramid at that many images.
+    ctx: a libia Context to run the reductions on the GPU (ia_gaussian_pyramid: the same
+    arithmetic, operation for operation, so the levels are bit-identical)."""
     img = np.asarray(img, dtype=np.float64)
     side = min(img.shape[:2])
     reductions = 0
@@ -86,6 +103,16 @@ def compute_gaussian_pyramid(img, min_size, n_levels=None):
     if n_levels is not None:
         reductions = min(reductions, int(n_levels) - 1)
     pyr = [img]
+    if ctx is not None:
+        # a reduction that leaves the shape unchanged (1-pixel sides) ends the host loop below;
+        # ceil-halving changes the shape unless both sides are 1
+        n = 0
+        h, w = img.shape[:2]
+        while n < reductions and (h, w) != (1, 1):
+            h, w = (h + 1) // 2, (w + 1) // 2
+            n += 1
+        pyr += ctx.gaussian_pyramid(img, n, gaussian_weights())
+        reductions = 0
     for _ in range(reductions):
         nxt = _pyramid_reduce(pyr[-1])
         if nxt.shape == pyr[-1].shape:

@@ -175,6 +175,20 @@ int ia_coherence_batch(ia_index *index, const double *q, int64_t nq, const int32
                        const int32_t *s, const int32_t *im, int64_t n_s, int a_h, int a_w,
                        int bp_w, int pad, int32_t *p_out, int32_t *img_out, int32_t *rstar_out);
 
+/* ---- GPU preprocessing (img_setup, image_analogies.py:17-94) -------------------- */
+/* n_reduce steps of skimage 0.18.3 pyramid_reduce (img_preprocess.py:47-63): scipy.ndimage
+ * gaussian_filter (sigma 2/3, mode 'reflect', 7 taps: weights7 = scipy's kernel, symmetric;
+ * axes 0 and 1, a colour axis unsmoothed) + order-1 resize to ceil(h/2) x ceil(w/2) clipped to
+ * the smoothed image's range.  img (h, w, ch) fp64; out = the n_reduce reduced levels, finest
+ * first, concatenated.  Bit-identical to ia_amd.img_preprocess.compute_gaussian_pyramid. */
+int ia_gaussian_pyramid(ia_ctx *ctx, const double *img, int h, int w, int ch, int n_reduce,
+                        const double *weights7, double *out, int mem);
+/* out[p, i] = sum_j M9[3 i + j] in[p, j] for npx pixels of 3 channels, in numpy's
+ * einsum('ij,klj->kli') order (m0 x0 + m2 x2) + m1 x1 (convert_to_YIQ / convert_to_RGB,
+ * img_preprocess.py:6-22). */
+int ia_color_matrix(ia_ctx *ctx, const double *in, int64_t npx, const double *M9, double *out,
+                    int mem);
+
 /* ---- kernel tuning ------------------------------------------------------------------------- */
 /* Time the split-f16 distance scan (K3h, current "k3_variant") alone: n_rows random DB rows
  * (1 channel), M <= 352 random queries, `reps` back-to-back launches on the context's stream;
