@@ -630,7 +630,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   const size_t tile_bytes = use_h ? (size_t)ia_k3h_tile_bytes(g.KS) : (size_t)IA_TILE * DP * 4;  // one stored DB tile
 
   // per-level scratch
-  if ((rc = c->db.ensure((size_t)std::max(ns, 1) * IA_TILE * db_row_bytes)) || (rc = c->mu.ensure(4 * g.ch * 8)) ||
+  if ((rc = c->db.ensure((size_t)std::max(ns, 1) * IA_TILE * db_row_bytes)) || (rc = c->mu.ensure((16 + 4 * 3 * 128) * 8)) ||
       (rc = c->db64.ensure((size_t)g.NA * ia_db64_stride(g.ch) * 8)) ||
       (rc = c->Rbits.ensure(4)) || (rc = c->q64.ensure((size_t)Mpad_max * g.D * 8)) ||
       (rc = c->qn2.ensure((size_t)Mpad_max * 8)) || (rc = c->qf.ensure((size_t)Mpad_max * db_row_bytes)) ||

@@ -323,14 +323,19 @@ __device__ __forceinline__ void wave_min_di(double &d, int64_t &idx) {
 // ------------------------------------------------------------------------------------------
 // K0: per-(part, channel) means of the A-side images (deterministic tree reduction)
 // ------------------------------------------------------------------------------------------
+// grid (IA_MEAN_CHUNKS, 4 CH): workgroup (b, part*CH + ch) sums chunk b of that image's pixels
+// (fixed-order strided loop + tree), then k_part_means_fold adds the chunks in order: the same
+// value on every run (a deterministic centring; any fixed mu keeps the results exact)
+#define IA_MEAN_CHUNKS 128
 template <int CH>
-__global__ void __launch_bounds__(IA_WG) k_part_means(Imgs A, int n_ap, double *mu_part) {
-  const int part = blockIdx.x / CH, ch = blockIdx.x % CH;
+__global__ void __launch_bounds__(IA_WG) k_part_means(Imgs A, int n_ap, double *part_sums) {
+  const int pc = blockIdx.y, part = pc / CH, ch = pc % CH, b = blockIdx.x;
   const double *base = part == 0 ? A.p0 : part == 1 ? A.p1 : part == 2 ? A.p2 : A.p3;
   int64_t npx = (part & 1) ? (int64_t)A.h * A.w : (int64_t)A.hc * A.wc;
   if (part >= 2) npx *= n_ap;  // A' images are contiguous
+  const int64_t i0 = npx * b / IA_MEAN_CHUNKS, i1 = npx * (b + 1) / IA_MEAN_CHUNKS;
   double s = 0.;
-  for (int64_t i = threadIdx.x; i < npx; i += IA_WG) s += base[i * CH + ch];
+  for (int64_t i = i0 + threadIdx.x; i < i1; i += IA_WG) s += base[i * CH + ch];
   __shared__ double red[IA_WG];
   red[threadIdx.x] = s;
   __syncthreads();
@@ -338,7 +343,18 @@ __global__ void __launch_bounds__(IA_WG) k_part_means(Imgs A, int n_ap, double *
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
-  if (threadIdx.x == 0) mu_part[blockIdx.x] = red[0] / (double)npx;
+  if (threadIdx.x == 0) part_sums[pc * IA_MEAN_CHUNKS + b] = red[0];
+}
+template <int CH>
+__global__ void __launch_bounds__(IA_WG) k_part_means_fold(Imgs A, int n_ap, const double *part_sums, double *mu_part) {
+  const int pc = threadIdx.x;
+  if (pc >= 4 * CH) return;
+  const int part = pc / CH;
+  int64_t npx = (part & 1) ? (int64_t)A.h * A.w : (int64_t)A.hc * A.wc;
+  if (part >= 2) npx *= n_ap;
+  double s = 0.;
+  for (int b = 0; b < IA_MEAN_CHUNKS; b++) s += part_sums[pc * IA_MEAN_CHUNKS + b];
+  mu_part[pc] = s / (double)npx;
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1722,7 +1738,10 @@ static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1
 
 template <int CH>
 static void launch_means_t(const Imgs &A, int n_ap, double *mu, hipStream_t st) {
-  hipLaunchKernelGGL(k_part_means<CH>, dim3(4 * CH), dim3(IA_WG), 0, st, A, n_ap, mu);
+  // partial sums live behind the 4 CH means in the same buffer (ia_capi.cpp sizes it)
+  double *parts = mu + 16;
+  hipLaunchKernelGGL(k_part_means<CH>, dim3(IA_MEAN_CHUNKS, 4 * CH), dim3(IA_WG), 0, st, A, n_ap, parts);
+  hipLaunchKernelGGL(k_part_means_fold<CH>, dim3(1), dim3(IA_WG), 0, st, A, n_ap, (const double *)parts, mu);
 }
 void ia_launch_means(int ch, const Imgs &A, int n_ap, double *mu, hipStream_t st) {
   if (ch == 1) launch_means_t<1>(A, n_ap, mu, st);
