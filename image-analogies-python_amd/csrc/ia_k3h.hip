@@ -299,6 +299,19 @@ __device__ __forceinline__ void k3p_pipe(const h16x8 (&a)[2 * KS], const h16x8 *
   }
 }
 
+// one accumulator at a time (k3h_prune3 with NBUF = 1: 4 waves per SIMD interleave the chains)
+template <int KS, int QT, int Q>
+__device__ __forceinline__ void k3p_singles(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, int t, float (&b1)[QT],
+                                            float (&b2)[QT], int (&i1)[QT]) {
+  if constexpr (Q < QT) {
+    if ((msk >> Q) & 1u) {
+      const f32x16 c = k3p_chain<KS>(a, lq + Q * 2 * KS * IA_WAVE);
+      k3p_epi1(c, t, b1[Q], b2[Q], i1[Q]);
+    }
+    k3p_singles<KS, QT, Q + 1>(a, lq, msk, t, b1, b2, i1);
+  }
+}
+
 template <int KS, int QT, int QP>
 __device__ __forceinline__ void k3p_pairs(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, int t, float (&b1)[QT],
                                           float (&b2)[QT], int (&i1)[QT]) {
@@ -731,7 +744,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
 
   // ---- 1. one global round
   h16x8 a[NP], an[NP], an2[NP];
-  {
+  if constexpr (!(INTER && NBUF == 1)) {
     ld_tile<KS>(a, db, tk(min(wave, K - 1)), lane);
   }
   if constexpr (PRE) {
@@ -949,11 +962,16 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     // while tile k is contracted, the next needed tile's load is in flight and the need tests
     // after it run on the VALU (two buffers in rotation)
     const bool cl = lane < QT;
-    const float4 ctl = cl ? tlo[lane] : make_float4(0.f, 0.f, 0.f, 0.f), cth = cl ? thi[lane] : ctl;
-    const float ctu = cl ? tU[lane] : -INFINITY;
+    // NBUF = 1 (128 VGPRs): the query-tile boxes are re-read from LDS per test, not held
+    const float4 ctl = cl && NBUF != 1 ? tlo[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 cth = cl && NBUF != 1 ? thi[lane] : ctl;
+    const float ctu = cl && NBUF != 1 ? tU[lane] : -INFINITY;
     auto need_k = [&](int k) -> unsigned {
       const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
-      const unsigned coarse = (unsigned)__ballot(cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
+      const bool cpass = NBUF == 1 ? (cl && prune_lb(blo, bhi, tlo[lane < QT ? lane : 0], thi[lane < QT ? lane : 0]) <=
+                                                tU[lane < QT ? lane : 0])
+                                   : (cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
+      const unsigned coarse = (unsigned)__ballot(cpass);
       unsigned msk = 0;
 #pragma unroll
       for (int pr = 0; pr < NPAIR; pr++) {
@@ -984,6 +1002,22 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     };
     unsigned m;
     int k = next_k(wave, m);
+    if constexpr (NBUF == 1) {
+      // one tile buffer (NW = 16: 4 waves per SIMD within 128 VGPRs): the tile's load is in
+      // flight while the need tests of the next tile run; the other waves of the SIMD cover
+      // the rest of the latency
+      while (k < K) {
+        ld_tile<KS>(a, db, tk(k), lane);
+        unsigned mn;
+        const int kn = next_k(DYN ? grab() : k + NW, mn);
+        asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
+        k3p_singles<KS, QT, 0>(a, ldsh + lane, m, tk(k), b1, b2, i1);
+        cnt += __popc(m);
+        ntl++;
+        k = kn;
+        m = mn;
+      }
+    } else {
     // (re)load the first needed tile unconditionally (usually the speculative one again: a
     // cache hit), so the loop is entered with the same outstanding loads on every path
     ld_tile<KS>(a, db, tk(k < K ? k : min(wave, K - 1)), lane);
@@ -1011,6 +1045,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       if (k >= K) break;
       step(an, a);
     }
+    }  // NBUF != 1
   } else {
   // ---- 3. need masks of the workgroup's tiles
   {
@@ -1107,6 +1142,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   }
 
   // ---- 5. merge the 2*NW subsets of each query; records go to the original query slots
+  // (PRE: the slice order is read before the reduction area, which may extend past the
+  // fragments for NW = 16, overwrites it)
+  const int mq_pre = PRE && tid < NQ ? (int)skey[tid] : 0;
   __syncthreads();
   if (lane == 0) {
     wpairs[wave] = cnt;
@@ -1130,7 +1168,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     Top2 m = red[x];
 #pragma unroll
     for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
-    const int mq = PRE ? (int)skey[x] : order[s0 + x];
+    const int mq = PRE ? (WGT >= NQ ? mq_pre : (int)skey[x]) : order[s0 + x];
     if (mq < M) {
       const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
       const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
@@ -1199,6 +1237,7 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 #endif
     if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
     if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true>;
+    if (variant == 12) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, 16, 1, true, true, false, false, true>;
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

@@ -2002,22 +2002,24 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
   const int kmax = (NT + nwg - 1) / nwg;  // DB tiles per workgroup
-  const int rev = (variant == 7 || variant == 8 || variant == 10 || variant == 11) ? (step & 1) : 0;  // alternate steps walk in reverse
+  const int rev = (variant == 7 || variant == 8 || variant == 10 || variant >= 11) ? (step & 1) : 0;  // alternate steps walk in reverse
   if (variant == 7) variant = 6;  // 8: + the previous step's query order (no sort)
   if (variant == 10) variant = 9;  // 9: 6 + pipelined single chains; 10: 9 + reverse walks
-  if (variant != 11 && variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // v3/v4 limits (ia_k3h.hip IA_K3P3_*)
-  if (variant == 11 && kmax > 512) variant = 1;  // (never with presorted queries: the caller only uses 11 below)
+  if (variant < 11 && variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // v3/v4 limits (ia_k3h.hip IA_K3P3_*)
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t NQ = (size_t)qt * IA_TILE;
-  const size_t lds = variant == 11 ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 +
-                                         NQ * 4 + (size_t)kmax * 40
-                                   : ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
-  static int attr_lds[12][16] = {};
-  const int vi = variant < 0 || variant > 11 ? 1 : variant;
+  const int nthr = variant == 12 ? 16 * IA_WAVE : IA_WGH;  // v12: 16 waves (4 per SIMD), one tile buffer
+  size_t lds = variant >= 11 ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 +
+                                   NQ * 4 + (size_t)kmax * 40
+                             : ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
+  const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
+  lds = lds > red ? lds : red;
+  static int attr_lds[13][16] = {};
+  const int vi = variant < 0 || variant > 12 ? 1 : variant;
   if ((int)lds > attr_lds[vi][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_lds[vi][qt] = (int)lds;
   }
-  hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WGH), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row, NT,
+  hipLaunchKernelGGL(fn, dim3(nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row, NT,
                      qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox);
 }
