@@ -178,21 +178,44 @@ __global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__
                                                       float4 *__restrict__ tbox) {
   __shared__ unsigned key[4096];
   const int tid = threadIdx.x;
-  for (int i = tid; i < NS; i += QS_WG)
-    key[i] = i < Mpad ? ((__float_as_uint(qinfo[3 * i + 2].y) & 0xFFFFF000u) | (unsigned)i) : 0xFFFFFFFFu;
-  __syncthreads();
-  for (int k = 2; k <= NS; k <<= 1) {
-    for (int j = k >> 1; j > 0; j >>= 1) {
-      for (int i = tid; i < NS / 2; i += QS_WG) {
-        const int lo = 2 * i - (i & (j - 1)), hi = lo + j;
-        const unsigned a = key[lo], b = key[hi];
-        const bool up = (lo & k) == 0;
-        if ((a > b) == up) {
-          key[lo] = b;
-          key[hi] = a;
+  if (NS <= QS_WG) {
+    // one key per thread: exchanges below distance 64 are lane shuffles (no barrier), the wider
+    // ones go through LDS
+    unsigned v = tid < Mpad ? ((__float_as_uint(qinfo[3 * tid + 2].y) & 0xFFFFF000u) | (unsigned)tid) : 0xFFFFFFFFu;
+    for (int k = 2; k <= NS; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        unsigned o;
+        if (j >= 64) {
+          key[tid] = v;
+          __syncthreads();
+          o = key[tid ^ j];
+          __syncthreads();
+        } else {
+          o = (unsigned)__shfl_xor((int)v, j, 64);
         }
+        const bool keep_min = ((tid & k) == 0) == ((tid & j) == 0);
+        v = keep_min ? min(v, o) : max(v, o);
       }
-      __syncthreads();
+    }
+    key[tid] = v;
+    __syncthreads();
+  } else {
+    for (int i = tid; i < NS; i += QS_WG)
+      key[i] = i < Mpad ? ((__float_as_uint(qinfo[3 * i + 2].y) & 0xFFFFF000u) | (unsigned)i) : 0xFFFFFFFFu;
+    __syncthreads();
+    for (int k = 2; k <= NS; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < NS / 2; i += QS_WG) {
+          const int lo = 2 * i - (i & (j - 1)), hi = lo + j;
+          const unsigned a = key[lo], b = key[hi];
+          const bool up = (lo & k) == 0;
+          if ((a > b) == up) {
+            key[lo] = b;
+            key[hi] = a;
+          }
+        }
+        __syncthreads();
+      }
     }
   }
   for (int x = tid; x < Mpad; x += QS_WG) {
