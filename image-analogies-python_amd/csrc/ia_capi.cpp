@@ -277,7 +277,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   }
 #ifdef IA_K3H_DIAG  // DIAG=1 builds: every kernel version of DESIGN.md §4b's progression
   if (!std::strcmp(name, "k3p_variant")) {
-    if (value < 0 || value > 12) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..12");
+    if (value < 0 || value > 13) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..13");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -288,8 +288,8 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   }
 #else  // product build: the default kernels only (7: pruned scan, 1: packed-index K3h)
   if (!std::strcmp(name, "k3p_variant")) {  // 7: in-kernel sort up to 512 queries, presorted above; 11: always presorted
-    if (value != 7 && value != 11 && value != 12)
-      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11 or 12 (other versions are in DIAG=1 builds only)");
+    if (value != 7 && value != 11 && value != 12 && value != 13)
+      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 12 or 13 (other versions are in DIAG=1 builds only)");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -554,7 +554,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   }
   if ((rc = c->jobs.ensure(sizeof(JobPtrs) * J))) return rc;
   HIP_TRY(hipMemcpyAsync(c->jobs.p, jp.data(), sizeof(JobPtrs) * J, hipMemcpyHostToDevice, c->st));
-  const JobSet djobs{jp[0], c->jobs.as<JobPtrs>()};
+  const JobSet djobs{jp[0], c->jobs.as<JobPtrs>(), J};
 
   // matcher: split-f16 when the channel count has a K3h instance and every image value fits
   // (IA_F16_MAXABS, one 4-byte read-back per level); otherwise the fp32 MFMA scan
@@ -741,8 +741,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                        c->st);
     // pruned scan: queries sorted once per step (K2s) when the step is wider than the in-kernel
     // sort of v6/v7 (512) or variant 11 is selected
-    const int k3v = c->k3p_variant >= 11 ? c->k3p_variant : (prune && sd.Mpad > 512 ? 11 : c->k3p_variant);
-    if (prune && k3v >= 11)
+    // (variants 11, 12: presorted; 7, 13: in-kernel sort up to 512 queries, presorted v11 / v12 above)
+    const int k3v = (c->k3p_variant == 11 || c->k3p_variant == 12) ? c->k3p_variant
+                    : (prune && sd.Mpad > 512 ? (c->k3p_variant == 13 ? 12 : 11) : c->k3p_variant);
+    if (prune && (k3v == 11 || k3v == 12))
       ia_launch_query_sort(c->qinfo.as<float4>(), c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
                            c->qs_frag.p, c->qs_tbox.as<float4>(), c->st);
     if (ns > 0) {
@@ -757,7 +759,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         int qt0 = 0;
         for (int b = 0; b < nqb; b++) {
           const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
-          if (prune && k3v >= 11)
+          if (prune && (k3v == 11 || k3v == 12))
             ia_launch_k3p(qt, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t,
@@ -766,7 +768,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
             ia_launch_k3p(qt, dbp, c->qf.p, c->qinfo.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
-                          c->k3p_variant, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
+                          k3v, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
                           c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, c->st);
           else if (use_h)
             ia_launch_k3h(g.KS, qt, dbp, c->qf.p, n, x.tpw, qt0, Mt, x.nwg, m.pos0, g.n_tiles, (float4 *)m.rec,

@@ -164,12 +164,26 @@ struct JobPtrs {
   const double *weights;       // compute_distance weights
   double kf;                   // kappa factor 1 + 2^(level - L) k
 };
-// the jobs of a launch: job 0 travels in the kernel arguments (a single job - the common case -
-// costs no extra dependent load), the others in a device array
-struct JobSet {
+// the jobs of a launch.  A single job (the common case) travels in the kernel arguments
+// (JobArg1: its pointers are plain kernel-argument loads, as before batching); a batch reads
+// them from a device array with a wave-uniform index (JobArgN).  The kernels are templated on
+// the two, so neither pays for the other (a runtime select between a by-value argument and a
+// global array made the compiler spill the argument to LDS and read every pointer with flat
+// loads: +5 us per K2p launch).
+struct JobArg1 {
+  static constexpr bool single = true;  // the launcher also puts its images into the Imgs argument
   JobPtrs j0;
-  const JobPtrs *rest;  // device JobPtrs[n_jobs] (entry 0 unused by kernels)
-  __device__ __forceinline__ JobPtrs get(int job) const { return job == 0 ? j0 : rest[job]; }
+  __device__ __forceinline__ JobPtrs get(int) const { return j0; }
+};
+struct JobArgN {
+  static constexpr bool single = false;
+  const JobPtrs *rest;
+  __device__ __forceinline__ JobPtrs get(int job) const { return rest[job]; }
+};
+struct JobSet {   // host side: what the launchers dispatch on
+  JobPtrs j0;
+  const JobPtrs *rest;  // device JobPtrs[n_jobs]
+  int J;
 };
 struct QPix {
   int job, r, c, qi;           // job, pixel (r, c) and its raster index in the B level

@@ -1142,9 +1142,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   }
 
   // ---- 5. merge the 2*NW subsets of each query; records go to the original query slots
-  // (PRE: the slice order is read before the reduction area, which may extend past the
+  // (the slice's query order is read before the reduction area, which extends past the
   // fragments for NW = 16, overwrites it)
-  const int mq_pre = PRE && tid < NQ ? (int)skey[tid] : 0;
+  const int mq_pre = tid < NQ ? (PRE ? (int)skey[tid] : order[s0 + tid]) : 0;
   __syncthreads();
   if (lane == 0) {
     wpairs[wave] = cnt;
@@ -1168,7 +1168,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     Top2 m = red[x];
 #pragma unroll
     for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
-    const int mq = PRE ? (WGT >= NQ ? mq_pre : (int)skey[x]) : order[s0 + x];
+    const int mq = WGT >= NQ ? mq_pre : (PRE ? (int)skey[x] : order[s0 + x]);
     if (mq < M) {
       const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
       const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
@@ -1238,6 +1238,7 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
     if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true>;
     if (variant == 12) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, 16, 1, true, true, false, false, true>;
+    if (variant == 13) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, 16, 1, true, true>;  // 12 with the in-kernel sort
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

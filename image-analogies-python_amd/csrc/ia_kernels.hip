@@ -451,21 +451,21 @@ __device__ __forceinline__ void put_qfrag(float *qf, int m, int f, float v) {
   qf[(((int64_t)qt * G::KP + s / 4) * IA_WAVE + h * IA_TILE + j) * 4 + (s % 4)] = v;
 }
 
-template <int CH>
-__global__ void __launch_bounds__(IA_WG) k_gather_query(LevelGeo g, StepDesc sd, Imgs B, JobSet jobs,
+template <int CH, class JS>
+__global__ void __launch_bounds__(IA_WG) k_gather_query(LevelGeo g, StepDesc sd, Imgs B, JS jobs,
                                                          const double *__restrict__ mu_part,
                                                          double *__restrict__ q64, double *__restrict__ qn2,
                                                          float *__restrict__ qf) {
   using G = Geo<CH>;
   const int lane = threadIdx.x & 63;
-  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6));  // wave-uniform
   if (m >= sd.Mpad) return;
   if (m >= sd.J * sd.M) {
     for (int f = lane; f < G::DP; f += IA_WAVE) put_qfrag<CH>(qf, m, f, 0.f);
     return;
   }
   const QPix px = ia_qpix(sd, g.bw, m);
-  B = job_imgs(B, jobs.get(px.job));
+  if constexpr (!JS::single) B = job_imgs(B, jobs.get(px.job));  // single job: B already holds its images
   const int r = px.r, c = px.c;
   double ss = 0.;
   for (int f = lane; f < G::DP; f += IA_WAVE) {
@@ -732,21 +732,21 @@ __device__ __forceinline__ void put_qh(_Float16 *qf, int m, int f, double v) {
   qf[base + IA_WAVE * 8] = lo;
 }
 
-template <int CH, int KS>
-__global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc sd, Imgs B, JobSet jobs,
+template <int CH, int KS, class JS>
+__global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc sd, Imgs B, JS jobs,
                                                            const double *__restrict__ mu_part,
                                                            double *__restrict__ q64, double *__restrict__ qn2,
                                                            _Float16 *__restrict__ qf) {
   constexpr int D = 55 * CH, KD = 16 * KS;
   const int lane = threadIdx.x & 63;
-  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6));  // wave-uniform
   if (m >= sd.Mpad) return;
   if (m >= sd.J * sd.M) {
     for (int f = lane; f < KD; f += IA_WAVE) put_qh<KS>(qf, m, f, 0.);
     return;
   }
   const QPix px = ia_qpix(sd, g.bw, m);
-  B = job_imgs(B, jobs.get(px.job));
+  if constexpr (!JS::single) B = job_imgs(B, jobs.get(px.job));  // single job: B already holds its images
   const int r = px.r, c = px.c;
   double ss = 0.;
   for (int f = lane; f < KD; f += IA_WAVE) {
@@ -1112,8 +1112,8 @@ __device__ __forceinline__ double wave_sum_d_x(double v) {  // fixed butterfly o
 //                           shifted source pixels, all final at this wavefront step), the
 //                           Morton key of the projection (sort order of the query tiles)
 // ------------------------------------------------------------------------------------------
-template <int KS, bool IMG>
-__global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc sd, Imgs B, JobSet jobs,
+template <int KS, bool IMG, class JS>
+__global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc sd, Imgs B, JS jobs,
                                                           const double *__restrict__ mu_part,
                                                           double *__restrict__ q64, double *__restrict__ qn2,
                                                           _Float16 *__restrict__ qf, const double *__restrict__ db64,
@@ -1122,7 +1122,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
   constexpr int D = 55, KD = 16 * KS;
   static_assert(KD <= IA_WAVE, "one feature per lane");
   __shared__ double qsh[IA_WG / IA_WAVE][Geo<1>::DS];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m = blockIdx.x * (IA_WG / IA_WAVE) + wv;
   if (m >= sd.Mpad) return;
   if (m >= sd.J * sd.M) {
@@ -1136,7 +1136,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
   }
   const QPix px = ia_qpix(sd, g.bw, m);
   const JobPtrs jp = jobs.get(px.job);
-  B = job_imgs(B, jp);
+  if constexpr (!JS::single) B = job_imgs(B, jp);  // single job: B already holds its images
   const int32_t *__restrict__ s = jp.s, *__restrict__ im = jp.im;
   const int r = px.r, c = px.c, qi = px.qi;
   // coherence candidate of this lane (lanes 0..14, product(rows, cols) order as merge_fused)
@@ -1484,10 +1484,10 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
 #endif
 }
 
-template <int CH, bool FUSED, bool IMG = false>
+template <int CH, bool FUSED, bool IMG, class JS>
 __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, Winner *__restrict__ win,
-                                                        JobSet jobs) {
-  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+                                                        JS jobs) {
+  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6));  // wave-uniform
   if (m >= sd.J * sd.M) return;
   const QPix px = ia_qpix(sd, g.bw, m);
   const JobPtrs jp = jobs.get(px.job);
@@ -1529,12 +1529,12 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
 }
 
 // multi-rank finish: global winner over the all-gathered per-rank winners, then coherence
-template <int CH>
+template <int CH, class JS>
 __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd, Imgs A, const double *__restrict__ db64,
                                                          const double *__restrict__ q64,
                                                          const Winner *__restrict__ allwin, int world, int Mstride,
-                                                         JobSet jobs) {
-  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+                                                         JS jobs) {
+  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6));  // wave-uniform
   if (m >= sd.J * sd.M) return;
   double bd = DBL_MAX;
   int64_t bi = INT64_MAX;
@@ -1623,7 +1623,7 @@ __global__ void __launch_bounds__(IA_WG) k_dense_query(const double *__restrict_
                                                         float *__restrict__ qf) {
   constexpr int KP = KH / 4;
   const int lane = threadIdx.x & 63;
-  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6));  // wave-uniform
   if (m >= Mpad) return;
   double ss = 0.;
   for (int f = lane; f < 2 * KH; f += IA_WAVE) {
@@ -1644,7 +1644,7 @@ __global__ void __launch_bounds__(IA_WG) k_dense_query(const double *__restrict_
 
 __global__ void __launch_bounds__(IA_WG) k_merge_dense(MergeArgs ma, const double *__restrict__ pts, int d, const double *__restrict__ q,
                                                         int64_t nq, int64_t *__restrict__ idx_out, double *__restrict__ dist_out) {
-  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6));  // wave-uniform
   if (m >= nq) return;
   const double *qm = q + (int64_t)m * d;
   unsigned stat;
@@ -1674,7 +1674,7 @@ __global__ void __launch_bounds__(IA_WG) k_coherence_batch(const double *__restr
                                                             int bp_w, int pad, int32_t *__restrict__ p_out,
                                                             int32_t *__restrict__ img_out, int32_t *__restrict__ r_out,
                                                             unsigned *__restrict__ err) {
-  const int m = blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6);
+  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6));  // wave-uniform
   const int lane = threadIdx.x & 63;
   if (m >= nq) return;
   const int row = px[2 * m], col = px[2 * m + 1], wd = 2 * pad + 1;
@@ -1735,6 +1735,13 @@ __global__ void __launch_bounds__(IA_WG) k_coherence_batch(const double *__restr
 #include "ia_launch.h"
 
 static inline unsigned cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
+static inline Imgs job0_imgs(Imgs B, const JobSet &jobs) {  // a single job's images in the Imgs argument
+  B.p0 = jobs.j0.Bc;
+  B.p1 = jobs.j0.B;
+  B.p2 = jobs.j0.Bpc;
+  B.p3 = jobs.j0.Bp;
+  return B;
+}
 
 template <int CH>
 static void launch_means_t(const Imgs &A, int n_ap, double *mu, hipStream_t st) {
@@ -1763,8 +1770,12 @@ void ia_launch_db_build(const LevelGeo &g, const Imgs &A, const double *mu, floa
 template <int CH>
 static void launch_gather_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                             double *q64, double *qn2, float *qf, hipStream_t st) {
-  hipLaunchKernelGGL(k_gather_query<CH>, dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs, mu, q64,
-                     qn2, qf);
+  const dim3 grid(cdiv(sd.Mpad, IA_WG / IA_WAVE));
+  if (jobs.J == 1)
+    hipLaunchKernelGGL((k_gather_query<CH, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, job0_imgs(B, jobs), JobArg1{jobs.j0}, mu,
+                       q64, qn2, qf);
+  else
+    hipLaunchKernelGGL((k_gather_query<CH, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64, qn2, qf);
 }
 void ia_launch_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu, double *q64,
                       double *qn2, float *qf, hipStream_t st) {
@@ -1800,23 +1811,28 @@ void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tile
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WG), lds, st, db, qf, n_tiles, tpw, qt0, M, nwg, row0, NT, rec, recT);
 }
 
+template <int CH, bool FUSED, bool IMG>
+static void launch_merge_j(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
+                           const JobSet &jobs, hipStream_t st) {
+  const dim3 grid(cdiv(sd.J * sd.M, IA_WG / IA_WAVE));
+  if (jobs.J == 1)
+    hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, JobArg1{jobs.j0});
+  else
+    hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win,
+                       JobArgN{jobs.rest});
+}
 template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
                            const JobSet &jobs, bool fused, hipStream_t st) {
-  dim3 grid(cdiv(sd.J * sd.M, IA_WG / IA_WAVE));
   if constexpr (CH == 1) {  // row_source = 1 (exact rows from the images): 1 channel only
     if (ma.img_rows) {
-      if (fused)
-        hipLaunchKernelGGL((k_merge_level<CH, true, true>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
-      else
-        hipLaunchKernelGGL((k_merge_level<CH, false, true>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
+      if (fused) launch_merge_j<CH, true, true>(g, sd, A, ma, win, jobs, st);
+      else launch_merge_j<CH, false, true>(g, sd, A, ma, win, jobs, st);
       return;
     }
   }
-  if (fused)
-    hipLaunchKernelGGL((k_merge_level<CH, true>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
-  else
-    hipLaunchKernelGGL((k_merge_level<CH, false>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, jobs);
+  if (fused) launch_merge_j<CH, true, false>(g, sd, A, ma, win, jobs, st);
+  else launch_merge_j<CH, false, false>(g, sd, A, ma, win, jobs, st);
 }
 void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
                      const JobSet &jobs, bool fused, hipStream_t st) {
@@ -1828,8 +1844,13 @@ void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const
 template <int CH>
 static void launch_finish_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
                             const Winner *allwin, int world, int Mstride, const JobSet &jobs, hipStream_t st) {
-  hipLaunchKernelGGL(k_finish_level<CH>, dim3(cdiv(sd.J * sd.M, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, A, db64, q64,
-                     allwin, world, Mstride, jobs);
+  const dim3 grid(cdiv(sd.J * sd.M, IA_WG / IA_WAVE));
+  if (jobs.J == 1)
+    hipLaunchKernelGGL((k_finish_level<CH, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, A, db64, q64, allwin, world, Mstride,
+                       JobArg1{jobs.j0});
+  else
+    hipLaunchKernelGGL((k_finish_level<CH, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, A, db64, q64, allwin, world, Mstride,
+                       JobArgN{jobs.rest});
 }
 void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
                       const Winner *allwin, int world, int Mstride, const JobSet &jobs, hipStream_t st) {
@@ -1936,8 +1957,13 @@ void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *mu, vo
 template <int CH, int KS>
 static void launch_gather_h_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                               double *q64, double *qn2, void *qf, hipStream_t st) {
-  hipLaunchKernelGGL((k_gather_query_h<CH, KS>), dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs,
-                     mu, q64, qn2, (_Float16 *)qf);
+  const dim3 grid(cdiv(sd.Mpad, IA_WG / IA_WAVE));
+  if (jobs.J == 1)
+    hipLaunchKernelGGL((k_gather_query_h<CH, KS, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, job0_imgs(B, jobs), JobArg1{jobs.j0},
+                       mu, q64, qn2, (_Float16 *)qf);
+  else
+    hipLaunchKernelGGL((k_gather_query_h<CH, KS, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64,
+                       qn2, (_Float16 *)qf);
 }
 void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, hipStream_t st) {
@@ -1945,15 +1971,23 @@ void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
   else launch_gather_h_t<2, 7>(g, sd, B, jobs, mu, q64, qn2, qf, st);
 }
 
+template <bool IMG>
+static void launch_gather_p_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
+                              double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
+                              float4 *qinfo, const Imgs &A, hipStream_t st) {
+  const dim3 grid(cdiv(sd.Mpad, IA_WG / IA_WAVE));
+  if (jobs.J == 1)
+    hipLaunchKernelGGL((k_gather_query_p<4, IMG, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, job0_imgs(B, jobs), JobArg1{jobs.j0},
+                       mu, q64, qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A);
+  else
+    hipLaunchKernelGGL((k_gather_query_p<4, IMG, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64,
+                       qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A);
+}
 void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
                         float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st) {
-  if (img_rows)
-    hipLaunchKernelGGL((k_gather_query_p<4, true>), dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs,
-                       mu, q64, qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A);
-  else
-    hipLaunchKernelGGL((k_gather_query_p<4, false>), dim3(cdiv(sd.Mpad, IA_WG / IA_WAVE)), dim3(IA_WG), 0, st, g, sd, B, jobs,
-                       mu, q64, qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A);
+  if (img_rows) launch_gather_p_t<true>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, st);
+  else launch_gather_p_t<false>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, st);
 }
 
 // split-f16 distance kernels live in ia_k3h.hip, compiled once per (KS, QT) instance
@@ -2005,17 +2039,18 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   const int rev = (variant == 7 || variant == 8 || variant == 10 || variant >= 11) ? (step & 1) : 0;  // alternate steps walk in reverse
   if (variant == 7) variant = 6;  // 8: + the previous step's query order (no sort)
   if (variant == 10) variant = 9;  // 9: 6 + pipelined single chains; 10: 9 + reverse walks
-  if (variant < 11 && variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // v3/v4 limits (ia_k3h.hip IA_K3P3_*)
+  if ((variant < 11 || variant == 13) && variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // in-kernel sort: <= 512
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t NQ = (size_t)qt * IA_TILE;
-  const int nthr = variant == 12 ? 16 * IA_WAVE : IA_WGH;  // v12: 16 waves (4 per SIMD), one tile buffer
-  size_t lds = variant >= 11 ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 +
-                                   NQ * 4 + (size_t)kmax * 40
-                             : ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
+  const int nthr = variant >= 12 ? 16 * IA_WAVE : IA_WGH;  // v12/13: 16 waves (4 per SIMD), one tile buffer
+  size_t lds = (variant == 11 || variant == 12)
+                   ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 +
+                         (size_t)kmax * 40
+                   : ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
   const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
   lds = lds > red ? lds : red;
-  static int attr_lds[13][16] = {};
-  const int vi = variant < 0 || variant > 12 ? 1 : variant;
+  static int attr_lds[14][16] = {};
+  const int vi = variant < 0 || variant > 13 ? 1 : variant;
   if ((int)lds > attr_lds[vi][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_lds[vi][qt] = (int)lds;

@@ -12,14 +12,14 @@ mkdir -p gpurun_out/ab
 for i in 1 2; do
   timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab/head_$i.json 2> gpurun_out/ab/head_$i.err || { echo "head bench failed"; exit 1; }
   timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --k3p-variant 12 > gpurun_out/ab/v12_$i.json 2> gpurun_out/ab/v12_$i.err || { echo "v12 bench failed"; tail -5 gpurun_out/ab/v12_$i.err; exit 1; }
+  timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --k3p-variant 13 > gpurun_out/ab/v13_$i.json 2> gpurun_out/ab/v13_$i.err || { echo "v13 bench failed"; tail -5 gpurun_out/ab/v13_$i.err; exit 1; }
   if [ -d ab_base ]; then (cd ab_base && timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > ../gpurun_out/ab/base_$i.json 2> ../gpurun_out/ab/base_$i.err) || echo "base bench failed"; fi
 done
 for f in gpurun_out/ab/*.json; do echo "$f $(python3 -c "import json,sys; d=json.load(open('$f')); print(round(d['value']), round(d['ms_per_step'],1), round(d['roofline'].get('k3_us_per_launch',0),1))")"; done
 TAG=cfg3 bash scripts/gpu_prof.sh || exit 1
-TAG=cfg3_row1 bash scripts/gpu_prof.sh --row-source 1 || exit 1
-TAG=cfg3_v11 bash scripts/gpu_prof.sh --k3p-variant 11 || exit 1
 TAG=cfg3_v12 bash scripts/gpu_prof.sh --k3p-variant 12 || exit 1
-for W in 2 4 8; do TAG=shard$W bash scripts/gpu_prof.sh --shard-emulate $W || exit 1; done
-TAG=cfg5_prune bash scripts/gpu_prof.sh --config cfg5 --prune-min-rows 262144 || exit 1
-IA_LIBIA=image-analogies-python_amd/libia_probe32.so TAG=probe32 bash scripts/gpu_prof.sh || echo "probe32 failed (diagnostic only)"
+TAG=cfg3_v13 bash scripts/gpu_prof.sh --k3p-variant 13 || exit 1
+TAG=cfg4_v13 bash scripts/gpu_prof.sh --config cfg4 --k3p-variant 13 || exit 1
+TAG=cfg4 bash scripts/gpu_prof.sh --config cfg4 || exit 1
+TAG=cfg5 bash scripts/gpu_prof.sh --config cfg5 || exit 1
 echo ALL-OK
