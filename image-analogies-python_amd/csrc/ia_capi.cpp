@@ -288,8 +288,8 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   }
 #else  // product build: the default kernels only (7: pruned scan, 1: packed-index K3h)
   if (!std::strcmp(name, "k3p_variant")) {  // 7: in-kernel sort up to 512 queries, presorted above; 11: always presorted
-    if (value != 7 && value != 11 && value != 12 && value != 13)
-      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 12 or 13 (other versions are in DIAG=1 builds only)");
+    if (value != 7 && value != 11)
+      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7 or 11 (other versions are in DIAG=1 builds only)");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -304,7 +304,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
   if (!std::strcmp(name, "row_source")) {
+#ifdef IA_K3H_DIAG
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: row_source must be 0 (row DB) or 1 (images)");
+#else  // the image-gather rows measured slower: DIAG=1 builds only
+    if (value != 0) return fail(IA_EINVAL, "ia_set_option: row_source 1 is built with DIAG=1 only (measured slower)");
+#endif
     c->row_source = value;
     return IA_OK;
   }

@@ -1234,11 +1234,12 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     if (variant == 5) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true>;
     if (variant == 8) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, true>;
     if (variant == 9) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, true>;
+    // 16 waves per workgroup, one tile buffer: slower than 6/11 on cfg3 and cfg4
+    if (variant == 12) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, 16, 1, true, true, false, false, true>;
+    if (variant == 13) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, 16, 1, true, true>;  // 12 with the in-kernel sort
 #endif
     if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
     if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true>;
-    if (variant == 12) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, 16, 1, true, true, false, false, true>;
-    if (variant == 13) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, 16, 1, true, true>;  // 12 with the in-kernel sort
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

@@ -1824,13 +1824,15 @@ static void launch_merge_j(const LevelGeo &g, const StepDesc &sd, const Imgs &A,
 template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
                            const JobSet &jobs, bool fused, hipStream_t st) {
-  if constexpr (CH == 1) {  // row_source = 1 (exact rows from the images): 1 channel only
+#ifdef IA_K3H_DIAG  // row_source = 1 (exact rows from the images, 1 channel): measured slower, DIAG=1 builds only
+  if constexpr (CH == 1) {
     if (ma.img_rows) {
       if (fused) launch_merge_j<CH, true, true>(g, sd, A, ma, win, jobs, st);
       else launch_merge_j<CH, false, true>(g, sd, A, ma, win, jobs, st);
       return;
     }
   }
+#endif
   if (fused) launch_merge_j<CH, true, false>(g, sd, A, ma, win, jobs, st);
   else launch_merge_j<CH, false, false>(g, sd, A, ma, win, jobs, st);
 }
@@ -1986,8 +1988,14 @@ static void launch_gather_p_t(const LevelGeo &g, const StepDesc &sd, const Imgs 
 void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
                         float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st) {
-  if (img_rows) launch_gather_p_t<true>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, st);
-  else launch_gather_p_t<false>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, st);
+#ifdef IA_K3H_DIAG
+  if (img_rows) {
+    launch_gather_p_t<true>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, st);
+    return;
+  }
+#endif
+  (void)img_rows;
+  launch_gather_p_t<false>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, st);
 }
 
 // split-f16 distance kernels live in ia_k3h.hip, compiled once per (KS, QT) instance

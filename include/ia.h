@@ -124,8 +124,8 @@ int ia_version(void);
  * k3p_variant 7 (default: the pruned scan sorts a step's queries itself up to 512 of them, a
  * step wider than that is sorted once by k_query_sort) or 11 (always presorted) and
  * k3_variant 1; DIAG=1 builds every version.
- * "row_source" = 0 (default: exact rows of the rerank / coherence / pruning bound from the fp64
- * row DB) or 1 (gathered from the A-side pyramid images, 1 channel).
+ * "row_source" = 0 (exact rows of the rerank / coherence / pruning bound from the fp64 row DB);
+ * 1 (gathered from the A-side pyramid images, 1 channel) is in DIAG=1 builds only (slower).
  * "shard_emulate" = W (1 = off): on a single-rank context, every level with >= 64 W DB tiles
  * runs as a W-way DB shard on this device (per-shard scans and certified winners, then the
  * multi-rank finish; no RCCL): the sharded code path, testable on one GPU.

@@ -49,11 +49,11 @@ def _run(ctx, job, prune, variant=7):
                                                       (1024, 2, 1), (512, 1, 0), (512, 1, 2)])
 def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     """variant = the pruned-scan kernel version (option k3p_variant; the product build holds the
-    default 7, 11 (queries presorted once per step by k_query_sort), 12 (presorted, 16 waves with
-    one tile buffer each: 4 waves per SIMD), 13 (12 with the in-kernel sort) and the fallback 1 only,
-    DIAG=1 builds the rest): every one is exact"""
+    default 7, 11 (queries presorted once per step by k_query_sort) and the fallback 1 only; DIAG=1
+    builds the rest, e.g. 12 (presorted, 16 waves with one tile buffer each: 4 waves per SIMD) and
+    13 (12 with the in-kernel sort), both measured slower): every one is exact"""
     from ia_amd import synth
-    if variant not in (7, 11, 12, 13) and not _diag_build(ctx):
+    if variant not in (7, 11) and not _diag_build(ctx):
         pytest.skip('kernel version %d is built with DIAG=1 only' % variant)
     job = synth.make_job(size)
     Bp0, S0, IM0, st0 = _run(ctx, job, 0)
@@ -79,7 +79,8 @@ def test_prune_option_rejects_bad_values(ctx):
     with pytest.raises(_native.IAError):
         ctx.set_option('k3p_variant', 14)
     if not _diag_build(ctx):
-        with pytest.raises(_native.IAError):
-            ctx.set_option('k3p_variant', 6)
+        for v in (6, 12, 13):
+            with pytest.raises(_native.IAError):
+                ctx.set_option('k3p_variant', v)
     with pytest.raises(_native.IAError):
         ctx.set_option('prune_min_rows', 0)

@@ -8,7 +8,7 @@ import sys
 
 
 def short(name):
-    for k in ('k3h_prune', 'k_gather_query_p', 'k3h_scan', 'k3h_dist', 'k3_dist', 'k_merge_level', 'k_gather_query_h', 'k_gather_query', 'k_part_means',
+    for k in ('k_part_means_fold', 'k3h_prune', 'k_gather_query_p', 'k3h_scan', 'k3h_dist', 'k3_dist', 'k_merge_level', 'k_gather_query_h', 'k_gather_query', 'k_part_means',
               'k_db_build_h', 'k_db_build', 'k_absmax', 'k_reduce_stats', 'k_finish_level', 'k_step_fused'):
         if k in name:
             return k
@@ -29,6 +29,7 @@ for r in rows:
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
     cur[k][0] += 1
     cur[k][1] += d
+    cur[k].append(d)
 per_job = 9
 sel = levels[job * per_job:(job + 1) * per_job] if len(levels) >= per_job else levels
 tot = collections.defaultdict(float)
@@ -38,4 +39,13 @@ for i, lv in enumerate(sel):
                                                           for k, v in sorted(lv.items(), key=lambda x: -x[1][1]) if v[1] > 100))
     for k, v in lv.items():
         tot[k] += v[1]
+# duration percentiles of the finest level's per-step kernels (median vs mean: the tail's share)
+if sel:
+    lv = sel[-1]
+    for k, v in sorted(lv.items(), key=lambda x: -x[1][1]):
+        ds = sorted(v[2:])
+        if len(ds) >= 100:
+            q = lambda f: ds[min(len(ds) - 1, int(f * len(ds)))]
+            print('  %s finest level: mean %.1f p10 %.1f p50 %.1f p90 %.1f p99 %.1f max %.1f us (tail above p90: %.1f ms)'
+                  % (k, v[1] / v[0], q(.1), q(.5), q(.9), q(.99), ds[-1], sum(x - q(.9) for x in ds if x > q(.9)) / 1e3))
 print('total %.1f ms: ' % (sum(tot.values()) / 1e3) + ', '.join('%s %.1f' % (k, v / 1e3) for k, v in sorted(tot.items(), key=lambda x: -x[1])))
