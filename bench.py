@@ -144,7 +144,7 @@ def main():
                     help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select (DIAG=1 builds)')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
-    ap.add_argument('--k3p-variant', type=int, default=7, choices=list(range(14)),
+    ap.add_argument('--k3p-variant', type=int, default=7, choices=list(range(16)),
                     help='pruned-scan kernel version (ia_k3h.hip k3h_prune*; other than 7: DIAG=1 builds): 0 = first version, 1 = boxes in '
                          'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
                          'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks')
@@ -306,6 +306,10 @@ def main():
     roofline['fp32_mfma_equiv_tflops'] = fp32_equiv / 1e12
     roofline['fp32_mfma_equiv_frac'] = fp32_equiv / FP32_MFMA_PEAK
     roofline['pairs_frac'] = st['dist_pairs'] / max(st['dist_pairs_full'], 1.)
+    if st['dist_pairs_corrected'] > 0:
+        # k3p_variant 14/15: every box-needed pair runs the hi x hi product; only this share also
+        # runs the two correction products and the top-2 epilogue (mfma_* above count 3 products)
+        roofline['pairs_corrected_frac'] = st['dist_pairs_corrected'] / max(st['dist_pairs'], 1.)
     out = {'metric': METRIC, 'value': value, 'unit': "B' px/s", 'n_gpus': world, 'steps': args.steps,
            'warmup': args.warmup, 'ms_per_step': elapsed * 1e3 / args.steps, 'higher_is_better': True,
            'scaling': 'strong' if (args.mode == 'shard' or sw is not None) else 'weak', 'vs_baseline': None,
@@ -335,7 +339,8 @@ def main():
            'roofline': roofline,
            'stats': {k: st[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
                                         'synth_ms', 'bound_violations', 'kappa_ambiguous', 'f16_levels', 'pruned_levels',
-                                        'dist_pairs', 'dist_pairs_full', 'dist_tiles', 'dist_tiles_full')}}
+                                        'dist_pairs', 'dist_pairs_full', 'dist_tiles', 'dist_tiles_full',
+                                        'dist_pairs_corrected')}}
     if sw is not None:
         out['config']['sweep'] = {'jobs': len(sw.jobs), 'batched': not args.sequential, 'max_batch': args.max_batch,
                                   'kappas': sorted({j.k for j in sw.jobs}), 'depths': sorted(set(sw.L))}

@@ -91,7 +91,8 @@ struct ia_ctx {
   DevBuf db, db64, mu, Rbits, q64, qn2, qf, rec, recT, win, allwin, counters, absmax;
   // certified pruned scan (option "prune"): per-level basis, sorted DB table, tile boxes
   DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs, ord;
-  DevBuf qs_order, qs_info, qs_frag, qs_tbox;  // presorted queries of a step (k3p_variant 11, K2s)
+  DevBuf qs_order, qs_info, qs_frag, qs_tbox;
+  DevBuf tnorm;  // per DB tile of a pruned level: R_t >= max |a'| over its rows (k3p_variant 14/15)  // presorted queries of a step (k3p_variant 11, K2s)
   DevBuf py_in, py_tmp, py_sm, py_mm, py_out;  // GPU preprocessing (ia_gaussian_pyramid, ia_color_matrix)
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
   int64_t prune_min_rows = IA_PRUNE_MIN_ROWS;  // option "prune_min_rows": smallest DB that prunes
@@ -172,9 +173,10 @@ int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac)
   const int64_t stride = std::max<int64_t>(1, NA / 65536), nsamp = (NA + stride - 1) / stride;
   int rc;
   if ((rc = c->pr_part.ensure((size_t)NWG_COV * NPAIR * 8)) || (rc = c->pr_cov.ensure((size_t)NPAIR * 8)) ||
-      (rc = c->pr_basis.ensure((size_t)(IA_NPC * D + IA_NPC) * 8)) || (rc = c->pr_proj.ensure((size_t)NA * IA_NPC * 8)) ||
+      (rc = c->pr_basis.ensure((size_t)(IA_NPC * D + IA_NPC) * 8)) || (rc = c->pr_proj.ensure((size_t)NA * (IA_NPC * 8 + 4))) ||
       (rc = c->pr_keys.ensure((size_t)NA * 8)) || (rc = c->pr_rows.ensure((size_t)NA * 8)) ||
-      (rc = c->pos2row.ensure((size_t)NT * IA_TILE * 4)) || (rc = c->boxes.ensure((size_t)NT * 2 * IA_NPC * 4)))
+      (rc = c->pos2row.ensure((size_t)NT * IA_TILE * 4)) || (rc = c->boxes.ensure((size_t)NT * 2 * IA_NPC * 4)) ||
+      (rc = c->tnorm.ensure((size_t)NT * 4)))
     return rc;
   const size_t sort_bytes = ia_sort_temp_bytes(NA);
   if ((rc = c->pr_tmp.ensure(sort_bytes))) return rc;
@@ -210,10 +212,13 @@ int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac)
   HIP_TRY(hipMemcpyAsync(c->pr_basis.p, c->basis_h.data(), c->basis_h.size() * 8, hipMemcpyHostToDevice, c->st));
   unsigned *keys = c->pr_keys.as<unsigned>();
   int *rows = c->pr_rows.as<int>();
-  ia_launch_proj_keys(c->db64.as<double>(), NA, mu, c->pr_basis.as<double>(), c->pr_proj.as<double>(), keys, rows, c->st);
+  float *rnorm = reinterpret_cast<float *>(c->pr_proj.as<double>() + NA * IA_NPC);  // |a'| per row, rounded up
+  ia_launch_proj_keys(c->db64.as<double>(), NA, mu, c->pr_basis.as<double>(), c->pr_proj.as<double>(), keys, rows, rnorm,
+                      c->st);
   if (ia_sort_pairs(c->pr_tmp.p, sort_bytes, keys, keys + NA, rows, rows + NA, NA, c->st) != 0)
     return fail(IA_EHIP, "prepare_prune: radix sort failed");
-  ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, W, c->pos2row.as<int>(), c->boxes.as<float>(), c->st);
+  ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, W, c->pos2row.as<int>(), c->boxes.as<float>(), rnorm,
+                        c->tnorm.as<float>(), c->st);
   HIP_TRY(hipGetLastError());
   g.pos2row = c->pos2row.as<int>();
   return IA_OK;
@@ -257,7 +262,7 @@ void ia_destroy(ia_ctx *c) {
   for (DevBuf *b : {&c->A, &c->Ac, &c->Ap, &c->Apc, &c->jobs, &c->db, &c->db64,
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
-                    &c->boxes, &c->qinfo, &c->pairs, &c->ord, &c->qs_order, &c->qs_info, &c->qs_frag, &c->qs_tbox,
+                    &c->boxes, &c->qinfo, &c->pairs, &c->ord, &c->qs_order, &c->qs_info, &c->qs_frag, &c->qs_tbox, &c->tnorm,
                     &c->py_in, &c->py_tmp, &c->py_sm, &c->py_mm, &c->py_out})
     b->release();
   for (hipEvent_t e : c->evs) hipEventDestroy(e);
@@ -277,7 +282,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   }
 #ifdef IA_K3H_DIAG  // DIAG=1 builds: every kernel version of DESIGN.md §4b's progression
   if (!std::strcmp(name, "k3p_variant")) {
-    if (value < 0 || value > 13) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..13");
+    if (value < 0 || value > 15) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..15");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -288,8 +293,8 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   }
 #else  // product build: the default kernels only (7: pruned scan, 1: packed-index K3h)
   if (!std::strcmp(name, "k3p_variant")) {  // 7: in-kernel sort up to 512 queries, presorted above; 11: always presorted
-    if (value != 7 && value != 11)
-      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7 or 11 (other versions are in DIAG=1 builds only)");
+    if (value != 7 && value != 11 && value != 14 && value != 15)
+      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14 or 15 (other versions are in DIAG=1 builds only)");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -746,9 +751,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     // pruned scan: queries sorted once per step (K2s) when the step is wider than the in-kernel
     // sort of v6/v7 (512) or variant 11 is selected
     // (variants 11, 12: presorted; 7, 13: in-kernel sort up to 512 queries, presorted v11 / v12 above)
-    const int k3v = (c->k3p_variant == 11 || c->k3p_variant == 12) ? c->k3p_variant
-                    : (prune && sd.Mpad > 512 ? (c->k3p_variant == 13 ? 12 : 11) : c->k3p_variant);
-    if (prune && (k3v == 11 || k3v == 12))
+    const int kv = c->k3p_variant;
+    const int k3v = (kv == 11 || kv == 12 || kv == 15) ? kv
+                    : (prune && sd.Mpad > 512 ? (kv == 13 ? 12 : kv == 14 ? 15 : 11) : kv);
+    const bool presorted = k3v == 11 || k3v == 12 || k3v == 15;
+    if (prune && presorted)
       ia_launch_query_sort(c->qinfo.as<float4>(), c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
                            c->qs_frag.p, c->qs_tbox.as<float4>(), c->st);
     if (ns > 0) {
@@ -763,17 +770,18 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         int qt0 = 0;
         for (int b = 0; b < nqb; b++) {
           const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
-          if (prune && (k3v == 11 || k3v == 12))
+          const float *tn = prune ? c->tnorm.as<float>() + x.t0 : nullptr;
+          if (prune && presorted)
             ia_launch_k3p(qt, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t,
-                          c->qs_order.as<int>(), 0, sd.r0, nullptr, c->qs_tbox.as<float4>(), c->st);
+                          c->qs_order.as<int>(), 0, sd.r0, nullptr, c->qs_tbox.as<float4>(), tn, c->st);
           else if (prune)
             ia_launch_k3p(qt, dbp, c->qf.p, c->qinfo.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
                           k3v, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
-                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, c->st);
+                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st);
           else if (use_h)
             ia_launch_k3h(g.KS, qt, dbp, c->qf.p, n, x.tpw, qt0, Mt, x.nwg, m.pos0, g.n_tiles, (float4 *)m.rec,
                           (float *)m.recT, c->k3_variant, c->st);
@@ -833,14 +841,22 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   if (prune) ia_k3p_probe_dump();
 #endif
   if (stats) {
-    unsigned long long ctr[5], prs[4];
+    unsigned long long ctr[5], prs[4], pfull = 0;
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
     {  // per-workgroup counter slots (no same-address atomics in the distance kernel)
       std::vector<unsigned long long> slots(4 * IA_NWG_H);
       HIP_TRY(hipMemcpy(slots.data(), c->pairs.p, slots.size() * 8, hipMemcpyDeviceToHost));
       for (int j = 0; j < 4; j++) {
         prs[j] = 0;
-        for (int w = 0; w < IA_NWG_H; w++) prs[j] += slots[j * IA_NWG_H + w];
+        for (int w = 0; w < IA_NWG_H; w++) {
+          const unsigned long long v = slots[j * IA_NWG_H + w];
+          if (j < 2) {  // pair slots: (pairs with corrections << 32) + pairs (k3p_variant 14/15)
+            prs[j] += v & 0xffffffffull;
+            pfull += v >> 32;
+          } else {
+            prs[j] += v;
+          }
+        }
       }
     }
     const double pair_flops = 2.0 * g.D * IA_TILE * IA_TILE;  // one (DB tile, query tile) pair
@@ -853,6 +869,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     stats->dist_pairs_full += pairs_full;
     stats->dist_tiles += prune ? (double)(prs[2] + prs[3]) : tiles_full;
     stats->dist_tiles_full += tiles_full;
+    stats->dist_pairs_corrected += (double)pfull;
     float ms_db = 0.f, ms_syn = 0.f;
     hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
     hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);

@@ -347,6 +347,71 @@ __device__ __forceinline__ void k3p_pairs(const h16x8 (&a)[2 * KS], const h16x8 
   }
 }
 
+// HHF (k3p_variant 14 / 15): each needed (DB tile, query tile) block first runs the hi x hi
+// product alone (4 MFMAs); its two correction products (8 MFMAs) and the top-2 epilogue follow
+// only when some value of the block can lie within its query's bound:
+//     c_hh <= lim_q = z_q + R_t (w_q + R_t 2^-9 + 2^-20)
+// where R_t >= max |a'| over the tile's rows and (z_q, w_q) come from K2p (ia_kernels.hip):
+// z_q >= U'_q - |q'|^2 + (rounding terms), w_q >= 2^-8 |q'|.  The hi-only value misses
+// sum(hi_a lo_q + lo_a hi_q + lo_a lo_q) and carries its fp32 accumulation error, together
+// < 2^-10 (|a'|^2 + 2|a'||q'|) + 2^-24 (16|a'| + 16|q'| + 300) (f16 rounding 2^-11 relative,
+// subnormal spacing 2^-25); lim_q takes twice the relative term.  A block that
+// fails the test holds only rows with |a - q|^2 > U'_q: they can neither be nor tie the NN, exactly
+// like the rows of a tile the box test skips, so the records stay certified.
+template <int KS>
+__device__ __forceinline__ f32x16 k3p_hh(const h16x8 (&a)[2 * KS], const h16x8 *qb) {
+  f32x16 c = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int s = 0; s < KS; s++) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], qb[(2 * s) * IA_WAVE], c, 0, 0, 0);
+  return c;
+}
+template <int KS>
+__device__ __forceinline__ void k3p_corr(const h16x8 (&a)[2 * KS], const h16x8 *qb, f32x16 &c) {
+#pragma unroll
+  for (int s = 0; s < KS; s++) {
+    const h16x8 xh = qb[(2 * s) * IA_WAVE], xl = qb[(2 * s + 1) * IA_WAVE];
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], xh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], xl, c, 0, 0, 0);
+  }
+}
+__device__ __forceinline__ float k3p_min16(const f32x16 &c) {
+  const float m0 = fminf(fminf(c[0], c[1]), c[2]), m1 = fminf(fminf(c[3], c[4]), c[5]);
+  const float m2 = fminf(fminf(c[6], c[7]), c[8]), m3 = fminf(fminf(c[9], c[10]), c[11]);
+  const float m4 = fminf(fminf(c[12], c[13]), c[14]);
+  return fminf(fminf(fminf(m0, m1), fminf(m2, m3)), fminf(m4, c[15]));
+}
+// query tiles QP.. of one DB tile t (rt = its R_t; qz = the lane's (z, w) slots, stride 32)
+template <int KS, int QT, int Q>
+__device__ __forceinline__ void k3p_filtered(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, int t, float rt,
+                                             const float *qzt, const float *qzw, float (&b1)[QT], float (&b2)[QT],
+                                             int (&i1)[QT], unsigned &nfull) {
+  if constexpr (Q < QT) {
+    constexpr int NP = 2 * KS;
+    const bool n0 = (msk >> Q) & 1u, n1 = Q + 1 < QT && ((msk >> (Q + 1)) & 1u);  // wave-uniform
+    const h16x8 *qb0 = lq + Q * NP * IA_WAVE, *qb1 = qb0 + NP * IA_WAVE;
+    const float rr = fmaf(rt, 0x1p-9f, 0x1p-20f);
+    f32x16 c0, c1;
+    if (n0) c0 = k3p_hh<KS>(a, qb0);
+    if constexpr (Q + 1 < QT) {
+      if (n1) c1 = k3p_hh<KS>(a, qb1);
+    }
+    const bool f0 = n0 && __ballot(k3p_min16(c0) <= fmaf(rt, qzw[Q * IA_TILE] + rr, qzt[Q * IA_TILE])) != 0ull;
+    bool f1 = false;
+    if constexpr (Q + 1 < QT)
+      f1 = n1 && __ballot(k3p_min16(c1) <= fmaf(rt, qzw[(Q + 1) * IA_TILE] + rr, qzt[(Q + 1) * IA_TILE])) != 0ull;
+    if (f0) k3p_corr<KS>(a, qb0, c0);
+    if constexpr (Q + 1 < QT) {
+      if (f1) k3p_corr<KS>(a, qb1, c1);
+    }
+    if (f0) k3p_epi1(c0, t, b1[Q], b2[Q], i1[Q]);
+    if constexpr (Q + 1 < QT) {
+      if (f1) k3p_epi1(c1, t, b1[Q + 1], b2[Q + 1], i1[Q + 1]);
+    }
+    nfull += (unsigned)f0 + (unsigned)f1;
+    k3p_filtered<KS, QT, Q + 2>(a, lq, msk, t, rt, qzt, qzw, b1, b2, i1, nfull);
+  }
+}
+
 // V (option "k3p_variant"): 0 = per-tile box loads and a full-key rank sort (first version);
 // 1 = the wave's tile boxes held in registers (one coalesced load per 64 tiles, read back with
 // v_readlane: the tile walk has no memory latency left), unique 20-bit-key rank sort;
@@ -357,7 +422,7 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
           const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
           float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
           unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
-           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox) {
+           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox, const float *__restrict__ tnorm) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   static_assert(QT <= 32, "need masks are 32-bit");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
@@ -704,14 +769,16 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // (ia_prune.hip): qf / qinfo hold them in sorted order (fragments; lo, hi, (U', key) per slot),
 // ord_in maps a sorted slot to its query and tbox holds the sorted query tiles' boxes, so phase
 // 1 loads only this launch's slice and phase 2 (sort, scatter, tile boxes) is skipped.
+// HHF (k3p_variant 14 / 15): the hi x hi block filter above (k3p_filtered); the per-WG pair
+// counter slot then holds (pairs with corrections << 32) + box-needed pairs.
 template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false, bool PIPE = false,
-          bool PRE = false>
+          bool PRE = false, bool HHF = false>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
            float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
            unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
-           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox) {
+           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox, const float *__restrict__ tnorm) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   constexpr int NE = PRE ? 1 : (IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE + WGT - 1) / WGT;  // unsorted fragments per thread
   static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
@@ -734,7 +801,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   float4 *wbox = reinterpret_cast<float4 *>(rankof + (PRE ? 0 : Mpad));  // [2K] the WG's tile boxes
   unsigned *kmask = reinterpret_cast<unsigned *>(wbox + 2 * K);        // [K] need mask per tile
   int *items = reinterpret_cast<int *>(kmask + K);                     // [K] needed tiles, in order
-  __shared__ unsigned wpairs[NW], wtiles[NW];
+  float *qzt = reinterpret_cast<float *>(items + K);                    // HHF: [NQ] z per sorted slot
+  float *qzw = qzt + NQ;                                                // HHF: [NQ] w per sorted slot
+  float *wR = qzw + NQ;                                                 // HHF: [K] R_t of the WG's tiles
+  __shared__ unsigned wpairs[NW], wtiles[NW], wfull[NW];
   __shared__ int wcnt[NW];
   const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -756,7 +826,12 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       const bool ok = sl < Mpad;
       qlo[x] = ok ? qinfo[3 * sl] : make_float4(0.f, 0.f, 0.f, 0.f);
       qhi[x] = ok ? qinfo[3 * sl + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
-      qU[x] = ok ? qinfo[3 * sl + 2].x : -INFINITY;
+      const float4 u = ok ? qinfo[3 * sl + 2] : make_float4(-INFINITY, 0.f, -INFINITY, 0.f);
+      qU[x] = u.x;
+      if constexpr (HHF) {
+        qzt[x] = u.z;
+        qzw[x] = u.w;
+      }
       skey[x] = ok ? ord_in[sl] : 0x7fffffff;  // slot -> query of this slice
     }
     if (tid < QT) {
@@ -768,6 +843,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       const int t = tk(tid);
       wbox[2 * tid] = boxes[2 * t];
       wbox[2 * tid + 1] = boxes[2 * t + 1];
+      if constexpr (HHF) wR[tid] = tnorm[t];
     }
   }
   __shared__ int kctr;  // DYN: next tile index to hand out
@@ -775,13 +851,15 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   if constexpr (PRE) __syncthreads();
   if constexpr (!PRE) {
   float4 mlo = make_float4(0.f, 0.f, 0.f, 0.f), mhi = mlo;
-  float mU = -INFINITY;
+  float mU = -INFINITY, mzt = -INFINITY, mzw = 0.f;
   unsigned mkey = 0xFFFFFFFFu;
   if (!PRE && tid < Mpad) {
     mlo = qinfo[3 * tid];
     mhi = qinfo[3 * tid + 1];
     const float4 u = qinfo[3 * tid + 2];
     mU = u.x;
+    mzt = u.z;
+    mzw = u.w;
     mkey = (__float_as_uint(u.y) & 0xFFFFF000u) | (unsigned)tid;  // unique (Mpad <= 4096)
   }
   const int ne = Mpad / IA_TILE * NP * IA_WAVE;
@@ -795,6 +873,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     const int t = tk(tid);
     wbox[2 * tid] = boxes[2 * t];
     wbox[2 * tid + 1] = boxes[2 * t + 1];
+    if constexpr (HHF) wR[tid] = tnorm[t];
   }
   if (tid < Mpad) {
     skey[tid] = mkey;
@@ -852,6 +931,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         qlo[x] = mlo;
         qhi[x] = mhi;
         qU[x] = mU;
+        if constexpr (HHF) {
+          qzt[x] = mzt;
+          qzw[x] = mzw;
+        }
       }
     }
   } else if (DYN && Mpad > 256) {  // (uniform) below 256 queries the rank count is cheaper
@@ -889,6 +972,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         qlo[x] = mlo;
         qhi[x] = mhi;
         qU[x] = mU;
+        if constexpr (HHF) {
+          qzt[x] = mzt;
+          qzw[x] = mzw;
+        }
       }
     }
   } else if (tid < Mpad) {
@@ -904,6 +991,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       qlo[x] = mlo;
       qhi[x] = mhi;
       qU[x] = mU;
+      if constexpr (HHF) {
+        qzt[x] = mzt;
+        qzw[x] = mzw;
+      }
     }
   }
   __syncthreads();
@@ -955,7 +1046,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     b2[q] = FLT_MAX;
     i1[q] = 0x7fffffff;
   }
-  unsigned cnt = 0, ntl = 0;
+  unsigned cnt = 0, ntl = 0, nfull = 0;
   if constexpr (INTER) {
     K3P_T(ph[3]);
     // ---- 3'/4'. need tests interleaved with the contraction: wave v walks tiles k = v mod NW;
@@ -1029,7 +1120,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       // makes the MFMAs below wait for the prefetch itself
       ld_tile<KS>(nxt, db, tk(kn < K ? kn : k), lane);
       asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-      if constexpr (PIPE) {
+      if constexpr (HHF) {
+        k3p_filtered<KS, QT, 0>(cur, ldsh + lane, m, tk(k), wR[k], qzt + (lane & 31), qzw + (lane & 31), b1, b2, i1,
+                                nfull);
+      } else if constexpr (PIPE) {
         f32x16 acc[2];
         k3p_pipe<KS, QT, 0>(cur, ldsh + lane, m, tk(k), b1, b2, i1, acc);
       } else {
@@ -1149,6 +1243,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   if (lane == 0) {
     wpairs[wave] = cnt;
     wtiles[wave] = ntl;
+    wfull[wave] = nfull;
   }
   Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32], inside the query-fragment area
 #pragma unroll
@@ -1177,13 +1272,14 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
   }
   if (tid == 0) {  // the workgroup's own counter slots (stream-ordered launches: no atomics)
-    unsigned long long sp = 0, st = 0;
+    unsigned long long sp = 0, st = 0, sf = 0;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
       sp += wpairs[w];
       st += wtiles[w];
+      sf += wfull[w];
     }
-    pairs[wg] += sp;
+    pairs[wg] += sp + (HHF ? sf << 32 : 0ull);
     tiles[wg] += st;
   }
 #if IA_PROBE & 16
@@ -1240,6 +1336,8 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 #endif
     if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
     if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true>;
+    if (variant == 14) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true>;
+    if (variant == 15) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true>;
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

@@ -1130,7 +1130,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
     if (lane == 0) {
       qinfo[3 * m] = make_float4(0.f, 0.f, 0.f, 0.f);
       qinfo[3 * m + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      qinfo[3 * m + 2] = make_float4(-INFINITY, __uint_as_float(IA_PRUNE_KEY_PAD), 0.f, 0.f);
+      qinfo[3 * m + 2] = make_float4(-INFINITY, __uint_as_float(IA_PRUNE_KEY_PAD), -INFINITY, 0.f);
     }
     return;
   }
@@ -1182,7 +1182,16 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
                                    round_up_f(p[2] + IA_PRUNE_MABS), round_up_f(p[3] + IA_PRUNE_MABS));
     const bool fin = u < DBL_MAX;
     const unsigned key = fin ? prune_key(p, basis + IA_NPC * D) : IA_PRUNE_KEY_INF;
-    qinfo[3 * m + 2] = make_float4(fin ? round_up_f(u * ufac) : INFINITY, __uint_as_float(key), 0.f, 0.f);
+    const float up = fin ? round_up_f(u * ufac) : INFINITY;
+    // K3p's hi x hi block filter (k3p_variant 14/15, ia_k3h.hip k3p_filtered): value bound
+    // z >= U' - |q'|^2 with the f32 rounding of z and of the kernel's lim = z + R_t (...)
+    // (2^-22 (|q'|^2 + U')) and the subnormal / norm-column terms (2^-24 (16 |q'| + 300));
+    // w = 2^-8 |q'| (twice the relative error term's |q'| part)
+    const double qn = sqrt(ss);
+    const float z = fin ? round_up_f((double)up - ss + 0x1p-22 * (ss + (double)up) + 0x1p-24 * (16.0 * qn + 300.0))
+                        : INFINITY;
+    const float w = round_up_f(0x1p-8 * qn * (1.0 + 0x1p-40));
+    qinfo[3 * m + 2] = make_float4(up, __uint_as_float(key), z, w);
   }
 }
 
@@ -2039,7 +2048,7 @@ size_t ia_k3p_lds(int qt, int Mpad) {
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
-                   const float4 *tbox, hipStream_t st) {
+                   const float4 *tbox, const float *tnorm, hipStream_t st) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
@@ -2047,22 +2056,24 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   const int rev = (variant == 7 || variant == 8 || variant == 10 || variant >= 11) ? (step & 1) : 0;  // alternate steps walk in reverse
   if (variant == 7) variant = 6;  // 8: + the previous step's query order (no sort)
   if (variant == 10) variant = 9;  // 9: 6 + pipelined single chains; 10: 9 + reverse walks
-  if ((variant < 11 || variant == 13) && variant >= 3 && (Mpad > 512 || kmax > 512)) variant = 1;  // in-kernel sort: <= 512
+  if ((variant < 11 || variant == 13 || variant == 14) && variant >= 3 && (Mpad > 512 || kmax > 512))
+    variant = variant == 14 && Mpad > 512 ? 15 : 1;  // in-kernel sort: <= 512 (14 -> 15: the host ran K2s)
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t NQ = (size_t)qt * IA_TILE;
-  const int nthr = variant >= 12 ? 16 * IA_WAVE : IA_WGH;  // v12/13: 16 waves (4 per SIMD), one tile buffer
-  size_t lds = (variant == 11 || variant == 12)
-                   ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 +
+  const bool pre = variant == 11 || variant == 12 || variant == 15, hhf = variant == 14 || variant == 15;
+  const int nthr = variant == 12 || variant == 13 ? 16 * IA_WAVE : IA_WGH;  // v12/13: 16 waves (4 per SIMD), one tile buffer
+  size_t lds = pre ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 +
                          (size_t)kmax * 40
                    : ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
+  if (hhf) lds += NQ * 8 + (size_t)kmax * 4;  // (z, w) per sorted query slot, R_t per tile
   const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
   lds = lds > red ? lds : red;
-  static int attr_lds[14][16] = {};
-  const int vi = variant < 0 || variant > 13 ? 1 : variant;
+  static int attr_lds[16][16] = {};
+  const int vi = variant < 0 || variant > 15 ? 1 : variant;
   if ((int)lds > attr_lds[vi][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_lds[vi][qt] = (int)lds;
   }
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row, NT,
-                     qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox);
+                     qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm);
 }

@@ -43,12 +43,12 @@ void ia_launch_fill_random_f16(void *p, int64_t n, unsigned seed, hipStream_t st
 void ia_launch_cov(const double *db64, int64_t NA, int64_t stride, int nwg, const double *mu_part, double *part,
                    double *cov, hipStream_t st);
 void ia_launch_proj_keys(const double *db64, int64_t NA, const double *mu_part, const double *basis, double *proj,
-                         unsigned *keys, int *rows, hipStream_t st);
+                         unsigned *keys, int *rows, float *rnorm, hipStream_t st);
 size_t ia_sort_temp_bytes(int64_t n);
 int ia_sort_pairs(void *temp, size_t temp_bytes, const unsigned *keys_in, unsigned *keys_out, const int *vals_in,
                   int *vals_out, int64_t n, hipStream_t st);
 void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int W, int *pos2row,
-                           float *boxes, hipStream_t st);
+                           float *boxes, const float *rnorm, float *tnorm, hipStream_t st);
 void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
                         float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st);
@@ -58,7 +58,7 @@ size_t ia_k3p_lds(int qt, int Mpad);
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
-                   const float4 *tbox, hipStream_t st);
+                   const float4 *tbox, const float *tnorm, hipStream_t st);
 // GPU preprocessing (ia_pyramid.hip)
 void ia_launch_pyramid_reduce(const double *in, double *out, double *tmp, double *sm, double *mm, int h, int w, int ch,
                               const double *w7, hipStream_t st);

@@ -86,7 +86,7 @@ __global__ void __launch_bounds__(PR_WG) k_cov_reduce(const double *__restrict__
 __global__ void __launch_bounds__(PR_WG) k_proj_keys(const double *__restrict__ db64, int64_t NA,
                                                      const double *__restrict__ mu_part, const double *__restrict__ basis,
                                                      double *__restrict__ proj, unsigned *__restrict__ keys,
-                                                     int *__restrict__ rows) {
+                                                     int *__restrict__ rows, float *__restrict__ rnorm) {
   constexpr int D = 55, DS = 56;
   __shared__ double ub[IA_NPC * D + IA_NPC];
   for (int i = threadIdx.x; i < IA_NPC * D + IA_NPC; i += PR_WG) ub[i] = basis[i];
@@ -94,7 +94,7 @@ __global__ void __launch_bounds__(PR_WG) k_proj_keys(const double *__restrict__ 
   const int64_t row = (int64_t)blockIdx.x * PR_WG + threadIdx.x;
   if (row >= NA) return;
   const double2 *a2 = reinterpret_cast<const double2 *>(db64 + row * DS);
-  double p[IA_NPC];
+  double p[IA_NPC], n2 = 0.;
 #pragma unroll
   for (int i = 0; i < IA_NPC; i++) p[i] = 0.;
 #pragma unroll
@@ -102,14 +102,19 @@ __global__ void __launch_bounds__(PR_WG) k_proj_keys(const double *__restrict__ 
     const double2 v = a2[k];
     const int f0 = 2 * k, f1 = 2 * k + 1;
     const double x0 = v.x - mu_part[prune_part1(f0)];
+    n2 += x0 * x0;
 #pragma unroll
     for (int i = 0; i < IA_NPC; i++) p[i] += ub[i * D + f0] * x0;
     if (f1 < D) {
       const double x1 = v.y - mu_part[prune_part1(f1)];
+      n2 += x1 * x1;
 #pragma unroll
       for (int i = 0; i < IA_NPC; i++) p[i] += ub[i * D + f1] * x1;
     }
   }
+  // |a'| (the centred row of the split-f16 DB, k_db_build_h), rounded up: fp64 sum and sqrt
+  // err by < 2^-46 relative, covered by the (1 + 2^-40) factor
+  rnorm[row] = round_up_f(sqrt(n2) * (1.0 + 0x1p-40));
 #pragma unroll
   for (int i = 0; i < IA_NPC; i++) proj[row * IA_NPC + i] = p[i];
   keys[row] = prune_key(p, ub + IA_NPC * D);
@@ -138,7 +143,8 @@ __global__ void __launch_bounds__(PR_WG) k_make_table(const int *__restrict__ so
 
 // K5d': per-tile boxes of the projections (lo[IA_NPC], hi[IA_NPC]) over the tile's real rows
 __global__ void __launch_bounds__(PR_WG) k_tile_boxes(const int *__restrict__ pos2row, const double *__restrict__ proj,
-                                                      int64_t NA, int n_tiles, float *__restrict__ boxes) {
+                                                      int64_t NA, int n_tiles, float *__restrict__ boxes,
+                                                      const float *__restrict__ rnorm, float *__restrict__ tnorm) {
   const int t = blockIdx.x * PR_WG + threadIdx.x;
   if (t >= n_tiles) return;
   double lo[IA_NPC], hi[IA_NPC];
@@ -147,9 +153,11 @@ __global__ void __launch_bounds__(PR_WG) k_tile_boxes(const int *__restrict__ po
     lo[i] = DBL_MAX;
     hi[i] = -DBL_MAX;
   }
+  float rt = 0.f;  // R_t = max |a'| over the tile's real rows (K3p's hi x hi filter, k3p_variant 14/15)
   for (int j = 0; j < IA_TILE; j++) {
     const int row = pos2row[(int64_t)t * IA_TILE + j];
     if (row >= NA) continue;
+    rt = fmaxf(rt, rnorm[row]);
 #pragma unroll
     for (int i = 0; i < IA_NPC; i++) {
       const double v = proj[(int64_t)row * IA_NPC + i];
@@ -163,6 +171,7 @@ __global__ void __launch_bounds__(PR_WG) k_tile_boxes(const int *__restrict__ po
     boxes[(int64_t)t * 2 * IA_NPC + i] = empty ? INFINITY : round_down_f(lo[i]);
     boxes[(int64_t)t * 2 * IA_NPC + IA_NPC + i] = empty ? -INFINITY : round_up_f(hi[i]);
   }
+  tnorm[t] = rt;
 }
 
 // K2s: one sort of a wavefront step's queries for the pruned scan (k3p_variant 11).  One
@@ -281,8 +290,9 @@ void ia_launch_cov(const double *db64, int64_t NA, int64_t stride, int nwg, cons
 }
 
 void ia_launch_proj_keys(const double *db64, int64_t NA, const double *mu_part, const double *basis, double *proj,
-                         unsigned *keys, int *rows, hipStream_t st) {
-  hipLaunchKernelGGL(k_proj_keys, dim3(pr_cdiv(NA, PR_WG)), dim3(PR_WG), 0, st, db64, NA, mu_part, basis, proj, keys, rows);
+                         unsigned *keys, int *rows, float *rnorm, hipStream_t st) {
+  hipLaunchKernelGGL(k_proj_keys, dim3(pr_cdiv(NA, PR_WG)), dim3(PR_WG), 0, st, db64, NA, mu_part, basis, proj, keys, rows,
+                     rnorm);
 }
 
 size_t ia_sort_temp_bytes(int64_t n) {
@@ -298,8 +308,9 @@ int ia_sort_pairs(void *temp, size_t temp_bytes, const unsigned *keys_in, unsign
 }
 
 void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int W, int *pos2row,
-                           float *boxes, hipStream_t st) {
+                           float *boxes, const float *rnorm, float *tnorm, hipStream_t st) {
   hipLaunchKernelGGL(k_make_table, dim3(pr_cdiv((int64_t)n_tiles * IA_TILE, PR_WG)), dim3(PR_WG), 0, st, sorted_rows, NA,
                      n_tiles, W, pos2row);
-  hipLaunchKernelGGL(k_tile_boxes, dim3(pr_cdiv(n_tiles, PR_WG)), dim3(PR_WG), 0, st, pos2row, proj, NA, n_tiles, boxes);
+  hipLaunchKernelGGL(k_tile_boxes, dim3(pr_cdiv(n_tiles, PR_WG)), dim3(PR_WG), 0, st, pos2row, proj, NA, n_tiles, boxes,
+                     rnorm, tnorm);
 }

@@ -73,6 +73,8 @@ typedef struct {
                              * compute_distance's `** 2` (libm pow on a numpy scalar) rounded a
                              * near-midpoint square the other way than y * y does (audit; no
                              * fixture has one) */
+  double dist_pairs_corrected; /* k3p_variant 14/15: pairs whose hi x hi value passed the bound
+                                * (correction products + top-2 epilogue run); else 0 */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),

@@ -69,12 +69,15 @@ def test_batched_levels_match_separate_and_reference(ctx, name, mode):
         assert stb.pruned_levels == len(jb) * (z['L'] - 1)
 
 
-def test_batched_512_pruned_wide_step(ctx):
+@pytest.mark.parametrize('variant', [7, 14])
+def test_batched_512_pruned_wide_step(ctx, variant):
     """3 jobs on a 512^2 level with the pruned scan forced: 513 queries per step in one scan (the
-    separate runs sort 171 per step) - a different kernel path, the same decisions."""
+    separate runs sort 171 per step) - a different kernel path, the same decisions.  variant 14
+    (hi x hi block filter) runs its presorted form 15 on the wide steps."""
     from ia_amd import synth
     job = synth.make_job(512, n_levels=3)
     ctx.set_option('prune_min_rows', 1)
+    ctx.set_option('k3p_variant', variant)
     try:
         z = {'L': job.L, 'A_pyr': job.A_pyr, 'Ap_pyr': job.Ap_pyr_list, 'B_pyr': job.B_pyr, 'weights': job.weights,
              'Bp_init': job.Bp_init}
@@ -84,6 +87,7 @@ def test_batched_512_pruned_wide_step(ctx):
         Ss, IMs, sts = _run(ctx, z, js, False)
     finally:
         ctx.set_option('prune_min_rows', 524288)
+        ctx.set_option('k3p_variant', 7)
     for j in range(len(jb)):
         for level in range(1, job.L):
             assert np.array_equal(Sb[j][level], Ss[j][level]) and np.array_equal(IMb[j][level], IMs[j][level])

@@ -19,9 +19,10 @@ from golden_util import BIG_CASES, E2E_CASES, load_e2e
 pytestmark = pytest.mark.gpu
 
 
-def _run_debug(ctx, z, prune_all=False):
+def _run_debug(ctx, z, prune_all=False, variant=7):
     """prune_all: option prune_min_rows = 1, so every 1-channel level goes through the certified
-    pruned scan (K2p -> K3p) instead of only DB levels of >= 2^19 rows."""
+    pruned scan (K2p -> K3p) instead of only DB levels of >= 2^19 rows; variant:
+    the pruned-scan kernel (14: with the hi x hi block filter)."""
     from ia_amd import _native
     L, k = z['L'], float(z['k'])
     Bp = [x.copy() for x in z['Bp_init']]
@@ -29,6 +30,7 @@ def _run_debug(ctx, z, prune_all=False):
     st = _native.Stats()
     if prune_all:
         ctx.set_option('prune_min_rows', 1)
+    ctx.set_option('k3p_variant', variant)
     try:
         for level in range(1, L):
             kf = 1 + (2 ** (level - L)) * k
@@ -40,20 +42,23 @@ def _run_debug(ctx, z, prune_all=False):
             out[level] = (s, im, dbg)
     finally:
         ctx.set_option('prune_min_rows', 524288)
+        ctx.set_option('k3p_variant', 7)
     return out, Bp, st
 
 
-@pytest.mark.parametrize('prune_all', [False, True], ids=['default', 'pruned'])
+@pytest.mark.parametrize('prune_all,variant', [(False, 7), (True, 7), (True, 14)], ids=['default', 'pruned', 'pruned_hhf'])
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
-def test_debug_records_match_reference_calls(ctx, name, prune_all):
+def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     """Every NN pick, coherence pick and compute_distance value of the reference run.  With
     prune_all, the pruned scan K3p decides every 1-channel level (the bench's
     dominant kernel checked directly against the reference's own per-pixel picks)."""
     z = load_e2e(name)
-    out, Bp, st = _run_debug(ctx, z, prune_all)
+    out, Bp, st = _run_debug(ctx, z, prune_all, variant)
     ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]
     if prune_all:
         assert st.pruned_levels == (z['L'] - 1 if ch == 1 else 0)
+    if variant == 14 and ch == 1:
+        assert 0 < st.dist_pairs_corrected <= st.dist_pairs
     assert st.bound_violations == 0 and st.kappa_ambiguous == 0
     app, coh, dist = [], [], []
     for level in range(1, z['L']):
