@@ -144,7 +144,7 @@ def main():
                     help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select (DIAG=1 builds)')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
-    ap.add_argument('--k3p-variant', type=int, default=7, choices=list(range(16)),
+    ap.add_argument('--k3p-variant', type=int, default=14, choices=list(range(16)),
                     help='pruned-scan kernel version (ia_k3h.hip k3h_prune*; other than 7: DIAG=1 builds): 0 = first version, 1 = boxes in '
                          'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
                          'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks')
@@ -205,7 +205,7 @@ def main():
     if args.k3_variant != 1:
         ctx.set_option('k3_variant', args.k3_variant)       # DIAG=1 builds only
     ctx.set_option('prune', args.prune)
-    if args.k3p_variant != 7:
+    if args.k3p_variant != 14:
         ctx.set_option('k3p_variant', args.k3p_variant)     # DIAG=1 builds only
     ctx.set_option('prune_min_rows', args.prune_min_rows)
     if args.row_source:

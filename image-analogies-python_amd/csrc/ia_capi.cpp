@@ -100,7 +100,7 @@ struct ia_ctx {
   int row_source = 0;            // option "row_source": exact rows from 0 = the fp64 row DB, 1 = the A images
   int shard_emulate = 1;         // option "shard_emulate": W > 1 runs a W-way DB shard on this device
   int matcher = IA_MATCH_F16X3;  // option "matcher"
-  int k3p_variant = 7;           // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
+  int k3p_variant = 14;          // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   // per-step K3 timing (optional)
   int time_dist = 0;
@@ -292,7 +292,8 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
 #else  // product build: the default kernels only (7: pruned scan, 1: packed-index K3h)
-  if (!std::strcmp(name, "k3p_variant")) {  // 7: in-kernel sort up to 512 queries, presorted above; 11: always presorted
+  if (!std::strcmp(name, "k3p_variant")) {  // 14 (default) / 7: in-kernel sort up to 512 queries, presorted (15 / 11)
+                                            // above; 15 / 11: always presorted; 14, 15: hi x hi block filter
     if (value != 7 && value != 11 && value != 14 && value != 15)
       return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14 or 15 (other versions are in DIAG=1 builds only)");
     c->k3p_variant = value;

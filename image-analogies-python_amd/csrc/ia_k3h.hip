@@ -348,8 +348,8 @@ __device__ __forceinline__ void k3p_pairs(const h16x8 (&a)[2 * KS], const h16x8 
 }
 
 // HHF (k3p_variant 14 / 15): each needed (DB tile, query tile) block first runs the hi x hi
-// product alone (4 MFMAs); its two correction products (8 MFMAs) and the top-2 epilogue follow
-// only when some value of the block can lie within its query's bound:
+// product alone (4 MFMAs); its full product (12 MFMAs) and the top-2 epilogue follow only when
+// some value of the block can lie within its query's bound:
 //     c_hh <= lim_q = z_q + R_t (w_q + R_t 2^-9 + 2^-20)
 // where R_t >= max |a'| over the tile's rows and (z_q, w_q) come from K2p (ia_kernels.hip):
 // z_q >= U'_q - |q'|^2 + (rounding terms), w_q >= 2^-8 |q'|.  The hi-only value misses
@@ -365,50 +365,38 @@ __device__ __forceinline__ f32x16 k3p_hh(const h16x8 (&a)[2 * KS], const h16x8 *
   for (int s = 0; s < KS; s++) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], qb[(2 * s) * IA_WAVE], c, 0, 0, 0);
   return c;
 }
-template <int KS>
-__device__ __forceinline__ void k3p_corr(const h16x8 (&a)[2 * KS], const h16x8 *qb, f32x16 &c) {
-#pragma unroll
-  for (int s = 0; s < KS; s++) {
-    const h16x8 xh = qb[(2 * s) * IA_WAVE], xl = qb[(2 * s + 1) * IA_WAVE];
-    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], xh, c, 0, 0, 0);
-    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], xl, c, 0, 0, 0);
-  }
-}
 __device__ __forceinline__ float k3p_min16(const f32x16 &c) {
   const float m0 = fminf(fminf(c[0], c[1]), c[2]), m1 = fminf(fminf(c[3], c[4]), c[5]);
   const float m2 = fminf(fminf(c[6], c[7]), c[8]), m3 = fminf(fminf(c[9], c[10]), c[11]);
   const float m4 = fminf(fminf(c[12], c[13]), c[14]);
   return fminf(fminf(fminf(m0, m1), fminf(m2, m3)), fminf(m4, c[15]));
 }
-// query tiles QP.. of one DB tile t (rt = its R_t; qz = the lane's (z, w) slots, stride 32)
+// HHF, two phases per DB tile: (1) the hi x hi products of every needed block, software-
+// pipelined over two accumulators (the bound test of block q - 1 is issued after the MFMAs of
+// block q, so it overlaps the matrix core) -> the mask of blocks that can hold a value within
+// their query's bound; (2) those blocks only: the full 12-MFMA chains (k3p_pairs, the same
+// product order as v7, so their values and records are v7's) and the top-2 epilogue.
 template <int KS, int QT, int Q>
-__device__ __forceinline__ void k3p_filtered(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, int t, float rt,
-                                             const float *qzt, const float *qzw, float (&b1)[QT], float (&b2)[QT],
-                                             int (&i1)[QT], unsigned &nfull) {
-  if constexpr (Q < QT) {
+__device__ __forceinline__ void k3p_hhpipe(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, float rt,
+                                           const float *qzt, const float *qzw, f32x16 (&acc)[2], unsigned &pass) {
+  if constexpr (Q <= QT) {
     constexpr int NP = 2 * KS;
-    const bool n0 = (msk >> Q) & 1u, n1 = Q + 1 < QT && ((msk >> (Q + 1)) & 1u);  // wave-uniform
-    const h16x8 *qb0 = lq + Q * NP * IA_WAVE, *qb1 = qb0 + NP * IA_WAVE;
-    const float rr = fmaf(rt, 0x1p-9f, 0x1p-20f);
-    f32x16 c0, c1;
-    if (n0) c0 = k3p_hh<KS>(a, qb0);
-    if constexpr (Q + 1 < QT) {
-      if (n1) c1 = k3p_hh<KS>(a, qb1);
+    if constexpr (Q < QT) {
+      if ((msk >> Q) & 1u) acc[Q & 1] = k3p_hh<KS>(a, lq + Q * NP * IA_WAVE);
     }
-    const bool f0 = n0 && __ballot(k3p_min16(c0) <= fmaf(rt, qzw[Q * IA_TILE] + rr, qzt[Q * IA_TILE])) != 0ull;
-    bool f1 = false;
-    if constexpr (Q + 1 < QT)
-      f1 = n1 && __ballot(k3p_min16(c1) <= fmaf(rt, qzw[(Q + 1) * IA_TILE] + rr, qzt[(Q + 1) * IA_TILE])) != 0ull;
-    if (f0) k3p_corr<KS>(a, qb0, c0);
-    if constexpr (Q + 1 < QT) {
-      if (f1) k3p_corr<KS>(a, qb1, c1);
+    if constexpr (Q >= 1) {
+      if ((msk >> (Q - 1)) & 1u) {
+        const float lim = fmaf(rt, qzw[(Q - 1) * IA_TILE] + fmaf(rt, 0x1p-9f, 0x1p-20f), qzt[(Q - 1) * IA_TILE]);
+#if IA_PROBE & 64  // timing only (results invalid): no block passes (bit 31 keeps the test alive)
+        pass |= __ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull ? 1u << 31 : 0u;
+#elif IA_PROBE & 128  // timing only: every block passes (the filter's overhead alone)
+        pass |= (1u << (Q - 1)) | (__ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull ? 1u << 31 : 0u);
+#else
+        pass |= __ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull ? 1u << (Q - 1) : 0u;
+#endif
+      }
     }
-    if (f0) k3p_epi1(c0, t, b1[Q], b2[Q], i1[Q]);
-    if constexpr (Q + 1 < QT) {
-      if (f1) k3p_epi1(c1, t, b1[Q + 1], b2[Q + 1], i1[Q + 1]);
-    }
-    nfull += (unsigned)f0 + (unsigned)f1;
-    k3p_filtered<KS, QT, Q + 2>(a, lq, msk, t, rt, qzt, qzw, b1, b2, i1, nfull);
+    k3p_hhpipe<KS, QT, Q + 1>(a, lq, msk, rt, qzt, qzw, acc, pass);
   }
 }
 
@@ -769,7 +757,7 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // (ia_prune.hip): qf / qinfo hold them in sorted order (fragments; lo, hi, (U', key) per slot),
 // ord_in maps a sorted slot to its query and tbox holds the sorted query tiles' boxes, so phase
 // 1 loads only this launch's slice and phase 2 (sort, scatter, tile boxes) is skipped.
-// HHF (k3p_variant 14 / 15): the hi x hi block filter above (k3p_filtered); the per-WG pair
+// HHF (k3p_variant 14 / 15): the hi x hi block filter above (k3p_hhpipe); the per-WG pair
 // counter slot then holds (pairs with corrections << 32) + box-needed pairs.
 template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false, bool PIPE = false,
           bool PRE = false, bool HHF = false>
@@ -1121,8 +1109,11 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       ld_tile<KS>(nxt, db, tk(kn < K ? kn : k), lane);
       asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
       if constexpr (HHF) {
-        k3p_filtered<KS, QT, 0>(cur, ldsh + lane, m, tk(k), wR[k], qzt + (lane & 31), qzw + (lane & 31), b1, b2, i1,
-                                nfull);
+        f32x16 acc[2];
+        unsigned pass = 0;
+        k3p_hhpipe<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
+        if (pass) k3p_pairs<KS, QT, 0>(cur, ldsh + lane, pass, tk(k), b1, b2, i1);
+        nfull += __popc(pass);
       } else if constexpr (PIPE) {
         f32x16 acc[2];
         k3p_pipe<KS, QT, 0>(cur, ldsh + lane, m, tk(k), b1, b2, i1, acc);

@@ -123,8 +123,10 @@ int ia_version(void);
  * "prune_min_rows" DB rows (default 2^19): (DB tile, query tile) pairs a
  * projection bound proves farther than the query's best coherence candidate are skipped.
  * "k3p_variant" / "k3_variant": kernel versions of DESIGN.md §4b; the product build accepts
- * k3p_variant 7 (default: the pruned scan sorts a step's queries itself up to 512 of them, a
- * step wider than that is sorted once by k_query_sort) or 11 (always presorted) and
+ * k3p_variant 14 (default: the pruned scan sorts a step's queries itself up to 512 of them, a
+ * step wider than that is sorted once by k_query_sort and runs 15; every box-needed block runs
+ * the hi x hi product first and the full product + top-2 only when a value can lie within the
+ * query's bound), 15 (always presorted), 7 / 11 (14 / 15 without that block filter) and
  * k3_variant 1; DIAG=1 builds every version.
  * "row_source" = 0 (exact rows of the rerank / coherence / pruning bound from the fp64 row DB);
  * 1 (gathered from the A-side pyramid images, 1 channel) is in DIAG=1 builds only (slower).

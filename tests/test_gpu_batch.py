@@ -87,7 +87,7 @@ def test_batched_512_pruned_wide_step(ctx, variant):
         Ss, IMs, sts = _run(ctx, z, js, False)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 7)
+        ctx.set_option('k3p_variant', 14)
     for j in range(len(jb)):
         for level in range(1, job.L):
             assert np.array_equal(Sb[j][level], Ss[j][level]) and np.array_equal(IMb[j][level], IMs[j][level])

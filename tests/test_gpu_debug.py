@@ -19,7 +19,7 @@ from golden_util import BIG_CASES, E2E_CASES, load_e2e
 pytestmark = pytest.mark.gpu
 
 
-def _run_debug(ctx, z, prune_all=False, variant=7):
+def _run_debug(ctx, z, prune_all=False, variant=14):
     """prune_all: option prune_min_rows = 1, so every 1-channel level goes through the certified
     pruned scan (K2p -> K3p) instead of only DB levels of >= 2^19 rows; variant:
     the pruned-scan kernel (14: with the hi x hi block filter)."""
@@ -42,11 +42,11 @@ def _run_debug(ctx, z, prune_all=False, variant=7):
             out[level] = (s, im, dbg)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 7)
+        ctx.set_option('k3p_variant', 14)
     return out, Bp, st
 
 
-@pytest.mark.parametrize('prune_all,variant', [(False, 7), (True, 7), (True, 14)], ids=['default', 'pruned', 'pruned_hhf'])
+@pytest.mark.parametrize('prune_all,variant', [(False, 14), (True, 7), (True, 14)], ids=['default', 'pruned_v7', 'pruned'])
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
 def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     """Every NN pick, coherence pick and compute_distance value of the reference run.  With

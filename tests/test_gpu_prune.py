@@ -17,15 +17,14 @@ def _diag_build(ctx):
         ctx.set_option('k3p_variant', 6)
     except _native.IAError:
         return False
-    ctx.set_option('k3p_variant', 7)
+    ctx.set_option('k3p_variant', 14)
     return True
 
 
 def _run(ctx, job, prune, variant=7):
     from ia_amd import _native
     ctx.set_option('prune', prune)
-    if variant != 7:
-        ctx.set_option('k3p_variant', variant)
+    ctx.set_option('k3p_variant', variant)
     ctx.set_option('prune_min_rows', 262144)  # prune the 512^2 level too (default: 1024^2 and up)
     Bp = [x.copy() for x in job.Bp_init]
     S, IM = {}, {}
@@ -38,7 +37,7 @@ def _run(ctx, job, prune, variant=7):
                 Bp[level], job.weights, job.kappa_factor(level), st)
     finally:
         ctx.set_option('prune', 1)
-        ctx.set_option('k3p_variant', 7)
+        ctx.set_option('k3p_variant', 14)
         ctx.set_option('prune_min_rows', 524288)
     return Bp, S, IM, st
 

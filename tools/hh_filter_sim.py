@@ -78,6 +78,8 @@ for step in steps:
                '2^-9*(2Rt|q|+Rt^2)+2^-16 (tile max |a|)': None,
                '2^-9*(2R|q|+R^2)': lambda a, q: 2.0 ** -9 * (2 * R * q + R * R) + 0 * a}
     blocks, passing = 0, {k: 0 for k in margins}
+    tile_need = np.zeros(nt, bool)
+    tile_lo = {k: np.zeros(nt, bool) for k in margins}
     for j in range(-(-M // 32)):
         ids = qorder[j * 32:(j + 1) * 32]
         d = np.maximum(0, np.maximum(blo[None] - Qp[ids, None], Qp[ids, None] - bhi[None]))
@@ -87,6 +89,7 @@ for step in steps:
         rn = xn[pad].reshape(nt, 32)[tiles].reshape(-1)
         d2 = (rows ** 2).sum(axis=1)[:, None] - 2 * rows @ Q[ids].T + (Q[ids] ** 2).sum(axis=1)[None]
         blocks += len(tiles)
+        tile_need[tiles] = True
         Rt = np.repeat(rn.reshape(len(tiles), 32).max(axis=1), 32)
         for k, f in margins.items():
             if f is None:
@@ -95,7 +98,10 @@ for step in steps:
                 E = f(rn[:, None], qn[ids][None])
             hit = (d2 <= Uq[ids][None] + E).reshape(len(tiles), 32, len(ids)).any(axis=(1, 2))
             passing[k] += hit.sum()
+            tile_lo[k][tiles[hit]] = True
     print('step %d M %d: %d box-needed blocks (%.3f of all); pass fraction by margin: %s'
           % (step, M, blocks, blocks / (nt * -(-M // 32)),
              ', '.join('%s %.3f' % (k, v / blocks) for k, v in passing.items())))
     print('  median U %.4f, median |q - mu| %.3f' % (np.median(Uq), np.median(qn)))
+    print('  DB tiles loaded %.3f; of them needing the lo half: %s' % (tile_need.mean(), ', '.join(
+        '%s %.3f' % (k, tile_lo[k].sum() / tile_need.sum()) for k in margins)))
