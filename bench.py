@@ -144,10 +144,12 @@ def main():
                     help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select (DIAG=1 builds)')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
-    ap.add_argument('--k3p-variant', type=int, default=14, choices=list(range(16)),
-                    help='pruned-scan kernel version (ia_k3h.hip k3h_prune*; other than 7: DIAG=1 builds): 0 = first version, 1 = boxes in '
+    ap.add_argument('--k3p-variant', type=int, default=14, choices=list(range(18)),
+                    help='pruned-scan kernel version (ia_k3h.hip k3h_prune*): 0 = first version, 1 = boxes in '
                          'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
-                         'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks')
+                         'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks, 11 = 7 on queries presorted once per step, '
+                         '14 (default) / 15 = 7 / 11 with the hi x hi block filter, 16 / 17 = rotated DB with the '
+                         'principal-axis head filter (DESIGN.md §4f); product builds hold 7, 11, 14-17')
     ap.add_argument('--prune-min-rows', type=int, default=524288,
                     help='smallest DB (rows) the pruned scan is used on (default: the 1024^2 level)')
     ap.add_argument('--row-source', type=int, default=0, choices=[0, 1],
@@ -206,7 +208,7 @@ def main():
         ctx.set_option('k3_variant', args.k3_variant)       # DIAG=1 builds only
     ctx.set_option('prune', args.prune)
     if args.k3p_variant != 14:
-        ctx.set_option('k3p_variant', args.k3p_variant)     # DIAG=1 builds only
+        ctx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15, 17; the rest DIAG=1 builds only
     ctx.set_option('prune_min_rows', args.prune_min_rows)
     if args.row_source:
         ctx.set_option('row_source', args.row_source)
@@ -279,8 +281,13 @@ def main():
         roofline = {'bound': 'hbm', 'achieved': p_gbs, 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s',
                     'frac': p_gbs * 1e9 / HBM_PEAK, 'traffic': traffic,
                     'algorithmic_bytes_per_launch': p_bytes,
-                    'kernel': 'k3h_prune3 (certified pruned scan: PCA-box need tests, split-f16 '
-                              '3 x v_mfma_f32_32x32x16_f16, fused packed-index top-2)',
+                    'kernel': ('k3h_prune3 HF (certified pruned scan on the rotated DB: PCA-box need tests, '
+                               'principal-axis head filter = 3 x v_mfma_f32_32x32x16_f16 over 16 k per box-needed '
+                               'block, full split-f16 chain + packed-index top-2 for the passing blocks; bytes = 2 KiB '
+                               'heads + 8 KiB full-row tiles + boxes, queries, records)'
+                               if st.get('dist_tiles_rows', 0) > 0 else
+                               'k3h_prune3 (certified pruned scan: PCA-box need tests, split-f16 '
+                               '3 x v_mfma_f32_32x32x16_f16, fused packed-index top-2)'),
                     'k3_us_per_launch': st['prune_ms_timed'] * 1e3 / st['prune_launches_timed'],
                     'k3_launches_sampled': st['prune_launches_timed'],
                     'mfma_achieved_tflops': p_tf, 'mfma_peak_tflops': peak / 1e12,
@@ -308,8 +315,12 @@ def main():
     roofline['pairs_frac'] = st['dist_pairs'] / max(st['dist_pairs_full'], 1.)
     if st['dist_pairs_corrected'] > 0:
         # k3p_variant 14/15: every box-needed pair runs the hi x hi product; only this share also
-        # runs the two correction products and the top-2 epilogue (mfma_* above count 3 products)
+        # runs the two correction products and the top-2 epilogue (mfma_* above count 3 products).
+        # 16/17: every box-needed pair runs the 3-product head chain (16 of 64 k); only this share
+        # runs the full chain + epilogue, and only dist_tiles_rows of the heads' tiles load full rows
         roofline['pairs_corrected_frac'] = st['dist_pairs_corrected'] / max(st['dist_pairs'], 1.)
+    if st.get('dist_tiles_rows', 0) > 0:
+        roofline['tiles_rows_frac'] = st['dist_tiles_rows'] / max(st['dist_tiles'], 1.)
     out = {'metric': METRIC, 'value': value, 'unit': "B' px/s", 'n_gpus': world, 'steps': args.steps,
            'warmup': args.warmup, 'ms_per_step': elapsed * 1e3 / args.steps, 'higher_is_better': True,
            'scaling': 'strong' if (args.mode == 'shard' or sw is not None) else 'weak', 'vs_baseline': None,
@@ -340,7 +351,7 @@ def main():
            'stats': {k: st[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
                                         'synth_ms', 'bound_violations', 'kappa_ambiguous', 'f16_levels', 'pruned_levels',
                                         'dist_pairs', 'dist_pairs_full', 'dist_tiles', 'dist_tiles_full',
-                                        'dist_pairs_corrected')}}
+                                        'dist_pairs_corrected', 'dist_tiles_rows')}}
     if sw is not None:
         out['config']['sweep'] = {'jobs': len(sw.jobs), 'batched': not args.sequential, 'max_batch': args.max_batch,
                                   'kappas': sorted({j.k for j in sw.jobs}), 'depths': sorted(set(sw.L))}

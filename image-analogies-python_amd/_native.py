@@ -43,7 +43,8 @@ class Stats(ctypes.Structure):
                 ('dist_tiles', ctypes.c_double), ('dist_tiles_full', ctypes.c_double),
                 ('prune_ms_timed', ctypes.c_double), ('prune_launches_timed', ctypes.c_int64),
                 ('prune_flops_timed', ctypes.c_double), ('prune_bytes_timed', ctypes.c_double),
-                ('kappa_ambiguous', ctypes.c_int64), ('dist_pairs_corrected', ctypes.c_double)]
+                ('kappa_ambiguous', ctypes.c_int64), ('dist_pairs_corrected', ctypes.c_double),
+                ('dist_tiles_rows', ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

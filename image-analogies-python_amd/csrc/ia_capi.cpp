@@ -92,9 +92,11 @@ struct ia_ctx {
   // certified pruned scan (option "prune"): per-level basis, sorted DB table, tile boxes
   DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs, ord;
   DevBuf qs_order, qs_info, qs_frag, qs_tbox;
+  DevBuf pr_rot, pr_lut;  // rotated DB (k3p_variant 16 / 17): R^T (56 x 56) and the home-tile table
   DevBuf tnorm;  // per DB tile of a pruned level: R_t >= max |a'| over its rows (k3p_variant 14/15)  // presorted queries of a step (k3p_variant 11, K2s)
   DevBuf py_in, py_tmp, py_sm, py_mm, py_out;  // GPU preprocessing (ia_gaussian_pyramid, ia_color_matrix)
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
+  std::vector<double> rot_h;     // staging of R^T (rotated DB levels)
   int64_t prune_min_rows = IA_PRUNE_MIN_ROWS;  // option "prune_min_rows": smallest DB that prunes
   int prune = 1;
   int row_source = 0;            // option "row_source": exact rows from 0 = the fp64 row DB, 1 = the A images
@@ -167,7 +169,11 @@ void jacobi_eig(int n, std::vector<double> &A, std::vector<double> &V, std::vect
 // the centred fp64 DB (sampled) -> top IA_NPC eigenvectors (host Jacobi) -> projections and
 // Morton keys of every row -> radix sort -> position -> row table + per-tile projection boxes.
 // Sets g.pos2row; *ufac = the U' factor of ia_prune.h.  One host sync (the covariance).
-int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac) {
+// rot (k3p_variant 16 / 17): also R^T of all 55 axes (c->pr_rot), *eps_r (its
+// deviation from an orthogonal matrix + the fp64 rotation's rounding) and the
+// home-tile table of the sorted keys (c->pr_lut, 2^*lut_bits entries).
+int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac, bool rot = false, double *eps_r = nullptr,
+                  int *lut_bits = nullptr) {
   constexpr int D = 55, NPAIR = D * (D + 1) / 2, NWG_COV = 256;
   const int64_t NA = g.NA, NT = g.n_tiles;
   const int64_t stride = std::max<int64_t>(1, NA / 65536), nsamp = (NA + stride - 1) / stride;
@@ -210,6 +216,33 @@ int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac)
     }
   *ufac = (1.0 + 2.0 * (double)delta + 1e-15) * (1.0 + std::ldexp(1.0, -17)) * (1.0 + std::ldexp(1.0, -19));
   HIP_TRY(hipMemcpyAsync(c->pr_basis.p, c->basis_h.data(), c->basis_h.size() * 8, hipMemcpyHostToDevice, c->st));
+  if (rot) {
+    // R: row f = axis f (eigenvalues descending; rows 0..3 are the basis above, bit for bit),
+    // uploaded transposed with stride 56: rt[g * 56 + f] = R[f][g]
+    constexpr int DS = 56;
+    if ((rc = c->pr_rot.ensure((size_t)DS * DS * 8))) return rc;
+    c->rot_h.assign((size_t)DS * DS, 0.);
+    std::vector<double> Rm((size_t)D * D);
+    for (int f = 0; f < D; f++) {
+      double nrm = 0.;
+      for (int k = 0; k < D; k++) nrm += V[(size_t)k * D + idx[f]] * V[(size_t)k * D + idx[f]];
+      nrm = std::sqrt(nrm);
+      for (int k = 0; k < D; k++) Rm[(size_t)f * D + k] = V[(size_t)k * D + idx[f]] / nrm;
+    }
+    long double dr = 0.L;  // sum |R R^T - I| >= the spectral deviation of R^T R from I
+    for (int i = 0; i < D; i++)
+      for (int j = 0; j < D; j++) {
+        long double gij = 0.L;
+        for (int k = 0; k < D; k++) gij += (long double)Rm[(size_t)i * D + k] * Rm[(size_t)j * D + k];
+        dr += std::fabs((double)(gij - (i == j ? 1.L : 0.L)));
+      }
+    for (int f = 0; f < D; f++)
+      for (int k = 0; k < D; k++) c->rot_h[(size_t)k * DS + f] = Rm[(size_t)f * D + k];
+    // | |a'' - q''|^2 - |a - q|^2 | <= (delta + the fp64 rotation's rounding) (|a'| + |q'|)^2, and the
+    // same for |q''|^2 vs |q'|^2: twice (delta + 1e-12) covers both (55-term fp64 sums: < 1e-13)
+    *eps_r = 2.0 * ((double)dr + 1e-12);
+    HIP_TRY(hipMemcpyAsync(c->pr_rot.p, c->rot_h.data(), c->rot_h.size() * 8, hipMemcpyHostToDevice, c->st));
+  }
   unsigned *keys = c->pr_keys.as<unsigned>();
   int *rows = c->pr_rows.as<int>();
   float *rnorm = reinterpret_cast<float *>(c->pr_proj.as<double>() + NA * IA_NPC);  // |a'| per row, rounded up
@@ -219,6 +252,13 @@ int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac)
     return fail(IA_EHIP, "prepare_prune: radix sort failed");
   ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, W, c->pos2row.as<int>(), c->boxes.as<float>(), rnorm,
                         c->tnorm.as<float>(), c->st);
+  if (rot) {
+    int lb = 8;
+    while (lb < 20 && ((int64_t)1 << lb) < 4 * NA) lb++;
+    if ((rc = c->pr_lut.ensure(((size_t)1 << lb) * 4))) return rc;
+    ia_launch_key_lut(keys + NA, NA, (int)NT, lb, c->pr_lut.as<int>(), c->st);
+    *lut_bits = lb;
+  }
   HIP_TRY(hipGetLastError());
   g.pos2row = c->pos2row.as<int>();
   return IA_OK;
@@ -263,6 +303,7 @@ void ia_destroy(ia_ctx *c) {
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
                     &c->boxes, &c->qinfo, &c->pairs, &c->ord, &c->qs_order, &c->qs_info, &c->qs_frag, &c->qs_tbox, &c->tnorm,
+                    &c->pr_rot, &c->pr_lut,
                     &c->py_in, &c->py_tmp, &c->py_sm, &c->py_mm, &c->py_out})
     b->release();
   for (hipEvent_t e : c->evs) hipEventDestroy(e);
@@ -282,7 +323,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   }
 #ifdef IA_K3H_DIAG  // DIAG=1 builds: every kernel version of DESIGN.md §4b's progression
   if (!std::strcmp(name, "k3p_variant")) {
-    if (value < 0 || value > 15) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..15");
+    if (value < 0 || value > 17) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..17");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -292,10 +333,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
 #else  // product build: the default kernels only (7: pruned scan, 1: packed-index K3h)
-  if (!std::strcmp(name, "k3p_variant")) {  // 14 (default) / 7: in-kernel sort up to 512 queries, presorted (15 / 11)
-                                            // above; 15 / 11: always presorted; 14, 15: hi x hi block filter
-    if (value != 7 && value != 11 && value != 14 && value != 15)
-      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14 or 15 (other versions are in DIAG=1 builds only)");
+  if (!std::strcmp(name, "k3p_variant")) {  // 14 (default) / 15: hi x hi block filter (in-kernel sort up to
+                                            // 512 queries, presorted 15 above); 16 / 17: rotated DB + head
+                                            // filter (sharded levels run 14 / 15); 7 / 11: v7
+    if (value != 7 && value != 11 && value != 14 && value != 15 && value != 16 && value != 17)
+      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14, 15, 16 or 17 (other versions are in DIAG=1 builds only)");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -666,10 +708,19 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   HIP_TRY(hipEventRecord(c->lv0, c->st));
   ia_launch_means(g.ch, Aim, g.n_ap, c->mu.as<double>(), c->st);
   ia_launch_db64_build(g, Aim, c->db64.as<double>(), c->st);  // every row: coherence reads any row
-  double ufac = 0.;
-  if (prune && (rc = prepare_prune(c, g, c->mu.as<double>(), Wsh, &ufac))) return rc;  // sets g.pos2row
+  double ufac = 0., eps_r = 0.;
+  int lut_bits = 0;
+  // rotated DB + head-filtered scan (k3p_variant 16 / 17): unsharded pruned levels whose
+  // workgroups hold <= 512 tiles (the in-kernel tile lists)
+  const bool rot = prune && !multi && (c->k3p_variant == 16 || c->k3p_variant == 17) &&
+                   (g.n_tiles + IA_NWG_H - 1) / IA_NWG_H <= 512;
+  if (prune && (rc = prepare_prune(c, g, c->mu.as<double>(), Wsh, &ufac, rot, &eps_r, &lut_bits)))
+    return rc;  // sets g.pos2row
   if (ns > 0) {
-    if (use_h) ia_launch_db_build_h(g, Aim, c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
+    if (rot)
+      ia_launch_db_build_rot(c->db64.as<double>(), g.NA, g.n_tiles, g.pos2row, c->mu.as<double>(), c->pr_rot.as<double>(),
+                             c->db.p, c->Rbits.as<unsigned>(), c->st);
+    else if (use_h) ia_launch_db_build_h(g, Aim, c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
     else ia_launch_db_build(g, Aim, c->mu.as<double>(), c->db.as<float4>(), c->Rbits.as<unsigned>(), c->st);
   }
   HIP_TRY(hipEventRecord(c->lv1, c->st));
@@ -694,7 +745,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   ma.ufac = ufac;
   ma.img_rows = (c->row_source == 1 && g.ch == 1) ? 1 : 0;
   ma.eps_c = use_h ? ia_eps_c_h(g.KS, prune || c->k3_variant == 1) : ia_eps_c(DP);
-  ma.eps_a = use_h ? ia_eps_a_h() : 0.;
+  ma.eps_a = use_h ? ia_eps_a_h() * (rot ? 2.0 : 1.0) : 0.;  // rot: two norm columns
+  ma.eps_r = eps_r;
+  RotArgs ra{c->pr_rot.as<double>(), c->db.p, c->pr_lut.as<int>(), lut_bits, g.n_tiles, c->Rbits.as<unsigned>(),
+             ma.eps_c, ma.eps_a, eps_r};
   // per shard: its records, decomposition, DB positions (and table / boxes of a pruned level)
   std::vector<MergeArgs> mas(shards.size(), ma);
   std::vector<int64_t> shard_rows(shards.size(), 0);  // real DB rows in each shard (unpruned flops)
@@ -740,7 +794,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     }
     const int Mt = J * sd.M;  // queries of this step over all jobs
     sd.Mpad = (Mt + IA_TILE - 1) / IA_TILE * IA_TILE;
-    if (prune)
+    if (rot)
+      ia_launch_gather_r(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
+                         c->db64.as<double>(), c->pr_basis.as<double>(), ufac, ra, c->qinfo.as<float4>(), Aim, c->st);
+    else if (prune)
       ia_launch_gather_p(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
                          c->db64.as<double>(), c->pr_basis.as<double>(), ufac, c->qinfo.as<float4>(), Aim, ma.img_rows,
                          c->st);
@@ -752,10 +809,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     // pruned scan: queries sorted once per step (K2s) when the step is wider than the in-kernel
     // sort of v6/v7 (512) or variant 11 is selected
     // (variants 11, 12: presorted; 7, 13: in-kernel sort up to 512 queries, presorted v11 / v12 above)
-    const int kv = c->k3p_variant;
-    const int k3v = (kv == 11 || kv == 12 || kv == 15) ? kv
-                    : (prune && sd.Mpad > 512 ? (kv == 13 ? 12 : kv == 14 ? 15 : 11) : kv);
-    const bool presorted = k3v == 11 || k3v == 12 || k3v == 15;
+    const int kv = rot ? c->k3p_variant : (c->k3p_variant == 16 ? 14 : c->k3p_variant == 17 ? 15 : c->k3p_variant);
+    const int k3v = (kv == 11 || kv == 12 || kv == 15 || kv == 17) ? kv
+                    : (prune && sd.Mpad > 512 ? (kv == 13 ? 12 : kv == 14 ? 15 : kv == 16 ? 17 : 11) : kv);
+    const bool presorted = k3v == 11 || k3v == 12 || k3v == 15 || k3v == 17;
     if (prune && presorted)
       ia_launch_query_sort(c->qinfo.as<float4>(), c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
                            c->qs_frag.p, c->qs_tbox.as<float4>(), c->st);
@@ -842,7 +899,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   if (prune) ia_k3p_probe_dump();
 #endif
   if (stats) {
-    unsigned long long ctr[5], prs[4], pfull = 0;
+    unsigned long long ctr[5], prs[4], pfull = 0, prow[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
     {  // per-workgroup counter slots (no same-address atomics in the distance kernel)
       std::vector<unsigned long long> slots(4 * IA_NWG_H);
@@ -854,6 +911,9 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           if (j < 2) {  // pair slots: (pairs with corrections << 32) + pairs (k3p_variant 14/15)
             prs[j] += v & 0xffffffffull;
             pfull += v >> 32;
+          } else if (rot) {  // tile slots of the rotated scan: (full-row tiles << 32) + heads
+            prs[j] += v & 0xffffffffull;
+            prow[j] += v >> 32;
           } else {
             prs[j] += v;
           }
@@ -871,6 +931,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     stats->dist_tiles += prune ? (double)(prs[2] + prs[3]) : tiles_full;
     stats->dist_tiles_full += tiles_full;
     stats->dist_pairs_corrected += (double)pfull;
+    stats->dist_tiles_rows += (double)(prow[2] + prow[3]);
     float ms_db = 0.f, ms_syn = 0.f;
     hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
     hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);
@@ -900,7 +961,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         stats->prune_ms_timed += tot;
         stats->prune_launches_timed += launches_timed;
         stats->prune_flops_timed += flops_timed;
-        stats->prune_bytes_timed += (double)prs[3] * ia_k3h_tile_bytes(g.KS) + bytes_timed_fixed;
+        // rotated scan: 2 KiB heads + 8 KiB (head + tail) of the full-row tiles
+        stats->prune_bytes_timed += (rot ? 2048.0 * (double)prs[3] + 8192.0 * (double)prow[3]
+                                         : (double)prs[3] * ia_k3h_tile_bytes(g.KS)) +
+                                    bytes_timed_fixed;
       }
     }
   }

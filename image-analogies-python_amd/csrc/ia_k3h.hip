@@ -400,6 +400,42 @@ __device__ __forceinline__ void k3p_hhpipe(const h16x8 (&a)[2 * KS], const h16x8
   }
 }
 
+// HF (k3p_variant 16 / 17): the rotated DB (ia_internal.h).  A tile's head is
+// its k-step 0 (2 pieces, 2 KiB), its tail the other 6 (6 KiB, a separate array after the NT
+// heads).  The head chain (3 MFMAs) of a (DB tile, query tile) block yields the 15-axis partial
+// distance minus |q''_h|^2; a lane's 16 values belong to its query (lane & 31), whose z0 (K2r)
+// bounds every value a row within the query's U' can have.
+__device__ __forceinline__ void ld_head(h16x8 (&h)[2], const h16x8 *__restrict__ db, int64_t tile, int lane) {
+  const h16x8 *src = db + tile * 2 * IA_WAVE;
+  h[0] = src[lane];
+  h[1] = src[IA_WAVE + lane];
+}
+template <int KS>
+__device__ __forceinline__ void ld_rtile(h16x8 (&a)[2 * KS], const h16x8 *__restrict__ db, int64_t NT, int64_t tile, int lane) {
+  static_assert(KS == 4, "rotated DB: 1 channel");
+  const h16x8 *hs = db + tile * 2 * IA_WAVE;
+  const h16x8 *ts = db + NT * 2 * IA_WAVE + tile * 6 * IA_WAVE;
+  a[0] = hs[lane];
+  a[1] = hs[IA_WAVE + lane];
+#pragma unroll
+  for (int p = 2; p < 2 * KS; p++) a[p] = ts[(p - 2) * IA_WAVE + lane];
+}
+template <int KS, int QT, int Q>
+__device__ __forceinline__ void k3f_headpipe(const h16x8 (&hd)[2], const h16x8 *lq, unsigned msk, const float *qz0,
+                                             f32x16 (&acc)[2], unsigned &pass) {
+  if constexpr (Q <= QT) {
+    constexpr int NP = 2 * KS;
+    if constexpr (Q < QT) {
+      if ((msk >> Q) & 1u) acc[Q & 1] = k3p_chain<1>(hd, lq + Q * NP * IA_WAVE);
+    }
+    if constexpr (Q >= 1) {
+      if ((msk >> (Q - 1)) & 1u)
+        pass |= __ballot(k3p_min16(acc[(Q - 1) & 1]) <= qz0[(Q - 1) * IA_TILE]) != 0ull ? 1u << (Q - 1) : 0u;
+    }
+    k3f_headpipe<KS, QT, Q + 1>(hd, lq, msk, qz0, acc, pass);
+  }
+}
+
 // V (option "k3p_variant"): 0 = per-tile box loads and a full-key rank sort (first version);
 // 1 = the wave's tile boxes held in registers (one coalesced load per 64 tiles, read back with
 // v_readlane: the tile walk has no memory latency left), unique 20-bit-key rank sort;
@@ -760,7 +796,7 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // HHF (k3p_variant 14 / 15): the hi x hi block filter above (k3p_hhpipe); the per-WG pair
 // counter slot then holds (pairs with corrections << 32) + box-needed pairs.
 template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false, bool PIPE = false,
-          bool PRE = false, bool HHF = false>
+          bool PRE = false, bool HHF = false, bool HF = false>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
@@ -797,12 +833,12 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = qt0 * IA_TILE;
-  unsigned long long ph[6] = {0, 0, 0, 0, 0, 0};
+  unsigned long long ph[7] = {0, 0, 0, 0, 0, 0, 0};
   K3P_T(ph[0]);
 
   // ---- 1. one global round
   h16x8 a[NP], an[NP], an2[NP];
-  if constexpr (!(INTER && NBUF == 1)) {
+  if constexpr (!(INTER && NBUF == 1) && !HF) {
     ld_tile<KS>(a, db, tk(min(wave, K - 1)), lane);
   }
   if constexpr (PRE) {
@@ -816,7 +852,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       qhi[x] = ok ? qinfo[3 * sl + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 u = ok ? qinfo[3 * sl + 2] : make_float4(-INFINITY, 0.f, -INFINITY, 0.f);
       qU[x] = u.x;
-      if constexpr (HHF) {
+      if constexpr (HHF || HF) {
         qzt[x] = u.z;
         qzw[x] = u.w;
       }
@@ -919,7 +955,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         qlo[x] = mlo;
         qhi[x] = mhi;
         qU[x] = mU;
-        if constexpr (HHF) {
+        if constexpr (HHF || HF) {
           qzt[x] = mzt;
           qzw[x] = mzw;
         }
@@ -960,7 +996,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         qlo[x] = mlo;
         qhi[x] = mhi;
         qU[x] = mU;
-        if constexpr (HHF) {
+        if constexpr (HHF || HF) {
           qzt[x] = mzt;
           qzw[x] = mzw;
         }
@@ -979,7 +1015,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       qlo[x] = mlo;
       qhi[x] = mhi;
       qU[x] = mU;
-      if constexpr (HHF) {
+      if constexpr (HHF || HF) {
         qzt[x] = mzt;
         qzw[x] = mzw;
       }
@@ -1035,7 +1071,132 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     i1[q] = 0x7fffffff;
   }
   unsigned cnt = 0, ntl = 0, nfull = 0;
-  if constexpr (INTER) {
+  int nitems_wg = 0;  // HF: tiles whose full rows were loaded
+  if constexpr (HF) {
+    // ---- HF (k3p_variant 16 / 17), three list phases with deterministic item ->
+    // wave assignment (item j -> wave j mod NW), so no phase waits on a dependent load:
+    //   0. box need masks of all the workgroup's tiles (wave v: tiles v, v + NW, ...), the needed
+    //      tiles compacted in tile order;
+    //   1. their heads (2 KiB) streamed three items ahead; per needed block the 3-MFMA head
+    //      chain and the z0 test -> pass mask per tile; the passing tiles compacted in order;
+    //   2. their full rows (head + tail, 8 KiB) two items ahead; the full 12-MFMA chains and the
+    //      packed top-2 epilogue of the passing blocks.
+    unsigned *kpass = reinterpret_cast<unsigned *>(wR);  // [K] pass mask per tile
+    int *items2 = reinterpret_cast<int *>(wR + K);        // [K] passing tiles, in order
+    {
+      // box need masks as the !INTER path: the query-tile box test (lane q < QT), then per
+      // needed pair of query tiles the per-query test with the lane's query intervals held in
+      // registers (no LDS reads in the loop)
+      float4 fl[NPAIR], fh[NPAIR];
+      float fu[NPAIR];
+#pragma unroll
+      for (int pr = 0; pr < NPAIR; pr++) {
+        const int jq = 2 * pr + half, x = jq * IA_TILE + (lane & 31);
+        fl[pr] = jq < QT ? qlo[x] : make_float4(0.f, 0.f, 0.f, 0.f);
+        fh[pr] = jq < QT ? qhi[x] : make_float4(0.f, 0.f, 0.f, 0.f);
+        fu[pr] = jq < QT ? qU[x] : -INFINITY;
+      }
+      const bool cl = lane < QT;
+      const float4 ctl = cl ? tlo[lane] : make_float4(0.f, 0.f, 0.f, 0.f), cth = cl ? thi[lane] : ctl;
+      const float ctu = cl ? tU[lane] : -INFINITY;
+      for (int k = wave; k < K; k += NW) {
+        const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
+        const unsigned coarse = (unsigned)__ballot(cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
+        unsigned msk = 0;
+#pragma unroll
+        for (int pr = 0; pr < NPAIR; pr++) {
+          if ((coarse >> (2 * pr)) & 3u) {
+            const unsigned long long b = __ballot(prune_lb(blo, bhi, fl[pr], fh[pr]) <= fu[pr]);
+            msk |= (((unsigned)b != 0u ? 1u : 0u) | ((unsigned)(b >> 32) != 0u ? 2u : 0u)) << (2 * pr);
+          }
+        }
+        if (lane == 0) {
+          kmask[k] = msk & coarse;
+          kpass[k] = 0u;
+        }
+      }
+    }
+    // ordered compaction of the tiles k < K with pred(k) into list[]: returns the count
+    auto compact = [&](auto pred, int *list) -> int {
+      __syncthreads();
+      const bool nd = tid < K && pred(tid);
+      const unsigned long long b = __ballot(nd);
+      const int pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
+      if (lane == 0) wcnt[wave] = __popcll(b);
+      __syncthreads();
+      int base = 0, n = 0;
+#pragma unroll
+      for (int w = 0; w < NW; w++) {
+        base += w < wave ? wcnt[w] : 0;
+        n += wcnt[w];
+      }
+      if (nd) list[base + pre] = tid;
+      __syncthreads();
+      return n;
+    };
+    const int n1 = compact([&](int k) { return kmask[k] != 0u; }, items);
+    K3P_T(ph[3]);
+    int j = wave;
+    if (j < n1) {
+      auto itm = [&](int jj) { return tk(items[jj < n1 ? jj : n1 - 1]); };  // past the end: the last item again
+      // six head buffers in rotation, five items ahead (the compiler's wait at the loop's top
+      // is one item conservative, so the effective depth is four)
+      h16x8 g0[2], g1[2], g2[2], g3[2], g4[2], g5[2];
+      ld_head(g0, db, itm(j), lane);
+      ld_head(g1, db, itm(j + NW), lane);
+      ld_head(g2, db, itm(j + 2 * NW), lane);
+      ld_head(g3, db, itm(j + 3 * NW), lane);
+      ld_head(g4, db, itm(j + 4 * NW), lane);
+      auto hs = [&](const h16x8(&cur)[2], h16x8(&nx5)[2], int jj) {
+        ld_head(nx5, db, itm(jj + 5 * NW), lane);  // unconditional: equal vmcnt on every path
+        asm volatile("" ::: "memory");
+        const int k = items[jj];
+        const unsigned m = kmask[k];
+        f32x16 acc[2];
+        unsigned pass = 0;
+        k3f_headpipe<KS, QT, 0>(cur, ldsh + lane, m, qzt + (lane & 31), acc, pass);
+        if (lane == 0) kpass[k] = pass;
+        cnt += __popc(m);
+        nfull += __popc(pass);
+        ntl++;
+      };
+      for (; j < n1; j += 6 * NW) {
+        hs(g0, g5, j);
+        if (j + NW >= n1) break;
+        hs(g1, g0, j + NW);
+        if (j + 2 * NW >= n1) break;
+        hs(g2, g1, j + 2 * NW);
+        if (j + 3 * NW >= n1) break;
+        hs(g3, g2, j + 3 * NW);
+        if (j + 4 * NW >= n1) break;
+        hs(g4, g3, j + 4 * NW);
+        if (j + 5 * NW >= n1) break;
+        hs(g5, g4, j + 5 * NW);
+      }
+    }
+    K3P_T(ph[6]);
+    const int n2 = compact([&](int k) { return kpass[k] != 0u; }, items2);
+    nitems_wg = n2;
+    j = wave;
+    if (j < n2) {
+      auto itm2 = [&](int jj) { return tk(items2[jj < n2 ? jj : n2 - 1]); };
+      ld_rtile<KS>(a, db, NT, itm2(j), lane);
+      ld_rtile<KS>(an, db, NT, itm2(j + NW), lane);
+      auto fs = [&](const h16x8(&cur)[NP], h16x8(&nx2)[NP], int jj) {
+        ld_rtile<KS>(nx2, db, NT, itm2(jj + 2 * NW), lane);
+        asm volatile("" ::: "memory");
+        const int k = items2[jj];
+        k3p_pairs<KS, QT, 0>(cur, ldsh + lane, kpass[k], tk(k), b1, b2, i1);
+      };
+      for (; j < n2; j += 3 * NW) {
+        fs(a, an2, j);
+        if (j + NW >= n2) break;
+        fs(an, a, j + NW);
+        if (j + 2 * NW >= n2) break;
+        fs(an2, an, j + 2 * NW);
+      }
+    }
+  } else if constexpr (INTER) {
     K3P_T(ph[3]);
     // ---- 3'/4'. need tests interleaved with the contraction: wave v walks tiles k = v mod NW;
     // while tile k is contracted, the next needed tile's load is in flight and the need tests
@@ -1270,8 +1431,8 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       st += wtiles[w];
       sf += wfull[w];
     }
-    pairs[wg] += sp + (HHF ? sf << 32 : 0ull);
-    tiles[wg] += st;
+    pairs[wg] += sp + (HHF || HF ? sf << 32 : 0ull);
+    tiles[wg] += st + (HF ? (unsigned long long)nitems_wg << 32 : 0ull);
   }
 #if IA_PROBE & 16
   K3P_T(ph[5]);
@@ -1281,6 +1442,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     atomicAdd(&k3p_prof[2], ph[3] - ph[2]);
     atomicAdd(&k3p_prof[3], ph[4] - ph[3]);
     atomicAdd(&k3p_prof[7], ph[5] - ph[4]);
+    if (HF) atomicAdd(&k3p_prof[8], ph[6] - ph[3]);  // HF: phase 1 (heads); [3] - [8] = phase 2
     atomicAdd(&k3p_prof[4], 1ull);
     atomicAdd(&k3p_prof[5], (unsigned long long)ntl);
     atomicAdd(&k3p_prof[6], (unsigned long long)cnt);
@@ -1296,7 +1458,8 @@ void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau w
     fprintf(stderr, "K3P_PROBE write phase: merge=%.0f pos2row=%.0f stores=%.0f atomics=%.0f\n", (double)v[7] / v[10],
             (double)v[8] / v[10], (double)v[9] / v[10], (double)v[11] / v[10]);
   fprintf(stderr, "K3P_PROBE v3 phases if variant>=3: load=setup, sort+scatter=need, need=loop, loop=tail, tail=[7]\n");
-  fprintf(stderr, "K3P_PROBE [7]=%.0f\n", (double)v[7] / v[4]);
+  fprintf(stderr, "K3P_PROBE [7]=%.0f [8]=%.0f (HF: [8] = phase 1, loop - [8] = phase 2)\n", (double)v[7] / v[4],
+          (double)v[8] / v[4]);
   fprintf(stderr, "K3P_PROBE waves=%llu setup=%.0f need=%.0f loop=%.0f tail=%.0f tiles/wave=%.2f pairs/wave=%.2f (cycles/wave)\n",
           v[4], (double)v[0] / v[4], (double)v[1] / v[4], (double)v[2] / v[4], (double)v[3] / v[4], (double)v[5] / v[4],
           (double)v[6] / v[4]);
@@ -1329,6 +1492,8 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true>;
     if (variant == 14) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true>;
     if (variant == 15) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true>;
+    if (variant == 16) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, false, true>;
+    if (variant == 17) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, false, true>;
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

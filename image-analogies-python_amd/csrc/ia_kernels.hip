@@ -34,6 +34,12 @@
 #else
 #define IA_STAMP(k) do { } while (0)
 #endif
+#if IA_PROBE & 256  // diagnostic build only: s_memtime phase stamps of sampled K2r waves
+#define IA_STAMP2(k) do { __builtin_amdgcn_sched_barrier(0); st2[k] = __builtin_amdgcn_s_memtime(); \
+                          __builtin_amdgcn_sched_barrier(0); } while (0)
+#else
+#define IA_STAMP2(k) do { } while (0)
+#endif
 
 
 // ------------------------------------------------------------------------------------------
@@ -830,7 +836,8 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
   for (int j = 0; j < RPL; j++) a1 = fminf(a1, v1[j]);
   a1 = wave_min_f(a1);
   const double qn = sqrt(qn2);
-  const double eps = a.eps_c * (R * R + 2.0 * R * qn) + a.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0);
+  const double eps = a.eps_c * (R * R + 2.0 * R * qn) + a.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0) +
+                     a.eps_r * (R + qn) * (R + qn);
   const double thr = (double)a1 + 2.0 * eps;
 
   // rerank every listed candidate that could be the exact winner
@@ -1195,6 +1202,169 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
   }
 }
 
+// ------------------------------------------------------------------------------------------
+// K2r: K2p for the rotated DB and its head-filtered scan (k3p_variant 16 / 17),
+// one wave per query.  Lane c of the wave owns MFMA column c:
+//   * q' (centred, fp64) in LDS; q''_f = sum_g R[f][g] q'_g (lane f < 55, coalesced reads of R^T)
+//   * fragments -2 q'' in the rotated column order (ia_rot_col), 256 in both norm columns
+//   * the pruning record as K2p (projections = q''_0..3, Morton key), with a tighter bound U:
+//     besides the coherence candidates' exact distances, the rows of the query's home tiles
+//     (k_key_lut: the Morton tile where its key falls, +-1; the causal neighbour's home tiles,
+//     whose loads could start with the kernel, gave a looser bound: 43 % instead of 27 % of
+//     the tiles' full rows loaded at 1024^2) are evaluated in f32 from their hi + lo parts;
+//     each gives a rigorous upper bound of the exact distance of a DB row
+//       sqrt(|a - q|^2) <= sqrt(d32) (1 + 2^-17) + 2^-20 (R + |q'| + 1)  (rotated space:
+//       hi + lo within 2^-22 |a''| + 2^-25 per column, f32 q'' within 2^-24, f32 sums within
+//       gamma_64), plus eps_r (R + |q'|)^2 back to unrotated distances
+//   * z0 = U' - |q''_h|^2 + eps + eps_r (R + |q'|)^2: a head value V0 > z0 proves every row of
+//     the value's (row, query) pair farther than U' (K3f's head filter)
+// ------------------------------------------------------------------------------------------
+template <bool IMG, class JS>
+__global__ void __launch_bounds__(IA_WG) k_gather_query_r(LevelGeo g, StepDesc sd, Imgs B, JS jobs,
+                                                          const double *__restrict__ mu_part,
+                                                          double *__restrict__ q64, double *__restrict__ qn2,
+                                                          _Float16 *__restrict__ qf, const double *__restrict__ db64,
+                                                          const double *__restrict__ basis, double ufac, RotArgs ra,
+                                                          float4 *__restrict__ qinfo, Imgs A) {
+  constexpr int D = 55, DS = 56, KS = 4, NWV = IA_WG / IA_WAVE;
+  __shared__ double qsh[NWV][DS], qcs[NWV][DS];
+  __shared__ float qcol[NWV][IA_WAVE];
+  __shared__ double rts[DS * DS];  // R^T of the level (staged once per workgroup, before any exit)
+#if IA_PROBE & 256
+  unsigned long long st2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#endif
+  IA_STAMP2(0);
+  for (int i = threadIdx.x; i < DS * DS / 2; i += IA_WG)
+    reinterpret_cast<double2 *>(rts)[i] = reinterpret_cast<const double2 *>(ra.rt)[i];
+  __syncthreads();
+  IA_STAMP2(1);
+  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int m = blockIdx.x * NWV + wv;
+  if (m >= sd.Mpad) return;
+  if (m >= sd.J * sd.M) {
+    put_qh<KS>(qf, m, lane, 0.);
+    if (lane == 0) {
+      qinfo[3 * m] = make_float4(0.f, 0.f, 0.f, 0.f);
+      qinfo[3 * m + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
+      qinfo[3 * m + 2] = make_float4(-INFINITY, __uint_as_float(IA_PRUNE_KEY_PAD), -INFINITY, 0.f);
+    }
+    return;
+  }
+  const QPix px = ia_qpix(sd, g.bw, m);
+  const JobPtrs jp = jobs.get(px.job);
+  if constexpr (!JS::single) B = job_imgs(B, jp);
+  const int32_t *__restrict__ s = jp.s, *__restrict__ im = jp.im;
+  const int r = px.r, c = px.c, qi = px.qi;
+  int crow = -1;
+  if (qi > 0 && lane < 15) {
+    const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
+    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
+      const int nb = nr * g.bw + nc;
+      const int tr = s[2 * nb] + r - nr, tc = s[2 * nb + 1] + c - nc;
+      if (tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) crow = (im[nb] * g.ah + tr) * g.aw + tc;
+    }
+  }
+  double ss = 0.;
+  if (lane < D) {
+    const double v = feat<1>(B, lane, r, c, 0);
+    q64[(int64_t)m * D + lane] = v;
+    qsh[wv][lane] = v;
+    const double qc = v - mu_part[feat_part<1>(lane)];
+    qcs[wv][lane] = qc;
+    ss = qc * qc;
+  } else if (lane == D) {
+    qcs[wv][lane] = 0.;
+  }
+  ss = wave_sum_d(ss);
+  IA_STAMP2(2);
+  __builtin_amdgcn_wave_barrier();  // qsh / qcs written by this wave's lanes, read below
+  double y = 0.;  // q''_lane (lanes < 55)
+  if (lane < DS) {
+#pragma unroll 8
+    for (int gg = 0; gg < D; gg++) y = fma(rts[gg * DS + lane], qcs[wv][gg], y);
+  }
+  // column c = lane: axis ia_rot_col^-1(c), or a norm / padding column
+  const bool pcol = lane != IA_ROT_HNORM && lane < IA_ROT_TNORM;
+  const double yc = __shfl(y, lane < IA_ROT_HNORM ? lane : lane - 1, 64);
+  put_qh<KS>(qf, m, lane, pcol ? -2.0 * yc : (lane == IA_ROT_HNORM || lane == IA_ROT_TNORM) ? IA_NORM_SCALE : 0.);
+  qcol[wv][lane] = pcol ? (float)yc : 0.f;
+  const double hs = wave_sum_d(lane < IA_ROT_HNORM ? y * y : 0.);  // |q''_h|^2
+  double p[IA_NPC];
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) p[i] = __shfl(y, i, 64);
+  const unsigned key = prune_key(p, basis + IA_NPC * D);
+  IA_STAMP2(3);
+  // the key's home tile (one table load) and its two neighbours: rows' f32 distances from hi + lo
+  const int hp = ra.lut[key >> (32 - ra.lb)];
+  const h16x8 *__restrict__ hd = reinterpret_cast<const h16x8 *>(ra.db);
+  const h16x8 *__restrict__ tl = hd + (int64_t)ra.NT * 2 * IA_WAVE;
+  h16x8 pc[3][8];
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    int t = hp - 1 + k;
+    t = t < 0 ? 0 : t >= ra.NT ? ra.NT - 1 : t;
+    pc[k][0] = hd[(t * 2 + 0) * IA_WAVE + lane];
+    pc[k][1] = hd[(t * 2 + 1) * IA_WAVE + lane];
+#pragma unroll
+    for (int q = 0; q < 6; q++) pc[k][2 + q] = tl[((int64_t)t * 6 + q) * IA_WAVE + lane];
+  }
+  double u = DBL_MAX;
+  if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh[wv], IMG ? &A : nullptr);
+  u = wave_min_d_x(u);
+  IA_STAMP2(4);
+  __builtin_amdgcn_wave_barrier();  // qcol
+  const int hh = lane >> 5;
+  float best = INFINITY;
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    float part = 0.f;
+#pragma unroll
+    for (int st = 0; st < 4; st++) {
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const int cc = 16 * st + 8 * hh + e;
+        const float x = (float)pc[k][2 * st][e] + (float)pc[k][2 * st + 1][e];
+        const float d = x - qcol[wv][cc];
+        const bool use = !((st == 0 && hh == 1 && e == 7) || (st == 3 && hh == 1));
+        part = use ? fmaf(d, d, part) : part;
+      }
+    }
+    const bool padh = hh == 1 && (float)pc[k][0][7] >= 50000.f;  // head norm column of a padding row
+    const bool pad = padh || __shfl_xor((int)padh, 32, 64);
+    const float tot = part + __shfl_xor(part, 32, 64);
+    if (!pad) best = fminf(best, tot);
+  }
+  best = wave_min_f_x(best);
+  IA_STAMP2(5);
+  const double R = (double)__uint_as_float(*ra.Rbits);
+  const double qn = sqrt(ss);
+  const double er = ra.eps_r * (R + qn) * (R + qn);
+  if (best < INFINITY) {
+    const double sq = sqrt((double)best) * (1.0 + 0x1p-17) + 0x1p-20 * (R + qn + 1.0);
+    u = fmin(u, sq * sq * (1.0 + 0x1p-40) + er);
+  }
+  if (lane == 0) {
+    qn2[m] = ss;
+    qinfo[3 * m] = make_float4(round_down_f(p[0] - IA_PRUNE_MABS), round_down_f(p[1] - IA_PRUNE_MABS),
+                               round_down_f(p[2] - IA_PRUNE_MABS), round_down_f(p[3] - IA_PRUNE_MABS));
+    qinfo[3 * m + 1] = make_float4(round_up_f(p[0] + IA_PRUNE_MABS), round_up_f(p[1] + IA_PRUNE_MABS),
+                                   round_up_f(p[2] + IA_PRUNE_MABS), round_up_f(p[3] + IA_PRUNE_MABS));
+    const bool fin = u < DBL_MAX;
+    const float up = fin ? round_up_f(u * ufac) : INFINITY;
+    const double eps = ra.eps_c * (R * R + 2.0 * R * qn) + ra.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0);
+    const float z0 = fin ? round_up_f(((double)up - hs * (1.0 - 1e-12) + eps + er) * (1.0 + 1e-12)) : INFINITY;
+    qinfo[3 * m + 2] = make_float4(up, __uint_as_float(fin ? key : IA_PRUNE_KEY_INF), z0, 0.f);
+  }
+#if IA_PROBE & 256
+  if (lane == 0 && m == sd.M / 2 && (sd.t % 256) == 128) {
+    __builtin_amdgcn_s_waitcnt(0);
+    const unsigned long long t6 = __builtin_amdgcn_s_memtime();
+    printf("K2R t=%d M=%d stage=%llu feat=%llu rot+key=%llu coh=%llu u2=%llu end=%llu\n", sd.t, sd.M, st2[1] - st2[0],
+           st2[2] - st2[1], st2[3] - st2[2], st2[4] - st2[3], st2[5] - st2[4], t6 - st2[5]);
+  }
+#endif
+}
+
 // Fused single-rank merge of query m: certified exact NN + coherence + kappa + writeback.
 // Memory is touched in two dependent rounds: (1) the K3 records, the coherence neighbours'
 // s/im and the query/weights (staged in LDS), (2) ONE fp64-DB row per lane, in which lane
@@ -1271,7 +1441,8 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   for (int j = 0; j < RPL; j++) a1 = fminf(a1, v1[j]);
   a1 = wave_min_f_x(a1);
   const double qn = sqrt(qn2);
-  const double eps = a.eps_c * (R * R + 2.0 * R * qn) + a.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0);
+  const double eps = a.eps_c * (R * R + 2.0 * R * qn) + a.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0) +
+                     a.eps_r * (R + qn) * (R + qn);
   const double thr = (double)a1 + 2.0 * eps;
   unsigned cmask = 0;
 #pragma unroll
@@ -2007,6 +2178,18 @@ void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
   launch_gather_p_t<false>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, st);
 }
 
+void ia_launch_gather_r(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
+                        double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
+                        const RotArgs &ra, float4 *qinfo, const Imgs &A, hipStream_t st) {
+  const dim3 grid(cdiv(sd.Mpad, IA_WG / IA_WAVE));
+  if (jobs.J == 1)
+    hipLaunchKernelGGL((k_gather_query_r<false, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, job0_imgs(B, jobs),
+                       JobArg1{jobs.j0}, mu, q64, qn2, (_Float16 *)qf, db64, basis, ufac, ra, qinfo, A);
+  else
+    hipLaunchKernelGGL((k_gather_query_r<false, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64,
+                       qn2, (_Float16 *)qf, db64, basis, ufac, ra, qinfo, A);
+}
+
 // split-f16 distance kernels live in ia_k3h.hip, compiled once per (KS, QT) instance
 #define IA_K3H_DECL(ks, qt) k3h_fn ia_k3h_get_##ks##_##qt(int variant);
 IA_K3H_DECL(4, 1) IA_K3H_DECL(4, 2) IA_K3H_DECL(4, 3) IA_K3H_DECL(4, 4) IA_K3H_DECL(4, 5) IA_K3H_DECL(4, 6)
@@ -2058,18 +2241,21 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   if (variant == 10) variant = 9;  // 9: 6 + pipelined single chains; 10: 9 + reverse walks
   if ((variant < 11 || variant == 13 || variant == 14) && variant >= 3 && (Mpad > 512 || kmax > 512))
     variant = variant == 14 && Mpad > 512 ? 15 : 1;  // in-kernel sort: <= 512 (14 -> 15: the host ran K2s)
+  if (variant == 16 && Mpad > 512) variant = 17;   // rotated DB (the host keeps kmax <= 512 there)
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t NQ = (size_t)qt * IA_TILE;
-  const bool pre = variant == 11 || variant == 12 || variant == 15, hhf = variant == 14 || variant == 15;
+  const bool pre = variant == 11 || variant == 12 || variant == 15 || variant == 17;
+  const bool hhf = variant == 14 || variant == 15 || variant == 16 || variant == 17;
   const int nthr = variant == 12 || variant == 13 ? 16 * IA_WAVE : IA_WGH;  // v12/13: 16 waves (4 per SIMD), one tile buffer
   size_t lds = pre ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 +
                          (size_t)kmax * 40
                    : ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
   if (hhf) lds += NQ * 8 + (size_t)kmax * 4;  // (z, w) per sorted query slot, R_t per tile
+  if (variant == 16 || variant == 17) lds += (size_t)kmax * 4;  // HF: pass masks + passing-tile list
   const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
   lds = lds > red ? lds : red;
-  static int attr_lds[16][16] = {};
-  const int vi = variant < 0 || variant > 15 ? 1 : variant;
+  static int attr_lds[18][16] = {};
+  const int vi = variant < 0 || variant > 17 ? 1 : variant;
   if ((int)lds > attr_lds[vi][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
     (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     attr_lds[vi][qt] = (int)lds;

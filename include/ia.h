@@ -74,7 +74,10 @@ typedef struct {
                              * near-midpoint square the other way than y * y does (audit; no
                              * fixture has one) */
   double dist_pairs_corrected; /* k3p_variant 14/15: pairs whose hi x hi value passed the bound
-                                * (correction products + top-2 epilogue run); else 0 */
+                                * (correction products + top-2 epilogue run); 16/17: pairs whose
+                                * head (15-axis partial distance) passed; else 0 */
+  double dist_tiles_rows;   /* k3p_variant 16/17: DB tiles whose full rows were loaded after the
+                             * head filter (dist_tiles counts the heads); else 0 */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),

@@ -69,11 +69,12 @@ def test_batched_levels_match_separate_and_reference(ctx, name, mode):
         assert stb.pruned_levels == len(jb) * (z['L'] - 1)
 
 
-@pytest.mark.parametrize('variant', [7, 14])
+@pytest.mark.parametrize('variant', [7, 14, 16])
 def test_batched_512_pruned_wide_step(ctx, variant):
     """3 jobs on a 512^2 level with the pruned scan forced: 513 queries per step in one scan (the
     separate runs sort 171 per step) - a different kernel path, the same decisions.  variant 14
-    (hi x hi block filter) runs its presorted form 15 on the wide steps."""
+    (hi x hi block filter) and 16 (rotated DB, head filter) run their presorted forms 15 / 17 on
+    the wide steps."""
     from ia_amd import synth
     job = synth.make_job(512, n_levels=3)
     ctx.set_option('prune_min_rows', 1)

@@ -22,7 +22,7 @@ pytestmark = pytest.mark.gpu
 def _run_debug(ctx, z, prune_all=False, variant=14):
     """prune_all: option prune_min_rows = 1, so every 1-channel level goes through the certified
     pruned scan (K2p -> K3p) instead of only DB levels of >= 2^19 rows; variant:
-    the pruned-scan kernel (14: with the hi x hi block filter)."""
+    the pruned-scan kernel (14: hi x hi block filter, the default; 16: rotated DB + head filter)."""
     from ia_amd import _native
     L, k = z['L'], float(z['k'])
     Bp = [x.copy() for x in z['Bp_init']]
@@ -46,7 +46,8 @@ def _run_debug(ctx, z, prune_all=False, variant=14):
     return out, Bp, st
 
 
-@pytest.mark.parametrize('prune_all,variant', [(False, 14), (True, 7), (True, 14)], ids=['default', 'pruned_v7', 'pruned'])
+@pytest.mark.parametrize('prune_all,variant', [(False, 14), (True, 7), (True, 14), (True, 16)],
+                         ids=['default', 'pruned_v7', 'pruned', 'pruned_v16'])
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
 def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     """Every NN pick, coherence pick and compute_distance value of the reference run.  With
@@ -57,8 +58,10 @@ def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]
     if prune_all:
         assert st.pruned_levels == (z['L'] - 1 if ch == 1 else 0)
-    if variant == 14 and st.pruned_levels > 0:  # the hi x hi filter runs on pruned levels only
+    if variant in (14, 16) and st.pruned_levels > 0:  # the block filters run on pruned levels only
         assert 0 < st.dist_pairs_corrected <= st.dist_pairs
+    if variant == 16 and st.pruned_levels > 0:
+        assert 0 < st.dist_tiles_rows <= st.dist_tiles
     assert st.bound_violations == 0 and st.kappa_ambiguous == 0
     app, coh, dist = [], [], []
     for level in range(1, z['L']):

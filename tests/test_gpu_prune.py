@@ -42,7 +42,8 @@ def _run(ctx, job, prune, variant=7):
     return Bp, S, IM, st
 
 
-@pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 7), (1024, 2, 7), (512, 1, 11), (1024, 2, 11), (512, 1, 14), (1024, 2, 14),
+@pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 16), (1024, 2, 16), (512, 1, 17), (1024, 2, 17),
+                                                      (512, 1, 7), (1024, 2, 7), (512, 1, 11), (1024, 2, 11), (512, 1, 14), (1024, 2, 14),
                                                       (512, 1, 15), (1024, 2, 15), (512, 1, 12), (1024, 2, 12), (512, 1, 13), (1024, 2, 13),
                                                       (512, 1, 10), (1024, 2, 9), (512, 1, 8),
                                                       (1024, 2, 6), (1024, 2, 5), (1024, 2, 4), (1024, 2, 3),
@@ -53,7 +54,7 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     builds the rest, e.g. 12 (presorted, 16 waves with one tile buffer each: 4 waves per SIMD) and
     13 (12 with the in-kernel sort), both measured slower): every one is exact"""
     from ia_amd import synth
-    if variant not in (7, 11, 14, 15) and not _diag_build(ctx):
+    if variant not in (7, 11, 14, 15, 16, 17) and not _diag_build(ctx):
         pytest.skip('kernel version %d is built with DIAG=1 only' % variant)
     job = synth.make_job(size)
     Bp0, S0, IM0, st0 = _run(ctx, job, 0)
@@ -67,11 +68,16 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     assert st1.dist_pairs < st1.dist_pairs_full
     assert st1.dist_pairs_full == st0.dist_pairs_full
     assert st1.dist_tiles <= st1.dist_tiles_full and st1.dist_tiles_full == st0.dist_tiles_full
-    if variant in (14, 15):  # the hi x hi block filter skips the corrections of most box-needed pairs
+    if variant in (14, 15, 16, 17):  # block filters: most box-needed pairs stop after a cheap product
         assert 0 < st1.dist_pairs_corrected < st1.dist_pairs
-        print('corrected pairs %.3f of the box-needed ones' % (st1.dist_pairs_corrected / st1.dist_pairs))
+        print('filter-passing pairs %.3f of the box-needed ones' % (st1.dist_pairs_corrected / st1.dist_pairs))
     else:
         assert st1.dist_pairs_corrected == 0
+    if variant in (16, 17):  # the head filter leaves most DB tiles' full rows unread
+        assert 0 < st1.dist_tiles_rows < st1.dist_tiles
+        print('full-row tiles %.3f of the heads loaded' % (st1.dist_tiles_rows / st1.dist_tiles))
+    else:
+        assert st1.dist_tiles_rows == 0
     print('size %d: pairs left %.3f, DB tiles loaded %.3f, fallbacks %d -> %d'
           % (size, st1.dist_pairs / st1.dist_pairs_full, st1.dist_tiles / st1.dist_tiles_full, st0.fallbacks,
              st1.fallbacks))
@@ -82,7 +88,7 @@ def test_prune_option_rejects_bad_values(ctx):
     with pytest.raises(_native.IAError):
         ctx.set_option('prune', 2)
     with pytest.raises(_native.IAError):
-        ctx.set_option('k3p_variant', 16)
+        ctx.set_option('k3p_variant', 18)
     if not _diag_build(ctx):
         for v in (6, 12, 13):
             with pytest.raises(_native.IAError):
