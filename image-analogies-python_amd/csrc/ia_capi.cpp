@@ -101,6 +101,7 @@ struct ia_ctx {
   int prune = 1;
   int row_source = 0;            // option "row_source": exact rows from 0 = the fp64 row DB, 1 = the A images
   int shard_emulate = 1;         // option "shard_emulate": W > 1 runs a W-way DB shard on this device
+  int prune_group = 1;           // option "prune_group": Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)
   int matcher = IA_MATCH_F16X3;  // option "matcher"
   int k3p_variant = 14;          // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
@@ -250,7 +251,8 @@ int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac,
                       c->st);
   if (ia_sort_pairs(c->pr_tmp.p, sort_bytes, keys, keys + NA, rows, rows + NA, NA, c->st) != 0)
     return fail(IA_EHIP, "prepare_prune: radix sort failed");
-  ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, W, c->pos2row.as<int>(), c->boxes.as<float>(), rnorm,
+  ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, W, rot ? 1 : c->prune_group, c->pos2row.as<int>(),
+                        c->boxes.as<float>(), rnorm,
                         c->tnorm.as<float>(), c->st);
   if (rot) {
     int lb = 8;
@@ -346,6 +348,12 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
 #endif
+  if (!std::strcmp(name, "prune_group")) {
+    if (value != 1 && value != 2 && value != 4 && value != 8)
+      return fail(IA_EINVAL, "ia_set_option: prune_group must be 1, 2, 4 or 8");
+    c->prune_group = value;
+    return IA_OK;
+  }
   if (!std::strcmp(name, "prune_min_rows")) {
     if (value < 1) return fail(IA_EINVAL, "ia_set_option: prune_min_rows must be >= 1");
     c->prune_min_rows = value;

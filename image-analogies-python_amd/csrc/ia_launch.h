@@ -47,7 +47,7 @@ void ia_launch_proj_keys(const double *db64, int64_t NA, const double *mu_part, 
 size_t ia_sort_temp_bytes(int64_t n);
 int ia_sort_pairs(void *temp, size_t temp_bytes, const unsigned *keys_in, unsigned *keys_out, const int *vals_in,
                   int *vals_out, int64_t n, hipStream_t st);
-void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int W, int *pos2row,
+void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int W, int G, int *pos2row,
                            float *boxes, const float *rnorm, float *tnorm, hipStream_t st);
 void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,

@@ -125,19 +125,26 @@ __global__ void __launch_bounds__(PR_WG) k_proj_keys(const double *__restrict__ 
 // 8 * (k >> 3) + 4 * (k & 1): consecutive sorted rows alternate between the lane halves of the
 // MFMA output (half = (slot >> 2) & 1), i.e. between K3 subsets.  Positions past NA map to
 // rows >= NA (padding: never a candidate).
+// G > 1 (option "prune_group"): the Morton tiles of each full group of G hold the group's G x 32
+// sorted rows interleaved (tile r of the group: sorted rows r, r + G, r + 2G, ...), so sort
+// neighbours - near-duplicate rows - land in different tiles and hence in different K3p
+// workgroup chunks (tiles r, r + 1 of a group belong to chunks w, w + 1), where their near-tied
+// distances cannot leave a chunk's threshold within epsilon of its winner; a trailing partial
+// group keeps G = 1.  (The boxes follow the rows, so they grow with G.)
 // Shards (W > 1, DB sharded over W ranks): Morton tile m belongs to shard m mod W, and the
 // storage order groups each shard's tiles contiguously (shard r: storage tiles [off_r, off_r +
 // NT_r), NT_r = ceil((NT - r) / W), local tile k = Morton tile r + W k).  Every shard thus
 // covers the whole feature space evenly (balanced pruned work) and is a contiguous range of
 // the DB, the table and the boxes.
 __global__ void __launch_bounds__(PR_WG) k_make_table(const int *__restrict__ sorted_rows, int64_t NA, int n_tiles, int W,
-                                                      int *__restrict__ pos2row) {
+                                                      int G, int *__restrict__ pos2row) {
   const int64_t p = (int64_t)blockIdx.x * PR_WG + threadIdx.x;
   if (p >= (int64_t)n_tiles * IA_TILE) return;
   const int j = (int)(p & 31);
   const int k = (((j & 3) << 1) | ((j >> 2) & 1) | ((j >> 3) << 3));
   const int64_t tm = W > 1 ? ia_shard_morton_tile_(p >> 5, n_tiles, W) : (p >> 5);
-  const int64_t s = tm * IA_TILE + k;
+  const int64_t grp = tm / G;
+  const int64_t s = (grp + 1) * G <= n_tiles ? grp * G * IA_TILE + (int64_t)k * G + (tm - grp * G) : tm * IA_TILE + k;
   pos2row[p] = s < NA ? sorted_rows[s] : (int)s;
 }
 
@@ -405,10 +412,10 @@ int ia_sort_pairs(void *temp, size_t temp_bytes, const unsigned *keys_in, unsign
   return (int)hipcub::DeviceRadixSort::SortPairs(temp, temp_bytes, keys_in, keys_out, vals_in, vals_out, (int)n, 0, 32, st);
 }
 
-void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int W, int *pos2row,
+void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t NA, int n_tiles, int W, int G, int *pos2row,
                            float *boxes, const float *rnorm, float *tnorm, hipStream_t st) {
   hipLaunchKernelGGL(k_make_table, dim3(pr_cdiv((int64_t)n_tiles * IA_TILE, PR_WG)), dim3(PR_WG), 0, st, sorted_rows, NA,
-                     n_tiles, W, pos2row);
+                     n_tiles, W, G, pos2row);
   hipLaunchKernelGGL(k_tile_boxes, dim3(pr_cdiv(n_tiles, PR_WG)), dim3(PR_WG), 0, st, pos2row, proj, NA, n_tiles, boxes,
                      rnorm, tnorm);
 }

@@ -21,9 +21,10 @@ def _diag_build(ctx):
     return True
 
 
-def _run(ctx, job, prune, variant=7):
+def _run(ctx, job, prune, variant=7, group=1):
     from ia_amd import _native
     ctx.set_option('prune', prune)
+    ctx.set_option('prune_group', group)
     ctx.set_option('k3p_variant', variant)
     ctx.set_option('prune_min_rows', 262144)  # prune the 512^2 level too (default: 1024^2 and up)
     Bp = [x.copy() for x in job.Bp_init]
@@ -39,6 +40,7 @@ def _run(ctx, job, prune, variant=7):
         ctx.set_option('prune', 1)
         ctx.set_option('k3p_variant', 14)
         ctx.set_option('prune_min_rows', 524288)
+        ctx.set_option('prune_group', 1)
     return Bp, S, IM, st
 
 
@@ -83,10 +85,29 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
              st1.fallbacks))
 
 
+@pytest.mark.parametrize('size,group', [(512, 2), (1024, 4), (1024, 8)])
+def test_pruned_groups_equal_unpruned(ctx, size, group):
+    """option prune_group: Morton tiles interleaved in groups of G (sort neighbours in different
+    tiles and workgroup chunks): a different DB layout, the same decisions on every level"""
+    from ia_amd import synth
+    job = synth.make_job(size)
+    Bp0, S0, IM0, st0 = _run(ctx, job, 0)
+    Bp1, S1, IM1, st1 = _run(ctx, job, 1, 14, group)
+    for level in range(1, job.L):
+        assert np.array_equal(S0[level], S1[level]), level
+        assert np.array_equal(IM0[level], IM1[level]), level
+        assert np.array_equal(Bp0[level], Bp1[level]), level
+    assert st1.bound_violations == 0 and st1.pruned_levels >= 1
+    print('group %d: pairs left %.3f, DB tiles loaded %.3f, fallbacks %d' % (
+        group, st1.dist_pairs / st1.dist_pairs_full, st1.dist_tiles / st1.dist_tiles_full, st1.fallbacks))
+
+
 def test_prune_option_rejects_bad_values(ctx):
     from ia_amd import _native
     with pytest.raises(_native.IAError):
         ctx.set_option('prune', 2)
+    with pytest.raises(_native.IAError):
+        ctx.set_option('prune_group', 3)
     with pytest.raises(_native.IAError):
         ctx.set_option('k3p_variant', 18)
     if not _diag_build(ctx):
