@@ -789,6 +789,11 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // ------------------------------------------------------------------------------------------
 #define IA_K3P3_MAXQ 512   // queries per step (one per thread)
 #define IA_K3P3_MAXK 512   // DB tiles per workgroup
+// steps of up to IA_K3P_RANK_MAX queries are sorted by rank counting, wider ones by the bitonic
+// network (at 342 queries the network measured faster: profiles/r02/ab3)
+#ifndef IA_K3P_RANK_MAX
+#define IA_K3P_RANK_MAX 256
+#endif
 // PRE (k3p_variant 11, any Mpad <= 4096): the step's queries were sorted once by k_query_sort
 // (ia_prune.hip): qf / qinfo hold them in sorted order (fragments; lo, hi, (U', key) per slot),
 // ord_in maps a sorted slot to its query and tbox holds the sorted query tiles' boxes, so phase
@@ -961,7 +966,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         }
       }
     }
-  } else if (DYN && Mpad > 256) {  // (uniform) below 256 queries the rank count is cheaper
+  } else if (DYN && Mpad > IA_K3P_RANK_MAX) {  // (uniform) up to IA_K3P_RANK_MAX queries the rank count
     // bitonic network over the first 512 threads' unique keys (padding: 0xFFFFFFFF, last):
     // exchanges at distance < 64 are lane swaps, the 6 at distance >= 64 go through LDS (the
     // query-fragment area, free until the scatter below)

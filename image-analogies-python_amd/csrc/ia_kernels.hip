@@ -28,6 +28,9 @@
 #ifndef IA_PROBE
 #define IA_PROBE 0  // diagnostic phase-skipping builds (never set in the product build)
 #endif
+#ifndef IA_K4_RPL8
+#define IA_K4_RPL8 0  // 1: the fused merge always reads 8 records per lane (A/B builds)
+#endif
 #if IA_PROBE & 8  // diagnostic build only: s_memtime phase stamps of sampled merge waves
 #define IA_STAMP(k) do { __builtin_amdgcn_sched_barrier(0); stamp[k] = __builtin_amdgcn_s_memtime(); \
                          __builtin_amdgcn_sched_barrier(0); } while (0)
@@ -1373,7 +1376,7 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_r(LevelGeo g, StepDesc s
 // the weighted one (kappa rule) and its row's A' value (the B' write) from the same round.
 // Candidates beyond the 49 rerank lanes (rare) are evaluated by the lanes that listed them.
 // Wave reductions use DPP / permlane exchanges (no LDS round trips).
-template <int CH, bool IMG>
+template <int CH, bool IMG, int RPL>
 __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &a,
                                             int m, const JobPtrs &jp, const QPix &px,
                                             double *qs, double *ws, int *cand_row, float *cand_v) {
@@ -1381,7 +1384,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
   IA_STAMP(0);
-  constexpr int RPL = IA_WG_TARGET / IA_WAVE;
+  // RPL: records per lane (nwg <= 64 RPL); 4 for the split-f16 scans (<= 256 workgroups)
   constexpr int NCOH = 15, NRR = IA_WAVE - NCOH;  // lanes for coherence / rerank candidates
   const int lane = threadIdx.x & 63;
   const int r = px.r, c = px.c, qi = px.qi;
@@ -1664,7 +1667,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
 #endif
 }
 
-template <int CH, bool FUSED, bool IMG, class JS>
+template <int CH, bool FUSED, bool IMG, class JS, int RPL = IA_WG_TARGET / IA_WAVE>
 __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, Winner *__restrict__ win,
                                                         JS jobs) {
   const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6));  // wave-uniform
@@ -1677,7 +1680,7 @@ __global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, 
     __shared__ int crsh[IA_WG / IA_WAVE][IA_WAVE];
     __shared__ float cvsh[IA_WG / IA_WAVE][IA_WAVE];
     const int wv = threadIdx.x >> 6;
-    merge_fused<CH, IMG>(g, sd, A, ma, m, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv]);
+    merge_fused<CH, IMG, RPL>(g, sd, A, ma, m, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv]);
     return;
   }
 #endif
@@ -1995,11 +1998,22 @@ template <int CH, bool FUSED, bool IMG>
 static void launch_merge_j(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
                            const JobSet &jobs, hipStream_t st) {
   const dim3 grid(cdiv(sd.J * sd.M, IA_WG / IA_WAVE));
-  if (jobs.J == 1)
-    hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, JobArg1{jobs.j0});
-  else
-    hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win,
-                       JobArgN{jobs.rest});
+  // the fused merge with 4 records per lane when the scan ran <= 256 workgroups (every
+  // split-f16 scan): half the record loads and candidate tests of the 8-per-lane form
+  const bool r4 = FUSED && ma.nwg <= 4 * IA_WAVE && !IA_K4_RPL8;
+  if (jobs.J == 1) {
+    if (r4)
+      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArg1, 4>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, JobArg1{jobs.j0});
+    else
+      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, JobArg1{jobs.j0});
+  } else {
+    if (r4)
+      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArgN, 4>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win,
+                         JobArgN{jobs.rest});
+    else
+      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win,
+                         JobArgN{jobs.rest});
+  }
 }
 template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
