@@ -175,10 +175,18 @@ def main():
     from ia_amd import _native, synth
 
     dist = None
+    # rehearsal of the N > 1 path on a one-GPU box (IA_BENCH_SHARE_GPU=1: ranks share the visible
+    # GPUs, IA_BENCH_BACKEND=gloo: RCCL refuses two ranks on one device); never set by the driver
+    if os.environ.get('IA_BENCH_SHARE_GPU') == '1':
+        local = local % max(torch.cuda.device_count(), 1)
+    backend = os.environ.get('IA_BENCH_BACKEND', 'nccl')
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        if backend == 'nccl':
+            dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+        else:
+            dist.init_process_group(backend)
     dev = torch.device('cuda', local)
 
     kw, desc = synth.CONFIGS[args.config]
@@ -248,7 +256,7 @@ def main():
     elapsed = time.perf_counter() - t_start
     ctx.set_option('time_dist', 0)
     if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
