@@ -137,6 +137,9 @@ def main():
                     help='cfg5: run the sweep one job at a time (the reference\'s order) instead of batching the '
                          'jobs that share a GPU')
     ap.add_argument('--max-batch', type=int, default=16, help='cfg5: jobs per batched level call')
+    ap.add_argument('--streams', type=int, default=3,
+                    help='cfg5: libia contexts (HIP streams + host threads) the rank\'s jobs are dealt over '
+                         '(1 / 2 / 3: 7.7-8.0 / 9.1-9.4 / 9.7 M px/s on one MI355X, profiles/r02/streams)')
     ap.add_argument('--mode', default='replicas', choices=['replicas', 'shard'])
     ap.add_argument('--matcher', default='f16x3', choices=['f16x3', 'f32'],
                     help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
@@ -233,7 +236,16 @@ def main():
     if sw is not None:
         from ia_amd import sweep
         dsw = sweep.DeviceSweep(sw, mine, torch, dev)
-        run = lambda st: dsw.run(ctx, st, batched=not args.sequential, max_batch=args.max_batch)
+        ctxs = [ctx]
+        for _ in range(1, args.streams):
+            cx = _native.Context(local)
+            cx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
+            cx.set_option('prune', args.prune)
+            if args.k3p_variant != 14:
+                cx.set_option('k3p_variant', args.k3p_variant)
+            cx.set_option('prune_min_rows', args.prune_min_rows)
+            ctxs.append(cx)
+        run = lambda st: dsw.run(ctxs, st, batched=not args.sequential, max_batch=args.max_batch)
         dj = dsw
     else:
         dj = DeviceJob(job, torch, dev)
@@ -366,6 +378,7 @@ def main():
                                         'dist_pairs_corrected', 'dist_tiles_rows')}}
     if sw is not None:
         out['config']['sweep'] = {'jobs': len(sw.jobs), 'batched': not args.sequential, 'max_batch': args.max_batch,
+                                  'streams': args.streams,
                                   'kappas': sorted({j.k for j in sw.jobs}), 'depths': sorted(set(sw.L))}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out['cpu_baseline'] = (cpu_baseline_sweep(sw, args.cpu_seconds) if sw is not None

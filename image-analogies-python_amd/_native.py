@@ -49,6 +49,11 @@ class Stats(ctypes.Structure):
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
+    def add(self, other):
+        """accumulate another Stats (e.g. of a concurrent context) field by field"""
+        for k, _ in self._fields_:
+            setattr(self, k, getattr(self, k) + getattr(other, k))
+
 
 EXPORTS = {
     'ia_init': (ctypes.c_int, [ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),

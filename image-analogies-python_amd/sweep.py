@@ -124,12 +124,41 @@ class DeviceSweep(object):
         self.ch = 1 if sweep.A_pyr[0].ndim == 2 else sweep.A_pyr[0].shape[2]
 
     def run(self, ctx, stats, batched=True, max_batch=16):
+        """ctx: one libia Context, or a list of them: the jobs are then dealt round-robin over the
+        contexts (each with its own HIP stream) and synthesised by one host thread per context, so
+        one group's latency-bound merge / gather kernels overlap another group's scans (libia's
+        calls release the GIL; per-thread stats are summed into `stats`)."""
         for j in self.jobs:
             for a, b in zip(self.Bp[j], self.Bp0[j]):
                 a.copy_(b)
-        self.torch.cuda.synchronize()   # libia runs on its own stream
+        self.torch.cuda.synchronize()   # libia runs on its own stream(s)
+        if isinstance(ctx, (list, tuple)) and len(ctx) > 1:
+            import threading
+            from . import _native
+            groups = [self.jobs[i::len(ctx)] for i in range(len(ctx))]
+            sts = [_native.Stats() for _ in ctx]
+            errs = []
+
+            def work(c, jobs, st):
+                try:
+                    self._run_jobs(c, jobs, st, batched, max_batch)
+                except Exception as e:  # re-raised on the calling thread
+                    errs.append(e)
+            th = [threading.Thread(target=work, args=(c, g, st)) for c, g, st in zip(ctx, groups, sts)]
+            for t in th:
+                t.start()
+            for t in th:
+                t.join()
+            if errs:
+                raise errs[0]
+            for st in sts:
+                stats.add(st)
+            return
+        self._run_jobs(ctx[0] if isinstance(ctx, (list, tuple)) else ctx, self.jobs, stats, batched, max_batch)
+
+    def _run_jobs(self, ctx, jobs, stats, batched, max_batch):
         sw = self.sw
-        for f, part in sw.schedule(self.jobs, max_batch if batched else 1):
+        for f, part in sw.schedule(jobs, max_batch if batched else 1):
             ptrs = [dict(A=self.A[f].data_ptr(), Ac=self.A[f - 1].data_ptr(), Ap=self.Ap[f].data_ptr(),
                          Apc=self.Ap[f - 1].data_ptr(), B=self.B[f].data_ptr(), Bc=self.B[f - 1].data_ptr(),
                          Bpc=self.Bp[j][l - 1].data_ptr(), Bp=self.Bp[j][l].data_ptr(), weights=self.W.data_ptr(),

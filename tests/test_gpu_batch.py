@@ -4,6 +4,7 @@ one gather, one distance scan and one merge per step for all of them - and every
 and im must be bit-identical to running it alone (and, for the golden job, to the reference)."""
 import numpy as np
 import pytest
+import torch  # noqa: F401  (before libia loads: torch's HIP runtime must be the process's first)
 
 from golden_util import load_e2e
 
@@ -124,3 +125,27 @@ def test_sweep_batched_equals_sequential_and_oracle(ctx):
     for level in range(1, sw.L[j]):
         assert np.array_equal(rb[j][1][level], S[level]) and np.array_equal(rb[j][2][level], IM[level])
         assert np.array_equal(rb[j][0][level], Bp[level])
+
+
+def test_device_sweep_two_streams_equals_one(ctx):
+    """DeviceSweep.run over two contexts (HIP streams, one host thread each; bench.py --streams 2):
+    every job's B', s and im bit-identical to the one-context run, stats summed."""
+    from ia_amd import _native, sweep, synth
+    A = synth.smooth(96, 96, 2, 1)
+    jobs = [sweep.SweepJob(k, n, seed=5 + i) for i, (k, n) in enumerate([(0.5, 3), (5, 4), (25, 5), (1, None), (2, 3)])]
+    sw = sweep.Sweep(A, [synth.filt(A)], synth.smooth(96, 96, 2, 2), jobs)
+    dev = torch.device('cuda', 0)
+    ds = sweep.DeviceSweep(sw, range(len(jobs)), torch, dev)
+    st1, st2 = _native.Stats(), _native.Stats()
+    ds.run(ctx, st1)
+    one = {j: ([x.cpu().numpy() for x in ds.Bp[j]], [x.cpu().numpy() for x in ds.S[j]], [x.cpu().numpy() for x in ds.IM[j]])
+           for j in range(len(jobs))}
+    ctx2 = _native.Context(0)
+    ds.run([ctx, ctx2], st2)
+    torch.cuda.synchronize()
+    for j in range(len(jobs)):
+        for level in range(1, sw.L[j]):
+            assert np.array_equal(ds.Bp[j][level].cpu().numpy(), one[j][0][level])
+            assert np.array_equal(ds.S[j][level].cpu().numpy(), one[j][1][level])
+            assert np.array_equal(ds.IM[j][level].cpu().numpy(), one[j][2][level])
+    assert st2.pixels == st1.pixels and st2.coherence_wins == st1.coherence_wins and st2.bound_violations == 0
