@@ -28,6 +28,13 @@
 #ifndef IA_PROBE
 #define IA_PROBE 0  // diagnostic phase-skipping builds (never set in the product build)
 #endif
+// waves (= queries) per workgroup of the one-wave-per-query kernels K2h, K2p, K4: one, so a
+// step's few hundred latency-bound waves spread over as many CUs (their L1, TA and LDS) as
+// possible; 3.35 -> 3.44 M px/s against 4 per workgroup on one box (profiles/r02/wpb)
+#ifndef IA_PQ_WPB
+#define IA_PQ_WPB 1
+#endif
+#define IA_PQ_WG (IA_WAVE * IA_PQ_WPB)
 #ifndef IA_K4_RPL8
 #define IA_K4_RPL8 0  // 1: the fused merge always reads 8 records per lane (A/B builds)
 #endif
@@ -742,13 +749,13 @@ __device__ __forceinline__ void put_qh(_Float16 *qf, int m, int f, double v) {
 }
 
 template <int CH, int KS, class JS>
-__global__ void __launch_bounds__(IA_WG) k_gather_query_h(LevelGeo g, StepDesc sd, Imgs B, JS jobs,
+__global__ void __launch_bounds__(IA_PQ_WG) k_gather_query_h(LevelGeo g, StepDesc sd, Imgs B, JS jobs,
                                                            const double *__restrict__ mu_part,
                                                            double *__restrict__ q64, double *__restrict__ qn2,
                                                            _Float16 *__restrict__ qf) {
   constexpr int D = 55 * CH, KD = 16 * KS;
   const int lane = threadIdx.x & 63;
-  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6));  // wave-uniform
+  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * IA_PQ_WPB + (threadIdx.x >> 6));  // wave-uniform
   if (m >= sd.Mpad) return;
   if (m >= sd.J * sd.M) {
     for (int f = lane; f < KD; f += IA_WAVE) put_qh<KS>(qf, m, f, 0.);
@@ -1123,7 +1130,7 @@ __device__ __forceinline__ double wave_sum_d_x(double v) {  // fixed butterfly o
 //                           Morton key of the projection (sort order of the query tiles)
 // ------------------------------------------------------------------------------------------
 template <int KS, bool IMG, class JS>
-__global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc sd, Imgs B, JS jobs,
+__global__ void __launch_bounds__(IA_PQ_WG) k_gather_query_p(LevelGeo g, StepDesc sd, Imgs B, JS jobs,
                                                           const double *__restrict__ mu_part,
                                                           double *__restrict__ q64, double *__restrict__ qn2,
                                                           _Float16 *__restrict__ qf, const double *__restrict__ db64,
@@ -1131,9 +1138,9 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_p(LevelGeo g, StepDesc s
                                                           float4 *__restrict__ qinfo, Imgs A) {
   constexpr int D = 55, KD = 16 * KS;
   static_assert(KD <= IA_WAVE, "one feature per lane");
-  __shared__ double qsh[IA_WG / IA_WAVE][Geo<1>::DS];
+  __shared__ double qsh[IA_PQ_WPB][Geo<1>::DS];
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int m = blockIdx.x * (IA_WG / IA_WAVE) + wv;
+  const int m = blockIdx.x * IA_PQ_WPB + wv;
   if (m >= sd.Mpad) return;
   if (m >= sd.J * sd.M) {
     if (lane < KD) put_qh<KS>(qf, m, lane, 0.);
@@ -1668,17 +1675,17 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
 }
 
 template <int CH, bool FUSED, bool IMG, class JS, int RPL = IA_WG_TARGET / IA_WAVE>
-__global__ void __launch_bounds__(IA_WG) k_merge_level(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, Winner *__restrict__ win,
+__global__ void __launch_bounds__(IA_PQ_WG) k_merge_level(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, Winner *__restrict__ win,
                                                         JS jobs) {
-  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * (IA_WG / IA_WAVE) + (threadIdx.x >> 6));  // wave-uniform
+  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * IA_PQ_WPB + (threadIdx.x >> 6));  // wave-uniform
   if (m >= sd.J * sd.M) return;
   const QPix px = ia_qpix(sd, g.bw, m);
   const JobPtrs jp = jobs.get(px.job);
 #if (IA_PROBE & 3) == 0
   if constexpr (FUSED) {
-    __shared__ double qsh[IA_WG / IA_WAVE][Geo<CH>::DS], wsh[IA_WG / IA_WAVE][Geo<CH>::DS];
-    __shared__ int crsh[IA_WG / IA_WAVE][IA_WAVE];
-    __shared__ float cvsh[IA_WG / IA_WAVE][IA_WAVE];
+    __shared__ double qsh[IA_PQ_WPB][Geo<CH>::DS], wsh[IA_PQ_WPB][Geo<CH>::DS];
+    __shared__ int crsh[IA_PQ_WPB][IA_WAVE];
+    __shared__ float cvsh[IA_PQ_WPB][IA_WAVE];
     const int wv = threadIdx.x >> 6;
     merge_fused<CH, IMG, RPL>(g, sd, A, ma, m, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv]);
     return;
@@ -1997,21 +2004,21 @@ void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tile
 template <int CH, bool FUSED, bool IMG>
 static void launch_merge_j(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
                            const JobSet &jobs, hipStream_t st) {
-  const dim3 grid(cdiv(sd.J * sd.M, IA_WG / IA_WAVE));
+  const dim3 grid(cdiv(sd.J * sd.M, IA_PQ_WPB));
   // the fused merge with 4 records per lane when the scan ran <= 256 workgroups (every
   // split-f16 scan): half the record loads and candidate tests of the 8-per-lane form
   const bool r4 = FUSED && ma.nwg <= 4 * IA_WAVE && !IA_K4_RPL8;
   if (jobs.J == 1) {
     if (r4)
-      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArg1, 4>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, JobArg1{jobs.j0});
+      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArg1, 4>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, win, JobArg1{jobs.j0});
     else
-      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win, JobArg1{jobs.j0});
+      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, win, JobArg1{jobs.j0});
   } else {
     if (r4)
-      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArgN, 4>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win,
+      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArgN, 4>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, win,
                          JobArgN{jobs.rest});
     else
-      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, A, ma, win,
+      hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, win,
                          JobArgN{jobs.rest});
   }
 }
@@ -2153,12 +2160,12 @@ void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *mu, vo
 template <int CH, int KS>
 static void launch_gather_h_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                               double *q64, double *qn2, void *qf, hipStream_t st) {
-  const dim3 grid(cdiv(sd.Mpad, IA_WG / IA_WAVE));
+  const dim3 grid(cdiv(sd.Mpad, IA_PQ_WPB));
   if (jobs.J == 1)
-    hipLaunchKernelGGL((k_gather_query_h<CH, KS, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, job0_imgs(B, jobs), JobArg1{jobs.j0},
+    hipLaunchKernelGGL((k_gather_query_h<CH, KS, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, job0_imgs(B, jobs), JobArg1{jobs.j0},
                        mu, q64, qn2, (_Float16 *)qf);
   else
-    hipLaunchKernelGGL((k_gather_query_h<CH, KS, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64,
+    hipLaunchKernelGGL((k_gather_query_h<CH, KS, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64,
                        qn2, (_Float16 *)qf);
 }
 void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
@@ -2171,12 +2178,12 @@ template <bool IMG>
 static void launch_gather_p_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                               double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
                               float4 *qinfo, const Imgs &A, hipStream_t st) {
-  const dim3 grid(cdiv(sd.Mpad, IA_WG / IA_WAVE));
+  const dim3 grid(cdiv(sd.Mpad, IA_PQ_WPB));
   if (jobs.J == 1)
-    hipLaunchKernelGGL((k_gather_query_p<4, IMG, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, job0_imgs(B, jobs), JobArg1{jobs.j0},
+    hipLaunchKernelGGL((k_gather_query_p<4, IMG, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, job0_imgs(B, jobs), JobArg1{jobs.j0},
                        mu, q64, qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A);
   else
-    hipLaunchKernelGGL((k_gather_query_p<4, IMG, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64,
+    hipLaunchKernelGGL((k_gather_query_p<4, IMG, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64,
                        qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A);
 }
 void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
