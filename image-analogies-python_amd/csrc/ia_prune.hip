@@ -182,11 +182,13 @@ __global__ void __launch_bounds__(PR_WG) k_tile_boxes(const int *__restrict__ po
 }
 
 // K2s: one sort of a wavefront step's queries for the pruned scan (k3p_variant 11).  One
-// workgroup: unique keys (the Morton key's top 20 bits above the 12-bit query index; padding
-// slots and unused sort slots last) sorted by a bitonic network in LDS; then the step's
-// pruning records and split-f16 fragments are written in sorted order, with each sorted query
-// tile's box (min lo, max hi, max U' over its real queries), so every K3p launch loads just its
-// slice.  Any Mpad <= 4096 (the in-kernel sort of K3p v6/v7 is limited to 512).
+// workgroup per sorted query tile: each sorts the step's unique keys (the Morton key's top 20
+// bits above the 12-bit query index; padding slots and unused sort slots last) by a bitonic
+// network in LDS - the same order in every workgroup - and writes its tile's pruning records,
+// split-f16 fragments and box (min lo, max hi, max U' over its real queries) in sorted order,
+// so every K3p launch loads just its slice.  Any Mpad <= 4096 (the in-kernel sort of K3p v6/v7
+// is limited to 512).  (One workgroup for the whole step spent 20.7 us per cfg4 step, mostly
+// in the copies.)
 #define QS_WG 1024
 __global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__ qinfo, const h16x8 *__restrict__ qf,
                                                       int Mpad, int NS, int NP, int *__restrict__ order,
@@ -234,23 +236,23 @@ __global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__
       }
     }
   }
-  for (int x = tid; x < Mpad; x += QS_WG) {
+  const int xt0 = blockIdx.x;  // this workgroup's sorted query tile
+  for (int x = xt0 * IA_TILE + tid; x < (xt0 + 1) * IA_TILE && tid < IA_TILE; x += QS_WG) {
     const int q = (int)(key[x] & 0xFFFu);
     order[x] = q;
     sq[3 * x] = qinfo[3 * q];
     sq[3 * x + 1] = qinfo[3 * q + 1];
     sq[3 * x + 2] = qinfo[3 * q + 2];
   }
-  // fragments: sorted slot x of tile xt, piece p, lane L (k-half L >> 5, row L & 31)
-  const int ne = Mpad / IA_TILE * NP * IA_WAVE;
-  for (int e = tid; e < ne; e += QS_WG) {
+  // fragments of the tile: sorted slot x of tile xt, piece p, lane L (k-half L >> 5, row L & 31)
+  for (int e = xt0 * NP * IA_WAVE + tid; e < (xt0 + 1) * NP * IA_WAVE; e += QS_WG) {
     const int L = e & 63, pq = e >> 6, xt = pq / NP, p = pq - xt * NP;
     const int q = (int)(key[xt * IA_TILE + (L & 31)] & 0xFFFu);
     qfs[e] = qf[((q >> 5) * NP + p) * IA_WAVE + (L & 32) + (q & 31)];
   }
-  // sorted query-tile boxes: one 32-lane half-wave per tile
-  const int nt = Mpad / IA_TILE, lane = tid & 63;
-  for (int t = tid >> 5; t < nt; t += QS_WG / 32) {
+  // the tile's box: one 32-lane half-wave
+  const int lane = tid & 63;
+  for (int t = xt0 + (tid >> 5); t < xt0 + 1; t += QS_WG / 32) {
     const int q = (int)(key[t * IA_TILE + (lane & 31)] & 0xFFFu);
     const float4 u = qinfo[3 * q + 2];
     float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
@@ -383,8 +385,8 @@ void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS,
                           float4 *tbox, hipStream_t st) {
   int NS = 32;
   while (NS < Mpad) NS <<= 1;
-  hipLaunchKernelGGL(k_query_sort, dim3(1), dim3(QS_WG), 0, st, qinfo, (const h16x8 *)qf, Mpad, NS, 2 * KS, order, sq,
-                     (h16x8 *)qfs, tbox);
+  hipLaunchKernelGGL(k_query_sort, dim3(Mpad / IA_TILE), dim3(QS_WG), 0, st, qinfo, (const h16x8 *)qf, Mpad, NS, 2 * KS,
+                     order, sq, (h16x8 *)qfs, tbox);
 }
 static inline unsigned pr_cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 
