@@ -152,7 +152,7 @@ def main():
                          'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
                          'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks, 11 = 7 on queries presorted once per step, '
                          '14 (default) / 15 = 7 / 11 with the hi x hi block filter, 16 / 17 = rotated DB with the '
-                         'principal-axis head filter (DESIGN.md §4f); product builds hold 7, 11, 14-17')
+                         'principal-axis head filter (DESIGN.md §4f); product builds hold 7, 11, 14 and 15')
     ap.add_argument('--prune-group', type=int, default=1, choices=[1, 2, 4, 8],
                     help='pruned levels: Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)')
     ap.add_argument('--prune-min-rows', type=int, default=524288,

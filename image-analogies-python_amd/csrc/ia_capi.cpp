@@ -254,6 +254,7 @@ int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac,
   ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, W, rot ? 1 : c->prune_group, c->pos2row.as<int>(),
                         c->boxes.as<float>(), rnorm,
                         c->tnorm.as<float>(), c->st);
+#ifdef IA_K3H_DIAG
   if (rot) {
     int lb = 8;
     while (lb < 20 && ((int64_t)1 << lb) < 4 * NA) lb++;
@@ -261,6 +262,9 @@ int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac,
     ia_launch_key_lut(keys + NA, NA, (int)NT, lb, c->pr_lut.as<int>(), c->st);
     *lut_bits = lb;
   }
+#else
+  (void)lut_bits;
+#endif
   HIP_TRY(hipGetLastError());
   g.pos2row = c->pos2row.as<int>();
   return IA_OK;
@@ -336,10 +340,10 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   }
 #else  // product build: the default kernels only (7: pruned scan, 1: packed-index K3h)
   if (!std::strcmp(name, "k3p_variant")) {  // 14 (default) / 15: hi x hi block filter (in-kernel sort up to
-                                            // 512 queries, presorted 15 above); 16 / 17: rotated DB + head
-                                            // filter (sharded levels run 14 / 15); 7 / 11: v7
-    if (value != 7 && value != 11 && value != 14 && value != 15 && value != 16 && value != 17)
-      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14, 15, 16 or 17 (other versions are in DIAG=1 builds only)");
+                                            // 512 queries, presorted 15 above); 7 / 11: v7;
+                                            // 16 / 17 (rotated DB, §4f) are in DIAG=1 builds
+    if (value != 7 && value != 11 && value != 14 && value != 15)
+      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14 or 15 (other versions are in DIAG=1 builds only)");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -720,15 +724,23 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   int lut_bits = 0;
   // rotated DB + head-filtered scan (k3p_variant 16 / 17): unsharded pruned levels whose
   // workgroups hold <= 512 tiles (the in-kernel tile lists)
-  const bool rot = prune && !multi && (c->k3p_variant == 16 || c->k3p_variant == 17) &&
+#ifdef IA_K3H_DIAG
+  constexpr bool kRotBuilt = true;   // k3p_variant 16 / 17: DIAG=1 builds only
+#else
+  constexpr bool kRotBuilt = false;
+#endif
+  const bool rot = kRotBuilt && prune && !multi && (c->k3p_variant == 16 || c->k3p_variant == 17) &&
                    (g.n_tiles + IA_NWG_H - 1) / IA_NWG_H <= 512;
   if (prune && (rc = prepare_prune(c, g, c->mu.as<double>(), Wsh, &ufac, rot, &eps_r, &lut_bits)))
     return rc;  // sets g.pos2row
   if (ns > 0) {
+#ifdef IA_K3H_DIAG
     if (rot)
       ia_launch_db_build_rot(c->db64.as<double>(), g.NA, g.n_tiles, g.pos2row, c->mu.as<double>(), c->pr_rot.as<double>(),
                              c->db.p, c->Rbits.as<unsigned>(), c->st);
-    else if (use_h) ia_launch_db_build_h(g, Aim, c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
+    else
+#endif
+    if (use_h) ia_launch_db_build_h(g, Aim, c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
     else ia_launch_db_build(g, Aim, c->mu.as<double>(), c->db.as<float4>(), c->Rbits.as<unsigned>(), c->st);
   }
   HIP_TRY(hipEventRecord(c->lv1, c->st));
@@ -755,7 +767,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   ma.eps_c = use_h ? ia_eps_c_h(g.KS, prune || c->k3_variant == 1) : ia_eps_c(DP);
   ma.eps_a = use_h ? ia_eps_a_h() * (rot ? 2.0 : 1.0) : 0.;  // rot: two norm columns
   ma.eps_r = eps_r;
-  RotArgs ra{c->pr_rot.as<double>(), c->db.p, c->pr_lut.as<int>(), lut_bits, g.n_tiles, c->Rbits.as<unsigned>(),
+  [[maybe_unused]] RotArgs ra{c->pr_rot.as<double>(), c->db.p, c->pr_lut.as<int>(), lut_bits, g.n_tiles, c->Rbits.as<unsigned>(),
              ma.eps_c, ma.eps_a, eps_r};
   // per shard: its records, decomposition, DB positions (and table / boxes of a pruned level)
   std::vector<MergeArgs> mas(shards.size(), ma);
@@ -802,10 +814,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     }
     const int Mt = J * sd.M;  // queries of this step over all jobs
     sd.Mpad = (Mt + IA_TILE - 1) / IA_TILE * IA_TILE;
+#ifdef IA_K3H_DIAG
     if (rot)
       ia_launch_gather_r(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
                          c->db64.as<double>(), c->pr_basis.as<double>(), ufac, ra, c->qinfo.as<float4>(), Aim, c->st);
-    else if (prune)
+    else
+#endif
+    if (prune)
       ia_launch_gather_p(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
                          c->db64.as<double>(), c->pr_basis.as<double>(), ufac, c->qinfo.as<float4>(), Aim, ma.img_rows,
                          c->st);

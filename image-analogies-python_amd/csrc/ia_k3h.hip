@@ -1497,8 +1497,10 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true>;
     if (variant == 14) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true>;
     if (variant == 15) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true>;
+#ifdef IA_K3H_DIAG  // rotated DB + head filter: exact, not faster
     if (variant == 16) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, false, true>;
     if (variant == 17) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, false, true>;
+#endif
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

@@ -1212,6 +1212,7 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_gather_query_p(LevelGeo g, StepDes
   }
 }
 
+#ifdef IA_K3H_DIAG  // k3p_variant 16 / 17: DIAG=1 builds only
 // ------------------------------------------------------------------------------------------
 // K2r: K2p for the rotated DB and its head-filtered scan (k3p_variant 16 / 17),
 // one wave per query.  Lane c of the wave owns MFMA column c:
@@ -1374,6 +1375,8 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_r(LevelGeo g, StepDesc s
   }
 #endif
 }
+
+#endif  // IA_K3H_DIAG
 
 // Fused single-rank merge of query m: certified exact NN + coherence + kappa + writeback.
 // Memory is touched in two dependent rounds: (1) the K3 records, the coherence neighbours'
@@ -2199,6 +2202,7 @@ void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
   launch_gather_p_t<false>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, st);
 }
 
+#ifdef IA_K3H_DIAG
 void ia_launch_gather_r(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
                         const RotArgs &ra, float4 *qinfo, const Imgs &A, hipStream_t st) {
@@ -2210,6 +2214,7 @@ void ia_launch_gather_r(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
     hipLaunchKernelGGL((k_gather_query_r<false, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64,
                        qn2, (_Float16 *)qf, db64, basis, ufac, ra, qinfo, A);
 }
+#endif
 
 // split-f16 distance kernels live in ia_k3h.hip, compiled once per (KS, QT) instance
 #define IA_K3H_DECL(ks, qt) k3h_fn ia_k3h_get_##ks##_##qt(int variant);

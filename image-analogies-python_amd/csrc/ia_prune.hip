@@ -282,6 +282,7 @@ __global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__
   }
 }
 
+#ifdef IA_K3H_DIAG  // k3p_variant 16 / 17: DIAG=1 builds only
 // K5e: home-tile table of the rotated scan's query bound (k3p_variant 16 / 17, K2r).  Entry b
 // = the Morton tile where keys with top LB bits b start (lower bound in the sorted keys), so a
 // query's key locates the DB rows nearest to it in projection order with one load.
@@ -380,6 +381,8 @@ __global__ void __launch_bounds__(PR_WG) k_db_build_rot(const double *__restrict
   if ((threadIdx.x & 63) == 0 && R > 0.f) atomicMax(Rbits, __float_as_uint(R));
 }
 
+#endif  // IA_K3H_DIAG
+
 // ---- host launchers ---------------------------------------------------------------------------
 void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS, int *order, float4 *sq, void *qfs,
                           float4 *tbox, hipStream_t st) {
@@ -422,6 +425,7 @@ void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t N
                      rnorm, tnorm);
 }
 
+#ifdef IA_K3H_DIAG
 void ia_launch_key_lut(const unsigned *skeys, int64_t NA, int n_tiles, int lb, int *lut, hipStream_t st) {
   hipLaunchKernelGGL(k_key_lut, dim3(pr_cdiv((int64_t)1 << lb, PR_WG)), dim3(PR_WG), 0, st, skeys, NA, n_tiles, lb, lut);
 }
@@ -431,3 +435,4 @@ void ia_launch_db_build_rot(const double *db64, int64_t NA, int n_tiles, const i
   hipLaunchKernelGGL(k_db_build_rot, dim3(pr_cdiv((int64_t)n_tiles * IA_TILE, PR_WG)), dim3(PR_WG), 0, st, db64, NA, n_tiles,
                      pos2row, mu_part, rt, (h16x8 *)db, Rbits);
 }
+#endif

@@ -129,10 +129,10 @@ int ia_version(void);
  * k3p_variant 14 (default: the pruned scan sorts a step's queries itself up to 512 of them, a
  * step wider than that is sorted once by k_query_sort and runs 15; every box-needed block runs
  * the hi x hi product first and the full product + top-2 only when a value can lie within the
- * query's bound), 15 (always presorted), 7 / 11 (14 / 15 without that block filter), 16 / 17
- * (rotated DB: rows on the level's 55 principal axes, a 15-axis head filter before the full
- * rows; unsharded levels, else 14 / 15) and k3_variant 1; DIAG=1 builds every
- * version.
+ * query's bound), 15 (always presorted), 7 / 11 (14 / 15 without that block filter) and
+ * k3_variant 1; DIAG=1 builds every version, including 16 / 17 (rotated DB: rows on the level's
+ * 55 principal axes, a 15-axis head filter before the full rows; unsharded
+ * levels, else 14 / 15).
  * "prune_group" = G in {1 (default), 2, 4, 8}: pruned levels store each group of G Morton tiles
  * interleaved (sort neighbours in different tiles and scan chunks: fewer certification rescans,
  * looser tile boxes).

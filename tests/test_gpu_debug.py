@@ -53,6 +53,14 @@ def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     """Every NN pick, coherence pick and compute_distance value of the reference run.  With
     prune_all, the pruned scan K3p decides every 1-channel level (the bench's
     dominant kernel checked directly against the reference's own per-pixel picks)."""
+    if variant == 16:  # rotated DB + head filter (DESIGN.md §4f): DIAG=1 builds only
+        from ia_amd import _native
+        try:
+            ctx.set_option('k3p_variant', 16)
+        except _native.IAError:
+            pytest.skip('k3p_variant 16 is built with DIAG=1 only')
+        finally:
+            ctx.set_option('k3p_variant', 14)
     z = load_e2e(name)
     out, Bp, st = _run_debug(ctx, z, prune_all, variant)
     ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]
