@@ -685,7 +685,7 @@ __global__ void __launch_bounds__(IA_WG) k_absmax(AbsArrays arr, unsigned *__res
 template <int CH, int KS>
 __global__ void __launch_bounds__(IA_WG) k_db_build_h(LevelGeo g, Imgs A, const double *__restrict__ mu_part,
                                                        h16x8 *__restrict__ db, unsigned *__restrict__ Rbits) {
-  constexpr int D = 55 * CH, NP = 2 * KS;
+  constexpr int D = 55 * CH;
   static_assert(16 * KS >= D + 1, "k-steps must hold D features + the norm column");
   const int64_t pos = (int64_t)g.tile0 * IA_TILE + (int64_t)blockIdx.x * IA_WG + threadIdx.x;
   const bool inr = pos < (int64_t)g.tile1 * IA_TILE;
