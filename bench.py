@@ -163,7 +163,9 @@ def main():
     ap.add_argument('--shard-emulate', type=int, default=1,
                     help='run every large level as a W-way DB shard on this one GPU (the multi-rank kernels '
                          'without the all-gather: per-shard scans and winners, then the finish); for the cost model')
-    ap.add_argument('--time-stride', type=int, default=4, help='sample K3 timing every S-th wavefront step')
+    ap.add_argument('--time-stride', type=int, default=16,
+                    help='sample K3 timing every S-th wavefront step (HIP events on libia\'s stream; every 4th '
+                         'step cost 2 %% of the job, profiles/r02/stride)')
     ap.add_argument('--cpu-seconds', type=float, default=20.0)
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'k3p_traffic.json'),
