@@ -72,23 +72,56 @@ class DeviceJob(object):
                                         ptrs, self.job.kappa_factor(l), stats)
 
 
-def cpu_per_pixel(job, seconds):
-    """Reference loop (oracle restatement: per-pixel np.pad + exact fp64 numpy NN, 1 thread)
-    timed on bounded raster samples of the three finest levels; coarser levels are priced by
-    scaling the smallest sampled level's per-pixel cost with the DB size (the per-pixel cost is
-    a full DB scan + a full-level pad, position independent).  Returns ({level: s/px}, sample)."""
+LSH_NOTE = ('n/a: the reference snapshot has no LSH path (algorithms.py:69 hard-codes the kdtree index) and '
+            'pyflann / libflann are absent offline; the kd-tree path itself is approximate and unrunnable here, '
+            'so the baseline is the reference loop with its exact brute-force NN')
+
+
+def host_cores():
+    try:
+        return len(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+
+
+def _cpu_task(a):
+    """CPU-baseline worker (a spawned process): seconds per pixel of n consecutive raster pixels
+    of `level` from raster pixel `start` (oracle restatement of the reference loop)."""
+    A_pyr, Ap_pyr_list, B_pyr, Bp_init, level, L, k, weights, n, start = a
     from oracle import ia_oracle as O
+    return O.time_sample(A_pyr, Ap_pyr_list, B_pyr, Bp_init, level, L, k, weights, n, start=start)
+
+
+def cpu_per_pixel(job, seconds, S=256, procs=4):
+    """Reference loop (oracle restatement: per-pixel np.pad + exact fp64 numpy NN, one thread)
+    timed on S consecutive mid-level raster pixels of each of the three finest levels
+    (BASELINE.md §4).  The per-pixel work - a full-DB scan, a full-level pad and the 12 causal
+    coherence candidates - does not depend on the pixel values, so the sample runs on the job's
+    initial state and extrapolates to N_B pixels; coarser levels are priced by scaling the
+    smallest sampled level's per-pixel cost with the DB size.  The S pixels are split into
+    `procs` consecutive runs timed in spawned single-threaded worker processes, started before
+    this process touches the GPU (4 concurrent workers: little memory contention; 8 workers on
+    8 busy cores measured +17 % per pixel).  S shrinks if a level's estimate exceeds its share of
+    `seconds`.  Returns ({level: s/px}, [sample descriptions])."""
+    import multiprocessing as mp
     L = job.L
     lv = [l for l in range(L - 1, 0, -1)][:3]
     budget = seconds / len(lv)
     per_px, sample = {}, []
-    for l in lv:
-        n_b = int(np.prod(job.B_pyr[l].shape[:2]))
-        t2 = O.time_sample(job.A_pyr, job.Ap_pyr_list, job.B_pyr, job.Bp_init, l, L, job.k, job.weights, 2)
-        n = int(max(2, min(n_b, budget / max(t2, 1e-9))))
-        per_px[l] = O.time_sample(job.A_pyr, job.Ap_pyr_list, job.B_pyr, job.Bp_init, l, L, job.k, job.weights, n)
-        sample.append('%d px of level %d (%dx%d B, %dx%d A)' % (n, l, job.B_pyr[l].shape[0], job.B_pyr[l].shape[1],
-                                                                 job.A_pyr[l].shape[0], job.A_pyr[l].shape[1]))
+    base = (job.A_pyr, job.Ap_pyr_list, job.B_pyr, job.Bp_init)
+    with mp.get_context('spawn').Pool(procs) as pool:
+        for l in lv:
+            h, w = job.B_pyr[l].shape[:2]
+            n_b = h * w
+            mid = n_b // 2 + w // 2                      # an interior pixel half way down the level
+            t2 = pool.apply(_cpu_task, (base + (l, L, job.k, job.weights, 2, mid),))
+            n = int(max(procs, min(S, n_b - mid, budget * procs / max(t2, 1e-9))))
+            cuts = [mid + n * i // procs for i in range(procs + 1)]
+            res = pool.map(_cpu_task, [base + (l, L, job.k, job.weights, cuts[i + 1] - cuts[i], cuts[i])
+                                       for i in range(procs)])
+            per_px[l] = sum(r * (cuts[i + 1] - cuts[i]) for i, r in enumerate(res)) / n
+            sample.append('%d consecutive px from raster pixel %d of level %d (%dx%d B, %dx%d A; %.4f s/px)'
+                          % (n, mid, l, h, w, job.A_pyr[l].shape[0], job.A_pyr[l].shape[1], per_px[l]))
     lmin = min(lv)
     na_min = np.prod(job.A_pyr[lmin].shape[:2])
     for l in range(1, L):
@@ -97,16 +130,21 @@ def cpu_per_pixel(job, seconds):
     return per_px, sample
 
 
-def cpu_baseline(job, seconds):
-    per_px, sample = cpu_per_pixel(job, seconds)
+def _baseline(value, sample, procs, total):
+    return {'value': value, 'unit': "B' px/s", 'cores': 1, 'host_cores': host_cores(), 'sample_procs': procs,
+            'kind': 'port', 'extrapolated': True, 'lsh': LSH_NOTE,
+            'sample': ('oracle/ia_oracle.py reference-loop restatement (per-pixel pad, exact fp64 NN, one core per '
+                       'pixel as the reference runs), timed on ' + sample + '; coarser levels scaled by DB size; '
+                       'extrapolated whole-job time %.0f s on one core' % total)}
+
+
+def cpu_baseline(job, seconds, procs=4):
+    per_px, sample = cpu_per_pixel(job, seconds, procs=procs)
     total = sum(np.prod(job.B_pyr[l].shape[:2]) * per_px[l] for l in range(1, job.L))
-    return {'value': job.pixels / total, 'unit': "B' px/s", 'cores': 1, 'kind': 'port',
-            'sample': 'oracle/ia_oracle.py reference-loop restatement (per-pixel pad, exact fp64 NN), '
-                      'timed on ' + ', '.join(sample) + '; coarser levels scaled by DB size; '
-                      'extrapolated whole-job time %.0f s' % total}
+    return _baseline(job.pixels / total, ', '.join(sample), procs, total)
 
 
-def cpu_baseline_sweep(sw, seconds):
+def cpu_baseline_sweep(sw, seconds, procs=4):
     """cfg5: per-pixel costs of each resolution from the deepest job, summed over every job's
     levels (the reference runs the jobs one after the other, multi_script.py:19-32)."""
     from ia_amd import synth
@@ -114,16 +152,63 @@ def cpu_baseline_sweep(sw, seconds):
     off = sw.offset(deep)
     job = synth.Job(sw.A_pyr[off:], [p[off:] for p in sw.Ap_pyr_list], sw.B_pyr[off:], sw.Bp_init[deep],
                     sw.jobs[deep].k, sw.weights)
-    per_px, sample = cpu_per_pixel(job, seconds)
+    per_px, sample = cpu_per_pixel(job, seconds, procs=procs)
     total = 0.
     for j in range(len(sw.jobs)):
         for l in range(1, sw.L[j]):
             f = sw.offset(j) + l
             total += np.prod(sw.B_pyr[f].shape[:2]) * per_px[f - off]
-    return {'value': sw.pixels() / total, 'unit': "B' px/s", 'cores': 1, 'kind': 'port',
-            'sample': 'oracle/ia_oracle.py reference-loop restatement, timed on ' + ', '.join(sample) +
-                      ' of the deepest job; every job of the sweep priced per level; extrapolated sweep time '
-                      '%.0f s' % total}
+    return _baseline(sw.pixels() / total, ', '.join(sample) + ' of the deepest job; every job of the sweep priced '
+                     'per level', procs, total)
+
+
+def make_context(args, local):
+    """One libia context with every option of the command line (each context of a multi-stream
+    cfg5 run gets the same settings)."""
+    from ia_amd import _native
+    cx = _native.Context(local)
+    cx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
+    if args.k3_variant != 1:
+        cx.set_option('k3_variant', args.k3_variant)       # DIAG=1 builds only
+    cx.set_option('prune', args.prune)
+    if args.k3p_variant != 14:
+        cx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15; the rest DIAG=1 builds only
+    cx.set_option('prune_min_rows', args.prune_min_rows)
+    if args.prune_group != 1:
+        cx.set_option('prune_group', args.prune_group)
+    if args.row_source:
+        cx.set_option('row_source', args.row_source)
+    if args.shard_emulate > 1:
+        cx.set_option('shard_emulate', args.shard_emulate)
+    return cx
+
+
+def gather_rooflines(st):
+    """K1 / K1b (per level) and K2 (sampled steps) against the HBM roofline: algorithmic bytes
+    (include/ia.h ia_stats) / device time from libia's HIP events."""
+    out = {}
+
+    def one(name, ms, nbytes, launches, bound, what):
+        if ms <= 0 or launches <= 0:
+            return
+        gbs = nbytes / (ms * 1e-3) / 1e9
+        out[name] = {'achieved': gbs, 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s', 'frac': gbs * 1e9 / HBM_PEAK,
+                     'us_per_launch': ms * 1e3 / launches, 'algorithmic_bytes_per_launch': nbytes / launches,
+                     'launches': launches, 'bound': bound, 'bytes': what}
+    one('k_db64_build', st['k1b_ms'], st['k1b_bytes'], st['build_levels'], 'hbm',
+        'A-side images read once + N_A rows x DS x 8 B written')
+    one('k_db_build_h', st['k1_ms'], st['k1_bytes'], st['build_levels'], 'hbm',
+        'fp64 rows read (N_A x DS x 8 B) + split-f16 tiles written (7 KiB per 32 rows)')
+    one('k_gather_query', st['gather_ms_timed'], st['gather_bytes_timed'], st['gather_launches_timed'],
+        'latency (one wave per query: dependent window, coherence-row and DB loads)',
+        'per query: 55 features + 12 coherence candidate rows (pruned levels) read, fp64 row + f16 fragments + '
+        '|q|^2 + pruning record written')
+    if st['merge_launches_timed'] > 0:
+        out['k_merge_level'] = {'us_per_launch': st['merge_ms_timed'] * 1e3 / st['merge_launches_timed'],
+                                'launches': st['merge_launches_timed'],
+                                'bound': 'latency (one wave per query: record, rerank-row and coherence-row loads '
+                                         'in dependent rounds)'}
+    return out
 
 
 def main():
@@ -140,7 +225,14 @@ def main():
     ap.add_argument('--streams', type=int, default=3,
                     help='cfg5: libia contexts (HIP streams + host threads) the rank\'s jobs are dealt over '
                          '(1 / 2 / 3: 7.7-8.0 / 9.1-9.4 / 9.7 M px/s on one MI355X, profiles/r02/streams)')
-    ap.add_argument('--mode', default='replicas', choices=['replicas', 'shard'])
+    ap.add_argument('--mode', default='auto', choices=['auto', 'replicas', 'shard'],
+                    help='N > 1: shard (default for cfg2/cfg3/cfg4: BASELINE config 3 as named, one job whose DB '
+                         'is sharded over the ranks, one winner exchange per wavefront step; the replicas aggregate '
+                         'rides along as value_replicas) or replicas (one independent job per GPU)')
+    ap.add_argument('--no-replicas-extra', action='store_true',
+                    help='N > 1 shard mode: skip the extra replicas measurement (value_replicas)')
+    ap.add_argument('--cpu-procs', type=int, default=4,
+                    help='worker processes the CPU-baseline sample is split over (each single-threaded)')
     ap.add_argument('--matcher', default='f16x3', choices=['f16x3', 'f32'],
                     help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
     ap.add_argument('--k3-variant', type=int, default=1, choices=[0, 1],
@@ -166,15 +258,25 @@ def main():
     ap.add_argument('--time-stride', type=int, default=16,
                     help='sample K3 timing every S-th wavefront step (HIP events on libia\'s stream; every 4th '
                          'step cost 2 %% of the job, profiles/r02/stride)')
-    ap.add_argument('--cpu-seconds', type=float, default=20.0)
+    ap.add_argument('--cpu-seconds', type=float, default=30.0,
+                    help='wall-time budget of the CPU-baseline sample (about 10 s per sampled level)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
-    ap.add_argument('--traffic-json', default=os.path.join(ROOT, 'profiles', 'k3p_traffic.json'),
-                    help='per-launch HBM bytes of the dominant K3 kernel from a rocprofv3 --pmc pass (optional)')
+    ap.add_argument('--traffic-json', default=None,
+                    help='per-launch HBM bytes of the dominant K3 kernel from a rocprofv3 --pmc pass of THIS '
+                         'config (default: profiles/k3p_traffic_<config>.json; absent -> traffic null)')
     args = ap.parse_args()
 
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if args.mode == 'auto':
+        args.mode = 'shard' if (world > 1 and args.config != 'cfg5') else 'replicas'
+    if args.config == 'cfg5' and args.mode == 'shard':
+        ap.error('cfg5 is a sweep of independent jobs (replicas only): --mode shard does not apply')
+    if args.config == 'cfg5' and args.shard_emulate > 1 and not args.sequential:
+        ap.error('--shard-emulate takes one job per level call: add --sequential for cfg5')
+    if args.traffic_json is None:
+        args.traffic_json = os.path.join(ROOT, 'profiles', 'k3p_traffic_%s.json' % args.config)
     import torch
     import ia_amd  # noqa: F401
     from ia_amd import _native, synth
@@ -217,67 +319,76 @@ def main():
         log('[bench] rank %d: job %s built in %.1fs: L=%d, %d B\' px/step, %.3e NN flops/step'
             % (rank, args.config, time.time() - t0, job.L, job.pixels, job.flops()))
 
-    ctx = _native.Context(local)
-    ctx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
-    if args.k3_variant != 1:
-        ctx.set_option('k3_variant', args.k3_variant)       # DIAG=1 builds only
-    ctx.set_option('prune', args.prune)
-    if args.k3p_variant != 14:
-        ctx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15, 17; the rest DIAG=1 builds only
-    ctx.set_option('prune_min_rows', args.prune_min_rows)
-    if args.prune_group != 1:
-        ctx.set_option('prune_group', args.prune_group)
-    if args.row_source:
-        ctx.set_option('row_source', args.row_source)
-    if args.shard_emulate > 1:
-        ctx.set_option('shard_emulate', args.shard_emulate)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        # host reference loop, sampled in spawned workers BEFORE this process initialises the GPU
+        t1 = time.time()
+        cpu = (cpu_baseline_sweep(sw, args.cpu_seconds, args.cpu_procs) if sw is not None
+               else cpu_baseline(job, args.cpu_seconds, args.cpu_procs))
+        log('[bench] CPU baseline sampled in %.1fs: %.3g px/s' % (time.time() - t1, cpu['value']))
+    ctx = make_context(args, local)
     if args.mode == 'shard' and world > 1:
         uid = [_native.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         ctx.comm_init(rank, world, uid[0])
+    ctxs = [ctx]
     if sw is not None:
         from ia_amd import sweep
         dsw = sweep.DeviceSweep(sw, mine, torch, dev)
-        ctxs = [ctx]
-        for _ in range(1, args.streams):
-            cx = _native.Context(local)
-            cx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
-            cx.set_option('prune', args.prune)
-            if args.k3p_variant != 14:
-                cx.set_option('k3p_variant', args.k3p_variant)
-            cx.set_option('prune_min_rows', args.prune_min_rows)
-            ctxs.append(cx)
-        run = lambda st: dsw.run(ctxs, st, batched=not args.sequential, max_batch=args.max_batch)
+        ctxs += [make_context(args, local) for _ in range(1, args.streams)]
+        run = lambda st, cs=ctxs: dsw.run(cs, st, batched=not args.sequential, max_batch=args.max_batch)
         dj = dsw
     else:
         dj = DeviceJob(job, torch, dev)
-        run = lambda st: dj.run(ctx, torch, st)
+        run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
+
+    def timed(steps, fn, sample_events):
+        """steps x fn between barriers + device syncs; max over ranks"""
+        if sample_events and args.time_stride > 0:
+            ctx.set_option('time_dist', args.time_stride)
+        stats = _native.Stats()
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t_start = time.perf_counter()
+        for _ in range(steps):
+            fn(stats)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        el = time.perf_counter() - t_start
+        ctx.set_option('time_dist', 0)
+        if dist:
+            tt = torch.tensor([el], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
+            dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+            el = float(tt.item())
+        return el, stats
 
     for _ in range(args.warmup):
         run(_native.Stats())
-    if args.time_stride > 0:
-        ctx.set_option('time_dist', args.time_stride)
-    stats = _native.Stats()
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    t_start = time.perf_counter()
-    for _ in range(args.steps):
-        run(stats)
-    torch.cuda.synchronize()
-    if dist:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
-    ctx.set_option('time_dist', 0)
-    if dist:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+    # with several streams (cfg5), HIP events around one stream's K3 launches also time the other
+    # streams' kernels: the timed steps then run without events and the roofline comes from one
+    # extra single-stream pass below
+    concurrent = len(ctxs) > 1
+    elapsed, stats = timed(args.steps, run, not concurrent)
+    if concurrent:
+        _, stats_rl = timed(1, lambda st: run(st, [ctx]), True)
+    else:
+        stats_rl = stats
+    value_replicas = None
+    if world > 1 and args.mode == 'shard' and not args.no_replicas_extra:
+        # the other multi-GPU reading: one independent job per GPU (no collective), the aggregate
+        # carried as value_replicas (never `value`: BASELINE config 3 is the sharded job)
+        rctx = make_context(args, local)
+        el_r, _ = timed(args.steps, lambda st: dj.run(rctx, torch, st), False)
+        value_replicas = job_pixels * args.steps * world / el_r
+        rctx.close()
 
     jobs = world if (args.mode == 'replicas' and sw is None) else 1   # cfg5: the ranks split one sweep
     pixels = job_pixels * args.steps * jobs
     value = pixels / elapsed
-    st = stats.as_dict()
+    st = stats_rl.as_dict()
+    st_all = stats.as_dict()
     log('[bench] rank %d stats: %s' % (rank, json.dumps(st)))
 
     k3_ms_per_launch = st['dist_ms'] / max(st['dist_launches_timed'], 1)
@@ -336,6 +447,17 @@ def main():
     # do that work (certified pruning skips most (DB tile, query tile) pairs), so this is an
     # "equivalent" rate and may exceed the peak; pairs_frac is the share actually contracted.
     fp32_equiv = job_flops * args.steps * jobs / elapsed
+    roofline['note'] = ('headline = the HBM frac of the dominant kernel (the certified pruned scan streams the DB '
+                        'tiles it needs); SURVEY §8(d)\'s fp32-MFMA basis (brute-force 2*D*N_A*N_B flops vs the fp32 '
+                        'matrix peak) does not apply under certified pruning, which skips most of that work on '
+                        'purpose: fp32_mfma_equiv_* is a work-equivalent rate, not a utilisation'
+                        if st['prune_launches_timed'] > 0 else
+                        'distance scan on MFMA; flops are the algorithmic 2*D*N_A*M per launch')
+    if concurrent:
+        roofline['k3_share_of_step'] = None   # single-stream pass vs concurrent timed steps: not comparable
+        roofline['timing'] = ('K3/K2/K4 device times from one extra single-stream pass (the timed steps ran %d '
+                              'concurrent streams, whose HIP events would overlap)' % len(ctxs))
+    roofline['gathers'] = gather_rooflines(st)
     roofline['fp32_mfma_equiv_tflops'] = fp32_equiv / 1e12
     roofline['fp32_mfma_equiv_frac'] = fp32_equiv / FP32_MFMA_PEAK
     roofline['pairs_frac'] = st['dist_pairs'] / max(st['dist_pairs_full'], 1.)
@@ -374,7 +496,7 @@ def main():
                                                             '%.0f MB, <1%% of the step) is excluded'
                                                             % (job_pixels * 20 / 1e6))},
            'roofline': roofline,
-           'stats': {k: st[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
+           'stats': {k: st_all[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
                                         'synth_ms', 'bound_violations', 'kappa_ambiguous', 'f16_levels', 'pruned_levels',
                                         'dist_pairs', 'dist_pairs_full', 'dist_tiles', 'dist_tiles_full',
                                         'dist_pairs_corrected', 'dist_tiles_rows')}}
@@ -382,12 +504,16 @@ def main():
         out['config']['sweep'] = {'jobs': len(sw.jobs), 'batched': not args.sequential, 'max_batch': args.max_batch,
                                   'streams': args.streams,
                                   'kappas': sorted({j.k for j in sw.jobs}), 'depths': sorted(set(sw.L))}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out['cpu_baseline'] = (cpu_baseline_sweep(sw, args.cpu_seconds) if sw is not None
-                               else cpu_baseline(job, args.cpu_seconds))
+    if value_replicas is not None:
+        out['value_replicas'] = value_replicas
+        out['config']['replicas'] = ('value_replicas = %d independent cfg jobs, one per GPU, no collective '
+                                     '(B\' px/s aggregate)' % world)
+    if cpu is not None:
+        out['cpu_baseline'] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for cx in ctxs:
+        cx.close()
     if dist:
         dist.destroy_process_group()
 

@@ -44,7 +44,12 @@ class Stats(ctypes.Structure):
                 ('prune_ms_timed', ctypes.c_double), ('prune_launches_timed', ctypes.c_int64),
                 ('prune_flops_timed', ctypes.c_double), ('prune_bytes_timed', ctypes.c_double),
                 ('kappa_ambiguous', ctypes.c_int64), ('dist_pairs_corrected', ctypes.c_double),
-                ('dist_tiles_rows', ctypes.c_double)]
+                ('dist_tiles_rows', ctypes.c_double),
+                ('k1b_ms', ctypes.c_double), ('k1b_bytes', ctypes.c_double), ('k1_ms', ctypes.c_double),
+                ('k1_bytes', ctypes.c_double), ('build_levels', ctypes.c_int64),
+                ('gather_ms_timed', ctypes.c_double), ('gather_launches_timed', ctypes.c_int64),
+                ('gather_bytes_timed', ctypes.c_double), ('merge_ms_timed', ctypes.c_double),
+                ('merge_launches_timed', ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -63,6 +68,8 @@ EXPORTS = {
     'ia_set_option': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_int]),
     'ia_comm_unique_id': (ctypes.c_int, [ctypes.c_char_p]),
     'ia_comm_init': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
+    'ia_xchg_alloc': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]),
+    'ia_xchg_open': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
     'ia_synthesize_level': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LevelArgs), ctypes.POINTER(Stats)]),
     'ia_synthesize_levels': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LevelArgs), ctypes.c_int,
                                             ctypes.POINTER(Stats)]),
@@ -225,6 +232,17 @@ class Context(object):
 
     def comm_init(self, rank, world, uid):
         check(lib().ia_comm_init(self._h, rank, world, bytes(uid)), 'ia_comm_init')
+
+    def xchg_init(self, rank, world, all_gather):
+        """Peer-write winner exchange of sharded levels (include/ia.h ia_xchg_alloc/open):
+        all_gather(bytes) -> list of every rank's bytes in rank order (e.g. a torch.distributed
+        all_gather_object wrapper).  Makes this context rank `rank` of a world-rank DB shard."""
+        h = ctypes.create_string_buffer(64)
+        check(lib().ia_xchg_alloc(self._h, world, h), 'ia_xchg_alloc')
+        hs = all_gather(h.raw)
+        if len(hs) != world or any(len(x) != 64 for x in hs):
+            raise IAError('xchg_init: expected %d handles of 64 bytes' % world)
+        check(lib().ia_xchg_open(self._h, rank, world, b''.join(hs)), 'ia_xchg_open')
 
     def synthesize_level(self, A, Ac, Ap_list, Apc_list, B, Bc, Bpc, Bp, weights, kappa_factor, stats=None,
                          debug=None):

@@ -107,11 +107,19 @@ struct ia_ctx {
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   // per-step K3 timing (optional)
   int time_dist = 0;
-  std::vector<hipEvent_t> evs;
+  std::vector<hipEvent_t> evs, evg, evm;  // sampled steps: K3, K2 and K4 brackets
   hipEvent_t lv0 = nullptr, lv1 = nullptr, lv2 = nullptr;
+  hipEvent_t kb[4] = {nullptr, nullptr, nullptr, nullptr};  // per level: K1b start / end, K1 start / end
   // multi-GPU
   int rank = 0, world = 1;
   ncclComm_t comm = nullptr;
+  int exchange = 0;               // option "exchange": 0 = RCCL all-gather + finish, 1 = peer-write merge
+  void *xbuf = nullptr;           // this process's exchange buffer (uncached, IPC-exportable)
+  int xbuf_w = 0;                 // ranks the buffer was sized for
+  XSlot *xpeer[IA_XCHG_MAXW] = {};  // every rank's buffer in this address space (ia_xchg_open)
+  bool xmapped[IA_XCHG_MAXW] = {};  // opened through hipIpcOpenMemHandle (closed on destroy)
+  unsigned xseq = 0;              // exchange sequence number (one per sharded step, same on every rank)
+  DevBuf xerr;
 };
 
 struct ia_index {
@@ -296,6 +304,7 @@ int ia_init(int device, ia_ctx **out) {
   hipEventCreate(&c->lv0);
   hipEventCreate(&c->lv1);
   hipEventCreate(&c->lv2);
+  for (hipEvent_t &e : c->kb) hipEventCreate(&e);
   *out = c;
   return IA_OK;
 }
@@ -312,11 +321,17 @@ void ia_destroy(ia_ctx *c) {
                     &c->pr_rot, &c->pr_lut,
                     &c->py_in, &c->py_tmp, &c->py_sm, &c->py_mm, &c->py_out})
     b->release();
-  for (hipEvent_t e : c->evs) hipEventDestroy(e);
+  for (auto *v : {&c->evs, &c->evg, &c->evm})
+    for (hipEvent_t e : *v) hipEventDestroy(e);
+  for (hipEvent_t e : c->kb) hipEventDestroy(e);
   hipEventDestroy(c->lv0);
   hipEventDestroy(c->lv1);
   hipEventDestroy(c->lv2);
   if (c->comm) ncclCommDestroy(c->comm);
+  for (int p = 0; p < IA_XCHG_MAXW; p++)
+    if (c->xmapped[p]) hipIpcCloseMemHandle(c->xpeer[p]);
+  if (c->xbuf) hipFree(c->xbuf);
+  c->xerr.release();
   hipStreamDestroy(c->st);
   delete c;
 }
@@ -382,6 +397,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     c->prune = value;
     return IA_OK;
   }
+  if (!std::strcmp(name, "exchange")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: exchange must be 0 (RCCL) or 1 (peer write)");
+    c->exchange = value;
+    return IA_OK;
+  }
   if (!std::strcmp(name, "matcher")) {
     if (value != IA_MATCH_F32 && value != IA_MATCH_F16X3) return fail(IA_EINVAL, "ia_set_option: matcher must be 0 or 1");
     c->matcher = value;
@@ -409,6 +429,65 @@ int ia_comm_init(ia_ctx *c, int rank, int world, const unsigned char id[128]) {
   ncclUniqueId uid;
   std::memcpy(&uid, id, 128);
   NCCL_TRY(ncclCommInitRank(&c->comm, world, uid, rank));
+  return IA_OK;
+}
+
+static int xchg_alloc(ia_ctx *c, int world) {
+  if (c->xbuf && c->xbuf_w >= world) return IA_OK;
+  if (c->xbuf) hipFree(c->xbuf);
+  c->xbuf = nullptr;
+  const size_t bytes = (size_t)2 * world * IA_XCHG_MAXQ * sizeof(XSlot);
+  // uncached: peers' xGMI stores and this device's polling loads meet in memory, not in an L2
+  HIP_TRY(hipExtMallocWithFlags(&c->xbuf, bytes, hipDeviceMallocUncached));
+  HIP_TRY(hipMemset(c->xbuf, 0, bytes));
+  HIP_TRY(hipDeviceSynchronize());
+  c->xbuf_w = world;
+  c->xseq = 0;
+  int rc;
+  if ((rc = c->xerr.ensure(4))) return rc;
+  return IA_OK;
+}
+
+int ia_xchg_alloc(ia_ctx *c, int world, unsigned char handle_out[64]) {
+  if (!c || !handle_out || world < 1 || world > IA_XCHG_MAXW) return fail(IA_EINVAL, "ia_xchg_alloc: world must be 1..16");
+  static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t size");
+  HIP_TRY(hipSetDevice(c->dev));
+  int rc;
+  if ((rc = xchg_alloc(c, world))) return rc;
+  hipIpcMemHandle_t h;
+  HIP_TRY(hipIpcGetMemHandle(&h, c->xbuf));
+  std::memcpy(handle_out, &h, 64);
+  return IA_OK;
+}
+
+int ia_xchg_open(ia_ctx *c, int rank, int world, const unsigned char *handles) {
+  if (!c || !handles || world < 1 || world > IA_XCHG_MAXW || rank < 0 || rank >= world)
+    return fail(IA_EINVAL, "ia_xchg_open: bad rank / world");
+  if (!c->xbuf || c->xbuf_w != world) return fail(IA_EINVAL, "ia_xchg_open: call ia_xchg_alloc with this world first");
+  HIP_TRY(hipSetDevice(c->dev));
+  for (int p = 0; p < IA_XCHG_MAXW; p++)
+    if (c->xmapped[p]) {
+      hipIpcCloseMemHandle(c->xpeer[p]);
+      c->xmapped[p] = false;
+    }
+  for (int p = 0; p < world; p++) {
+    if (p == rank) {
+      c->xpeer[p] = (XSlot *)c->xbuf;
+      continue;
+    }
+    hipIpcMemHandle_t h;
+    std::memcpy(&h, handles + (size_t)64 * p, 64);
+    void *ptr = nullptr;
+    HIP_TRY(hipIpcOpenMemHandle(&ptr, h, hipIpcMemLazyEnablePeerAccess));
+    c->xpeer[p] = (XSlot *)ptr;
+    c->xmapped[p] = true;
+  }
+  if (c->comm) ncclCommDestroy(c->comm);
+  c->comm = nullptr;
+  c->rank = rank;
+  c->world = world;
+  c->exchange = 1;
+  c->xseq = 0;
   return IA_OK;
 }
 
@@ -558,6 +637,14 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   const int Wsh = sharded ? c->world : emulated ? c->shard_emulate : 1;  // shards of this level
   const bool multi = Wsh > 1;
   if (multi && J > 1) return fail(IA_EINVAL, "ia_synthesize_levels: sharded levels take one job per call");
+  const bool xchg = multi && c->exchange == 1;  // peer-write winner exchange (k_merge_xchg)
+  if (xchg) {
+    if (sharded && !c->xpeer[0]) return fail(IA_EINVAL, "ia_synthesize_level: exchange = 1 needs ia_xchg_open");
+    if (emulated && (rc = xchg_alloc(c, Wsh))) return rc;
+    if ((int64_t)std::min(g.bh, (g.bw + 2) / 3) > IA_XCHG_MAXQ)
+      return fail(IA_EINVAL, "ia_synthesize_level: wavefront steps wider than the exchange slots");
+    HIP_TRY(hipMemsetAsync(c->xerr.p, 0, 4, c->st));
+  }
   for (int j = 0; j < J; j++)
     if (multi && args[j].dbg_src)
       return fail(IA_EINVAL, "ia_synthesize_level: debug outputs are produced by single-rank levels only");
@@ -648,7 +735,8 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   ia_wavefront_shape(g.bh, g.bw, &T, &Mmax);
   const int64_t Mtmax = Mmax * J;  // queries of the widest step over all jobs
   const int64_t Mpad_max = (Mtmax + IA_TILE - 1) / IA_TILE * IA_TILE;
-  const bool prune = c->prune && use_h && g.ch == 1 && g.NA >= c->prune_min_rows && Mpad_max <= 4096;
+  const bool prune = c->prune && use_h && g.ch == 1 && g.NA >= c->prune_min_rows && Mpad_max <= 4096 &&
+                     (g.n_tiles + IA_NWG_H - 1) / IA_NWG_H <= IA_K3P_MAXK_LDS;
   // Pruned levels: every rank holds the whole Morton-sorted DB, its tiles stored shard by shard
   // (ia_internal.h ia_shard_morton_tile: shard r = Morton tiles r, r + W, ...), and scans its own
   // contiguous storage range.  Unpruned levels: contiguous tile ranges (ia_shard_tiles).
@@ -719,7 +807,9 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
 
   HIP_TRY(hipEventRecord(c->lv0, c->st));
   ia_launch_means(g.ch, Aim, g.n_ap, c->mu.as<double>(), c->st);
+  HIP_TRY(hipEventRecord(c->kb[0], c->st));
   ia_launch_db64_build(g, Aim, c->db64.as<double>(), c->st);  // every row: coherence reads any row
+  HIP_TRY(hipEventRecord(c->kb[1], c->st));
   double ufac = 0., eps_r = 0.;
   int lut_bits = 0;
   // rotated DB + head-filtered scan (k3p_variant 16 / 17): unsharded pruned levels whose
@@ -733,6 +823,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                    (g.n_tiles + IA_NWG_H - 1) / IA_NWG_H <= 512;
   if (prune && (rc = prepare_prune(c, g, c->mu.as<double>(), Wsh, &ufac, rot, &eps_r, &lut_bits)))
     return rc;  // sets g.pos2row
+  HIP_TRY(hipEventRecord(c->kb[2], c->st));
   if (ns > 0) {
 #ifdef IA_K3H_DIAG
     if (rot)
@@ -740,9 +831,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                              c->db.p, c->Rbits.as<unsigned>(), c->st);
     else
 #endif
-    if (use_h) ia_launch_db_build_h(g, Aim, c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
+    if (use_h) ia_launch_db_build_h(g, Aim, c->db64.as<double>(), c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
     else ia_launch_db_build(g, Aim, c->mu.as<double>(), c->db.as<float4>(), c->Rbits.as<unsigned>(), c->st);
   }
+  HIP_TRY(hipEventRecord(c->kb[3], c->st));
   HIP_TRY(hipEventRecord(c->lv1, c->st));
 
   MergeArgs ma;
@@ -795,11 +887,19 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   const int qtmax = use_h ? ia_k3h_qtmax(g.KS) : ia_k3_qtmax(g.KH);
   const int stride = c->time_dist > 0 ? c->time_dist : 0;
   const int64_t n_timed = stride ? (T + stride - 1) / stride : 0;
-  if ((int64_t)c->evs.size() < 2 * n_timed) {
-    size_t old = c->evs.size();
-    c->evs.resize(2 * n_timed);
-    for (size_t i = old; i < c->evs.size(); i++) hipEventCreate(&c->evs[i]);
-  }
+  for (auto *v : {&c->evs, &c->evg, &c->evm})
+    if ((int64_t)v->size() < 2 * n_timed) {
+      size_t old = v->size();
+      v->resize(2 * n_timed);
+      for (size_t i = old; i < v->size(); i++) hipEventCreate(&(*v)[i]);
+    }
+  // algorithmic bytes of one query's gather (K2h / K2p): its 55*ch features read, (K2p) the 12
+  // causal coherence candidates' fp64 rows for U, the fp64 row + MFMA fragments + |q'|^2 (+ K2p's
+  // pruning record) written
+  const double gq_bytes = 55.0 * g.ch * 8 + (prune ? 12.0 * ia_db64_stride(g.ch) * 8 : 0.) + g.D * 8.0 +
+                          (use_h ? 16.0 * g.KS * 4 : DP * 4.0) + 8.0 + (prune ? 48.0 : 0.);
+  int64_t n_gm = 0;                        // sampled steps (gather / merge brackets)
+  double gather_bytes_timed = 0.;
   int64_t dist_launches = 0, launches_timed = 0, n_rec = 0;
   double dist_flops = 0., flops_timed = 0., pairs_full = 0., tiles_full = 0., bytes_timed_fixed = 0.;
   int ord_n = 0;  // pruned scan (k3p_variant 8): queries in the previous step's key order
@@ -814,6 +914,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     }
     const int Mt = J * sd.M;  // queries of this step over all jobs
     sd.Mpad = (Mt + IA_TILE - 1) / IA_TILE * IA_TILE;
+    const bool timed_gm = stride && t % stride == 0;
+    if (timed_gm) {
+      hipEventRecord(c->evg[2 * n_gm], c->st);
+      gather_bytes_timed += gq_bytes * Mt;
+    }
 #ifdef IA_K3H_DIAG
     if (rot)
       ia_launch_gather_r(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
@@ -829,6 +934,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     else
       ia_launch_gather(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(),
                        c->st);
+    if (timed_gm) hipEventRecord(c->evg[2 * n_gm + 1], c->st);
     // pruned scan: queries sorted once per step (K2s) when the step is wider than the in-kernel
     // sort of v6/v7 (512) or variant 11 is selected
     // (variants 11, 12: presorted; 7, 13: in-kernel sort up to 512 queries, presorted v11 / v12 above)
@@ -888,8 +994,23 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       if (timed) hipEventRecord(c->evs[2 * n_rec++ + 1], c->st);
       ord_n = prune && J == 1 && !multi && sd.Mpad <= 4096 ? sd.M : 0;
     }
+    if (timed_gm) hipEventRecord(c->evm[2 * n_gm], c->st);
     if (!multi) {
       ia_launch_merge(g, sd, Aim, mas[0], c->win.as<Winner>(), djobs, true, c->st);
+    } else if (xchg) {
+      // one-shot peer-write exchange fused into the merge: each shard's winner goes into every
+      // rank's buffer; the last launch of this process waits for all W and finishes the pixels
+      XchgArgs xa;
+      for (int p = 0; p < IA_XCHG_MAXW; p++) xa.peer[p] = sharded ? c->xpeer[p] : (XSlot *)c->xbuf;
+      xa.local = sharded ? c->xpeer[c->rank] : (XSlot *)c->xbuf;
+      xa.W = Wsh;
+      xa.seq = ++c->xseq;
+      xa.err = c->xerr.as<unsigned>();
+      xa.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
+      for (size_t i = 0; i < shards.size(); i++) {
+        xa.rank = sharded ? c->rank : (int)i;
+        ia_launch_merge_xchg(g, sd, Aim, mas[i], xa, djobs, i + 1 == shards.size(), c->st);
+      }
     } else {
       // certified per-shard winners, then the global winner (smallest exact distance, lowest row)
       // and coherence / kappa / writeback, identical on every rank
@@ -901,6 +1022,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       ia_launch_finish(g, sd, Aim, c->db64.as<double>(), c->q64.as<double>(), c->allwin.as<Winner>(), Wsh, sd.M, djobs,
                        c->st);
     }
+    if (timed_gm) hipEventRecord(c->evm[2 * n_gm++ + 1], c->st);
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->lv2, c->st));
@@ -921,6 +1043,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
 #if IA_PROBE & 16
   if (prune) ia_k3p_probe_dump();
 #endif
+  if (xchg) {
+    unsigned xe = 0;
+    HIP_TRY(hipMemcpy(&xe, c->xerr.p, 4, hipMemcpyDeviceToHost));
+    if (xe) return fail(IA_ECOMM, "ia_synthesize_level: a peer's shard winner did not arrive within 20 s (peer-write exchange)");
+  }
   if (stats) {
     unsigned long long ctr[5], prs[4], pfull = 0, prow[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
@@ -955,9 +1082,31 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     stats->dist_tiles_full += tiles_full;
     stats->dist_pairs_corrected += (double)pfull;
     stats->dist_tiles_rows += (double)(prow[2] + prow[3]);
-    float ms_db = 0.f, ms_syn = 0.f;
+    float ms_db = 0.f, ms_syn = 0.f, ms_k1b = 0.f, ms_k1 = 0.f;
     hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
     hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);
+    hipEventElapsedTime(&ms_k1b, c->kb[0], c->kb[1]);
+    hipEventElapsedTime(&ms_k1, c->kb[2], c->kb[3]);
+    {  // K1b: A-side images read once, every fp64 row written; K1: this process's rows read, tiles written
+      const int DSb = ia_db64_stride(g.ch);
+      stats->k1b_ms += ms_k1b;
+      stats->k1b_bytes += (double)(nA + nAc) * (1 + g.n_ap) * 8 + (double)g.NA * DSb * 8;
+      if (ns > 0 && use_h && !rot) {
+        stats->k1_ms += ms_k1;
+        stats->k1_bytes += (double)std::min<int64_t>((int64_t)ns * IA_TILE, g.NA) * DSb * 8 + (double)ns * tile_bytes;
+      }
+      stats->build_levels += 1;
+    }
+    for (int64_t i = 0; i < n_gm; i++) {
+      float mg = 0.f, mm = 0.f;
+      hipEventElapsedTime(&mg, c->evg[2 * i], c->evg[2 * i + 1]);
+      hipEventElapsedTime(&mm, c->evm[2 * i], c->evm[2 * i + 1]);
+      stats->gather_ms_timed += mg;
+      stats->merge_ms_timed += mm;
+    }
+    stats->gather_launches_timed += n_gm;
+    stats->merge_launches_timed += n_gm;
+    stats->gather_bytes_timed += gather_bytes_timed;
     stats->pixels += NB * J;
     stats->steps += T;
     stats->reranked += (int64_t)ctr[0];

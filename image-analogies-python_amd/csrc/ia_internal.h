@@ -166,6 +166,9 @@ inline int64_t ia_shard_off(int64_t NT, int W, int r) { return r * (NT / W) + (r
 #define IA_NPC 4
 #define IA_PRUNE_MIN_ROWS 524288  // default of option "prune_min_rows": at 512^2 (262,144 rows) the
                                   // unpruned scan + cheaper gather/merge is still faster
+// DB tiles per workgroup the pruned scan takes (its tile boxes, need masks and R_t in LDS: 44 B
+// per tile next to <= 11 query tiles); larger DBs (> 8.4 M rows per shard) scan unpruned
+#define IA_K3P_MAXK_LDS 1024
 
 // per-step wavefront description: pixels (r, t - 3r), r in [r0, r0 + M), of each of J jobs.
 // Query m of the step (0 <= m < J*M) is job m / M, row r0 + m % M; Mpad = J*M rounded up to
@@ -225,6 +228,31 @@ struct Winner {
   double d;
   int64_t idx;
 };
+
+// One-shot peer-write winner exchange of a sharded level (option "exchange" = 1):
+// every rank's exchange buffer holds, per step parity (2) x rank (W) x query (IA_XCHG_MAXQ), a
+// 16-byte slot: the certified shard winner's exact distance, then (row | step sequence << 32)
+// written last with release semantics at system scope.  The merge of each rank writes its
+// winner into the slot of every peer (xGMI stores into the peers' buffers, opened through HIP
+// IPC handles) and polls its own buffer for the W winners of the step.  Two parities suffice: a
+// rank can be at most one step ahead of any peer (its step t+1 needs every step-t winner).
+#define IA_XCHG_MAXQ 4096  // queries per step (>= the widest 1-job step: min(h, ceil(w / 3)))
+#define IA_XCHG_MAXW 16    // ranks of one exchange
+struct XSlot {
+  double d;
+  unsigned long long row_seq;  // row (low 32 bits) | sequence number (high 32 bits)
+};
+struct XchgArgs {
+  XSlot *peer[IA_XCHG_MAXW];   // every rank's exchange buffer in this process's address space
+  XSlot *local;                // this process's buffer (polled)
+  int W, rank;                 // ranks (shards) and the shard this launch publishes as
+  unsigned seq;                // exchange sequence number of the step (identical on every rank)
+  unsigned *err;               // bit 0: a peer's winner did not arrive in time
+  long long timeout_ticks;     // s_memrealtime ticks (100 MHz) before giving up
+};
+__host__ __device__ inline size_t ia_xslot(unsigned seq, int W, int rank, int m) {
+  return ((size_t)(seq & 1u) * W + rank) * IA_XCHG_MAXQ + m;
+}
 
 __host__ __device__ inline int ia_reflect(int i, int n) {
   // np.pad(mode='symmetric') index map (img_preprocess.py:81-83).  Windows reach at most 2

@@ -811,6 +811,8 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   constexpr int NE = PRE ? 1 : (IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE + WGT - 1) / WGT;  // unsorted fragments per thread
   static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
+  // the in-kernel sort holds one query per thread; the tile lists of the !INTER and HF paths one
+  // tile per thread (the launcher keeps K <= IA_K3P3_MAXK there); INTER walks any K
   static_assert(WGT >= IA_K3P3_MAXQ && WGT >= IA_K3P3_MAXK, "one query / one tile per thread");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
   float4 *qlo = reinterpret_cast<float4 *>(ldsh + QT * NP * IA_WAVE);  // [NQ]
@@ -823,7 +825,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   int *order = reinterpret_cast<int *>(skey + (PRE ? NQ : Mpad));       // [Mpad] sorted -> query
   int *rankof = order + (PRE ? 0 : Mpad);                               // [Mpad] query -> sorted
   const int wg = blockIdx.x;
-  const int K = (NT - wg + nwg - 1) / nwg;  // tiles wg + nwg*k, k < K (host: nwg <= NT, K <= MAXK)
+  const int K = (NT - wg + nwg - 1) / nwg;  // tiles wg + nwg*k, k < K (host: nwg <= NT, K <= IA_K3P_MAXK_LDS)
   // rev: this step walks the workgroup's tiles in reverse (alternate steps: the tiles read last
   // by one step are read first by the next, while they are still in the memory-side cache)
   auto tk = [&](int k) { return wg + nwg * (rev ? K - 1 - k : k); };
@@ -868,11 +870,11 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       thi[tid] = tbox[3 * (qt0 + tid) + 1];
       tU[tid] = tbox[3 * (qt0 + tid) + 2].x;
     }
-    if (tid < K) {
-      const int t = tk(tid);
-      wbox[2 * tid] = boxes[2 * t];
-      wbox[2 * tid + 1] = boxes[2 * t + 1];
-      if constexpr (HHF) wR[tid] = tnorm[t];
+    for (int x = tid; x < K; x += WGT) {  // K may exceed WGT (INTER variants: up to IA_K3P_MAXK_LDS)
+      const int t = tk(x);
+      wbox[2 * x] = boxes[2 * t];
+      wbox[2 * x + 1] = boxes[2 * t + 1];
+      if constexpr (HHF) wR[x] = tnorm[t];
     }
   }
   __shared__ int kctr;  // DYN: next tile index to hand out
@@ -898,11 +900,11 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     const int e = tid + WGT * i;
     qe[i] = qf[e < ne ? e : 0];  // unconditional: equal vmcnt on every path
   }
-  if (tid < K) {
-    const int t = tk(tid);
-    wbox[2 * tid] = boxes[2 * t];
-    wbox[2 * tid + 1] = boxes[2 * t + 1];
-    if constexpr (HHF) wR[tid] = tnorm[t];
+  for (int x = tid; x < K; x += WGT) {
+    const int t = tk(x);
+    wbox[2 * x] = boxes[2 * t];
+    wbox[2 * x + 1] = boxes[2 * t + 1];
+    if constexpr (HHF) wR[x] = tnorm[t];
   }
   if (tid < Mpad) {
     skey[tid] = mkey;

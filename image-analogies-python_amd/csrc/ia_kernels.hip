@@ -22,6 +22,9 @@
 #include <float.h>
 #include <stdint.h>
 
+#include <mutex>
+#include <unordered_set>
+
 #include "ia_internal.h"
 #include "ia_prune.h"
 
@@ -31,6 +34,9 @@
 // waves (= queries) per workgroup of the one-wave-per-query kernels K2h, K2p, K4: one, so a
 // step's few hundred latency-bound waves spread over as many CUs (their L1, TA and LDS) as
 // possible; 3.35 -> 3.44 M px/s against 4 per workgroup on one box (profiles/r02/wpb)
+#ifndef IA_K1_GATHER
+#define IA_K1_GATHER 0  // 1: the round-2 image-gathering DB builds (same-box A/B only)
+#endif
 #ifndef IA_PQ_WPB
 #define IA_PQ_WPB 1
 #endif
@@ -433,6 +439,7 @@ __global__ void __launch_bounds__(IA_WG) k_db_build(LevelGeo g, Imgs A, const do
 // The merge reranks candidates from it with contiguous 16-byte loads instead of re-gathering
 // four symmetric-padded images per row.  One thread per (row, 8 features): coalesced stores.
 // ------------------------------------------------------------------------------------------
+#if IA_K1_GATHER  // round-2 K1b (A/B builds only): one thread per (row, 8 features), 0.89 TB/s at 1024^2
 template <int CH>
 __global__ void __launch_bounds__(IA_WG) k_db64_build(LevelGeo g, Imgs A, double *__restrict__ db64) {
   using G = Geo<CH>;
@@ -456,6 +463,40 @@ __global__ void __launch_bounds__(IA_WG) k_db64_build(LevelGeo g, Imgs A, double
 #pragma unroll
   for (int e = 0; e < 4; e++) dst[e] = make_double2(v[2 * e], v[2 * e + 1]);
 }
+#else
+// One wave per 64 consecutive DB rows (= raster pixels of one A' image, so lane-adjacent rows are
+// pixel-adjacent): every feature load of the wave reads 64 consecutive image values (coalesced),
+// the rows are assembled in LDS (odd row stride: conflict-light) and leave as one contiguous
+// 64 * DS * 8 B block of 1 KiB global_store_dwordx4 per instruction.
+template <int CH>
+__global__ void __launch_bounds__(IA_WAVE) k_db64_build(LevelGeo g, Imgs A, double *__restrict__ db64) {
+  using G = Geo<CH>;
+  constexpr int DS = G::DS, LS = DS + 1, H2 = DS / 2;
+  __shared__ double t[IA_WAVE * LS];
+  const int64_t r0 = (int64_t)blockIdx.x * IA_WAVE;
+  const int lane = threadIdx.x;
+  const int64_t row = r0 + lane;
+  if (row < g.NA) {
+    const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
+    const int img = (int)((unsigned)row / hw);
+    const unsigned rem = (unsigned)row - (unsigned)img * hw;
+    const int pr = (int)(rem / (unsigned)g.aw), pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
+    const Px P = make_px<CH>(A, pr, pc);
+    double v[G::D];
+#pragma unroll
+    for (int f = 0; f < G::D; f++) v[f] = featp<CH>(A, P, f, img);  // all loads in flight together
+#pragma unroll
+    for (int f = 0; f < DS; f++) t[lane * LS + f] = f < G::D ? v[f] : 0.;
+  }
+  __syncthreads();
+  const int nrows = (int)min<int64_t>(IA_WAVE, g.NA - r0);
+  double2 *dst = reinterpret_cast<double2 *>(db64 + r0 * DS);
+  for (int i = lane; i < nrows * H2; i += IA_WAVE) {
+    const int rr = i / H2, cc = 2 * (i - rr * H2);
+    dst[i] = make_double2(t[rr * LS + cc], t[rr * LS + cc + 1]);
+  }
+}
+#endif
 
 // ------------------------------------------------------------------------------------------
 // K2: queries of one wavefront step (one wave per query pixel)
@@ -682,6 +723,7 @@ __global__ void __launch_bounds__(IA_WG) k_absmax(AbsArrays arr, unsigned *__res
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
+#if IA_K1_GATHER  // round-2 K1 (A/B builds only): one thread per row gathering from the images
 template <int CH, int KS>
 __global__ void __launch_bounds__(IA_WG) k_db_build_h(LevelGeo g, Imgs A, const double *__restrict__ mu_part,
                                                        h16x8 *__restrict__ db, unsigned *__restrict__ Rbits) {
@@ -737,6 +779,99 @@ __global__ void __launch_bounds__(IA_WG) k_db_build_h(LevelGeo g, Imgs A, const 
   for (int o = 32; o > 0; o >>= 1) R = fmaxf(R, __shfl_xor(R, o, 64));
   if ((threadIdx.x & 63) == 0 && R > 0.f) atomicMax(Rbits, __float_as_uint(R));
 }
+#else
+// One wave per DB tile (32 rows x 64 columns in v_mfma_f32_32x32x16_f16 operand order): lane L
+// (row j = L & 31, column half h = L >> 5) holds columns 16s + 8h .. + 7 of every k-step s, i.e.
+// 64 contiguous bytes of its row in the fp64 row DB (K1b, written just before: rows are whole
+// 128 B lines, no image gathers).  Centre by mu, |a'|^2 = the two lane halves' partial sums (the
+// certified bound does not depend on its rounding order), split into f16 hi + lo, and store
+// each piece as one 1 KiB coalesced wave store.  Grid-stride over tiles: one atomicMax of R per
+// workgroup.
+template <int CH, int KS>
+__global__ void __launch_bounds__(IA_WG) k_db_build_h(LevelGeo g, const double *__restrict__ db64,
+                                                       const double *__restrict__ mu_part, h16x8 *__restrict__ db,
+                                                       unsigned *__restrict__ Rbits) {
+  constexpr int D = 55 * CH, DS = Geo<CH>::DS;
+  static_assert(16 * KS >= D + 1, "k-steps must hold D features + the norm column");
+  static_assert(DS % 8 == 0, "64-byte row pieces");
+  __shared__ float wR[IA_WG / IA_WAVE];
+  const int lane = threadIdx.x & 63, j = lane & 31, h = lane >> 5, wave = threadIdx.x >> 6;
+  const int64_t nloc = (int64_t)g.tile1 - g.tile0;
+  double mu[KS][8];  // this lane's feature means (the lane's columns are fixed)
+#pragma unroll
+  for (int s = 0; s < KS; s++)
+#pragma unroll
+    for (int e = 0; e < 8; e++) {
+      const int f = 16 * s + 8 * h + e;
+      mu[s][e] = f < D ? mu_part[feat_part<CH>(f) * CH + feat_ch<CH>(f)] : 0.;
+    }
+  float Rmax = 0.f;
+  for (int64_t lt = (int64_t)blockIdx.x * (IA_WG / IA_WAVE) + wave; lt < nloc; lt += (int64_t)gridDim.x * (IA_WG / IA_WAVE)) {
+    const int64_t pos = (g.tile0 + lt) * IA_TILE + j;
+    const int64_t row = ia_pos_row_t(pos, g.n_tiles, g.pos2row);
+    const bool real = row < g.NA;
+    double a[KS][8];
+#pragma unroll
+    for (int s = 0; s < KS; s++) {
+      const int f0 = 16 * s + 8 * h;
+      double2 v[4];
+      if (real && f0 < DS) {
+        const double2 *src = reinterpret_cast<const double2 *>(db64 + row * DS + f0);
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = src[e];
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; e++) v[e] = make_double2(0., 0.);
+      }
+#pragma unroll
+      for (int e = 0; e < 4; e++) {
+        a[s][2 * e] = v[e].x;
+        a[s][2 * e + 1] = v[e].y;
+      }
+    }
+    double nrm = 0.;
+#pragma unroll
+    for (int s = 0; s < KS; s++)
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        const int f = 16 * s + 8 * h + e;
+        a[s][e] = f < D ? a[s][e] - mu[s][e] : 0.;
+        nrm += a[s][e] * a[s][e];
+      }
+    nrm += __shfl_xor(nrm, 32, 64);  // both halves: p0 + p1 (addition commutes exactly)
+    const int64_t tb = lt * TileFmt<KS>::STRIDE;
+#pragma unroll
+    for (int s = 0; s < KS; s++) {
+      h16x8 vh, vl;
+#pragma unroll
+      for (int e = 0; e < 8; e++) {
+        double x = a[s][e];
+        if (16 * s + 8 * h + e == D) x = real ? nrm * (1.0 / IA_NORM_SCALE) : 60000.0;  // padding rows: never a candidate
+        _Float16 hi, lo;
+        split_h(x, hi, lo);
+        vh[e] = hi;
+        vl[e] = lo;
+      }
+      if (!(TileFmt<KS>::CMP && s == KS - 1 && h == 1)) {  // (compact: padding half not stored)
+        db[tb + TileFmt<KS>::off(2 * s, lane)] = vh;
+        db[tb + TileFmt<KS>::off(2 * s + 1, lane)] = vl;
+      }
+    }
+    if (real) Rmax = fmaxf(Rmax, (float)(sqrt(nrm) * (1.0 + 1e-6)));
+  }
+  // R = max |a'| (certification bound): wave, then workgroup max, one atomic per workgroup
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) Rmax = fmaxf(Rmax, __shfl_xor(Rmax, o, 64));
+  if (lane == 0) wR[wave] = Rmax;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float m = wR[0];
+#pragma unroll
+    for (int w = 1; w < IA_WG / IA_WAVE; w++) m = fmaxf(m, wR[w]);
+    if (m > 0.f) atomicMax(Rbits, __float_as_uint(m));
+  }
+}
+#endif
 
 template <int KS>
 __device__ __forceinline__ void put_qh(_Float16 *qf, int m, int f, double v) {
@@ -1742,6 +1877,72 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
                    jp.pstat, prev);
 }
 
+// Sharded level, peer-write exchange (option "exchange" = 1): the certified winner of this
+// rank's shard (as k_merge_level<FUSED = false>) is written into every rank's exchange buffer;
+// with FIN the wave then polls its own buffer for the W winners of its query, takes the global
+// winner (smallest exact distance, then lowest row: the lexicographic minimum, independent of
+// arrival order) and finishes the pixel (coherence, kappa, writeback) exactly as
+// k_finish_level.  One launch per step replaces merge + all-gather + finish.  Emulated shards on
+// one device (shard_emulate) publish with FIN = false for shards 0..W-2 and FIN = true for the
+// last.  A wait beyond xa.timeout_ticks sets *err and finishes with the winners that arrived
+// (the host reports IA_ECOMM): no wave spins forever.
+template <int CH, bool FIN, class JS>
+__global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, XchgArgs xa, JS jobs) {
+  const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * IA_PQ_WPB + (threadIdx.x >> 6));  // wave-uniform
+  if (m >= sd.J * sd.M) return;
+  const int lane = threadIdx.x & 63;
+  const QPix px = ia_qpix(sd, g.bw, m);
+  const JobPtrs jp = jobs.get(px.job);
+  const double *q = ma.q64 + (int64_t)m * Geo<CH>::D;
+  unsigned stat = 0;
+  const Winner wn = certified_winner(ma, m, [&](int64_t row) { return exact_dist_level<CH>(ma.db64, row, q); }, &stat);
+  if (lane < xa.W) {  // lane p publishes to rank p
+    XSlot *sl = xa.peer[lane] + ia_xslot(xa.seq, xa.W, xa.rank, m);
+    const unsigned row = wn.idx == INT64_MAX ? 0xffffffffu : (unsigned)wn.idx;
+    __hip_atomic_store(reinterpret_cast<unsigned long long *>(&sl->d), (unsigned long long)__double_as_longlong(wn.d),
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    __hip_atomic_store(&sl->row_seq, (unsigned long long)row | ((unsigned long long)xa.seq << 32), __ATOMIC_RELEASE,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  if constexpr (!FIN) {
+    if (lane == 0 && jp.pstat) jp.pstat[px.qi] = stat;
+    return;
+  } else {
+    double bd = DBL_MAX;
+    int64_t bi = INT64_MAX;
+    bool late = false;
+    if (lane < xa.W) {  // lane p reads rank p's winner
+      XSlot *sl = xa.local + ia_xslot(xa.seq, xa.W, lane, m);
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      unsigned long long rs = __hip_atomic_load(&sl->row_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      while ((unsigned)(rs >> 32) != xa.seq) {
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
+          late = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+        rs = __hip_atomic_load(&sl->row_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (!late) {
+        const unsigned long long db =
+            __hip_atomic_load(reinterpret_cast<unsigned long long *>(&sl->d), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        const unsigned row = (unsigned)rs;
+        if (row < (unsigned)ma.NA) {  // 0xffffffff: the shard holds no row within the bound
+          bd = __longlong_as_double((long long)db);
+          bi = (int64_t)row;
+        }
+      }
+    }
+    if (__ballot(late) != 0ull && lane == 0) atomicOr(xa.err, 1u);
+    wave_min_di(bd, bi);  // lexicographic (d, row) minimum: the same on every rank
+    if (bi == INT64_MAX) {  // no shard reported a row (only after a timeout): keep every index in range
+      bi = 0;
+      if (lane == 0) atomicOr(xa.err, 2u);
+    }
+    finish_pixel<CH>(g, A, ma.db64, px.r, px.c, bi, q, jp.s, jp.im, jp.Bp, jp.weights, jp.kf, jp.pstat, stat);
+  }
+}
+
 // per-level statistics: sum the per-pixel stats words.  Grid-stride loop over up to 256
 // workgroups; each workgroup reduces in LDS and adds its five integer sums with one u64
 // atomicAdd per counter (integer sums are order-free; counters are zeroed per level)
@@ -1988,6 +2189,20 @@ struct K3Table {
 };
 int ia_k3_qtmax(int KH) { return KH == 28 ? 11 : KH == 56 ? 5 : 3; }
 
+// Allow a kernel the architecture's whole LDS as dynamic shared memory (gfx950: 160 KiB per CU;
+// the default cap is 64 KiB), once per kernel.  Several host threads launch through one libia
+// (one context each: DeviceSweep, bench --streams), so the set is guarded; the attribute is the
+// arch maximum rather than the launch's size, so no thread can lower it under another's launch.
+static void allow_full_lds(const void *fn) {
+  static std::mutex mu;
+  static std::unordered_set<const void *> done;
+  std::lock_guard<std::mutex> lk(mu);
+  if (!done.insert(fn).second) return;
+  hipFuncAttributes fa;  // dynamic + static shared memory must fit the CU's 160 KiB
+  const int stat = hipFuncGetAttributes(&fa, fn) == hipSuccess ? (int)fa.sharedSizeBytes : 1024;
+  (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024 - stat);
+}
+
 void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tiles, int tpw, int qt0, int M, int nwg,
                   int row0, int NT, float4 *rec, float *recT, hipStream_t st) {
   k3_fn fn;
@@ -1995,12 +2210,7 @@ void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tile
   else if (KH == 56) fn = K3Table<56, 1, 2, 3, 4, 5>::get(qt);
   else fn = K3Table<84, 1, 2, 3>::get(qt);
   const size_t lds = (size_t)qt * (KH / 4) * IA_WAVE * sizeof(float4);
-  static bool attr_set[3][16] = {};
-  const int ki = KH == 28 ? 0 : KH == 56 ? 1 : 2;
-  if (!attr_set[ki][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set[ki][qt] = true;
-  }
+  allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(IA_WG), lds, st, db, qf, n_tiles, tpw, qt0, M, nwg, row0, NT, rec, recT);
 }
 
@@ -2066,9 +2276,29 @@ void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, cons
 }
 
 template <int CH>
+static void launch_xchg_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const XchgArgs &xa,
+                          const JobSet &jobs, bool fin, hipStream_t st) {
+  const dim3 grid(cdiv(sd.J * sd.M, IA_PQ_WPB));
+  if (fin)
+    hipLaunchKernelGGL((k_merge_xchg<CH, true, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
+  else
+    hipLaunchKernelGGL((k_merge_xchg<CH, false, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
+}
+void ia_launch_merge_xchg(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const XchgArgs &xa,
+                          const JobSet &jobs, bool fin, hipStream_t st) {
+  if (g.ch == 1) launch_xchg_t<1>(g, sd, A, ma, xa, jobs, fin, st);
+  else if (g.ch == 2) launch_xchg_t<2>(g, sd, A, ma, xa, jobs, fin, st);
+  else launch_xchg_t<3>(g, sd, A, ma, xa, jobs, fin, st);
+}
+
+template <int CH>
 static void launch_db64_t(const LevelGeo &g, const Imgs &A, double *db64, hipStream_t st) {
+#if IA_K1_GATHER
   const int64_t n = g.NA * (Geo<CH>::DS / 8);
   hipLaunchKernelGGL(k_db64_build<CH>, dim3(cdiv(n, IA_WG)), dim3(IA_WG), 0, st, g, A, db64);
+#else
+  hipLaunchKernelGGL(k_db64_build<CH>, dim3(cdiv(g.NA, IA_WAVE)), dim3(IA_WAVE), 0, st, g, A, db64);
+#endif
 }
 void ia_launch_db64_build(const LevelGeo &g, const Imgs &A, double *db64, hipStream_t st) {
   if (g.ch == 1) launch_db64_t<1>(g, A, db64, st);
@@ -2151,13 +2381,23 @@ void ia_launch_absmax(const double *const *p, const int64_t *n, unsigned *out, h
 }
 
 template <int CH, int KS>
-static void launch_db_h_t(const LevelGeo &g, const Imgs &A, const double *mu, void *db, unsigned *Rbits, hipStream_t st) {
+static void launch_db_h_t(const LevelGeo &g, const Imgs &A, const double *db64, const double *mu, void *db, unsigned *Rbits,
+                          hipStream_t st) {
+#if IA_K1_GATHER
+  (void)db64;
   const int64_t rows = (int64_t)(g.tile1 - g.tile0) * IA_TILE;
   hipLaunchKernelGGL((k_db_build_h<CH, KS>), dim3(cdiv(rows, IA_WG)), dim3(IA_WG), 0, st, g, A, mu, (h16x8 *)db, Rbits);
+#else
+  (void)A;
+  const int64_t tiles = (int64_t)g.tile1 - g.tile0;  // one wave per tile, <= 4 tiles per wave
+  const int64_t nwg = std::max<int64_t>(1, std::min<int64_t>(cdiv(tiles, IA_WG / IA_WAVE), 2048));
+  hipLaunchKernelGGL((k_db_build_h<CH, KS>), dim3((unsigned)nwg), dim3(IA_WG), 0, st, g, db64, mu, (h16x8 *)db, Rbits);
+#endif
 }
-void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *mu, void *db, unsigned *Rbits, hipStream_t st) {
-  if (g.ch == 1) launch_db_h_t<1, 4>(g, A, mu, db, Rbits, st);
-  else launch_db_h_t<2, 7>(g, A, mu, db, Rbits, st);
+void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *db64, const double *mu, void *db, unsigned *Rbits,
+                          hipStream_t st) {
+  if (g.ch == 1) launch_db_h_t<1, 4>(g, A, db64, mu, db, Rbits, st);
+  else launch_db_h_t<2, 7>(g, A, db64, mu, db, Rbits, st);
 }
 
 template <int CH, int KS>
@@ -2235,12 +2475,7 @@ void ia_launch_k3h(int KS, int qt, const void *db, const void *qf, int n_tiles, 
   const k3h_fn fn = k3h_get(KS, qt, variant);
   const int nw = k3h_waves(KS, qt, variant);
   const size_t lds = k3h_lds(KS, qt, nw);
-  static bool attr_set[4][2][16] = {};
-  const int ki = KS == 4 ? 0 : 1, vi = variant & 3;
-  if (!attr_set[vi][ki][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_set[vi][ki][qt] = true;
-  }
+  allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(nw * IA_WAVE), lds, st, (const h16x8 *)db, (const h16x8 *)qf, n_tiles, tpw, qt0, M, nwg,
                      row0, NT, rec, recT);
 }
@@ -2265,8 +2500,13 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   const int rev = (variant == 7 || variant == 8 || variant == 10 || variant >= 11) ? (step & 1) : 0;  // alternate steps walk in reverse
   if (variant == 7) variant = 6;  // 8: + the previous step's query order (no sort)
   if (variant == 10) variant = 9;  // 9: 6 + pipelined single chains; 10: 9 + reverse walks
-  if ((variant < 11 || variant == 13 || variant == 14) && variant >= 3 && (Mpad > 512 || kmax > 512))
-    variant = variant == 14 && Mpad > 512 ? 15 : 1;  // in-kernel sort: <= 512 (14 -> 15: the host ran K2s)
+  // the in-kernel sort (3..10, 13, 14) holds <= 512 queries (14 -> 15: the host ran K2s); the
+  // one-tile-per-thread lists of 3, 4 (!INTER) and 16, 17 (HF) <= 512 tiles per workgroup.  The
+  // INTER variants (5..15) walk any number of tiles (the host keeps kmax <= IA_K3P_MAXK_LDS).
+  const bool in_kernel_sort = (variant < 11 || variant == 13 || variant == 14) && variant >= 3;
+  const bool tile_lists = variant == 3 || variant == 4 || variant == 16 || variant == 17;
+  if (in_kernel_sort && Mpad > 512) variant = variant == 14 ? 15 : 1;
+  else if (tile_lists && kmax > 512) variant = 1;
   if (variant == 16 && Mpad > 512) variant = 17;   // rotated DB (the host keeps kmax <= 512 there)
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t NQ = (size_t)qt * IA_TILE;
@@ -2280,12 +2520,7 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   if (variant == 16 || variant == 17) lds += (size_t)kmax * 4;  // HF: pass masks + passing-tile list
   const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
   lds = lds > red ? lds : red;
-  static int attr_lds[18][16] = {};
-  const int vi = variant < 0 || variant > 17 ? 1 : variant;
-  if ((int)lds > attr_lds[vi][qt]) {  // allow > 64 KiB of dynamic LDS (gfx950 has 160 KiB per CU)
-    (void)hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    attr_lds[vi][qt] = (int)lds;
-  }
+  allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row, NT,
                      qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm);
 }

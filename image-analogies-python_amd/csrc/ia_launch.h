@@ -33,7 +33,8 @@ double ia_k3h_tile_bytes(int KS);  // HBM bytes of one split-f16 DB tile (TileFm
 int ia_k3h_qtmax(int KS);
 size_t ia_k3h_lds(int KS, int qt);
 void ia_launch_absmax(const double *const *p, const int64_t *n, unsigned *out, hipStream_t st);
-void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *mu, void *db, unsigned *Rbits, hipStream_t st);
+void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *db64, const double *mu, void *db, unsigned *Rbits,
+                          hipStream_t st);
 void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, hipStream_t st);
 void ia_launch_k3h(int KS, int qt, const void *db, const void *qf, int n_tiles, int tpw, int qt0, int M, int nwg, int row0,
@@ -70,3 +71,7 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
 void ia_launch_pyramid_reduce(const double *in, double *out, double *tmp, double *sm, double *mm, int h, int w, int ch,
                               const double *w7, hipStream_t st);
 void ia_launch_color3(const double *in, double *out, int64_t npx, const double *M, hipStream_t st);
+// sharded level, peer-write winner exchange (option "exchange" = 1): shard winner -> every rank's
+// buffer; fin: wait for the W winners of each query and finish the pixel (one job per call)
+void ia_launch_merge_xchg(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const XchgArgs &xa,
+                          const JobSet &jobs, bool fin, hipStream_t st);

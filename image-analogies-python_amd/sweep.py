@@ -17,6 +17,8 @@ run together:
 The kappa factor of a job's level l is 1 + 2^(l - L_j) k_j with L_j its own pyramid depth
 (image_analogies.py:206).
 """
+import warnings
+
 import numpy as np
 
 from . import _native
@@ -44,14 +46,25 @@ class Sweep(object):
     """Host side of a sweep: the full pyramids of A, A'_i, B and each job's B' pyramid.
     full_levels(j) maps job j's level l to the full pyramid's index f = l + (Lf - L_j)."""
 
-    def __init__(self, A, Ap_list, B, jobs, weights=None, min_size=None):
+    def __init__(self, A, Ap_list, B, jobs, weights=None, min_size=None, level_align='coarse'):
+        """level_align (config.level_align): how pyramids of unequal depth pair up.  'coarse' is
+        the reference's rule (image_analogies.py:82-86): the coarsest levels pair and the deeper
+        pyramid's extra fine levels are dropped, with the reference's warning; 'fine' pairs the
+        finest levels (B level k + d <-> A level k, cfg4's pairing)."""
         min_size = _config.n_sm if min_size is None else min_size
+        if level_align not in ('coarse', 'fine'):
+            raise ValueError("level_align must be 'coarse' or 'fine'")
         self.A_pyr = compute_gaussian_pyramid(A, min_size)
         self.Ap_pyr_list = [compute_gaussian_pyramid(Ap, min_size) for Ap in Ap_list]
         self.B_pyr = compute_gaussian_pyramid(B, min_size)
         Lf = min(len(self.A_pyr), len(self.B_pyr))
-        self.A_pyr, self.B_pyr = self.A_pyr[-Lf:], self.B_pyr[-Lf:]
-        self.Ap_pyr_list = [p[-Lf:] for p in self.Ap_pyr_list]
+        if len(self.A_pyr) != len(self.B_pyr):
+            warnings.warn('Warning: input images are very different sizes! The minimum number of levels will be used.')
+        sl = slice(None, Lf) if level_align == 'coarse' else slice(-Lf, None)
+        self.A_pyr, self.B_pyr = self.A_pyr[sl], self.B_pyr[sl]
+        self.Ap_pyr_list = [p[sl] for p in self.Ap_pyr_list]
+        for a, b in zip(self.A_pyr, self.B_pyr):   # paired levels: same depth below the coarsest
+            assert a.ndim == b.ndim, 'A and B differ in channels'
         self.Lf = Lf
         ch = 1 if A.ndim == 2 else A.shape[2]
         self.weights = (_config.compute_weights(_config.n_sm, _config.n_lg, _config.n_half, ch)

@@ -78,6 +78,18 @@ typedef struct {
                                 * head (15-axis partial distance) passed; else 0 */
   double dist_tiles_rows;   /* k3p_variant 16/17: DB tiles whose full rows were loaded after the
                              * head filter (dist_tiles counts the heads); else 0 */
+  /* feature-gather kernels (bench.py roofline.gathers; DESIGN.md §4 algorithmic bytes) */
+  double k1b_ms;            /* K1b k_db64_build (fp64 row DB), device ms summed over levels */
+  double k1b_bytes;         /* its algorithmic bytes: A-side images read once + N_A rows written */
+  double k1_ms;             /* K1 k_db_build_h (split-f16 tiles), device ms summed over levels */
+  double k1_bytes;          /* its algorithmic bytes: fp64 rows read + tiles written */
+  int64_t build_levels;     /* levels whose K1 / K1b were timed (every level) */
+  double gather_ms_timed;   /* K2 (k_gather_query_*) of the sampled steps ("time_dist"): device ms */
+  int64_t gather_launches_timed;
+  double gather_bytes_timed; /* their algorithmic bytes: 55 features + 12 coherence rows read,
+                              * fp64 row + fragments + pruning record written per query */
+  double merge_ms_timed;    /* K4 (k_merge_level) of the sampled steps: device ms */
+  int64_t merge_launches_timed;
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
@@ -152,6 +164,17 @@ int ia_set_option(ia_ctx *ctx, const char *name, int value);
  * ia_comm_init on every rank. */
 int ia_comm_unique_id(unsigned char id_out[128]);
 int ia_comm_init(ia_ctx *ctx, int rank, int world, const unsigned char id[128]);
+/* One-shot peer-write winner exchange for sharded levels (replaces the RCCL
+ * all-gather + finish of ia_comm_init with one fused merge per step).  Every rank calls
+ * ia_xchg_alloc (an uncached device buffer of 2 x world x 4096 16-byte slots, zeroed) and
+ * publishes the returned 64-byte HIP IPC handle; after gathering all world handles (rank order,
+ * world x 64 bytes) it calls ia_xchg_open, which maps the peers' buffers and makes the context a
+ * rank of a world-rank DB shard (option "exchange" = 1).  No RCCL communicator is needed.  A
+ * peer that stops publishing makes the level fail with IA_ECOMM after 20 s instead of hanging.
+ * With option "shard_emulate" = W and "exchange" = 1 a single process runs the same kernels
+ * over a local buffer. */
+int ia_xchg_alloc(ia_ctx *ctx, int world, unsigned char handle_out[64]);
+int ia_xchg_open(ia_ctx *ctx, int rank, int world, const unsigned char *handles);
 
 /* ---- fast path: one level ----------------------------------------------------------------- */
 int ia_synthesize_level(ia_ctx *ctx, const ia_level_args *args, ia_stats *stats);
@@ -192,12 +215,15 @@ int ia_coherence_batch(ia_index *index, const double *q, int64_t nq, const int32
  * gaussian_filter (sigma 2/3, mode 'reflect', 7 taps: weights7 = scipy's kernel, symmetric;
  * axes 0 and 1, a colour axis unsmoothed) + order-1 resize to ceil(h/2) x ceil(w/2) clipped to
  * the smoothed image's range.  img (h, w, ch) fp64; out = the n_reduce reduced levels, finest
- * first, concatenated.  Bit-identical to ia_amd.img_preprocess.compute_gaussian_pyramid. */
+ * first, concatenated.  Bit-identical to ia_amd.img_preprocess.compute_gaussian_pyramid.
+ * mem selects host or device memory for img and out; weights7 is ALWAYS a host array (its
+ * four distinct taps travel in the kernel arguments). */
 int ia_gaussian_pyramid(ia_ctx *ctx, const double *img, int h, int w, int ch, int n_reduce,
                         const double *weights7, double *out, int mem);
 /* out[p, i] = sum_j M9[3 i + j] in[p, j] for npx pixels of 3 channels, in numpy's
  * einsum('ij,klj->kli') order (m0 x0 + m2 x2) + m1 x1 (convert_to_YIQ / convert_to_RGB,
- * img_preprocess.py:6-22). */
+ * img_preprocess.py:6-22).  mem selects host or device memory for in and out; M9 is ALWAYS a
+ * host array (copied to the device per call). */
 int ia_color_matrix(ia_ctx *ctx, const double *in, int64_t npx, const double *M9, double *out,
                     int mem);
 

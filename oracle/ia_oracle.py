@@ -180,23 +180,27 @@ def compute_distance_blas(a, q, weights):
 
 # ----------------------------------------------------------------------------- the level loop
 def synthesize_level(A_pyr, Ap_pyr_list, B_feat_l, Bp_pyr, level, L, k, weights,
-                     As=None, faithful_pad=False, max_pixels=None, log=None):
+                     As=None, faithful_pad=False, max_pixels=None, log=None, start_pixel=0, s_state=None,
+                     im_state=None):
     """One level of image_analogies_main's raster loop (image_analogies.py:130-239).
 
     Bp_pyr[level] is updated in place (as the reference does).  Returns s (N,2), im (N,).
     faithful_pad: re-pad the B' pair on every pixel like image_analogies.py:166 (CPU-baseline
     cost model); the decisions are identical either way.
-    max_pixels: stop after that many raster pixels (bounded CPU-baseline sample)."""
+    max_pixels: stop after that many raster pixels (bounded CPU-baseline sample).
+    start_pixel, s_state, im_state: resume at raster pixel start_pixel of a level whose earlier
+    pixels are already synthesised (Bp_pyr[level] and s_state / im_state hold them, e.g. a GPU
+    run's final state; bench.py's mid-level CPU-baseline sample)."""
     if As is None:
         As = build_db(A_pyr, Ap_pyr_list, level)
     h, w = Bp_pyr[level].shape[:2]
     A_h, A_w = Ap_pyr_list[0][level].shape[:2]
-    n = h * w if max_pixels is None else min(h * w, max_pixels)
-    s = np.zeros((h * w, 2), dtype=np.int64)
-    im = np.zeros(h * w, dtype=np.int64)
+    n = h * w if max_pixels is None else min(h * w, start_pixel + max_pixels)
+    s = np.zeros((h * w, 2), dtype=np.int64) if s_state is None else np.array(s_state, dtype=np.int64)
+    im = np.zeros(h * w, dtype=np.int64) if im_state is None else np.array(im_state, dtype=np.int64)
     kf = 1 + (2 ** (level - L)) * k
     ch = nch(Bp_pyr[level])
-    for qi in range(n):
+    for qi in range(start_pixel, n):
         r, c = divmod(qi, w)
         if faithful_pad:
             p1 = ((1, 1), (1, 1)) + (((0, 0),) if ch > 1 else ())
@@ -281,13 +285,20 @@ def decide_pixel(As, B_feat_l, Bp_sm, Bp_final, Bp_init, s, im, A_h, A_w, level,
 
 
 # ----------------------------------------------------------------------------- CPU baseline
-def time_sample(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, level, L, k, weights, n_pixels):
-    """Time the reference loop (faithful per-pixel pad, exact fp64 NN) on the first n_pixels
-    raster pixels of `level`; returns seconds per pixel (SURVEY §8(d) CPU-baseline plan)."""
-    B_feat = feature_array(B_pyr, level, True)
-    As = build_db(A_pyr, Ap_pyr_list, level)
+def time_sample(A_pyr, Ap_pyr_list, B_pyr, Bp_pyr, level, L, k, weights, n_pixels, start=0, state=None,
+                As=None, B_feat=None):
+    """Time the reference loop (faithful per-pixel pad, exact fp64 NN) on n_pixels consecutive
+    raster pixels of `level` from raster pixel `start`; returns seconds per pixel (SURVEY §8(d)
+    CPU-baseline plan).  state = (Bp level, s, im) of an already synthesised level (a mid-level
+    sample resumes on it); As / B_feat may be passed in (shared by several sampling threads)."""
+    B_feat = feature_array(B_pyr, level, True) if B_feat is None else B_feat
+    As = build_db(A_pyr, Ap_pyr_list, level) if As is None else As
     Bp = [x.copy() for x in Bp_pyr]
+    s0 = im0 = None
+    if state is not None:
+        Bp[level] = np.array(state[0], dtype=np.float64).reshape(Bp[level].shape)
+        s0, im0 = state[1], state[2]
     t0 = time.perf_counter()
     synthesize_level(A_pyr, Ap_pyr_list, B_feat, Bp, level, L, k, weights, As=As,
-                     faithful_pad=True, max_pixels=n_pixels)
+                     faithful_pad=True, max_pixels=n_pixels, start_pixel=start, s_state=s0, im_state=im0)
     return (time.perf_counter() - t0) / n_pixels

@@ -9,7 +9,7 @@ timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -1 gpurun_out/pytest_gpu.log
 timeout -k 10 200 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { echo "smoke failed"; tail -20 gpurun_out/smoke.log; exit 1; }
 timeout -k 10 200 bash tools/pmc_k3p.sh gpurun_out/pmc_k3p || exit 1
-python3 tools/k3p_traffic.py gpurun_out/pmc_k3p profiles/k3p_traffic.json > gpurun_out/k3p_traffic.txt 2>&1 || { echo "traffic failed"; tail gpurun_out/k3p_traffic.txt; exit 1; }
+python3 tools/k3p_traffic.py gpurun_out/pmc_k3p profiles/k3p_traffic_cfg3.json cfg3 4093 > gpurun_out/k3p_traffic.txt 2>&1 || { echo "traffic failed"; tail gpurun_out/k3p_traffic.txt; exit 1; }
 timeout -k 10 300 python -u bench.py --steps 3 --warmup 1 --cpu-seconds 15 > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed"; tail -20 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 -u bench.py --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1 || { echo "rocprof failed"; exit 1; }

@@ -156,3 +156,87 @@ def test_device_sweep_two_streams_equals_one(ctx):
             assert np.array_equal(ds.S[j][level].cpu().numpy(), one[j][1][level])
             assert np.array_equal(ds.IM[j][level].cpu().numpy(), one[j][2][level])
     assert st2.pixels == st1.pixels and st2.coherence_wins == st1.coherence_wins and st2.bound_violations == 0
+
+
+@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_v11'])
+def test_batched_g256_wide_steps_match_reference(ctx, mode):
+    """8 jobs on the golden g256 run's A side: job 0 is the reference's own
+    run, jobs 1..7 other kappas and B' seeds.  On the 256^2 level a step holds 8 x 86 = 688
+    queries = 22 query tiles, above one launch's 11 (ia_k3h_qtmax) and the in-kernel sort's 512:
+      unpruned: the split-f16 scan in two query blocks per step (nqb = 2);
+      pruned: prune_min_rows = 1, the presorted wide-step path K2s + v15 in two launches;
+      pruned_v11: the same without the hi x hi block filter.
+    Job 0 must reproduce the reference's s, im and B' on every level; every job must equal its
+    own separate run (86-query steps: a single launch, the in-kernel sort)."""
+    z = load_e2e('g256')
+    if mode != 'unpruned':
+        ctx.set_option('prune_min_rows', 1)
+    if mode == 'pruned_v11':
+        ctx.set_option('k3p_variant', 11)
+    try:
+        jb = _jobs_g32(z, kappas=(0.5, 5.0, 25.0, 1.0, 2.0, 10.0, 15.0, 20.0))
+        js = [(k, [x.copy() for x in Bp]) for k, Bp in jb]
+        Sb, IMb, stb = _run(ctx, z, jb, True)
+        Ss, IMs, sts = _run(ctx, z, js, False)
+    finally:
+        ctx.set_option('prune_min_rows', 524288)
+        ctx.set_option('k3p_variant', 14)
+    h, w = z['B_pyr'][-1].shape
+    assert 8 * min(h, (w + 2) // 3) > 512
+    for level in range(1, z['L']):   # job 0 is the reference's own run
+        assert np.array_equal(Sb[0][level], z['s'][level]) and np.array_equal(IMb[0][level], z['im'][level])
+        assert np.array_equal(jb[0][1][level], z['Bp_final'][level])
+    for j in range(len(jb)):
+        for level in range(1, z['L']):
+            assert np.array_equal(Sb[j][level], Ss[j][level]) and np.array_equal(IMb[j][level], IMs[j][level])
+            assert np.array_equal(jb[j][1][level], js[j][1][level])
+    assert stb.pixels == sts.pixels and stb.coherence_wins == sts.coherence_wins
+    assert stb.bound_violations == 0 and stb.kappa_ambiguous == 0
+    if mode != 'unpruned':
+        assert stb.pruned_levels == 8 * (z['L'] - 1)
+    # the batched run needs more scan launches than steps on the 256^2 level (two query blocks)
+    assert stb.dist_launches > stb.steps
+
+
+def test_cfg5_sweep_full_size(ctx):
+    """BASELINE config 5 at its own size (multi_script.py:19-32): the 64-job
+    kappa x depth sweep (sweep.cfg5_jobs) on 512^2 images, device-resident, batched 16 jobs per
+    level call over three contexts (HIP streams + host threads, bench.py --streams 3).  Every job
+    must equal the one-job-at-a-time run (the reference's order); the deepest kappa-25 job is
+    teacher-forced on >= 50 pixels of every level against the oracle."""
+    from ia_amd import _native, sweep, synth
+    from test_gpu_scale import _invariants, _teacher_force
+    n = synth.CONFIGS['cfg5'][0]['size']
+    A = synth.smooth(n, n, 2, 1)
+    sw = sweep.Sweep(A, [synth.filt(A)], synth.smooth(n, n, 2, 2), sweep.cfg5_jobs())
+    assert len(sw.jobs) == 64 and sw.B_pyr[-1].shape == (512, 512)
+    dev = torch.device('cuda', 0)
+    ds = sweep.DeviceSweep(sw, range(len(sw.jobs)), torch, dev)
+    ctxs = [ctx, _native.Context(0), _native.Context(0)]
+    stb = _native.Stats()
+    ds.run(ctxs, stb, batched=True, max_batch=16)
+    torch.cuda.synchronize()
+    assert stb.pixels == sw.pixels() and stb.bound_violations == 0 and stb.kappa_ambiguous == 0
+    sts = _native.Stats()
+    seq = sw.run(ctx, batched=False, stats=sts)
+    assert sts.pixels == stb.pixels and sts.coherence_wins == stb.coherence_wins
+    for j in range(len(sw.jobs)):
+        Bps, Ss, IMs = seq[j]
+        for level in range(1, sw.L[j]):
+            assert np.array_equal(ds.S[j][level].cpu().numpy(), Ss[level]), (j, level)
+            assert np.array_equal(ds.IM[j][level].cpu().numpy(), IMs[level]), (j, level)
+            assert np.array_equal(ds.Bp[j][level].cpu().numpy(), Bps[level]), (j, level)
+    deep = max(j for j in range(len(sw.jobs)) if sw.L[j] == max(sw.L) and sw.jobs[j].k == 25)
+    off = sw.offset(deep)
+    job = synth.Job(sw.A_pyr[off:], [p[off:] for p in sw.Ap_pyr_list], sw.B_pyr[off:], sw.Bp_init[deep],
+                    sw.jobs[deep].k, sw.weights)
+    Bp, S, IM = seq[deep]
+    _invariants(job, Bp, S, IM)
+    for level in range(1, job.L):
+        n_b = int(np.prod(job.B_pyr[level].shape[:2]))
+        npx, mism = _teacher_force(job, Bp, S, IM, level, 60 if n_b > 1024 else 8 * n_b, seed=50 + level)
+        assert npx >= min(50, n_b), (level, npx)
+        assert all(near for _, near, _, _ in mism), (level, mism)
+        assert len(mism) <= max(1, npx // 100), (level, mism)
+    for c in ctxs[1:]:
+        c.close()

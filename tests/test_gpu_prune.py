@@ -116,3 +116,43 @@ def test_prune_option_rejects_bad_values(ctx):
                 ctx.set_option('k3p_variant', v)
     with pytest.raises(_native.IAError):
         ctx.set_option('prune_min_rows', 0)
+
+
+@pytest.mark.parametrize('variant', [14, 15, 7, 11])
+def test_pruned_scan_over_512_tiles_per_workgroup(ctx, variant):
+    """a DB of more than 256 x 512 tiles (> 4.19 M rows: here A 2048 x 2080,
+    133,120 tiles, 520 per workgroup) against a small B.  The pruned scan keeps every workgroup's
+    tile boxes in LDS (up to IA_K3P_MAXK_LDS tiles); every tile must be scanned, in the
+    in-kernel-sort (14, 7) and the presorted (15, 11) forms: the level must equal the unpruned
+    scan bit for bit."""
+    from ia_amd import _native, synth
+    from ia_amd import config as _c
+    ah, aw, bh, bw = 2048, 2080, 48, 48
+    A = synth.smooth(ah, aw, 2, 1)
+    Ap = synth.filt(A)
+    Ac, Apc = np.ascontiguousarray(A[::2, ::2]), np.ascontiguousarray(Ap[::2, ::2])
+    B = synth.smooth(bh, bw, 2, 2)
+    Bc = np.ascontiguousarray(B[::2, ::2])
+    rs = np.random.RandomState(7)
+    Bpc, Bp_init = rs.rand(bh // 2, bw // 2), rs.rand(bh, bw)
+    w = _c.compute_weights(_c.n_sm, _c.n_lg, _c.n_half, 1)
+    assert -(-ah * aw // 32) > 256 * 512
+    out = []
+    for prune in (0, 1):
+        Bp = Bp_init.copy()
+        st = _native.Stats()
+        ctx.set_option('prune', prune)
+        ctx.set_option('prune_min_rows', 1)
+        ctx.set_option('k3p_variant', variant)
+        try:
+            s, im = ctx.synthesize_level(A, Ac, [Ap], [Apc], B, Bc, Bpc, Bp, w, 1.25, st)
+        finally:
+            ctx.set_option('prune', 1)
+            ctx.set_option('prune_min_rows', 524288)
+            ctx.set_option('k3p_variant', 14)
+        out.append((s, im, Bp, st))
+    (s0, im0, Bp0, st0), (s1, im1, Bp1, st1) = out
+    assert st0.pruned_levels == 0 and st1.pruned_levels == 1
+    assert st1.bound_violations == 0 and st0.bound_violations == 0
+    assert np.array_equal(s0, s1) and np.array_equal(im0, im1) and np.array_equal(Bp0, Bp1)
+    assert st1.dist_tiles < st1.dist_tiles_full

@@ -45,3 +45,24 @@ def test_cfg5_jobs():
     jobs = sweep.cfg5_jobs()
     assert len(jobs) == 64 and {j.n_levels for j in jobs} == set(range(2, 10))
     assert {j.k for j in jobs} == {0.5, 1, 2, 5, 10, 15, 20, 25}
+
+
+def test_unequal_pyramids_pair_coarse_levels_like_the_reference():
+    """image_analogies.py:82-86: max_levels = min(len(A_pyr), len(B_pyr)) and the loop walks levels
+    0..max_levels-1 of both coarsest-first lists, i.e. the coarsest levels pair and the deeper
+    pyramid's extra fine levels are dropped (with a warning).  'fine' pairs the finest levels."""
+    import warnings
+    A = synth.smooth(40, 40, 2, 1)
+    B = synth.smooth(80, 80, 2, 2)
+    Af, Bf = compute_gaussian_pyramid(A, 3), compute_gaussian_pyramid(B, 3)
+    assert len(Bf) == len(Af) + 1
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        sw = sweep.Sweep(A, [synth.filt(A)], B, [sweep.SweepJob(0.5)])
+    assert any('different sizes' in str(x.message) for x in w)
+    assert sw.Lf == len(Af)
+    assert all(np.array_equal(a, b) for a, b in zip(sw.B_pyr, Bf[:len(Af)]))
+    assert all(np.array_equal(a, b) for a, b in zip(sw.A_pyr, Af))
+    fine = sweep.Sweep(A, [synth.filt(A)], B, [sweep.SweepJob(0.5)], level_align='fine')
+    assert all(np.array_equal(a, b) for a, b in zip(fine.B_pyr, Bf[1:]))
+    assert fine.B_pyr[-1].shape == (80, 80) and sw.B_pyr[-1].shape == (40, 40)

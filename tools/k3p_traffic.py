@@ -1,16 +1,19 @@
 """HBM bytes per launch of the pruned scan (k3h_prune3) from tools/pmc_k3p.sh output, with the
 gfx950 correction of MI355X_MICROARCH.md (FETCH_SIZE reports half the bytes of wide coalesced
-streaming reads: x2; WRITE_SIZE is exact).  Averaged over the 1024^2 plateau: the middle half
-of the finest level's dispatches (the last 4093 of the step).  Writes profiles/k3p_traffic.json
-and prints the SQ counters of the same dispatches.
-  python3 tools/k3p_traffic.py <pmc_dir> [out.json]"""
+streaming reads: x2; WRITE_SIZE is exact).  hbm_bytes_per_launch = the mean over every pruned
+dispatch of the bench step (the mix bench.py samples); plateau_* = the middle half of the
+finest level's dispatches (the last <finest_dispatches> of the step).  Writes
+profiles/k3p_traffic_<config>.json and prints the SQ counters of the plateau dispatches.
+  python3 tools/k3p_traffic.py <pmc_dir> [out.json] [config] [finest_dispatches]
+(cfg3: 4093 = the 1024^2 level's steps; cfg4: 16378 = 8189 steps of 2 launches each)"""
 import csv
 import glob
 import json
 import os
 import sys
 
-LEVEL9_STEPS = 4093  # wavefront steps of a 1024^2 level (w + 3(h - 1))
+CONFIG = sys.argv[3] if len(sys.argv) > 3 else 'cfg3'
+LEVEL9_STEPS = int(sys.argv[4]) if len(sys.argv) > 4 else 4093  # finest level's pruned dispatches
 
 
 def per_dispatch(d, counter):
@@ -30,7 +33,7 @@ def plateau(v):
 
 d = sys.argv[1]
 out = sys.argv[2] if len(sys.argv) > 2 else os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
-                                                         'profiles', 'k3p_traffic.json')
+                                                         'profiles', 'k3p_traffic_%s.json' % CONFIG)
 fa, wa = per_dispatch(os.path.join(d, 'fetch'), 'FETCH_SIZE'), per_dispatch(os.path.join(d, 'write'), 'WRITE_SIZE')
 fp, wp = plateau(fa), plateau(wa)
 rd = 2.0 * 1024 * sum(fa) / len(fa)  # every dispatch of the step: the same mix bench.py samples
@@ -42,8 +45,8 @@ res = {'hbm_bytes_per_launch': rd + wr, 'read_bytes_per_launch': rd, 'write_byte
        'plateau_write_bytes_per_launch': wrp, 'plateau_launches': len(fp), 'kernel': 'k3h_prune3',
        'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes; KB units), FETCH_SIZE x2 per '
                  'MI355X_MICROARCH.md gfx950 note (Infinity-Cache hits are counted); mean over every k3h_prune3 '
-                 'dispatch of one cfg3 step (levels 512^2 and 1024^2, as bench.py samples them); plateau_* = the '
-                 'middle half of the 1024^2 level (M = 342)'}
+                 'dispatch of one %s bench step (as bench.py samples them); plateau_* = the middle half of the '
+                 'finest level\'s dispatches' % CONFIG, 'config': CONFIG}
 sq = {}
 for c in ('SQ_WAVE_CYCLES', 'SQ_BUSY_CYCLES', 'SQ_INSTS_VALU', 'SQ_INSTS_MFMA', 'SQ_INSTS_LDS',
           'SQ_VALU_MFMA_BUSY_CYCLES', 'SQ_LDS_BANK_CONFLICT', 'GRBM_GUI_ACTIVE'):
