@@ -10,17 +10,22 @@ the start of each step).  `value` = B' pixels of all ranks / wall time of K time
   python bench.py [--gpus N --steps K --warmup W]           # N=1 default
   torchrun --nproc-per-node N bench.py --gpus N ...         # one process per GPU
 
-Multi-GPU: --mode replicas (default) runs one independent job per GPU (multi_script-style,
-no collective, "scaling": "weak"); --mode shard splits each level's A database across the
-ranks with one RCCL all-gather of certified winners per wavefront step ("strong").
+Multi-GPU (N > 1): --mode shard (the default for cfg2/cfg3/cfg4: BASELINE config 3 as named)
+splits each large level's A database across the ranks, one job, one winner exchange per
+wavefront step ("strong"; --exchange peer = one-shot xGMI peer writes fused into the merge,
+rccl = ncclAllGather + finish); the replicas aggregate (one independent job per GPU, no
+collective) rides along as value_replicas.  --mode replicas makes that the value ("weak").
+cfg5 splits its 64-job sweep job j -> rank j mod N (no collective).
 
 Besides the contract fields the JSON line carries:
-  roofline     the MFMA distance kernel (k3_dist): algorithmic flops sum 2*D*N_A*M over
-               launches / its device time, sampled live with HIP events (every --time-stride-th
-               wavefront step), against the fp32 MFMA dense peak (MI355X_MICROARCH.md).
+  roofline     the dominant kernel (the certified pruned scan k3h_prune3: HBM roofline, algorithmic
+               bytes / device time sampled live with HIP events every --time-stride-th wavefront
+               step; traffic = PMC bytes per launch of the same config from profiles/), plus
+               roofline.gathers: K1 / K1b DB builds and the K2 query gather against HBM peak.
   cpu_baseline the oracle's restatement of the reference loop (per-pixel pad + exact fp64 NN,
-               1 thread) timed on bounded samples of the same job on this host, extrapolated to
-               the whole job (rank 0 at N=1 only).
+               1 thread per pixel) timed on S = 256 consecutive mid-level pixels of the three
+               finest levels in spawned workers before the GPU is touched, extrapolated to the
+               whole job (rank 0 at N=1 only).
 """
 import argparse
 import json
@@ -180,6 +185,7 @@ def make_context(args, local):
         cx.set_option('row_source', args.row_source)
     if args.shard_emulate > 1:
         cx.set_option('shard_emulate', args.shard_emulate)
+        cx.set_option('exchange', 1 if args.exchange == 'peer' else 0)   # the emulated shards' exchange kernels
     return cx
 
 
@@ -229,6 +235,10 @@ def main():
                     help='N > 1: shard (default for cfg2/cfg3/cfg4: BASELINE config 3 as named, one job whose DB '
                          'is sharded over the ranks, one winner exchange per wavefront step; the replicas aggregate '
                          'rides along as value_replicas) or replicas (one independent job per GPU)')
+    ap.add_argument('--exchange', default='peer', choices=['peer', 'rccl'],
+                    help='shard mode: winner exchange per wavefront step - peer = one-shot xGMI peer writes fused '
+                         'into the merge (HIP IPC buffers, include/ia.h ia_xchg_*), rccl = ncclAllGather + a finish '
+                         'kernel')
     ap.add_argument('--no-replicas-extra', action='store_true',
                     help='N > 1 shard mode: skip the extra replicas measurement (value_replicas)')
     ap.add_argument('--cpu-procs', type=int, default=4,
@@ -239,12 +249,13 @@ def main():
                     help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select (DIAG=1 builds)')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
-    ap.add_argument('--k3p-variant', type=int, default=14, choices=list(range(18)),
+    ap.add_argument('--k3p-variant', type=int, default=14, choices=list(range(20)),
                     help='pruned-scan kernel version (ia_k3h.hip k3h_prune*): 0 = first version, 1 = boxes in '
                          'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
                          'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks, 11 = 7 on queries presorted once per step, '
                          '14 (default) / 15 = 7 / 11 with the hi x hi block filter, 16 / 17 = rotated DB with the '
-                         'principal-axis head filter (DESIGN.md §4f); product builds hold 7, 11, 14 and 15')
+                         'principal-axis head filter (DESIGN.md §4f), 18 / 19 = 14 / 15 with the correction products fused onto the '
+                         'hi x hi accumulator; product builds hold 7, 11, 14, 15, 18 and 19')
     ap.add_argument('--prune-group', type=int, default=1, choices=[1, 2, 4, 8],
                     help='pruned levels: Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)')
     ap.add_argument('--prune-min-rows', type=int, default=524288,
@@ -328,9 +339,16 @@ def main():
         log('[bench] CPU baseline sampled in %.1fs: %.3g px/s' % (time.time() - t1, cpu['value']))
     ctx = make_context(args, local)
     if args.mode == 'shard' and world > 1:
-        uid = [_native.comm_unique_id() if rank == 0 else None]
-        dist.broadcast_object_list(uid, src=0)
-        ctx.comm_init(rank, world, uid[0])
+        if args.exchange == 'rccl':
+            uid = [_native.comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(uid, src=0)
+            ctx.comm_init(rank, world, uid[0])
+        else:
+            def all_gather(b):
+                out = [None] * world
+                dist.all_gather_object(out, b)
+                return out
+            ctx.xchg_init(rank, world, all_gather)
     ctxs = [ctx]
     if sw is not None:
         from ia_amd import sweep
@@ -479,6 +497,7 @@ def main():
                                            'px_per_step': job_pixels, 'nn_flops_per_step': job_flops,
                                            'mode': 'sweep' if sw is not None else args.mode,
                                            'shard_emulate': args.shard_emulate, 'row_source': args.row_source,
+                                           'exchange': args.exchange if (args.mode == 'shard' and world > 1) else None,
                                            'parallelism': (('jobs%d' % world) if sw is not None else
                                                            ('replicas%d' if args.mode == 'replicas' else 'dbshard%d')
                                                            % world),

@@ -11,7 +11,7 @@ import threading
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get('IA_LIBIA', os.path.join(_HERE, 'libia.so'))  # override: diagnostic builds
+LIB_PATH = os.environ.get('IA_LIBIA') or os.path.join(_HERE, 'libia.so')  # override: diagnostic builds
 
 IA_MEM_HOST, IA_MEM_DEVICE = 0, 1
 IA_MATCH_F32, IA_MATCH_F16X3 = 0, 1   # option "matcher" (include/ia.h)

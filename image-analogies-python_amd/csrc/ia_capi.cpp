@@ -344,7 +344,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   }
 #ifdef IA_K3H_DIAG  // DIAG=1 builds: every kernel version of DESIGN.md §4b's progression
   if (!std::strcmp(name, "k3p_variant")) {
-    if (value < 0 || value > 17) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..17");
+    if (value < 0 || value > 19) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..19");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -357,8 +357,9 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "k3p_variant")) {  // 14 (default) / 15: hi x hi block filter (in-kernel sort up to
                                             // 512 queries, presorted 15 above); 7 / 11: v7;
                                             // 16 / 17 (rotated DB, §4f) are in DIAG=1 builds
-    if (value != 7 && value != 11 && value != 14 && value != 15)
-      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14 or 15 (other versions are in DIAG=1 builds only)");
+    if (value != 7 && value != 11 && value != 14 && value != 15 && value != 18 && value != 19)
+      return fail(IA_EINVAL,
+                  "ia_set_option: k3p_variant is 7, 11, 14, 15, 18 or 19 (other versions are in DIAG=1 builds only)");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -640,6 +641,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   const bool xchg = multi && c->exchange == 1;  // peer-write winner exchange (k_merge_xchg)
   if (xchg) {
     if (sharded && !c->xpeer[0]) return fail(IA_EINVAL, "ia_synthesize_level: exchange = 1 needs ia_xchg_open");
+    if (Wsh > IA_XCHG_MAXW) return fail(IA_EINVAL, "ia_synthesize_level: the peer-write exchange takes <= 16 shards");
     if (emulated && (rc = xchg_alloc(c, Wsh))) return rc;
     if ((int64_t)std::min(g.bh, (g.bw + 2) / 3) > IA_XCHG_MAXQ)
       return fail(IA_EINVAL, "ia_synthesize_level: wavefront steps wider than the exchange slots");
@@ -939,9 +941,9 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     // sort of v6/v7 (512) or variant 11 is selected
     // (variants 11, 12: presorted; 7, 13: in-kernel sort up to 512 queries, presorted v11 / v12 above)
     const int kv = rot ? c->k3p_variant : (c->k3p_variant == 16 ? 14 : c->k3p_variant == 17 ? 15 : c->k3p_variant);
-    const int k3v = (kv == 11 || kv == 12 || kv == 15 || kv == 17) ? kv
-                    : (prune && sd.Mpad > 512 ? (kv == 13 ? 12 : kv == 14 ? 15 : kv == 16 ? 17 : 11) : kv);
-    const bool presorted = k3v == 11 || k3v == 12 || k3v == 15 || k3v == 17;
+    const int k3v = (kv == 11 || kv == 12 || kv == 15 || kv == 17 || kv == 19) ? kv
+                    : (prune && sd.Mpad > 512 ? (kv == 13 ? 12 : kv == 14 ? 15 : kv == 18 ? 19 : kv == 16 ? 17 : 11) : kv);
+    const bool presorted = k3v == 11 || k3v == 12 || k3v == 15 || k3v == 17 || k3v == 19;
     if (prune && presorted)
       ia_launch_query_sort(c->qinfo.as<float4>(), c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
                            c->qs_frag.p, c->qs_tbox.as<float4>(), c->st);

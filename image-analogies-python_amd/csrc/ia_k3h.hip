@@ -400,6 +400,41 @@ __device__ __forceinline__ void k3p_hhpipe(const h16x8 (&a)[2 * KS], const h16x8
   }
 }
 
+// HHX (k3p_variant 18 / 19 = 14 / 15 with the corrections fused): the same hi x hi filter, but a
+// passing block keeps its hi x hi accumulator and only adds the 8 correction products (lo x hi,
+// hi x lo) before the top-2 epilogue: 12 MFMAs per passing block instead of 4 + 12.  The
+// products are v14's, summed in another order; ia_eps_c_h bounds the fp32 accumulation for any
+// order, so the records stay certified.  Pipelined like k3p_hhpipe: the hi x hi chain of block q
+// is issued before the test (and corrections, epilogue) of block q - 1.
+template <int KS, int QT, int Q>
+__device__ __forceinline__ void k3p_hhfuse(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, float rt,
+                                           const float *qzt, const float *qzw, int t, float (&b1)[QT], float (&b2)[QT],
+                                           int (&i1)[QT], f32x16 (&acc)[2], unsigned &pass) {
+  if constexpr (Q <= QT) {
+    constexpr int NP = 2 * KS;
+    if constexpr (Q < QT) {
+      if ((msk >> Q) & 1u) acc[Q & 1] = k3p_hh<KS>(a, lq + Q * NP * IA_WAVE);
+    }
+    if constexpr (Q >= 1) {
+      if ((msk >> (Q - 1)) & 1u) {
+        const float lim = fmaf(rt, qzw[(Q - 1) * IA_TILE] + fmaf(rt, 0x1p-9f, 0x1p-20f), qzt[(Q - 1) * IA_TILE]);
+        if (__ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull) {  // wave-uniform
+          pass |= 1u << (Q - 1);
+          f32x16 &c = acc[(Q - 1) & 1];
+          const h16x8 *qb = lq + (Q - 1) * NP * IA_WAVE;
+#pragma unroll
+          for (int s = 0; s < KS; s++) {
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], qb[(2 * s) * IA_WAVE], c, 0, 0, 0);
+            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], qb[(2 * s + 1) * IA_WAVE], c, 0, 0, 0);
+          }
+          k3p_epi1(c, t, b1[Q - 1], b2[Q - 1], i1[Q - 1]);
+        }
+      }
+    }
+    k3p_hhfuse<KS, QT, Q + 1>(a, lq, msk, rt, qzt, qzw, t, b1, b2, i1, acc, pass);
+  }
+}
+
 // HF (k3p_variant 16 / 17): the rotated DB (ia_internal.h).  A tile's head is
 // its k-step 0 (2 pieces, 2 KiB), its tail the other 6 (6 KiB, a separate array after the NT
 // heads).  The head chain (3 MFMAs) of a (DB tile, query tile) block yields the 15-axis partial
@@ -801,7 +836,7 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // HHF (k3p_variant 14 / 15): the hi x hi block filter above (k3p_hhpipe); the per-WG pair
 // counter slot then holds (pairs with corrections << 32) + box-needed pairs.
 template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false, bool PIPE = false,
-          bool PRE = false, bool HHF = false, bool HF = false>
+          bool PRE = false, bool HHF = false, bool HF = false, bool HHX = false>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
@@ -1276,7 +1311,13 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       // makes the MFMAs below wait for the prefetch itself
       ld_tile<KS>(nxt, db, tk(kn < K ? kn : k), lane);
       asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-      if constexpr (HHF) {
+      if constexpr (HHF && HHX) {
+        f32x16 acc[2];
+        unsigned pass = 0;
+        k3p_hhfuse<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), tk(k), b1, b2, i1, acc,
+                              pass);
+        nfull += __popc(pass);
+      } else if constexpr (HHF) {
         f32x16 acc[2];
         unsigned pass = 0;
         k3p_hhpipe<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
@@ -1499,6 +1540,11 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true>;
     if (variant == 14) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true>;
     if (variant == 15) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true>;
+    // 18 / 19: 14 / 15 with the correction products fused onto the hi x hi accumulator (HHX)
+    if (variant == 18)
+      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true, false, true>;
+    if (variant == 19)
+      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true, false, true>;
 #ifdef IA_K3H_DIAG  // rotated DB + head filter: exact, not faster
     if (variant == 16) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, false, true>;
     if (variant == 17) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, false, true>;

@@ -158,7 +158,7 @@ def test_device_sweep_two_streams_equals_one(ctx):
     assert st2.pixels == st1.pixels and st2.coherence_wins == st1.coherence_wins and st2.bound_violations == 0
 
 
-@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_v11'])
+@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_v11', 'pruned_v18'])
 def test_batched_g256_wide_steps_match_reference(ctx, mode):
     """8 jobs on the golden g256 run's A side: job 0 is the reference's own
     run, jobs 1..7 other kappas and B' seeds.  On the 256^2 level a step holds 8 x 86 = 688
@@ -171,8 +171,8 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
     z = load_e2e('g256')
     if mode != 'unpruned':
         ctx.set_option('prune_min_rows', 1)
-    if mode == 'pruned_v11':
-        ctx.set_option('k3p_variant', 11)
+    if mode in ('pruned_v11', 'pruned_v18'):
+        ctx.set_option('k3p_variant', int(mode[-2:]))
     try:
         jb = _jobs_g32(z, kappas=(0.5, 5.0, 25.0, 1.0, 2.0, 10.0, 15.0, 20.0))
         js = [(k, [x.copy() for x in Bp]) for k, Bp in jb]

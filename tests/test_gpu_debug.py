@@ -46,9 +46,10 @@ def _run_debug(ctx, z, prune_all=False, variant=14):
     return out, Bp, st
 
 
-@pytest.mark.parametrize('prune_all,variant', [(False, 14), (True, 7), (True, 14), (True, 15), (True, 11), (True, 16)],
+@pytest.mark.parametrize('prune_all,variant', [(False, 14), (True, 7), (True, 14), (True, 15), (True, 11), (True, 18),
+                                                (True, 19), (True, 16)],
                          ids=['default', 'pruned_v7', 'pruned', 'pruned_presorted_v15', 'pruned_presorted_v11',
-                              'pruned_v16'])
+                              'pruned_v18', 'pruned_presorted_v19', 'pruned_v16'])
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
 def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     """Every NN pick, coherence pick and compute_distance value of the reference run.  With
@@ -56,7 +57,8 @@ def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     dominant kernel checked directly against the reference's own per-pixel picks).  Variants 15
     and 11 force the presorted wide-step path on every step: the per-step query sort K2s
     (k_query_sort) + the presorted scan with (15) and without (11) the hi x hi block filter -
-    the kernels cfg4's 2048^2 level and every batched step wider than 512 queries run."""
+    the kernels cfg4's 2048^2 level and every batched step wider than 512 queries run.  18 / 19:
+    14 / 15 with the correction products fused onto the hi x hi accumulator."""
     if variant == 16:  # rotated DB + head filter (DESIGN.md §4f): DIAG=1 builds only
         from ia_amd import _native
         try:
@@ -70,7 +72,7 @@ def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]
     if prune_all:
         assert st.pruned_levels == (z['L'] - 1 if ch == 1 else 0)
-    if variant in (14, 15, 16) and st.pruned_levels > 0:  # the block filters run on pruned levels only
+    if variant in (14, 15, 16, 18, 19) and st.pruned_levels > 0:  # the block filters run on pruned levels only
         assert 0 < st.dist_pairs_corrected <= st.dist_pairs
     if variant == 16 and st.pruned_levels > 0:
         assert 0 < st.dist_tiles_rows <= st.dist_tiles

@@ -46,7 +46,8 @@ def _run(ctx, job, prune, variant=7, group=1):
 
 @pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 16), (1024, 2, 16), (512, 1, 17), (1024, 2, 17),
                                                       (512, 1, 7), (1024, 2, 7), (512, 1, 11), (1024, 2, 11), (512, 1, 14), (1024, 2, 14),
-                                                      (512, 1, 15), (1024, 2, 15), (512, 1, 12), (1024, 2, 12), (512, 1, 13), (1024, 2, 13),
+                                                      (512, 1, 15), (1024, 2, 15), (512, 1, 18), (1024, 2, 18), (512, 1, 19), (1024, 2, 19),
+                                                      (512, 1, 12), (1024, 2, 12), (512, 1, 13), (1024, 2, 13),
                                                       (512, 1, 10), (1024, 2, 9), (512, 1, 8),
                                                       (1024, 2, 6), (1024, 2, 5), (1024, 2, 4), (1024, 2, 3),
                                                       (1024, 2, 1), (512, 1, 0), (512, 1, 2)])
@@ -56,7 +57,7 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     builds the rest, e.g. 12 (presorted, 16 waves with one tile buffer each: 4 waves per SIMD) and
     13 (12 with the in-kernel sort), both measured slower): every one is exact"""
     from ia_amd import synth
-    if variant not in (7, 11, 14, 15) and not _diag_build(ctx):
+    if variant not in (7, 11, 14, 15, 18, 19) and not _diag_build(ctx):
         pytest.skip('kernel version %d is built with DIAG=1 only' % variant)
     job = synth.make_job(size)
     Bp0, S0, IM0, st0 = _run(ctx, job, 0)
@@ -70,7 +71,7 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     assert st1.dist_pairs < st1.dist_pairs_full
     assert st1.dist_pairs_full == st0.dist_pairs_full
     assert st1.dist_tiles <= st1.dist_tiles_full and st1.dist_tiles_full == st0.dist_tiles_full
-    if variant in (14, 15, 16, 17):  # block filters: most box-needed pairs stop after a cheap product
+    if variant in (14, 15, 16, 17, 18, 19):  # block filters: most box-needed pairs stop after a cheap product
         assert 0 < st1.dist_pairs_corrected < st1.dist_pairs
         print('filter-passing pairs %.3f of the box-needed ones' % (st1.dist_pairs_corrected / st1.dist_pairs))
     else:
@@ -109,7 +110,7 @@ def test_prune_option_rejects_bad_values(ctx):
     with pytest.raises(_native.IAError):
         ctx.set_option('prune_group', 3)
     with pytest.raises(_native.IAError):
-        ctx.set_option('k3p_variant', 18)
+        ctx.set_option('k3p_variant', 20)
     if not _diag_build(ctx):
         for v in (6, 12, 13, 16, 17):
             with pytest.raises(_native.IAError):
@@ -118,7 +119,7 @@ def test_prune_option_rejects_bad_values(ctx):
         ctx.set_option('prune_min_rows', 0)
 
 
-@pytest.mark.parametrize('variant', [14, 15, 7, 11])
+@pytest.mark.parametrize('variant', [14, 15, 7, 11, 18, 19])
 def test_pruned_scan_over_512_tiles_per_workgroup(ctx, variant):
     """a DB of more than 256 x 512 tiles (> 4.19 M rows: here A 2048 x 2080,
     133,120 tiles, 520 per workgroup) against a small B.  The pruned scan keeps every workgroup's

@@ -4,7 +4,11 @@ certified per-shard winner (k_merge_level<FUSED=false>) run in turn, then the mu
 (k_finish_level: global winner = smallest exact distance, lowest row; coherence, kappa,
 writeback) - everything the RCCL path runs except the all-gather itself.  Pruned levels keep
 pruning under sharding (shard r = Morton tiles r, r + W, ..., stored contiguously).  Results must
-be bit-identical to the reference (golden runs) and to unsharded runs (1024^2)."""
+be bit-identical to the reference (golden runs) and to unsharded runs (1024^2).
+exchange = 1: the one-shot peer-write exchange instead (k_merge_xchg: each shard's winner is
+written into the exchange slots with a release store, the last shard's launch polls the W slots
+of every query with acquire loads and finishes the pixel) - the multi-rank kernels with the
+peers' buffers aliased to this process's own."""
 import numpy as np
 import pytest
 
@@ -13,13 +17,14 @@ from golden_util import BIG_CASES, load_e2e
 pytestmark = pytest.mark.gpu
 
 
-def _run(ctx, z, W, prune_all):
+def _run(ctx, z, W, prune_all, exchange=0):
     from ia_amd import _native
     L, k = z['L'], float(z['k'])
     Bp = [x.copy() for x in z['Bp_init']]
     st = _native.Stats()
     out = {}
     ctx.set_option('shard_emulate', W)
+    ctx.set_option('exchange', exchange)
     if prune_all:
         ctx.set_option('prune_min_rows', 1)
     try:
@@ -30,31 +35,33 @@ def _run(ctx, z, W, prune_all):
                                               1 + 2.0 ** (level - L) * k, st)
     finally:
         ctx.set_option('shard_emulate', 1)
+        ctx.set_option('exchange', 0)
         ctx.set_option('prune_min_rows', 524288)
     return out, Bp, st
 
 
+@pytest.mark.parametrize('exchange', [0, 1], ids=['allgather', 'peerwrite'])
 @pytest.mark.parametrize('prune_all', [False, True], ids=['unpruned', 'pruned'])
 @pytest.mark.parametrize('W', [2, 4, 8])
 @pytest.mark.parametrize('name', ['g64', 'ties128'] + [c for c in ('g128', 'g256') if c in BIG_CASES])
-def test_emulated_shards_match_reference(ctx, name, W, prune_all):
+def test_emulated_shards_match_reference(ctx, name, W, prune_all, exchange):
     z = load_e2e(name)
-    out, Bp, st = _run(ctx, z, W, prune_all)
+    out, Bp, st = _run(ctx, z, W, prune_all, exchange)
     for level, (s, im) in out.items():
         assert np.array_equal(s, z['s'][level]) and np.array_equal(im, z['im'][level]), level
         assert np.array_equal(Bp[level], z['Bp_final'][level]), level
     assert st.bound_violations == 0 and st.kappa_ambiguous == 0
 
 
-@pytest.mark.parametrize('W', [4, 8])
-def test_emulated_shards_1024_match_unsharded(ctx, W):
+@pytest.mark.parametrize('W,exchange', [(4, 0), (8, 0), (2, 1), (8, 1)])
+def test_emulated_shards_1024_match_unsharded(ctx, W, exchange):
     """cfg3 (pruned 1024^2 level, unpruned 512^2 level): W-way sharded == unsharded, every level."""
     from ia_amd import synth
     job = synth.make_job(1024)
     z = {'L': job.L, 'k': job.k, 'A_pyr': job.A_pyr, 'Ap_pyr': job.Ap_pyr_list, 'B_pyr': job.B_pyr,
          'Bp_init': job.Bp_init, 'weights': job.weights}
     ref, Bp_ref, _ = _run(ctx, z, 1, False)
-    out, Bp, st = _run(ctx, z, W, False)
+    out, Bp, st = _run(ctx, z, W, False, exchange)
     for level in range(1, job.L):
         assert np.array_equal(out[level][0], ref[level][0]) and np.array_equal(out[level][1], ref[level][1]), level
         assert np.array_equal(Bp[level], Bp_ref[level]), level
@@ -66,3 +73,21 @@ def test_shard_emulate_option_bounds(ctx):
     for bad in (0, 65):
         with pytest.raises(_native.IAError):
             ctx.set_option('shard_emulate', bad)
+
+
+def test_exchange_option_bounds(ctx):
+    from ia_amd import _native
+    with pytest.raises(_native.IAError):
+        ctx.set_option('exchange', 2)
+    ctx.set_option('exchange', 1)
+    ctx.set_option('shard_emulate', 32)   # more shards than exchange slots: refused per level
+    try:
+        z = load_e2e('g256')   # 2048 tiles at 256^2: a 32-way emulated shard level
+        with pytest.raises(_native.IAError):
+            L = z['L']
+            ctx.synthesize_level(z['A_pyr'][L - 1], z['A_pyr'][L - 2], [p[L - 1] for p in z['Ap_pyr']],
+                                 [p[L - 2] for p in z['Ap_pyr']], z['B_pyr'][L - 1], z['B_pyr'][L - 2],
+                                 z['Bp_init'][L - 2].copy(), z['Bp_init'][L - 1].copy(), z['weights'], 1.0)
+    finally:
+        ctx.set_option('shard_emulate', 1)
+        ctx.set_option('exchange', 0)

@@ -4,8 +4,9 @@ streaming reads: x2; WRITE_SIZE is exact).  hbm_bytes_per_launch = the mean over
 dispatch of the bench step (the mix bench.py samples); plateau_* = the middle half of the
 finest level's dispatches (the last <finest_dispatches> of the step).  Writes
 profiles/k3p_traffic_<config>.json and prints the SQ counters of the plateau dispatches.
-  python3 tools/k3p_traffic.py <pmc_dir> [out.json] [config] [finest_dispatches]
-(cfg3: 4093 = the 1024^2 level's steps; cfg4: 16378 = 8189 steps of 2 launches each)"""
+  python3 tools/k3p_traffic.py <pmc_dir> [out.json] [config] [finest_dispatches] [kernel]
+(cfg3: 4093 = the 1024^2 level's steps; cfg4: 16378 = 8189 steps of 2 launches each; kernel:
+the dominant kernel's name substring, k3h_prune3 by default, k3h_scan for cfg5's unpruned scans)"""
 import csv
 import glob
 import json
@@ -14,13 +15,14 @@ import sys
 
 CONFIG = sys.argv[3] if len(sys.argv) > 3 else 'cfg3'
 LEVEL9_STEPS = int(sys.argv[4]) if len(sys.argv) > 4 else 4093  # finest level's pruned dispatches
+KERNEL = sys.argv[5] if len(sys.argv) > 5 else 'k3h_prune3'
 
 
 def per_dispatch(d, counter):
     vals = {}
     for f in glob.glob(os.path.join(d, '**', '*counter_collection.csv'), recursive=True):
         for r in csv.DictReader(open(f)):
-            if r['Counter_Name'] == counter and 'k3h_prune3' in r['Kernel_Name']:
+            if r['Counter_Name'] == counter and KERNEL in r['Kernel_Name']:
                 k = int(r['Dispatch_Id'])
                 vals[k] = vals.get(k, 0.0) + float(r['Counter_Value'])
     return [vals[k] for k in sorted(vals)]
@@ -42,10 +44,10 @@ rdp = 2.0 * 1024 * sum(fp) / len(fp)
 wrp = 1024.0 * sum(wp) / len(wp)
 res = {'hbm_bytes_per_launch': rd + wr, 'read_bytes_per_launch': rd, 'write_bytes_per_launch': wr,
        'launches': len(fa), 'plateau_hbm_bytes_per_launch': rdp + wrp, 'plateau_read_bytes_per_launch': rdp,
-       'plateau_write_bytes_per_launch': wrp, 'plateau_launches': len(fp), 'kernel': 'k3h_prune3',
+       'plateau_write_bytes_per_launch': wrp, 'plateau_launches': len(fp), 'kernel': KERNEL,
        'source': 'rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE (separate passes; KB units), FETCH_SIZE x2 per '
                  'MI355X_MICROARCH.md gfx950 note (Infinity-Cache hits are counted); mean over every k3h_prune3 '
-                 'dispatch of one %s bench step (as bench.py samples them); plateau_* = the middle half of the '
+                 'dispatch of the kernel in one %s bench step (as bench.py samples them); plateau_* = the middle half of the '
                  'finest level\'s dispatches' % CONFIG, 'config': CONFIG}
 sq = {}
 for c in ('SQ_WAVE_CYCLES', 'SQ_BUSY_CYCLES', 'SQ_INSTS_VALU', 'SQ_INSTS_MFMA', 'SQ_INSTS_LDS',

@@ -1,0 +1,86 @@
+"""DESIGN.md §7 cost model of the DB-sharded path from a rocprofv3 kernel trace of
+`bench.py --shard-emulate W` (all W shards of every large level run back to back on one GPU).
+Per wavefront step of each level the trace holds: the query gather (K2), the W shard scans
+(K3h / K3p; + the query sort K2s on wide steps) and the W exchange merges (k_merge_xchg: W - 1
+publishing launches, then the finishing one) - or, on levels too small to shard, one scan and
+one merge.  On W real ranks each rank runs K2, ITS shard's scan and one finishing merge, so a
+step costs
+    K2 + max over shards (scan) + finishing merge + x
+with x the exchange latency (an xGMI store + the peers' polling: a parameter, default 3 us).
+Printed: measured kernel time per level (this one-GPU emulation) and the modelled per-rank time
+on W GPUs, per level and for the job; speedup and efficiency against the W = 1 model.
+  python3 tools/shard_model.py <run_kernel_trace.csv> <W> [x_us] [baseline_job_ms]"""
+import csv
+import re
+import sys
+
+rows = list(csv.DictReader(open(sys.argv[1])))
+rows.sort(key=lambda r: int(r['Start_Timestamp']))
+W = int(sys.argv[2])
+XLAT = float(sys.argv[3]) if len(sys.argv) > 3 else 3.0
+base = float(sys.argv[4]) if len(sys.argv) > 4 else None
+
+
+def kind(name):
+    if 'k_part_means' in name and 'fold' not in name:
+        return 'level'
+    if 'k_gather_query' in name:
+        return 'gather'
+    if 'k3h_' in name or 'k3_dist' in name:
+        return 'scan'
+    if 'k_query_sort' in name:
+        return 'sort'
+    if 'k_merge_xchg' in name or 'k_merge_level' in name or 'k_finish_level' in name:
+        return 'merge'
+    return 'other'
+
+
+levels = []   # per level: list of steps, each {gather, sort, scans[], merges[]}
+step = None
+for r in rows:
+    k = kind(r['Kernel_Name'])
+    d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
+    if k == 'level':
+        levels.append({'steps': [], 'other': 0.0})
+        step = None
+        continue
+    if not levels:
+        continue
+    lv = levels[-1]
+    if k == 'gather':
+        step = {'gather': d, 'sort': 0.0, 'scans': [], 'merges': []}
+        lv['steps'].append(step)
+    elif step is None:
+        lv['other'] += d
+    elif k == 'sort':
+        step['sort'] += d
+    elif k == 'scan':
+        step['scans'].append(d)
+    elif k == 'merge':
+        step['merges'].append(d)
+    else:
+        lv['other'] += d
+
+# the bench's timed step is the last job of the trace: its levels are the last L - 1 entries
+L = 9 if len(levels) >= 9 else len(levels)
+sel = levels[-L:]
+tot_meas = tot_model = 0.0
+for i, lv in enumerate(sel):
+    meas = model = 0.0
+    sharded = 0
+    for st in lv['steps']:
+        meas += st['gather'] + st['sort'] + sum(st['scans']) + sum(st['merges'])
+        nsh = len(st['merges'])
+        sharded += nsh > 1
+        model += st['gather'] + st['sort'] + (max(st['scans']) if st['scans'] else 0.0) + \
+            (st['merges'][-1] if st['merges'] else 0.0) + (XLAT if nsh > 1 else 0.0)
+    meas += lv['other']
+    model += lv['other']
+    tot_meas += meas
+    tot_model += model
+    print('level %d: %d steps (%d sharded %d ways): emulated %.1f ms, modelled per rank %.1f ms'
+          % (i + 1, len(lv['steps']), sharded, W, meas / 1e3, model / 1e3))
+print('job: emulated kernels %.1f ms on one GPU; modelled %.1f ms per rank on %d GPUs (exchange latency %.1f us/step)'
+      % (tot_meas / 1e3, tot_model / 1e3, W, XLAT))
+if base:
+    print('speedup vs %.1f ms: %.2fx, efficiency %.0f %%' % (base, base / (tot_model / 1e3), 100 * base / (tot_model / 1e3) / W))

@@ -8,7 +8,8 @@ import sys
 
 
 def short(name):
-    for k in ('k_part_means_fold', 'k3h_prune', 'k_gather_query_p', 'k3h_scan', 'k3h_dist', 'k3_dist', 'k_merge_level', 'k_gather_query_h', 'k_gather_query', 'k_part_means',
+    for k in ('k_part_means_fold', 'k3h_prune', 'k_gather_query_p', 'k3h_scan', 'k3h_dist', 'k3_dist', 'k_merge_level',
+              'k_merge_xchg', 'k_query_sort', 'k_gather_query_h', 'k_gather_query', 'k_part_means',
               'k_db_build_h', 'k_db_build', 'k_absmax', 'k_reduce_stats', 'k_finish_level', 'k_step_fused'):
         if k in name:
             return k

@@ -1,0 +1,87 @@
+"""Two-process rehearsal of the peer-write winner exchange (include/ia.h ia_xchg_*) on ONE GPU:
+both ranks open each other's exchange buffer through real HIP IPC handles and run a sharded
+synthesis whose every wavefront step publishes / polls across the process boundary.  Each rank
+checks its B', s, im replica against the golden reference run (g256, every level pruned) and
+against an unsharded run of a 1024^2 job (cfg3, pruned 1024^2 level) made by its own second
+context.  Launch (from the repo root, gloo carries only the 64-byte handles):
+  torchrun --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 tools/xchg_rehearsal.py
+"""
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, 'tests'))
+
+
+def run(ctx, z, prune_all):
+    from ia_amd import _native
+    L, k = z['L'], float(z['k'])
+    Bp = [x.copy() for x in z['Bp_init']]
+    st = _native.Stats()
+    out = {}
+    ctx.set_option('prune_min_rows', 1 if prune_all else 524288)
+    for level in range(1, L):
+        out[level] = ctx.synthesize_level(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
+                                          [p[level - 1] for p in z['Ap_pyr']], z['B_pyr'][level], z['B_pyr'][level - 1],
+                                          Bp[level - 1], Bp[level], z['weights'], 1 + 2.0 ** (level - L) * k, st)
+    return out, Bp, st
+
+
+def main():
+    import torch
+    import torch.distributed as dist
+    import ia_amd  # noqa: F401
+    from ia_amd import _native, synth
+    from golden_util import load_e2e
+    rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    dist.init_process_group('gloo')
+    ctx = _native.Context(0)
+
+    def all_gather(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+    ctx.xchg_init(rank, world, all_gather)
+    ok = True
+    z = load_e2e('g256')
+    dist.barrier()
+    t0 = time.time()
+    out, Bp, st = run(ctx, z, True)
+    t1 = time.time()
+    for level, (s, im) in out.items():
+        same = (np.array_equal(s, z['s'][level]) and np.array_equal(im, z['im'][level]) and
+                np.array_equal(Bp[level], z['Bp_final'][level]))
+        ok &= same
+    print('[rank %d] g256 pruned, %d-way peer-write shards: %s vs the reference run (%.2f s, bound_violations %d)'
+          % (rank, world, 'bit-identical' if ok else 'DIFFERENT', t1 - t0, st.bound_violations), flush=True)
+    job = synth.make_job(1024)
+    zj = {'L': job.L, 'k': job.k, 'A_pyr': job.A_pyr, 'Ap_pyr': job.Ap_pyr_list, 'B_pyr': job.B_pyr,
+          'Bp_init': job.Bp_init, 'weights': job.weights}
+    dist.barrier()
+    t0 = time.time()
+    out, Bp, st = run(ctx, zj, False)
+    t1 = time.time()
+    plain = _native.Context(0)   # unsharded reference on this rank
+    ref, Bp_ref, _ = run(plain, zj, False)
+    same = all(np.array_equal(out[l][0], ref[l][0]) and np.array_equal(out[l][1], ref[l][1]) and
+               np.array_equal(Bp[l], Bp_ref[l]) for l in range(1, job.L))
+    ok &= same
+    print('[rank %d] cfg3 1024^2, %d-way peer-write shards (pruned 1024^2 level): %s vs unsharded (%.2f s sharded, '
+          'pruned levels %d, bound_violations %d)' % (rank, world, 'bit-identical' if same else 'DIFFERENT', t1 - t0,
+                                                      st.pruned_levels, st.bound_violations), flush=True)
+    plain.close()
+    ctx.close()
+    flag = torch.tensor([0 if ok else 1])
+    dist.all_reduce(flag)
+    dist.destroy_process_group()
+    if rank == 0:
+        print('XCHG-REHEARSAL %s' % ('OK' if int(flag) == 0 else 'FAILED'), flush=True)
+    sys.exit(0 if int(flag) == 0 else 1)
+
+
+if __name__ == '__main__':
+    main()
