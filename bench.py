@@ -176,8 +176,8 @@ def make_context(args, local):
     if args.k3_variant != 1:
         cx.set_option('k3_variant', args.k3_variant)       # DIAG=1 builds only
     cx.set_option('prune', args.prune)
-    if args.k3p_variant != 14:
-        cx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15; the rest DIAG=1 builds only
+    if args.k3p_variant != 20:
+        cx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15, 18..21; the rest DIAG=1 builds only
     cx.set_option('prune_min_rows', args.prune_min_rows)
     if args.prune_group != 1:
         cx.set_option('prune_group', args.prune_group)
@@ -201,10 +201,11 @@ def gather_rooflines(st):
         out[name] = {'achieved': gbs, 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s', 'frac': gbs * 1e9 / HBM_PEAK,
                      'us_per_launch': ms * 1e3 / launches, 'algorithmic_bytes_per_launch': nbytes / launches,
                      'launches': launches, 'bound': bound, 'bytes': what}
+    lv = 'the level with the largest DB (%d rows)' % st['build_rows']
     one('k_db64_build', st['k1b_ms'], st['k1b_bytes'], st['build_levels'], 'hbm',
-        'A-side images read once + N_A rows x DS x 8 B written')
+        'A-side images read once + N_A rows x DS x 8 B written; ' + lv)
     one('k_db_build_h', st['k1_ms'], st['k1_bytes'], st['build_levels'], 'hbm',
-        'fp64 rows read (N_A x DS x 8 B) + split-f16 tiles written (7 KiB per 32 rows)')
+        'fp64 rows read (N_A x DS x 8 B) + split-f16 tiles written (7 KiB per 32 rows); ' + lv)
     one('k_gather_query', st['gather_ms_timed'], st['gather_bytes_timed'], st['gather_launches_timed'],
         'latency (one wave per query: dependent window, coherence-row and DB loads)',
         'per query: 55 features + 12 coherence candidate rows (pruned levels) read, fp64 row + f16 fragments + '
@@ -249,13 +250,15 @@ def main():
                     help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select (DIAG=1 builds)')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
-    ap.add_argument('--k3p-variant', type=int, default=14, choices=list(range(20)),
+    ap.add_argument('--k3p-variant', type=int, default=20, choices=list(range(22)),
                     help='pruned-scan kernel version (ia_k3h.hip k3h_prune*): 0 = first version, 1 = boxes in '
                          'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
                          'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks, 11 = 7 on queries presorted once per step, '
-                         '14 (default) / 15 = 7 / 11 with the hi x hi block filter, 16 / 17 = rotated DB with the '
+                         '14 / 15 = 7 / 11 with the hi x hi block filter, 16 / 17 = rotated DB with the '
                          'principal-axis head filter (DESIGN.md §4f), 18 / 19 = 14 / 15 with the correction products fused onto the '
-                         'hi x hi accumulator; product builds hold 7, 11, 14, 15, 18 and 19')
+                         'hi x hi accumulator (software-pipelined single chains), 20 (default) / 21 = the same on query-tile pairs '
+                         '(two chains); '
+                         'product builds hold 7, 11, 14, 15 and 18..21')
     ap.add_argument('--prune-group', type=int, default=1, choices=[1, 2, 4, 8],
                     help='pruned levels: Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)')
     ap.add_argument('--prune-min-rows', type=int, default=524288,

@@ -49,14 +49,22 @@ class Stats(ctypes.Structure):
                 ('k1_bytes', ctypes.c_double), ('build_levels', ctypes.c_int64),
                 ('gather_ms_timed', ctypes.c_double), ('gather_launches_timed', ctypes.c_int64),
                 ('gather_bytes_timed', ctypes.c_double), ('merge_ms_timed', ctypes.c_double),
-                ('merge_launches_timed', ctypes.c_int64)]
+                ('merge_launches_timed', ctypes.c_int64), ('build_rows', ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
     def add(self, other):
-        """accumulate another Stats (e.g. of a concurrent context) field by field"""
+        """accumulate another Stats (e.g. of a concurrent context) field by field (the DB-build
+        timings keep the largest level's, as libia does)"""
+        if other.build_rows > self.build_rows:
+            for k in ('k1b_ms', 'k1b_bytes', 'k1_ms', 'k1_bytes', 'build_levels'):
+                setattr(self, k, 0)
+            self.build_rows = other.build_rows
         for k, _ in self._fields_:
+            if k == 'build_rows' or (k in ('k1b_ms', 'k1b_bytes', 'k1_ms', 'k1_bytes', 'build_levels')
+                                     and other.build_rows < self.build_rows):
+                continue
             setattr(self, k, getattr(self, k) + getattr(other, k))
 
 

@@ -103,7 +103,7 @@ struct ia_ctx {
   int shard_emulate = 1;         // option "shard_emulate": W > 1 runs a W-way DB shard on this device
   int prune_group = 1;           // option "prune_group": Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)
   int matcher = IA_MATCH_F16X3;  // option "matcher"
-  int k3p_variant = 14;          // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
+  int k3p_variant = 20;          // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   // per-step K3 timing (optional)
   int time_dist = 0;
@@ -344,7 +344,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   }
 #ifdef IA_K3H_DIAG  // DIAG=1 builds: every kernel version of DESIGN.md §4b's progression
   if (!std::strcmp(name, "k3p_variant")) {
-    if (value < 0 || value > 19) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..19");
+    if (value < 0 || value > 21) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..21");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -354,12 +354,13 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
 #else  // product build: the default kernels only (7: pruned scan, 1: packed-index K3h)
-  if (!std::strcmp(name, "k3p_variant")) {  // 14 (default) / 15: hi x hi block filter (in-kernel sort up to
-                                            // 512 queries, presorted 15 above); 7 / 11: v7;
-                                            // 16 / 17 (rotated DB, §4f) are in DIAG=1 builds
-    if (value != 7 && value != 11 && value != 14 && value != 15 && value != 18 && value != 19)
-      return fail(IA_EINVAL,
-                  "ia_set_option: k3p_variant is 7, 11, 14, 15, 18 or 19 (other versions are in DIAG=1 builds only)");
+  if (!std::strcmp(name, "k3p_variant")) {  // 20 (default) / 21: hi x hi block filter with the correction
+                                            // products fused on query-tile pairs (in-kernel sort up to 512
+                                            // queries, presorted 21 above); 14 / 15: the filter, then full
+                                            // chains; 18 / 19: fused, single chains; 7 / 11: v7 (DESIGN.md
+                                            // §4b); 16 / 17 (rotated DB, §4f) are in DIAG=1 builds
+    if (value != 7 && value != 11 && value != 14 && value != 15 && value != 18 && value != 19 && value != 20 && value != 21)
+      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14, 15 or 18..21 (other versions are in DIAG=1 builds only)");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -941,9 +942,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     // sort of v6/v7 (512) or variant 11 is selected
     // (variants 11, 12: presorted; 7, 13: in-kernel sort up to 512 queries, presorted v11 / v12 above)
     const int kv = rot ? c->k3p_variant : (c->k3p_variant == 16 ? 14 : c->k3p_variant == 17 ? 15 : c->k3p_variant);
-    const int k3v = (kv == 11 || kv == 12 || kv == 15 || kv == 17 || kv == 19) ? kv
-                    : (prune && sd.Mpad > 512 ? (kv == 13 ? 12 : kv == 14 ? 15 : kv == 18 ? 19 : kv == 16 ? 17 : 11) : kv);
-    const bool presorted = k3v == 11 || k3v == 12 || k3v == 15 || k3v == 17 || k3v == 19;
+    const int k3v = (kv == 11 || kv == 12 || kv == 15 || kv == 17 || kv == 19 || kv == 21) ? kv
+                    : (prune && sd.Mpad > 512
+                           ? (kv == 13 ? 12 : kv == 14 ? 15 : kv == 18 ? 19 : kv == 20 ? 21 : kv == 16 ? 17 : 11)
+                           : kv);
+    const bool presorted = k3v == 11 || k3v == 12 || k3v == 15 || k3v == 17 || k3v == 19 || k3v == 21;
     if (prune && presorted)
       ia_launch_query_sort(c->qinfo.as<float4>(), c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
                            c->qs_frag.p, c->qs_tbox.as<float4>(), c->st);
@@ -1089,7 +1092,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);
     hipEventElapsedTime(&ms_k1b, c->kb[0], c->kb[1]);
     hipEventElapsedTime(&ms_k1, c->kb[2], c->kb[3]);
-    {  // K1b: A-side images read once, every fp64 row written; K1: this process's rows read, tiles written
+    if (g.NA >= stats->build_rows) {  // K1b: A-side images read once, every fp64 row written; K1: this
+                                      // process's rows read, tiles written (the largest level seen)
+      if (g.NA > stats->build_rows) {
+        stats->k1b_ms = stats->k1b_bytes = stats->k1_ms = stats->k1_bytes = 0.;
+        stats->build_levels = 0;
+        stats->build_rows = g.NA;
+      }
       const int DSb = ia_db64_stride(g.ch);
       stats->k1b_ms += ms_k1b;
       stats->k1b_bytes += (double)(nA + nAc) * (1 + g.n_ap) * 8 + (double)g.NA * DSb * 8;

@@ -435,6 +435,89 @@ __device__ __forceinline__ void k3p_hhfuse(const h16x8 (&a)[2 * KS], const h16x8
   }
 }
 
+// HHX paired (k3p_variant 20 / 21): the same fused corrections, organised like k3p_pairs - the
+// hi x hi chains of a query-tile pair run as two independent chains, both bound tests follow,
+// and the passing blocks' corrections run as two chains (both pass) or one, with the two-query
+// epilogue when both pass.  Two independent MFMA chains per pair instead of k3p_hhfuse's
+// software pipeline over single chains.
+template <int KS>
+__device__ __forceinline__ void k3p_corr(const h16x8 (&a)[2 * KS], const h16x8 *qb, f32x16 &c) {
+#pragma unroll
+  for (int s = 0; s < KS; s++) {
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], qb[(2 * s) * IA_WAVE], c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], qb[(2 * s + 1) * IA_WAVE], c, 0, 0, 0);
+  }
+}
+template <int KS, int QT, int QP>
+__device__ __forceinline__ void k3p_hhpairs(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, float rt,
+                                            const float *qzt, const float *qzw, int t, float (&b1)[QT], float (&b2)[QT],
+                                            int (&i1)[QT], unsigned &pass) {
+  if constexpr (2 * QP < QT) {
+    constexpr int NP = 2 * KS, q0 = 2 * QP, q1 = 2 * QP + 1;
+    const unsigned m2 = (msk >> q0) & 3u;
+    const h16x8 *qb0 = lq + q0 * NP * IA_WAVE, *qb1 = qb0 + NP * IA_WAVE;
+    const float rr = fmaf(rt, 0x1p-9f, 0x1p-20f);
+    if constexpr (q1 < QT) {
+      if (m2 == 3u) {
+        constexpr f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        f32x16 c0 = zero, c1 = zero;
+#pragma unroll
+        for (int s = 0; s < KS; s++) {
+          c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], qb0[(2 * s) * IA_WAVE], c0, 0, 0, 0);
+          c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], qb1[(2 * s) * IA_WAVE], c1, 0, 0, 0);
+        }
+        const bool p0 = __ballot(k3p_min16(c0) <= fmaf(rt, qzw[q0 * IA_TILE] + rr, qzt[q0 * IA_TILE])) != 0ull;
+        const bool p1 = __ballot(k3p_min16(c1) <= fmaf(rt, qzw[q1 * IA_TILE] + rr, qzt[q1 * IA_TILE])) != 0ull;
+        pass |= (p0 ? 1u << q0 : 0u) | (p1 ? 1u << q1 : 0u);
+        if (p0 && p1) {
+#pragma unroll
+          for (int s = 0; s < KS; s++) {
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], qb0[(2 * s) * IA_WAVE], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], qb1[(2 * s) * IA_WAVE], c1, 0, 0, 0);
+            c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], qb0[(2 * s + 1) * IA_WAVE], c0, 0, 0, 0);
+            c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], qb1[(2 * s + 1) * IA_WAVE], c1, 0, 0, 0);
+          }
+          k3h_epi2<QT, true>(c0, c1, q0, true, 0, t, b1, b2, i1);
+        } else if (p0) {
+          k3p_corr<KS>(a, qb0, c0);
+          k3p_epi1(c0, t, b1[q0], b2[q0], i1[q0]);
+        } else if (p1) {
+          k3p_corr<KS>(a, qb1, c1);
+          k3p_epi1(c1, t, b1[q1], b2[q1], i1[q1]);
+        }
+      } else if (m2 != 0u) {
+        const bool sel = m2 == 2u;
+        const h16x8 *qb = sel ? qb1 : qb0;
+        f32x16 c = k3p_hh<KS>(a, qb);
+        const int qq = sel ? q1 : q0;
+        if (__ballot(k3p_min16(c) <= fmaf(rt, qzw[qq * IA_TILE] + rr, qzt[qq * IA_TILE])) != 0ull) {
+          pass |= 1u << qq;
+          k3p_corr<KS>(a, qb, c);
+          float x1 = sel ? b1[q1] : b1[q0], x2 = sel ? b2[q1] : b2[q0];
+          int xi = sel ? i1[q1] : i1[q0];
+          k3p_epi1(c, t, x1, x2, xi);
+          b1[q0] = sel ? b1[q0] : x1;
+          b2[q0] = sel ? b2[q0] : x2;
+          i1[q0] = sel ? i1[q0] : xi;
+          b1[q1] = sel ? x1 : b1[q1];
+          b2[q1] = sel ? x2 : b2[q1];
+          i1[q1] = sel ? xi : i1[q1];
+        }
+      }
+    } else {
+      if (m2 == 1u) {
+        f32x16 c = k3p_hh<KS>(a, qb0);
+        if (__ballot(k3p_min16(c) <= fmaf(rt, qzw[q0 * IA_TILE] + rr, qzt[q0 * IA_TILE])) != 0ull) {
+          pass |= 1u << q0;
+          k3p_corr<KS>(a, qb0, c);
+          k3p_epi1(c, t, b1[q0], b2[q0], i1[q0]);
+        }
+      }
+    }
+    k3p_hhpairs<KS, QT, QP + 1>(a, lq, msk, rt, qzt, qzw, t, b1, b2, i1, pass);
+  }
+}
+
 // HF (k3p_variant 16 / 17): the rotated DB (ia_internal.h).  A tile's head is
 // its k-step 0 (2 pieces, 2 KiB), its tail the other 6 (6 KiB, a separate array after the NT
 // heads).  The head chain (3 MFMAs) of a (DB tile, query tile) block yields the 15-axis partial
@@ -836,7 +919,7 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // HHF (k3p_variant 14 / 15): the hi x hi block filter above (k3p_hhpipe); the per-WG pair
 // counter slot then holds (pairs with corrections << 32) + box-needed pairs.
 template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false, bool PIPE = false,
-          bool PRE = false, bool HHF = false, bool HF = false, bool HHX = false>
+          bool PRE = false, bool HHF = false, bool HF = false, int HHX = 0>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
@@ -1311,7 +1394,11 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       // makes the MFMAs below wait for the prefetch itself
       ld_tile<KS>(nxt, db, tk(kn < K ? kn : k), lane);
       asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-      if constexpr (HHF && HHX) {
+      if constexpr (HHF && HHX == 2) {
+        unsigned pass = 0;
+        k3p_hhpairs<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), tk(k), b1, b2, i1, pass);
+        nfull += __popc(pass);
+      } else if constexpr (HHF && HHX == 1) {
         f32x16 acc[2];
         unsigned pass = 0;
         k3p_hhfuse<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), tk(k), b1, b2, i1, acc,
@@ -1542,9 +1629,14 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     if (variant == 15) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true>;
     // 18 / 19: 14 / 15 with the correction products fused onto the hi x hi accumulator (HHX)
     if (variant == 18)
-      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true, false, true>;
+      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true, false, 1>;
     if (variant == 19)
-      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true, false, true>;
+      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true, false, 1>;
+    // 20 / 21: the fused corrections on query-tile pairs (two chains: k3p_hhpairs)
+    if (variant == 20)
+      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true, false, 2>;
+    if (variant == 21)
+      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true, false, 2>;
 #ifdef IA_K3H_DIAG  // rotated DB + head filter: exact, not faster
     if (variant == 16) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, false, true>;
     if (variant == 17) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, false, true>;

@@ -2503,15 +2503,15 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   // the in-kernel sort (3..10, 13, 14) holds <= 512 queries (14 -> 15: the host ran K2s); the
   // one-tile-per-thread lists of 3, 4 (!INTER) and 16, 17 (HF) <= 512 tiles per workgroup.  The
   // INTER variants (5..15) walk any number of tiles (the host keeps kmax <= IA_K3P_MAXK_LDS).
-  const bool in_kernel_sort = (variant < 11 || variant == 13 || variant == 14 || variant == 18) && variant >= 3;
+  const bool in_kernel_sort = (variant < 11 || variant == 13 || variant == 14 || variant == 18 || variant == 20) && variant >= 3;
   const bool tile_lists = variant == 3 || variant == 4 || variant == 16 || variant == 17;
-  if (in_kernel_sort && Mpad > 512) variant = variant == 14 ? 15 : variant == 18 ? 19 : 1;
+  if (in_kernel_sort && Mpad > 512) variant = variant == 14 ? 15 : variant == 18 ? 19 : variant == 20 ? 21 : 1;
   else if (tile_lists && kmax > 512) variant = 1;
   if (variant == 16 && Mpad > 512) variant = 17;   // rotated DB (the host keeps kmax <= 512 there)
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t NQ = (size_t)qt * IA_TILE;
-  const bool pre = variant == 11 || variant == 12 || variant == 15 || variant == 17 || variant == 19;
-  const bool hhf = variant == 14 || variant == 15 || variant == 16 || variant == 17 || variant == 18 || variant == 19;
+  const bool pre = variant == 11 || variant == 12 || variant == 15 || variant == 17 || variant == 19 || variant == 21;
+  const bool hhf = variant >= 14 && variant <= 21;  // (z, w) per query slot + R_t per tile in LDS (16 / 17: HF too)
   const int nthr = variant == 12 || variant == 13 ? 16 * IA_WAVE : IA_WGH;  // v12/13: 16 waves (4 per SIMD), one tile buffer
   size_t lds = pre ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 +
                          (size_t)kmax * 40

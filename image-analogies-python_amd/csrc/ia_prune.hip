@@ -72,14 +72,16 @@ __global__ void __launch_bounds__(PR_WG) k_cov_partial(const double *__restrict_
   }
 }
 
-// K5b: fixed-order sum of the partials
-__global__ void __launch_bounds__(PR_WG) k_cov_reduce(const double *__restrict__ part, int nwg, double *__restrict__ cov) {
+// K5b: fixed-order sum of the partials, one thread per pair (25 one-wave workgroups: the
+// partials of adjacent pairs are adjacent, so every load of a wave is one coalesced row)
+__global__ void __launch_bounds__(64) k_cov_reduce(const double *__restrict__ part, int nwg, double *__restrict__ cov) {
   constexpr int NPAIR = 55 * 56 / 2;
-  for (int p = threadIdx.x; p < NPAIR; p += PR_WG) {
-    double s = 0.;
-    for (int w = 0; w < nwg; w++) s += part[(int64_t)w * NPAIR + p];
-    cov[p] = s;
-  }
+  const int p = blockIdx.x * 64 + threadIdx.x;
+  if (p >= NPAIR) return;
+  double s = 0.;
+#pragma unroll 8
+  for (int w = 0; w < nwg; w++) s += part[(int64_t)w * NPAIR + p];
+  cov[p] = s;
 }
 
 // K5c: projections, keys and the identity row list of every DB row
@@ -396,7 +398,7 @@ static inline unsigned pr_cdiv(int64_t a, int64_t b) { return (unsigned)((a + b 
 void ia_launch_cov(const double *db64, int64_t NA, int64_t stride, int nwg, const double *mu_part, double *part,
                    double *cov, hipStream_t st) {
   hipLaunchKernelGGL(k_cov_partial, dim3(nwg), dim3(PR_WG), 0, st, db64, NA, stride, mu_part, part);
-  hipLaunchKernelGGL(k_cov_reduce, dim3(1), dim3(PR_WG), 0, st, part, nwg, cov);
+  hipLaunchKernelGGL(k_cov_reduce, dim3(pr_cdiv(55 * 56 / 2, 64)), dim3(64), 0, st, part, nwg, cov);
 }
 
 void ia_launch_proj_keys(const double *db64, int64_t NA, const double *mu_part, const double *basis, double *proj,

@@ -79,17 +79,19 @@ typedef struct {
   double dist_tiles_rows;   /* k3p_variant 16/17: DB tiles whose full rows were loaded after the
                              * head filter (dist_tiles counts the heads); else 0 */
   /* feature-gather kernels (bench.py roofline.gathers; DESIGN.md §4 algorithmic bytes) */
-  double k1b_ms;            /* K1b k_db64_build (fp64 row DB), device ms summed over levels */
+  double k1b_ms;            /* K1b k_db64_build (fp64 row DB), device ms summed over the levels */
   double k1b_bytes;         /* its algorithmic bytes: A-side images read once + N_A rows written */
-  double k1_ms;             /* K1 k_db_build_h (split-f16 tiles), device ms summed over levels */
+  double k1_ms;             /* K1 k_db_build_h (split-f16 tiles), device ms summed over the levels */
   double k1_bytes;          /* its algorithmic bytes: fp64 rows read + tiles written */
-  int64_t build_levels;     /* levels whose K1 / K1b were timed (every level) */
+  int64_t build_levels;     /* levels summed in k1*_ms / k1*_bytes: those with the largest DB
+                             * (build_rows) this ia_stats has seen (the bench's finest level) */
   double gather_ms_timed;   /* K2 (k_gather_query_*) of the sampled steps ("time_dist"): device ms */
   int64_t gather_launches_timed;
   double gather_bytes_timed; /* their algorithmic bytes: 55 features + 12 coherence rows read,
                               * fp64 row + fragments + pruning record written per query */
   double merge_ms_timed;    /* K4 (k_merge_level) of the sampled steps: device ms */
   int64_t merge_launches_timed;
+  int64_t build_rows;       /* DB rows of the levels in k1*_ms (the largest seen) */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),

@@ -83,7 +83,7 @@ def test_batched_512_pruned_wide_step(ctx, variant):
         except _native.IAError:
             pytest.skip('k3p_variant 16 is built with DIAG=1 only')
         finally:
-            ctx.set_option('k3p_variant', 14)
+            ctx.set_option('k3p_variant', 20)
     job = synth.make_job(512, n_levels=3)
     ctx.set_option('prune_min_rows', 1)
     ctx.set_option('k3p_variant', variant)
@@ -96,7 +96,7 @@ def test_batched_512_pruned_wide_step(ctx, variant):
         Ss, IMs, sts = _run(ctx, z, js, False)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 14)
+        ctx.set_option('k3p_variant', 20)
     for j in range(len(jb)):
         for level in range(1, job.L):
             assert np.array_equal(Sb[j][level], Ss[j][level]) and np.array_equal(IMb[j][level], IMs[j][level])
@@ -158,7 +158,7 @@ def test_device_sweep_two_streams_equals_one(ctx):
     assert st2.pixels == st1.pixels and st2.coherence_wins == st1.coherence_wins and st2.bound_violations == 0
 
 
-@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_v11', 'pruned_v18'])
+@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_v11', 'pruned_v18', 'pruned_v20'])
 def test_batched_g256_wide_steps_match_reference(ctx, mode):
     """8 jobs on the golden g256 run's A side: job 0 is the reference's own
     run, jobs 1..7 other kappas and B' seeds.  On the 256^2 level a step holds 8 x 86 = 688
@@ -171,7 +171,7 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
     z = load_e2e('g256')
     if mode != 'unpruned':
         ctx.set_option('prune_min_rows', 1)
-    if mode in ('pruned_v11', 'pruned_v18'):
+    if mode in ('pruned_v11', 'pruned_v18', 'pruned_v20'):
         ctx.set_option('k3p_variant', int(mode[-2:]))
     try:
         jb = _jobs_g32(z, kappas=(0.5, 5.0, 25.0, 1.0, 2.0, 10.0, 15.0, 20.0))
@@ -180,7 +180,7 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
         Ss, IMs, sts = _run(ctx, z, js, False)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 14)
+        ctx.set_option('k3p_variant', 20)
     h, w = z['B_pyr'][-1].shape
     assert 8 * min(h, (w + 2) // 3) > 512
     for level in range(1, z['L']):   # job 0 is the reference's own run

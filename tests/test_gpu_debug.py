@@ -19,10 +19,11 @@ from golden_util import BIG_CASES, E2E_CASES, load_e2e
 pytestmark = pytest.mark.gpu
 
 
-def _run_debug(ctx, z, prune_all=False, variant=14):
+def _run_debug(ctx, z, prune_all=False, variant=20):
     """prune_all: option prune_min_rows = 1, so every 1-channel level goes through the certified
     pruned scan (K2p -> K3p) instead of only DB levels of >= 2^19 rows; variant:
-    the pruned-scan kernel (14: hi x hi block filter, the default; 16: rotated DB + head filter)."""
+    the pruned-scan kernel (20: hi x hi block filter with fused corrections, the default; 14: the
+    filter followed by full chains; 16: rotated DB + head filter)."""
     from ia_amd import _native
     L, k = z['L'], float(z['k'])
     Bp = [x.copy() for x in z['Bp_init']]
@@ -42,14 +43,14 @@ def _run_debug(ctx, z, prune_all=False, variant=14):
             out[level] = (s, im, dbg)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 14)
+        ctx.set_option('k3p_variant', 20)
     return out, Bp, st
 
 
-@pytest.mark.parametrize('prune_all,variant', [(False, 14), (True, 7), (True, 14), (True, 15), (True, 11), (True, 18),
-                                                (True, 19), (True, 16)],
+@pytest.mark.parametrize('prune_all,variant', [(False, 20), (True, 7), (True, 14), (True, 15), (True, 11), (True, 18),
+                                                (True, 19), (True, 20), (True, 21), (True, 16)],
                          ids=['default', 'pruned_v7', 'pruned', 'pruned_presorted_v15', 'pruned_presorted_v11',
-                              'pruned_v18', 'pruned_presorted_v19', 'pruned_v16'])
+                              'pruned_v18', 'pruned_presorted_v19', 'pruned_v20', 'pruned_presorted_v21', 'pruned_v16'])
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
 def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     """Every NN pick, coherence pick and compute_distance value of the reference run.  With
@@ -66,13 +67,13 @@ def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
         except _native.IAError:
             pytest.skip('k3p_variant 16 is built with DIAG=1 only')
         finally:
-            ctx.set_option('k3p_variant', 14)
+            ctx.set_option('k3p_variant', 20)
     z = load_e2e(name)
     out, Bp, st = _run_debug(ctx, z, prune_all, variant)
     ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]
     if prune_all:
         assert st.pruned_levels == (z['L'] - 1 if ch == 1 else 0)
-    if variant in (14, 15, 16, 18, 19) and st.pruned_levels > 0:  # the block filters run on pruned levels only
+    if variant in (14, 15, 16, 18, 19, 20, 21) and st.pruned_levels > 0:  # the block filters run on pruned levels only
         assert 0 < st.dist_pairs_corrected <= st.dist_pairs
     if variant == 16 and st.pruned_levels > 0:
         assert 0 < st.dist_tiles_rows <= st.dist_tiles

@@ -17,7 +17,7 @@ def _diag_build(ctx):
         ctx.set_option('k3p_variant', 6)
     except _native.IAError:
         return False
-    ctx.set_option('k3p_variant', 14)
+    ctx.set_option('k3p_variant', 20)
     return True
 
 
@@ -38,7 +38,7 @@ def _run(ctx, job, prune, variant=7, group=1):
                 Bp[level], job.weights, job.kappa_factor(level), st)
     finally:
         ctx.set_option('prune', 1)
-        ctx.set_option('k3p_variant', 14)
+        ctx.set_option('k3p_variant', 20)
         ctx.set_option('prune_min_rows', 524288)
         ctx.set_option('prune_group', 1)
     return Bp, S, IM, st
@@ -47,6 +47,7 @@ def _run(ctx, job, prune, variant=7, group=1):
 @pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 16), (1024, 2, 16), (512, 1, 17), (1024, 2, 17),
                                                       (512, 1, 7), (1024, 2, 7), (512, 1, 11), (1024, 2, 11), (512, 1, 14), (1024, 2, 14),
                                                       (512, 1, 15), (1024, 2, 15), (512, 1, 18), (1024, 2, 18), (512, 1, 19), (1024, 2, 19),
+                                                      (512, 1, 20), (1024, 2, 20), (512, 1, 21), (1024, 2, 21),
                                                       (512, 1, 12), (1024, 2, 12), (512, 1, 13), (1024, 2, 13),
                                                       (512, 1, 10), (1024, 2, 9), (512, 1, 8),
                                                       (1024, 2, 6), (1024, 2, 5), (1024, 2, 4), (1024, 2, 3),
@@ -57,7 +58,7 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     builds the rest, e.g. 12 (presorted, 16 waves with one tile buffer each: 4 waves per SIMD) and
     13 (12 with the in-kernel sort), both measured slower): every one is exact"""
     from ia_amd import synth
-    if variant not in (7, 11, 14, 15, 18, 19) and not _diag_build(ctx):
+    if variant not in (7, 11, 14, 15, 18, 19, 20, 21) and not _diag_build(ctx):
         pytest.skip('kernel version %d is built with DIAG=1 only' % variant)
     job = synth.make_job(size)
     Bp0, S0, IM0, st0 = _run(ctx, job, 0)
@@ -71,7 +72,7 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     assert st1.dist_pairs < st1.dist_pairs_full
     assert st1.dist_pairs_full == st0.dist_pairs_full
     assert st1.dist_tiles <= st1.dist_tiles_full and st1.dist_tiles_full == st0.dist_tiles_full
-    if variant in (14, 15, 16, 17, 18, 19):  # block filters: most box-needed pairs stop after a cheap product
+    if variant in (14, 15, 16, 17, 18, 19, 20, 21):  # block filters: most box-needed pairs stop after a cheap product
         assert 0 < st1.dist_pairs_corrected < st1.dist_pairs
         print('filter-passing pairs %.3f of the box-needed ones' % (st1.dist_pairs_corrected / st1.dist_pairs))
     else:
@@ -110,7 +111,7 @@ def test_prune_option_rejects_bad_values(ctx):
     with pytest.raises(_native.IAError):
         ctx.set_option('prune_group', 3)
     with pytest.raises(_native.IAError):
-        ctx.set_option('k3p_variant', 20)
+        ctx.set_option('k3p_variant', 22)
     if not _diag_build(ctx):
         for v in (6, 12, 13, 16, 17):
             with pytest.raises(_native.IAError):
@@ -119,7 +120,7 @@ def test_prune_option_rejects_bad_values(ctx):
         ctx.set_option('prune_min_rows', 0)
 
 
-@pytest.mark.parametrize('variant', [14, 15, 7, 11, 18, 19])
+@pytest.mark.parametrize('variant', [14, 15, 7, 11, 18, 19, 20, 21])
 def test_pruned_scan_over_512_tiles_per_workgroup(ctx, variant):
     """a DB of more than 256 x 512 tiles (> 4.19 M rows: here A 2048 x 2080,
     133,120 tiles, 520 per workgroup) against a small B.  The pruned scan keeps every workgroup's
@@ -150,7 +151,7 @@ def test_pruned_scan_over_512_tiles_per_workgroup(ctx, variant):
         finally:
             ctx.set_option('prune', 1)
             ctx.set_option('prune_min_rows', 524288)
-            ctx.set_option('k3p_variant', 14)
+            ctx.set_option('k3p_variant', 20)
         out.append((s, im, Bp, st))
     (s0, im0, Bp0, st0), (s1, im1, Bp1, st1) = out
     assert st0.pruned_levels == 0 and st1.pruned_levels == 1

@@ -19,24 +19,28 @@ def short(name):
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 job = int(sys.argv[2]) if len(sys.argv) > 2 else 0
-levels, cur = [], None
+levels, cur, spans = [], None, []
 for r in rows:
     k = short(r['Kernel_Name'])
     if k == 'k_part_means':
         cur = collections.defaultdict(lambda: [0, 0.0])
         levels.append(cur)
+        spans.append([int(r['Start_Timestamp']), int(r['End_Timestamp'])])
     if cur is None:
         continue
+    spans[-1][1] = max(spans[-1][1], int(r['End_Timestamp']))
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
     cur[k][0] += 1
     cur[k][1] += d
     cur[k].append(d)
 per_job = 9
 sel = levels[job * per_job:(job + 1) * per_job] if len(levels) >= per_job else levels
+ssp = spans[job * per_job:(job + 1) * per_job] if len(levels) >= per_job else spans
 tot = collections.defaultdict(float)
 for i, lv in enumerate(sel):
     s = sum(v[1] for v in lv.values())
-    print('level %d: %.1f ms  ' % (i + 1, s / 1e3) + '  '.join('%s %d x %.1fus=%.1fms' % (k, v[0], v[1] / max(v[0], 1), v[1] / 1e3)
+    wall = (ssp[i][1] - ssp[i][0]) / 1e6
+    print('level %d: %.1f ms (wall %.1f ms: %.1f ms between kernels)  ' % (i + 1, s / 1e3, wall, wall - s / 1e3) + '  '.join('%s %d x %.1fus=%.1fms' % (k, v[0], v[1] / max(v[0], 1), v[1] / 1e3)
                                                           for k, v in sorted(lv.items(), key=lambda x: -x[1][1]) if v[1] > 100))
     for k, v in lv.items():
         tot[k] += v[1]
