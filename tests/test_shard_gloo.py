@@ -121,3 +121,114 @@ def test_merge_winners_skips_empty_shards():
     r = np.array([[2 ** 63 - 1, 7, 9], [3, 2 ** 63 - 1, 4]], dtype=np.int64)
     wd, wr = _native.merge_winners(d, r)
     assert list(wd) == [0.75, 0.5, 0.25] and list(wr) == [3, 7, 4]
+
+
+def _rank_xchg(rank, world, port, out_dir):
+    """Context.xchg_init's handle exchange over gloo with a stand-in libia (no GPU here): every
+    rank's 64-byte handle must reach ia_xchg_open on every rank, in rank order."""
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import ia_amd  # noqa: F401
+    from ia_amd import _native
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    seen = {}
+
+    class FakeLib(object):
+        def ia_xchg_alloc(self, h, w, buf):
+            seen['alloc_world'] = w
+            buf.raw = bytes([rank + 1]) * 64
+            return 0
+
+        def ia_xchg_open(self, h, r, w, handles):
+            seen['open'] = (r, w, bytes(handles))
+            return 0
+
+    _native._lib = FakeLib()
+    ctx = object.__new__(_native.Context)
+    ctx._h = None
+
+    def all_gather(b):
+        out = [None] * world
+        dist.all_gather_object(out, b)
+        return out
+    ctx.xchg_init(rank, world, all_gather)
+    r, w, hs = seen['open']
+    np.savez(os.path.join(out_dir, 'x%d.npz' % rank), r=r, w=w, alloc=seen['alloc_world'],
+             hs=np.frombuffer(hs, dtype=np.uint8))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 4])
+def test_xchg_handle_exchange_gloo(tmp_path, world):
+    mp.spawn(_rank_xchg, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    want = np.concatenate([np.full(64, r + 1, dtype=np.uint8) for r in range(world)])
+    for r in range(world):
+        z = np.load(os.path.join(str(tmp_path), 'x%d.npz' % r))
+        assert int(z['r']) == r and int(z['w']) == world and int(z['alloc']) == world
+        assert np.array_equal(z['hs'], want)
+
+
+def test_xchg_slot_protocol_two_parities_suffice():
+    """The peer-write exchange's slot discipline (ia_internal.h XSlot / ia_xslot, k_merge_xchg)
+    simulated with one thread per rank and random delays: a rank publishes its step-t winner
+    into slot (t & 1, rank, m) of every rank's buffer, then waits for the W slots of step t in
+    its own buffer and takes the lexicographic (d, row) minimum.  With two parities no slot is
+    overwritten before its reader consumed it (a rank is never two steps ahead of a peer), every
+    rank reads exactly step t's values, and all ranks agree on every winner."""
+    import threading
+    import time
+    rs = np.random.RandomState(1)
+    W, steps, M = 4, 60, 5
+    vals = rs.randint(0, 7, size=(steps, W, M)).astype(np.float64) / 4   # many exact ties
+    rows = rs.randint(0, 1000, size=(steps, W, M))
+    bufs = [dict() for _ in range(W)]          # (parity, rank, m) -> (d, row, seq)
+    consumed = [dict() for _ in range(W)]      # (parity, rank, m) -> seq its reader took
+    lock = threading.Lock()
+    got = np.zeros((W, steps, M, 2))
+    errors = []
+
+    def rank_main(r):
+        try:
+            rng = np.random.RandomState(100 + r)
+            for t in range(steps):
+                seq = t + 1
+                time.sleep(rng.rand() * 1e-3)
+                for p in range(W):               # publish into every peer (d, row, then seq)
+                    for m in range(M):
+                        with lock:
+                            old = bufs[p].get((seq & 1, r, m))
+                            if old is not None and consumed[p].get((seq & 1, r, m)) != old[2]:
+                                errors.append(('overwrote an unread slot', r, p, t, old[2]))
+                            bufs[p][(seq & 1, r, m)] = (vals[t, r, m], rows[t, r, m], seq)
+                deadline = time.time() + 10
+                for m in range(M):
+                    best = (np.inf, 2 ** 62)
+                    for p in range(W):           # poll own buffer
+                        while True:
+                            with lock:
+                                x = bufs[r].get((seq & 1, p, m))
+                            if x is not None and x[2] == seq:
+                                with lock:
+                                    consumed[r][(seq & 1, p, m)] = seq
+                                break
+                            if time.time() > deadline:
+                                raise RuntimeError('rank %d timed out at step %d' % (r, t))
+                            time.sleep(1e-5)
+                        best = min(best, (x[0], x[1]))
+                    got[r, t, m] = best
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=rank_main, args=(r,)) for r in range(W)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors, errors[:3]
+    for t in range(steps):
+        for m in range(M):
+            want = min(zip(vals[t, :, m], rows[t, :, m]))
+            for r in range(W):
+                assert tuple(got[r, t, m]) == want
