@@ -183,6 +183,8 @@ def make_context(args, local):
         cx.set_option('prune_group', args.prune_group)
     if args.row_source:
         cx.set_option('row_source', args.row_source)
+    if args.shard_unpruned:
+        cx.set_option('shard_unpruned', 1)
     if args.shard_emulate > 1:
         cx.set_option('shard_emulate', args.shard_emulate)
         cx.set_option('exchange', 1 if args.exchange == 'peer' else 0)   # the emulated shards' exchange kernels
@@ -266,6 +268,9 @@ def main():
     ap.add_argument('--row-source', type=int, default=0, choices=[0, 1],
                     help='exact rows of the rerank / coherence / pruning bound: 0 = fp64 row DB, 1 = gathered from '
                          'the A-side images (identical results)')
+    ap.add_argument('--shard-unpruned', action='store_true',
+                    help='shard (or emulate shards of) levels that scan unpruned too (default: only pruned levels, '
+                         'DESIGN.md §7)')
     ap.add_argument('--shard-emulate', type=int, default=1,
                     help='run every large level as a W-way DB shard on this one GPU (the multi-rank kernels '
                          'without the all-gather: per-shard scans and winners, then the finish); for the cost model')

@@ -101,6 +101,7 @@ struct ia_ctx {
   int prune = 1;
   int row_source = 0;            // option "row_source": exact rows from 0 = the fp64 row DB, 1 = the A images
   int shard_emulate = 1;         // option "shard_emulate": W > 1 runs a W-way DB shard on this device
+  int shard_unpruned = 0;        // option "shard_unpruned": 1 = shard levels that scan unpruned too
   int prune_group = 1;           // option "prune_group": Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)
   int matcher = IA_MATCH_F16X3;  // option "matcher"
   int k3p_variant = 20;          // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
@@ -399,6 +400,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     c->prune = value;
     return IA_OK;
   }
+  if (!std::strcmp(name, "shard_unpruned")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: shard_unpruned must be 0 or 1");
+    c->shard_unpruned = value;
+    return IA_OK;
+  }
   if (!std::strcmp(name, "exchange")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: exchange must be 0 (RCCL) or 1 (peer write)");
     c->exchange = value;
@@ -634,8 +640,14 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   // DB shards: over the ranks of ia_comm_init (world > 1), or emulated on this device (option
   // "shard_emulate" = W: the W shards' scans and per-shard certified winners run here one after
   // the other, then the multi-rank finish; no RCCL).  Levels under 64 tiles per shard replicate.
-  const bool sharded = shard_level(g.n_tiles, c->world);
-  const bool emulated = !sharded && c->world == 1 && c->shard_emulate > 1 && shard_level(g.n_tiles, c->shard_emulate);
+  // Only levels that run the pruned scan are sharded by default: the unpruned scan of a 512^2 or
+  // smaller DB gains nothing from 1/W of the tiles once the exchange is paid (DESIGN.md §7,
+  // profiles/r03/shard); option "shard_unpruned" = 1 shards those too (tests, very large DBs).
+  const bool shard_here = c->shard_unpruned ||
+                          (c->prune && c->matcher == IA_MATCH_F16X3 && g.ch == 1 && g.NA >= c->prune_min_rows);
+  const bool sharded = shard_here && shard_level(g.n_tiles, c->world);
+  const bool emulated = shard_here && !sharded && c->world == 1 && c->shard_emulate > 1 &&
+                        shard_level(g.n_tiles, c->shard_emulate);
   const int Wsh = sharded ? c->world : emulated ? c->shard_emulate : 1;  // shards of this level
   const bool multi = Wsh > 1;
   if (multi && J > 1) return fail(IA_EINVAL, "ia_synthesize_levels: sharded levels take one job per call");
@@ -652,8 +664,8 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     if (multi && args[j].dbg_src)
       return fail(IA_EINVAL, "ia_synthesize_level: debug outputs are produced by single-rank levels only");
   {
-    int64_t t0, t1;  // this rank's contiguous DB tiles (unpruned sharded levels hold only those)
-    ia_shard_tiles(g.NA, c->world, c->rank, &t0, &t1);
+    int64_t t0 = 0, t1 = g.n_tiles;  // this rank's contiguous DB tiles (unpruned sharded levels hold only those)
+    if (sharded) ia_shard_tiles(g.NA, c->world, c->rank, &t0, &t1);
     g.tile0 = (int)t0;
     g.tile1 = (int)t1;
   }

@@ -955,10 +955,10 @@ __device__ __forceinline__ double exact_dist_level(const double *__restrict__ db
   });
 }
 
-// the certified single-rank winner of query m (exact NN over this rank's shard)
-template <class DistFn>
+// the certified single-rank winner of query m (exact NN over this rank's shard); RPL records per
+// lane (nwg <= 64 RPL)
+template <int RPL = IA_WG_TARGET / IA_WAVE, class DistFn>
 __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, unsigned *stat_out) {
-  constexpr int RPL = IA_WG_TARGET / IA_WAVE;  // records per lane (nwg <= IA_WG_TARGET)
   const int lane = threadIdx.x & 63;
   const float4 *rr = a.rec + (int64_t)m * a.nwg;
   const float *rT = a.recT + (int64_t)m * a.nwg;
@@ -1075,13 +1075,57 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
   return Winner{bd, bi};
 }
 
-// coherence + kappa + writeback for query pixel (r, c) whose NN row is app_ix
-// (image_analogies.py:182-220, algorithms.py:92-135)
+// best_coherence_match's pick for query pixel (r, c) (algorithms.py:92-130): candidates in
+// product(rows, cols) order, first argmin of the unweighted norm.  Independent of the NN winner,
+// so the exchange merge runs it while the peers' winners are in flight.
+struct CohPick {
+  int pr, pc, img;
+  bool has;
+};
 template <int CH>
-__device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__restrict__ db64, int r, int c, int64_t app_ix,
-                             const double *q,
-                             int32_t *__restrict__ s, int32_t *__restrict__ im, double *__restrict__ Bp,
-                             const double *__restrict__ weights, double kf, unsigned *pstat, unsigned stat) {
+__device__ __forceinline__ CohPick coherence_pick(const LevelGeo &g, const double *__restrict__ db64, int r, int c,
+                                                  const double *q, const int32_t *__restrict__ s,
+                                                  const int32_t *__restrict__ im) {
+  const int lane = threadIdx.x & 63;
+  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
+  const int qi = r * g.bw + c;
+  CohPick k{-1, -1, 0, false};
+  if (qi == 0) return k;
+  double dk = DBL_MAX;
+  int64_t kk = INT64_MAX;
+  int cpr = -1, cpc = -1, cim = 0;
+  if (lane < 15) {
+    const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
+    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
+      const int nb = nr * g.bw + nc;
+      const int tr = s[2 * nb] + r - nr, tc = s[2 * nb + 1] + c - nc;
+      if (tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) {
+        cim = im[nb];
+        cpr = tr;
+        cpc = tc;
+        const int64_t row = (int64_t)cim * hw + (int64_t)tr * g.aw + tc;
+        dk = cr_sqrt(exact_dist_level<CH>(db64, row, q));
+        kk = lane;
+      }
+    }
+  }
+  wave_min_di(dk, kk);
+  if (kk != INT64_MAX) {
+    const int src = (int)kk;
+    k.pr = __shfl(cpr, src, 64);
+    k.pc = __shfl(cpc, src, 64);
+    k.img = __shfl(cim, src, 64);
+    k.has = true;
+  }
+  return k;
+}
+// kappa rule + writeback for query pixel (r, c) whose NN row is app_ix and coherence pick ck
+// (image_analogies.py:182-220, algorithms.py:133-135)
+template <int CH>
+__device__ void finish_pick(const LevelGeo &g, const Imgs &A, const double *__restrict__ db64, int r, int c,
+                            int64_t app_ix, const CohPick &ck, const double *q, int32_t *__restrict__ s,
+                            int32_t *__restrict__ im, double *__restrict__ Bp, const double *__restrict__ weights, double kf,
+                            unsigned *pstat, unsigned stat) {
   constexpr int D = Geo<CH>::D;
   const int lane = threadIdx.x & 63;
   const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
@@ -1090,49 +1134,23 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__r
   const unsigned rem = (unsigned)app_ix - (unsigned)img * hw;
   int pr = (int)(rem / (unsigned)g.aw), pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
   bool coh_won = false, kamb = false;
-  if (qi > 0) {
-    // best_coherence_match: candidates in product(rows, cols) order, first argmin of the norm
-    double dk = DBL_MAX;
-    int64_t kk = INT64_MAX;
-    int cpr = -1, cpc = -1, cim = 0;
-    if (lane < 15) {
-      const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
-      if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
-        const int nb = nr * g.bw + nc;
-        const int tr = s[2 * nb] + r - nr, tc = s[2 * nb + 1] + c - nc;
-        if (tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) {
-          cim = im[nb];
-          cpr = tr;
-          cpc = tc;
-          const int64_t row = (int64_t)cim * hw + (int64_t)tr * g.aw + tc;
-          dk = cr_sqrt(exact_dist_level<CH>(db64, row, q));
-          kk = lane;
-        }
-      }
+  if (ck.has) {
+    // compute_distance(AAp_feat, BBp_feat, weights) = norm((a - q) * w)**2 for app and coh
+    double part = 0.;
+    if (lane < 2) {
+      const int ii = lane == 0 ? img : ck.img, rr_ = lane == 0 ? pr : ck.pr, cc_ = lane == 0 ? pc : ck.pc;
+      const double *arow = db64 + ((int64_t)ii * hw + (int64_t)rr_ * g.aw + cc_) * Geo<CH>::DS;
+      part = blas_dot_sq<D>([&](int f) { return (arow[f] - q[f]) * weights[f]; });
+      part = cr_sqrt(part);
     }
-    wave_min_di(dk, kk);
-    if (kk != INT64_MAX) {
-      const int src = (int)kk;
-      cpr = __shfl(cpr, src, 64);
-      cpc = __shfl(cpc, src, 64);
-      cim = __shfl(cim, src, 64);
-      // compute_distance(AAp_feat, BBp_feat, weights) = norm((a - q) * w)**2 for app and coh
-      double part = 0.;
-      if (lane < 2) {
-        const int ii = lane == 0 ? img : cim, rr_ = lane == 0 ? pr : cpr, cc_ = lane == 0 ? pc : cpc;
-        const double *arow = db64 + ((int64_t)ii * hw + (int64_t)rr_ * g.aw + cc_) * Geo<CH>::DS;
-        part = blas_dot_sq<D>([&](int f) { return (arow[f] - q[f]) * weights[f]; });
-        part = cr_sqrt(part);
-      }
-      const double y_app = __shfl(part, 0, 64), y_coh = __shfl(part, 1, 64);
-      const double d_app = y_app * y_app, d_coh = y_coh * y_coh;
-      kamb = kappa_ambiguous(y_app, d_app, y_coh, d_coh, kf);
-      if (d_coh <= d_app * kf) {
-        img = cim;
-        pr = cpr;
-        pc = cpc;
-        coh_won = true;
-      }
+    const double y_app = __shfl(part, 0, 64), y_coh = __shfl(part, 1, 64);
+    const double d_app = y_app * y_app, d_coh = y_coh * y_coh;
+    kamb = kappa_ambiguous(y_app, d_app, y_coh, d_coh, kf);
+    if (d_coh <= d_app * kf) {
+      img = ck.img;
+      pr = ck.pr;
+      pc = ck.pc;
+      coh_won = true;
     }
   }
   if (lane < CH) Bp[(int64_t)qi * CH + lane] = A.p3[img * A.img_stride_f + ((int64_t)pr * g.aw + pc) * CH + lane];
@@ -1142,6 +1160,15 @@ __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__r
     im[qi] = img;
     if (pstat) pstat[qi] = stat | (kamb ? 1u << 29 : 0u) | (coh_won ? 1u << 30 : 0u);
   }
+}
+// coherence + kappa + writeback for query pixel (r, c) whose NN row is app_ix
+template <int CH>
+__device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__restrict__ db64, int r, int c, int64_t app_ix,
+                             const double *q,
+                             int32_t *__restrict__ s, int32_t *__restrict__ im, double *__restrict__ Bp,
+                             const double *__restrict__ weights, double kf, unsigned *pstat, unsigned stat) {
+  const CohPick ck = coherence_pick<CH>(g, db64, r, c, q, s, im);
+  finish_pick<CH>(g, A, db64, r, c, app_ix, ck, q, s, im, Bp, weights, kf, pstat, stat);
 }
 
 // Both distances of DB row `row` against query q from ONE set of feature loads (the row of the
@@ -1886,7 +1913,7 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
 // one device (shard_emulate) publish with FIN = false for shards 0..W-2 and FIN = true for the
 // last.  A wait beyond xa.timeout_ticks sets *err and finishes with the winners that arrived
 // (the host reports IA_ECOMM): no wave spins forever.
-template <int CH, bool FIN, class JS>
+template <int CH, bool FIN, class JS, int RPL>
 __global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, XchgArgs xa, JS jobs) {
   const int m = __builtin_amdgcn_readfirstlane(blockIdx.x * IA_PQ_WPB + (threadIdx.x >> 6));  // wave-uniform
   if (m >= sd.J * sd.M) return;
@@ -1895,7 +1922,7 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd
   const JobPtrs jp = jobs.get(px.job);
   const double *q = ma.q64 + (int64_t)m * Geo<CH>::D;
   unsigned stat = 0;
-  const Winner wn = certified_winner(ma, m, [&](int64_t row) { return exact_dist_level<CH>(ma.db64, row, q); }, &stat);
+  const Winner wn = certified_winner<RPL>(ma, m, [&](int64_t row) { return exact_dist_level<CH>(ma.db64, row, q); }, &stat);
   if (lane < xa.W) {  // lane p publishes to rank p
     XSlot *sl = xa.peer[lane] + ia_xslot(xa.seq, xa.W, xa.rank, m);
     const unsigned row = wn.idx == INT64_MAX ? 0xffffffffu : (unsigned)wn.idx;
@@ -1908,6 +1935,8 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd
     if (lane == 0 && jp.pstat) jp.pstat[px.qi] = stat;
     return;
   } else {
+    // the coherence pick does not depend on the NN winner: it runs while the peers' winners travel
+    const CohPick ck = coherence_pick<CH>(g, ma.db64, px.r, px.c, q, jp.s, jp.im);
     double bd = DBL_MAX;
     int64_t bi = INT64_MAX;
     bool late = false;
@@ -1939,7 +1968,7 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd
       bi = 0;
       if (lane == 0) atomicOr(xa.err, 2u);
     }
-    finish_pixel<CH>(g, A, ma.db64, px.r, px.c, bi, q, jp.s, jp.im, jp.Bp, jp.weights, jp.kf, jp.pstat, stat);
+    finish_pick<CH>(g, A, ma.db64, px.r, px.c, bi, ck, q, jp.s, jp.im, jp.Bp, jp.weights, jp.kf, jp.pstat, stat);
   }
 }
 
@@ -2279,10 +2308,16 @@ template <int CH>
 static void launch_xchg_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const XchgArgs &xa,
                           const JobSet &jobs, bool fin, hipStream_t st) {
   const dim3 grid(cdiv(sd.J * sd.M, IA_PQ_WPB));
-  if (fin)
-    hipLaunchKernelGGL((k_merge_xchg<CH, true, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
+  // 4 records per lane when the shard's scan ran <= 256 workgroups (every split-f16 scan)
+  const bool r4 = ma.nwg <= 4 * IA_WAVE;
+  if (fin && r4)
+    hipLaunchKernelGGL((k_merge_xchg<CH, true, JobArg1, 4>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
+  else if (fin)
+    hipLaunchKernelGGL((k_merge_xchg<CH, true, JobArg1, 8>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
+  else if (r4)
+    hipLaunchKernelGGL((k_merge_xchg<CH, false, JobArg1, 4>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
   else
-    hipLaunchKernelGGL((k_merge_xchg<CH, false, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
+    hipLaunchKernelGGL((k_merge_xchg<CH, false, JobArg1, 8>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
 }
 void ia_launch_merge_xchg(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const XchgArgs &xa,
                           const JobSet &jobs, bool fin, hipStream_t st) {

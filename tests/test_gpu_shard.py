@@ -17,7 +17,7 @@ from golden_util import BIG_CASES, load_e2e
 pytestmark = pytest.mark.gpu
 
 
-def _run(ctx, z, W, prune_all, exchange=0):
+def _run(ctx, z, W, prune_all, exchange=0, shard_unpruned=1):
     from ia_amd import _native
     L, k = z['L'], float(z['k'])
     Bp = [x.copy() for x in z['Bp_init']]
@@ -25,6 +25,7 @@ def _run(ctx, z, W, prune_all, exchange=0):
     out = {}
     ctx.set_option('shard_emulate', W)
     ctx.set_option('exchange', exchange)
+    ctx.set_option('shard_unpruned', shard_unpruned)
     if prune_all:
         ctx.set_option('prune_min_rows', 1)
     try:
@@ -36,6 +37,7 @@ def _run(ctx, z, W, prune_all, exchange=0):
     finally:
         ctx.set_option('shard_emulate', 1)
         ctx.set_option('exchange', 0)
+        ctx.set_option('shard_unpruned', 0)
         ctx.set_option('prune_min_rows', 524288)
     return out, Bp, st
 
@@ -91,3 +93,16 @@ def test_exchange_option_bounds(ctx):
     finally:
         ctx.set_option('shard_emulate', 1)
         ctx.set_option('exchange', 0)
+
+
+def test_unpruned_levels_replicate_by_default(ctx):
+    """Option shard_unpruned (default 0): only levels that run the pruned scan are sharded (the
+    unpruned scan of a small DB gains nothing from 1/W of the tiles).  g64 scans
+    unpruned: one distance launch per step unless shard_unpruned = 1 (then W on its large levels);
+    with every level pruned (prune_min_rows = 1) the large levels shard by default."""
+    z = load_e2e('g64')
+    _, _, st0 = _run(ctx, z, 2, False, 1, shard_unpruned=0)
+    _, _, st1 = _run(ctx, z, 2, False, 1, shard_unpruned=1)
+    _, _, st2 = _run(ctx, z, 2, True, 1, shard_unpruned=0)
+    assert st0.dist_launches <= st0.steps          # one scan per (non-empty) step
+    assert st1.dist_launches > st0.dist_launches and st2.dist_launches > st0.dist_launches
