@@ -11,10 +11,14 @@ the start of each step).  `value` = B' pixels of all ranks / wall time of K time
   torchrun --nproc-per-node N bench.py --gpus N ...         # one process per GPU
 
 Multi-GPU (N > 1): --mode shard (the default for cfg2/cfg3/cfg4: BASELINE config 3 as named)
-splits each large level's A database across the ranks, one job, one winner exchange per
-wavefront step ("strong"; --exchange peer = one-shot xGMI peer writes fused into the merge,
-rccl = ncclAllGather + finish); the replicas aggregate (one independent job per GPU, no
-collective) rides along as value_replicas.  --mode replicas makes that the value ("weak").
+splits each pruned level's A database across the N ranks and steps N jobs sharing that A
+(synth.make_jobs: job 0 is the cfg job, the others other B images) through it together: every
+rank scans its 1/N of the DB for the queries of all N jobs, one winner exchange per wavefront
+step (--exchange peer = one-shot xGMI peer writes fused into the merge, rccl = ncclAllGather +
+finish), every rank holding every job's B-side replica.  Per-GPU scan work stays one job's
+("weak"); --shard-jobs 1 gives the one-job latency form ("strong").  The replicas aggregate (one
+independent job per GPU, no collective) rides along as value_replicas; --mode replicas makes that
+the value.
 cfg5 splits its 64-job sweep job j -> rank j mod N (no collective).
 
 Besides the contract fields the JSON line carries:
@@ -51,11 +55,12 @@ def log(*a):
 class DeviceJob(object):
     """The job's pyramids as torch device tensors + per-level output buffers."""
 
-    def __init__(self, job, torch, dev):
+    def __init__(self, job, torch, dev, a_from=None):
         t = lambda x: torch.from_numpy(np.ascontiguousarray(x, dtype=np.float64)).to(dev)
         self.job = job
-        self.A = [t(x) for x in job.A_pyr]
-        self.Ap = [t(np.stack([p[l] for p in job.Ap_pyr_list])) for l in range(job.L)]
+        # jobs of one batch share the A side: the same device arrays (ia_synthesize_levels checks it)
+        self.A = a_from.A if a_from is not None else [t(x) for x in job.A_pyr]
+        self.Ap = a_from.Ap if a_from is not None else [t(np.stack([p[l] for p in job.Ap_pyr_list])) for l in range(job.L)]
         self.B = [t(x) for x in job.B_pyr[:job.L]]
         self.Bp0 = [t(x) for x in job.Bp_init[:job.L]]
         self.Bp = [x.clone() for x in self.Bp0]
@@ -75,6 +80,33 @@ class DeviceJob(object):
                         s_out=self.S[l].data_ptr(), im_out=self.IM[l].data_ptr())
             ctx.synthesize_level_device(self.ch, len(self.job.Ap_pyr_list), self.A[l].shape[:2], self.B[l].shape[:2],
                                         ptrs, self.job.kappa_factor(l), stats)
+
+
+class DeviceBatch(object):
+    """J jobs sharing the A side (synth.make_jobs) stepped together: one ia_synthesize_levels
+    call per level, i.e. one DB and one distance scan per wavefront step for all J jobs.  The
+    N > 1 shard mode runs J = N such jobs with the DB sharded N ways: every rank scans 1/N of the
+    DB for the queries of all N jobs (the scan work of one job per GPU) and holds every job's
+    B-side replica."""
+
+    def __init__(self, jobs, torch, dev):
+        self.dj = [DeviceJob(jobs[0], torch, dev)]
+        self.dj += [DeviceJob(j, torch, dev, a_from=self.dj[0]) for j in jobs[1:]]
+        self.ch = self.dj[0].ch
+
+    def run(self, ctx, torch, stats):
+        for d in self.dj:
+            for l in range(d.job.L):
+                d.Bp[l].copy_(d.Bp0[l])
+        torch.cuda.synchronize()
+        d0 = self.dj[0]
+        for l in range(1, d0.job.L):
+            ptrs = [dict(A=d0.A[l].data_ptr(), Ac=d0.A[l - 1].data_ptr(), Ap=d0.Ap[l].data_ptr(),
+                         Apc=d0.Ap[l - 1].data_ptr(), B=d.B[l].data_ptr(), Bc=d.B[l - 1].data_ptr(),
+                         Bpc=d.Bp[l - 1].data_ptr(), Bp=d.Bp[l].data_ptr(), weights=d.W.data_ptr(),
+                         s_out=d.S[l].data_ptr(), im_out=d.IM[l].data_ptr()) for d in self.dj]
+            ctx.synthesize_levels_device(self.ch, len(d0.job.Ap_pyr_list), d0.A[l].shape[:2], d0.B[l].shape[:2], ptrs,
+                                         [d.job.kappa_factor(l) for d in self.dj], stats)
 
 
 LSH_NOTE = ('n/a: the reference snapshot has no LSH path (algorithms.py:69 hard-codes the kdtree index) and '
@@ -179,6 +211,8 @@ def make_context(args, local):
     if args.k3p_variant != 20:
         cx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15, 18..21; the rest DIAG=1 builds only
     cx.set_option('prune_min_rows', args.prune_min_rows)
+    if args.k3p_blocks != 1:
+        cx.set_option('k3p_blocks', args.k3p_blocks)
     if args.prune_group != 1:
         cx.set_option('prune_group', args.prune_group)
     if args.row_source:
@@ -242,6 +276,10 @@ def main():
                     help='shard mode: winner exchange per wavefront step - peer = one-shot xGMI peer writes fused '
                          'into the merge (HIP IPC buffers, include/ia.h ia_xchg_*), rccl = ncclAllGather + a finish '
                          'kernel')
+    ap.add_argument('--shard-jobs', type=int, default=0,
+                    help='jobs stepped together over the sharded DB (0 = N in --mode shard at N > 1, else 1): J '
+                         'cfg jobs sharing A (synth.make_jobs), every rank scanning its 1/N of the DB for all of them '
+                         '(with --shard-emulate W on one GPU: the W-rank step for the cost model)')
     ap.add_argument('--no-replicas-extra', action='store_true',
                     help='N > 1 shard mode: skip the extra replicas measurement (value_replicas)')
     ap.add_argument('--cpu-procs', type=int, default=4,
@@ -261,6 +299,9 @@ def main():
                          'hi x hi accumulator (software-pipelined single chains), 20 (default) / 21 = the same on query-tile pairs '
                          '(two chains); '
                          'product builds hold 7, 11, 14, 15 and 18..21')
+    ap.add_argument('--k3p-blocks', type=int, default=1, choices=[0, 1],
+                    help='pruned scan of a step wider than 11 query tiles: 1 = one launch of (query block x DB '
+                         'chunk) workgroups, 0 = one launch per query block')
     ap.add_argument('--prune-group', type=int, default=1, choices=[1, 2, 4, 8],
                     help='pruned levels: Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)')
     ap.add_argument('--prune-min-rows', type=int, default=524288,
@@ -333,10 +374,13 @@ def main():
         log('[bench] rank %d: sweep of %d jobs (%d on this rank) built in %.1fs: %d B\' px/step'
             % (rank, len(sw.jobs), len(mine), time.time() - t0, job_pixels))
     else:
-        job = synth.make_job(**kw)
+        if args.shard_jobs <= 0:
+            args.shard_jobs = world if (args.mode == 'shard' and world > 1) else 1
+        jobs_b = synth.make_jobs(args.shard_jobs, **kw)
+        job = jobs_b[0]
         job_pixels, job_flops = job.pixels, job.flops()
-        log('[bench] rank %d: job %s built in %.1fs: L=%d, %d B\' px/step, %.3e NN flops/step'
-            % (rank, args.config, time.time() - t0, job.L, job.pixels, job.flops()))
+        log('[bench] rank %d: %d x job %s built in %.1fs: L=%d, %d B\' px/step, %.3e NN flops/step per job'
+            % (rank, args.shard_jobs, args.config, time.time() - t0, job.L, job.pixels, job.flops()))
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -364,6 +408,9 @@ def main():
         ctxs += [make_context(args, local) for _ in range(1, args.streams)]
         run = lambda st, cs=ctxs: dsw.run(cs, st, batched=not args.sequential, max_batch=args.max_batch)
         dj = dsw
+    elif args.shard_jobs > 1:
+        dj = DeviceBatch(jobs_b, torch, dev)
+        run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
     else:
         dj = DeviceJob(job, torch, dev)
         run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
@@ -406,11 +453,14 @@ def main():
         # the other multi-GPU reading: one independent job per GPU (no collective), the aggregate
         # carried as value_replicas (never `value`: BASELINE config 3 is the sharded job)
         rctx = make_context(args, local)
-        el_r, _ = timed(args.steps, lambda st: dj.run(rctx, torch, st), False)
+        dj1 = dj.dj[0] if isinstance(dj, DeviceBatch) else dj
+        el_r, _ = timed(args.steps, lambda st: dj1.run(rctx, torch, st), False)
         value_replicas = job_pixels * args.steps * world / el_r
         rctx.close()
 
-    jobs = world if (args.mode == 'replicas' and sw is None) else 1   # cfg5: the ranks split one sweep
+    # jobs whose pixels the timed steps produced: replicas one per rank; shard mode J jobs (every
+    # rank holds all J: counted once); cfg5: the ranks split one sweep
+    jobs = 1 if sw is not None else args.shard_jobs if args.shard_jobs > 1 else world if args.mode == 'replicas' else 1
     pixels = job_pixels * args.steps * jobs
     value = pixels / elapsed
     st = stats_rl.as_dict()
@@ -497,7 +547,8 @@ def main():
         roofline['tiles_rows_frac'] = st['dist_tiles_rows'] / max(st['dist_tiles'], 1.)
     out = {'metric': METRIC, 'value': value, 'unit': "B' px/s", 'n_gpus': world, 'steps': args.steps,
            'warmup': args.warmup, 'ms_per_step': elapsed * 1e3 / args.steps, 'higher_is_better': True,
-           'scaling': 'strong' if (args.mode == 'shard' or sw is not None) else 'weak', 'vs_baseline': None,
+           'scaling': 'strong' if (sw is not None or (args.mode == 'shard' and jobs < max(world, args.shard_emulate)))
+           else 'weak', 'vs_baseline': None,
            'dtype': 'f16x3' if f16 else 'f32',
            'data': 'synthetic', 'config': {'workload': '%s: %s' % (args.config, desc),
                                            'a_shape': list(job.A_pyr[-1].shape), 'b_shape': list(job.B_pyr[-1].shape),
@@ -507,8 +558,11 @@ def main():
                                            'shard_emulate': args.shard_emulate, 'row_source': args.row_source,
                                            'exchange': args.exchange if (args.mode == 'shard' and world > 1) else None,
                                            'parallelism': (('jobs%d' % world) if sw is not None else
-                                                           ('replicas%d' if args.mode == 'replicas' else 'dbshard%d')
-                                                           % world),
+                                                           ('replicas%d' % world) if args.mode == 'replicas' and
+                                                           args.shard_jobs <= 1 else
+                                                           'dbshard%d_jobs%d' % (max(world, args.shard_emulate),
+                                                                                 args.shard_jobs)),
+                                           'jobs_per_step': jobs,
                                            'nn': 'exact: %s MFMA candidates + certified fp64 rerank'
                                                  % ('split-f16 (hi/lo x3)' if f16 else 'fp32'),
                                            'precision': ('f16x3 = every operand split into f16 hi + lo, 3 MFMA '

@@ -106,6 +106,8 @@ struct ia_ctx {
   int matcher = IA_MATCH_F16X3;  // option "matcher"
   int k3p_variant = 20;          // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
+  int k3p_blocks = 1;            // option "k3p_blocks": 1 = a wide step's presorted pruned scan is one launch over
+                                 // all its query blocks (2-D grid); 0 = one launch per block
   // per-step K3 timing (optional)
   int time_dist = 0;
   std::vector<hipEvent_t> evs, evg, evm;  // sampled steps: K3, K2 and K4 brackets
@@ -405,6 +407,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     c->shard_unpruned = value;
     return IA_OK;
   }
+  if (!std::strcmp(name, "k3p_blocks")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: k3p_blocks must be 0 or 1");
+    c->k3p_blocks = value;
+    return IA_OK;
+  }
   if (!std::strcmp(name, "exchange")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: exchange must be 0 (RCCL) or 1 (peer write)");
     c->exchange = value;
@@ -650,14 +657,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                         shard_level(g.n_tiles, c->shard_emulate);
   const int Wsh = sharded ? c->world : emulated ? c->shard_emulate : 1;  // shards of this level
   const bool multi = Wsh > 1;
-  if (multi && J > 1) return fail(IA_EINVAL, "ia_synthesize_levels: sharded levels take one job per call");
   const bool xchg = multi && c->exchange == 1;  // peer-write winner exchange (k_merge_xchg)
   if (xchg) {
     if (sharded && !c->xpeer[0]) return fail(IA_EINVAL, "ia_synthesize_level: exchange = 1 needs ia_xchg_open");
     if (Wsh > IA_XCHG_MAXW) return fail(IA_EINVAL, "ia_synthesize_level: the peer-write exchange takes <= 16 shards");
     if (emulated && (rc = xchg_alloc(c, Wsh))) return rc;
-    if ((int64_t)std::min(g.bh, (g.bw + 2) / 3) > IA_XCHG_MAXQ)
-      return fail(IA_EINVAL, "ia_synthesize_level: wavefront steps wider than the exchange slots");
+    if ((int64_t)std::min(g.bh, (g.bw + 2) / 3) * J > IA_XCHG_MAXQ)
+      return fail(IA_EINVAL, "ia_synthesize_level: wavefront steps (all jobs) wider than the exchange slots");
     HIP_TRY(hipMemsetAsync(c->xerr.p, 0, 4, c->st));
   }
   for (int j = 0; j < J; j++)
@@ -954,8 +960,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     // sort of v6/v7 (512) or variant 11 is selected
     // (variants 11, 12: presorted; 7, 13: in-kernel sort up to 512 queries, presorted v11 / v12 above)
     const int kv = rot ? c->k3p_variant : (c->k3p_variant == 16 ? 14 : c->k3p_variant == 17 ? 15 : c->k3p_variant);
+    // steps wider than one launch's query tiles take the presorted form too when their blocks
+    // run as one launch (k3p_blocks): one K2s launch instead of a second scan launch
+    const bool wide = sd.Mpad > 512 || (c->k3p_blocks && sd.Mpad > qtmax * IA_TILE && !rot);
     const int k3v = (kv == 11 || kv == 12 || kv == 15 || kv == 17 || kv == 19 || kv == 21) ? kv
-                    : (prune && sd.Mpad > 512
+                    : (prune && wide
                            ? (kv == 13 ? 12 : kv == 14 ? 15 : kv == 18 ? 19 : kv == 20 ? 21 : kv == 16 ? 17 : 11)
                            : kv);
     const bool presorted = k3v == 11 || k3v == 12 || k3v == 15 || k3v == 17 || k3v == 19 || k3v == 21;
@@ -968,9 +977,34 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       if (timed) hipEventRecord(c->evs[2 * n_rec], c->st);
       for (size_t i = 0; i < shards.size(); i++) {
         const Shard &x = shards[i];
-        const MergeArgs &m = mas[i];
+        MergeArgs &m = mas[i];
         const int n = x.t1 - x.t0;
         const char *dbp = (const char *)c->db.p + (size_t)(x.t0 - g.tile0) * tile_bytes;
+        m.nwg = x.nwg;
+        if (prune && presorted && nqb > 1 && c->k3p_blocks) {
+          // one launch for all query blocks (option "k3p_blocks"): nqb blocks x nch DB chunks of
+          // the shard, nch a multiple of 8 (the blocks of a chunk on one XCD) when that loses
+          // little; records per query = nch, the merge's chunk count for this step
+          int nch = std::max(1, std::min(n, IA_NWG_H / nqb));
+          if (nch >= 64) nch &= ~7;
+          if ((n + nch - 1) / nch <= IA_K3P_MAXK_LDS) {
+            const int qtb = (qtt + nqb - 1) / nqb;
+            const float *tn = c->tnorm.as<float>() + x.t0;
+            ia_launch_k3p(qtb, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, 0, Mt, sd.Mpad, nch,
+                          (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
+                          c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t, c->qs_order.as<int>(),
+                          0, sd.r0, nullptr, c->qs_tbox.as<float4>(), tn, c->st, nqb, qtt);
+            m.nwg = nch;
+            pairs_full += (double)n * qtt;
+            tiles_full += (double)n * nqb;
+            dist_launches++;
+            if (timed) {
+              launches_timed++;
+              bytes_timed_fixed += (double)n * nqb * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) + (double)Mt * nch * 20;
+            }
+            continue;
+          }
+        }
         int qt0 = 0;
         for (int b = 0; b < nqb; b++) {
           const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
@@ -1032,11 +1066,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       // certified per-shard winners, then the global winner (smallest exact distance, lowest row)
       // and coherence / kappa / writeback, identical on every rank
       for (size_t i = 0; i < shards.size(); i++)
-        ia_launch_merge(g, sd, Aim, mas[i], (sharded ? c->win.as<Winner>() : c->allwin.as<Winner>() + i * sd.M), djobs,
+        ia_launch_merge(g, sd, Aim, mas[i], (sharded ? c->win.as<Winner>() : c->allwin.as<Winner>() + i * Mt), djobs,
                         false, c->st);
       if (sharded)
-        NCCL_TRY(ncclAllGather(c->win.p, c->allwin.p, (size_t)sd.M * sizeof(Winner), ncclUint8, c->comm, c->st));
-      ia_launch_finish(g, sd, Aim, c->db64.as<double>(), c->q64.as<double>(), c->allwin.as<Winner>(), Wsh, sd.M, djobs,
+        NCCL_TRY(ncclAllGather(c->win.p, c->allwin.p, (size_t)Mt * sizeof(Winner), ncclUint8, c->comm, c->st));
+      ia_launch_finish(g, sd, Aim, c->db64.as<double>(), c->q64.as<double>(), c->allwin.as<Winner>(), Wsh, Mt, djobs,
                        c->st);
     }
     if (timed_gm) hipEventRecord(c->evm[2 * n_gm++ + 1], c->st);

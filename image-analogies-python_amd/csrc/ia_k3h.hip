@@ -564,7 +564,8 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
           const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
           float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
           unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
-           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox, const float *__restrict__ tnorm) {
+           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox, const float *__restrict__ tnorm,
+           int /*nqb: one query block*/, int /*qt_end*/) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   static_assert(QT <= 32, "need masks are 32-bit");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
@@ -925,7 +926,8 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
            float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
            unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
-           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox, const float *__restrict__ tnorm) {
+           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox, const float *__restrict__ tnorm,
+           int nqb, int qt_end) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   constexpr int NE = PRE ? 1 : (IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE + WGT - 1) / WGT;  // unsorted fragments per thread
   static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
@@ -942,7 +944,25 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   unsigned *skey = reinterpret_cast<unsigned *>(tU + ((QT + 3) & ~3));  // [Mpad]   (PRE: [NQ] slice order)
   int *order = reinterpret_cast<int *>(skey + (PRE ? NQ : Mpad));       // [Mpad] sorted -> query
   int *rankof = order + (PRE ? 0 : Mpad);                               // [Mpad] query -> sorted
-  const int wg = blockIdx.x;
+  // PRE launches may cover several query blocks (nqb > 1): a grid of nqb x nwg workgroups, block
+  // b = the presorted query tiles [qt0 + b QT, min(qt0 + (b + 1) QT, qt_end)) against the DB
+  // chunk wg (tiles wg + nwg k), so one launch streams the DB once per block instead of one
+  // launch per block paying the setup and tail again.  When nwg is a multiple of 8 the blocks of
+  // one chunk get workgroup ids equal mod 8, i.e. the same XCD (round-robin dispatch): they read
+  // the same tiles at about the same time through one L2.
+  int wg = blockIdx.x, qblk = 0;
+  if (PRE && nqb > 1) {
+    if ((nwg & 7) == 0) {
+      const int grp = wg / (8 * nqb), r = wg - grp * 8 * nqb;
+      qblk = r >> 3;
+      wg = grp * 8 + (r & 7);
+    } else {
+      qblk = wg / nwg;
+      wg -= qblk * nwg;
+    }
+    qt0 += qblk * QT;
+  }
+  const int qtb = PRE ? min(QT, qt_end - qt0) : QT;  // query tiles of this block (PRE: the last may hold fewer)
   const int K = (NT - wg + nwg - 1) / nwg;  // tiles wg + nwg*k, k < K (host: nwg <= NT, K <= IA_K3P_MAXK_LDS)
   // rev: this step walks the workgroup's tiles in reverse (alternate steps: the tiles read last
   // by one step are read first by the next, while they are still in the memory-side cache)
@@ -969,10 +989,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   if constexpr (PRE) {
     // this launch's slice of the presorted queries, straight into LDS
     const h16x8 *qs = qf + (int64_t)qt0 * NP * IA_WAVE;
-    for (int e = tid; e < QT * NP * IA_WAVE; e += WGT) ldsh[e] = qs[e];
+    for (int e = tid; e < QT * NP * IA_WAVE; e += WGT) ldsh[e] = e < qtb * NP * IA_WAVE ? qs[e] : h16x8{};
     for (int x = tid; x < NQ; x += WGT) {
       const int sl = s0 + x;
-      const bool ok = sl < Mpad;
+      const bool ok = sl < Mpad && x < qtb * IA_TILE;  // slots past the block: padding (never contracted)
       qlo[x] = ok ? qinfo[3 * sl] : make_float4(0.f, 0.f, 0.f, 0.f);
       qhi[x] = ok ? qinfo[3 * sl + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 u = ok ? qinfo[3 * sl + 2] : make_float4(-INFINITY, 0.f, -INFINITY, 0.f);
@@ -984,9 +1004,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       skey[x] = ok ? ord_in[sl] : 0x7fffffff;  // slot -> query of this slice
     }
     if (tid < QT) {
-      tlo[tid] = tbox[3 * (qt0 + tid)];
-      thi[tid] = tbox[3 * (qt0 + tid) + 1];
-      tU[tid] = tbox[3 * (qt0 + tid) + 2].x;
+      const bool ok = tid < qtb;
+      tlo[tid] = ok ? tbox[3 * (qt0 + tid)] : make_float4(0.f, 0.f, 0.f, 0.f);
+      thi[tid] = ok ? tbox[3 * (qt0 + tid) + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+      tU[tid] = ok ? tbox[3 * (qt0 + tid) + 2].x : -INFINITY;
     }
     for (int x = tid; x < K; x += WGT) {  // K may exceed WGT (INTER variants: up to IA_K3P_MAXK_LDS)
       const int t = tk(x);
@@ -1566,8 +1587,8 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       st += wtiles[w];
       sf += wfull[w];
     }
-    pairs[wg] += sp + (HHF || HF ? sf << 32 : 0ull);
-    tiles[wg] += st + (HF ? (unsigned long long)nitems_wg << 32 : 0ull);
+    pairs[blockIdx.x] += sp + (HHF || HF ? sf << 32 : 0ull);
+    tiles[blockIdx.x] += st + (HF ? (unsigned long long)nitems_wg << 32 : 0ull);
   }
 #if IA_PROBE & 16
   K3P_T(ph[5]);

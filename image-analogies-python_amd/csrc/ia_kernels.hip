@@ -2304,20 +2304,28 @@ void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, cons
   else launch_finish_t<3>(g, sd, A, db64, q64, allwin, world, Mstride, jobs, st);
 }
 
+template <int CH, bool FIN, int RPL, class JS>
+static void launch_xchg_j(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const XchgArgs &xa,
+                          const JS &js, hipStream_t st) {
+  hipLaunchKernelGGL((k_merge_xchg<CH, FIN, JS, RPL>), dim3(cdiv(sd.J * sd.M, IA_PQ_WPB)), dim3(IA_PQ_WG), 0, st, g, sd, A, ma,
+                     xa, js);
+}
 template <int CH>
 static void launch_xchg_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const XchgArgs &xa,
                           const JobSet &jobs, bool fin, hipStream_t st) {
-  const dim3 grid(cdiv(sd.J * sd.M, IA_PQ_WPB));
   // 4 records per lane when the shard's scan ran <= 256 workgroups (every split-f16 scan)
   const bool r4 = ma.nwg <= 4 * IA_WAVE;
-  if (fin && r4)
-    hipLaunchKernelGGL((k_merge_xchg<CH, true, JobArg1, 4>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
-  else if (fin)
-    hipLaunchKernelGGL((k_merge_xchg<CH, true, JobArg1, 8>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
-  else if (r4)
-    hipLaunchKernelGGL((k_merge_xchg<CH, false, JobArg1, 4>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
-  else
-    hipLaunchKernelGGL((k_merge_xchg<CH, false, JobArg1, 8>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, xa, JobArg1{jobs.j0});
+  if (jobs.J == 1) {
+    if (fin && r4) launch_xchg_j<CH, true, 4>(g, sd, A, ma, xa, JobArg1{jobs.j0}, st);
+    else if (fin) launch_xchg_j<CH, true, 8>(g, sd, A, ma, xa, JobArg1{jobs.j0}, st);
+    else if (r4) launch_xchg_j<CH, false, 4>(g, sd, A, ma, xa, JobArg1{jobs.j0}, st);
+    else launch_xchg_j<CH, false, 8>(g, sd, A, ma, xa, JobArg1{jobs.j0}, st);
+  } else {  // several jobs per sharded level: every rank holds every job's replica
+    if (fin && r4) launch_xchg_j<CH, true, 4>(g, sd, A, ma, xa, JobArgN{jobs.rest}, st);
+    else if (fin) launch_xchg_j<CH, true, 8>(g, sd, A, ma, xa, JobArgN{jobs.rest}, st);
+    else if (r4) launch_xchg_j<CH, false, 4>(g, sd, A, ma, xa, JobArgN{jobs.rest}, st);
+    else launch_xchg_j<CH, false, 8>(g, sd, A, ma, xa, JobArgN{jobs.rest}, st);
+  }
 }
 void ia_launch_merge_xchg(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const XchgArgs &xa,
                           const JobSet &jobs, bool fin, hipStream_t st) {
@@ -2527,7 +2535,7 @@ size_t ia_k3p_lds(int qt, int Mpad) {
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
-                   const float4 *tbox, const float *tnorm, hipStream_t st) {
+                   const float4 *tbox, const float *tnorm, hipStream_t st, int nqb, int qt_end) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
@@ -2555,7 +2563,10 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   if (variant == 16 || variant == 17) lds += (size_t)kmax * 4;  // HF: pass masks + passing-tile list
   const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
   lds = lds > red ? lds : red;
+  // nqb > 1 (presorted variants only): one launch of nqb query blocks x nwg DB chunks
+  if (!pre) nqb = 1;
+  if (nqb == 1) qt_end = qt0 + qt;
   allow_full_lds((const void *)fn);
-  hipLaunchKernelGGL(fn, dim3(nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row, NT,
-                     qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm);
+  hipLaunchKernelGGL(fn, dim3(nqb * nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row,
+                     NT, qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm, nqb, qt_end);
 }

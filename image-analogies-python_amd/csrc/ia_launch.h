@@ -66,12 +66,12 @@ size_t ia_k3p_lds(int qt, int Mpad);
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
-                   const float4 *tbox, const float *tnorm, hipStream_t st);
+                   const float4 *tbox, const float *tnorm, hipStream_t st, int nqb = 1, int qt_end = 0);
 // GPU preprocessing (ia_pyramid.hip)
 void ia_launch_pyramid_reduce(const double *in, double *out, double *tmp, double *sm, double *mm, int h, int w, int ch,
                               const double *w7, hipStream_t st);
 void ia_launch_color3(const double *in, double *out, int64_t npx, const double *M, hipStream_t st);
 // sharded level, peer-write winner exchange (option "exchange" = 1): shard winner -> every rank's
-// buffer; fin: wait for the W winners of each query and finish the pixel (one job per call)
+// buffer; fin: wait for the W winners of each query and finish the pixel
 void ia_launch_merge_xchg(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const XchgArgs &xa,
                           const JobSet &jobs, bool fin, hipStream_t st);

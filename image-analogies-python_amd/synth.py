@@ -80,6 +80,23 @@ def make_job(size=1024, b_size=None, n_levels=None, k=0.5, seed_a=1, seed_b=2, s
     return Job(A_pyr, [Ap_pyr], B_pyr, Bp, k, weights)
 
 
+def make_jobs(n, **kw):
+    """n jobs of make_job(**kw) that share the A side (the same A / A' pyramid arrays: one
+    feature DB per level for all of them, ia_synthesize_levels) with different B images and B'
+    inits: job 0 is make_job(**kw) itself, job j > 0 draws B with seed_b + 100 j and B' with
+    seed_bp + 100 j (e.g. frames of one video through the same filter)."""
+    j0 = make_job(**kw)
+    out = [j0]
+    for j in range(1, n):
+        bh, bw = j0.B_pyr[-1].shape[:2]
+        B = smooth(bh, bw, 2, kw.get('seed_b', 2) + 100 * j)
+        B_pyr = compute_gaussian_pyramid(B, _config.n_sm, kw.get('n_levels'))
+        B_pyr = B_pyr[len(B_pyr) - j0.L:] if kw.get('level_align', 'coarse') == 'fine' else B_pyr[:j0.L]
+        Bp = initialize_Bp(B_pyr, init_rand=True, seed=kw.get('seed_bp', 3) + 100 * j)
+        out.append(Job(j0.A_pyr, j0.Ap_pyr_list, B_pyr, Bp, j0.k, j0.weights))
+    return out
+
+
 CONFIGS = {
     # name: (kwargs, description) — BASELINE.json configs
     'cfg1': (dict(size=(117, 180)), "shore-crop stand-in 117x180 (CPU reference path config)"),

@@ -140,13 +140,15 @@ int ia_version(void);
  * "prune_min_rows" DB rows (default 2^19): (DB tile, query tile) pairs a
  * projection bound proves farther than the query's best coherence candidate are skipped.
  * "k3p_variant" / "k3_variant": kernel versions of DESIGN.md §4b; the product build accepts
- * k3p_variant 14 (default: the pruned scan sorts a step's queries itself up to 512 of them, a
- * step wider than that is sorted once by k_query_sort and runs 15; every box-needed block runs
- * the hi x hi product first and the full product + top-2 only when a value can lie within the
- * query's bound), 15 (always presorted), 7 / 11 (14 / 15 without that block filter) and
- * k3_variant 1; DIAG=1 builds every version, including 16 / 17 (rotated DB: rows on the level's
- * 55 principal axes, a 15-axis head filter before the full rows; unsharded
- * levels, else 14 / 15).
+ * k3p_variant 20 (default: the pruned scan sorts a step's queries itself up to 512 of them, a
+ * step wider than that is sorted once by k_query_sort and runs 21; every box-needed block runs
+ * the hi x hi product first and adds the correction products + top-2 only when a value can lie
+ * within the query's bound), 21 (always presorted), 14 / 15 (filter, then full chains), 18 / 19
+ * (fused corrections, single chains), 7 / 11 (no block filter) and k3_variant 1; DIAG=1 builds
+ * every version, including 16 / 17 (rotated DB: rows on the level's 55 principal axes, a 15-axis
+ * head filter before the full rows; unsharded levels, else 14 / 15).
+ * "k3p_blocks" = 1 (default) / 0: a presorted pruned scan wider than one launch's 11 query tiles
+ * runs as ONE launch of (query block x DB chunk) workgroups instead of one launch per block.
  * "prune_group" = G in {1 (default), 2, 4, 8}: pruned levels store each group of G Morton tiles
  * interleaved (sort neighbours in different tiles and scan chunks: fewer certification rescans,
  * looser tile boxes).
@@ -155,6 +157,8 @@ int ia_version(void);
  * "shard_emulate" = W (1 = off): on a single-rank context, every level with >= 64 W DB tiles
  * runs as a W-way DB shard on this device (per-shard scans and certified winners, then the
  * multi-rank finish; no RCCL): the sharded code path, testable on one GPU.
+ * "shard_unpruned" = 0 (default) / 1: shard only the levels that run the pruned scan / every
+ * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge).
  * Identical results for every setting. */
 #define IA_MATCH_F32 0
 #define IA_MATCH_F16X3 1

@@ -158,14 +158,16 @@ def test_device_sweep_two_streams_equals_one(ctx):
     assert st2.pixels == st1.pixels and st2.coherence_wins == st1.coherence_wins and st2.bound_violations == 0
 
 
-@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_v11', 'pruned_v18', 'pruned_v20'])
+@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_seq', 'pruned_v11', 'pruned_v18', 'pruned_v20'])
 def test_batched_g256_wide_steps_match_reference(ctx, mode):
     """8 jobs on the golden g256 run's A side: job 0 is the reference's own
     run, jobs 1..7 other kappas and B' seeds.  On the 256^2 level a step holds 8 x 86 = 688
     queries = 22 query tiles, above one launch's 11 (ia_k3h_qtmax) and the in-kernel sort's 512:
       unpruned: the split-f16 scan in two query blocks per step (nqb = 2);
-      pruned: prune_min_rows = 1, the presorted wide-step path K2s + v15 in two launches;
-      pruned_v11: the same without the hi x hi block filter.
+      pruned: prune_min_rows = 1, the presorted wide-step path K2s + v21 as ONE launch of
+        2 query blocks x 128 DB chunks (k3p_blocks = 1, the default);
+      pruned_seq: the same as one launch per query block (k3p_blocks = 0);
+      pruned_v11: without the hi x hi block filter.
     Job 0 must reproduce the reference's s, im and B' on every level; every job must equal its
     own separate run (86-query steps: a single launch, the in-kernel sort)."""
     z = load_e2e('g256')
@@ -173,6 +175,8 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
         ctx.set_option('prune_min_rows', 1)
     if mode in ('pruned_v11', 'pruned_v18', 'pruned_v20'):
         ctx.set_option('k3p_variant', int(mode[-2:]))
+    if mode == 'pruned_seq':
+        ctx.set_option('k3p_blocks', 0)
     try:
         jb = _jobs_g32(z, kappas=(0.5, 5.0, 25.0, 1.0, 2.0, 10.0, 15.0, 20.0))
         js = [(k, [x.copy() for x in Bp]) for k, Bp in jb]
@@ -181,6 +185,7 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
     finally:
         ctx.set_option('prune_min_rows', 524288)
         ctx.set_option('k3p_variant', 20)
+        ctx.set_option('k3p_blocks', 1)
     h, w = z['B_pyr'][-1].shape
     assert 8 * min(h, (w + 2) // 3) > 512
     for level in range(1, z['L']):   # job 0 is the reference's own run
@@ -194,8 +199,12 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
     assert stb.bound_violations == 0 and stb.kappa_ambiguous == 0
     if mode != 'unpruned':
         assert stb.pruned_levels == 8 * (z['L'] - 1)
-    # the batched run needs more scan launches than steps on the 256^2 level (two query blocks)
-    assert stb.dist_launches > stb.steps
+    # two query blocks on the 256^2 level: more scan launches than steps, except in the pruned
+    # scan's one-launch form (one launch per step, twice the box-needed tile visits)
+    if mode in ('unpruned', 'pruned_seq'):
+        assert stb.dist_launches > stb.steps
+    else:
+        assert stb.dist_launches <= stb.steps
 
 
 def test_cfg5_sweep_full_size(ctx):

@@ -83,6 +83,7 @@ def test_exchange_option_bounds(ctx):
         ctx.set_option('exchange', 2)
     ctx.set_option('exchange', 1)
     ctx.set_option('shard_emulate', 32)   # more shards than exchange slots: refused per level
+    ctx.set_option('prune_min_rows', 1)   # a pruned level shards (shard_unpruned = 0)
     try:
         z = load_e2e('g256')   # 2048 tiles at 256^2: a 32-way emulated shard level
         with pytest.raises(_native.IAError):
@@ -93,6 +94,7 @@ def test_exchange_option_bounds(ctx):
     finally:
         ctx.set_option('shard_emulate', 1)
         ctx.set_option('exchange', 0)
+        ctx.set_option('prune_min_rows', 524288)
 
 
 def test_unpruned_levels_replicate_by_default(ctx):
@@ -106,3 +108,91 @@ def test_unpruned_levels_replicate_by_default(ctx):
     _, _, st2 = _run(ctx, z, 2, True, 1, shard_unpruned=0)
     assert st0.dist_launches <= st0.steps          # one scan per (non-empty) step
     assert st1.dist_launches > st0.dist_launches and st2.dist_launches > st0.dist_launches
+
+
+def _run_batch(ctx, z, jobs, W, exchange, prune_all=True):
+    """jobs = [(kappa, Bp pyramid)] sharing z's A side: one ia_synthesize_levels call per level
+    (every job's replica on every emulated rank, one scan per shard for all jobs' queries)."""
+    from ia_amd import _native
+    L = z['L']
+    S, IM = [dict() for _ in jobs], [dict() for _ in jobs]
+    st = _native.Stats()
+    ctx.set_option('shard_emulate', W)
+    ctx.set_option('exchange', exchange)
+    if prune_all:
+        ctx.set_option('prune_min_rows', 1)
+    try:
+        for level in range(1, L):
+            specs = [dict(B=z['B_pyr'][level], Bc=z['B_pyr'][level - 1], Bpc=Bp[level - 1], Bp=Bp[level],
+                          weights=z['weights'], kappa_factor=1 + 2.0 ** (level - L) * k) for k, Bp in jobs]
+            res = ctx.synthesize_levels(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
+                                        [p[level - 1] for p in z['Ap_pyr']], specs, st)
+            for j, (s, im) in enumerate(res):
+                S[j][level], IM[j][level] = s, im
+    finally:
+        ctx.set_option('shard_emulate', 1)
+        ctx.set_option('exchange', 0)
+        ctx.set_option('prune_min_rows', 524288)
+    return S, IM, st
+
+
+@pytest.mark.parametrize('exchange', [0, 1], ids=['allgather', 'peerwrite'])
+@pytest.mark.parametrize('W', [2, 4, 8])
+def test_emulated_shards_batched_jobs_match_reference(ctx, W, exchange):
+    """W jobs on the golden g256 run's A side stepped together over a W-way sharded DB (bench.py's
+    N > 1 shard mode: every rank scans its shard for all jobs' queries; on the 256^2 level 8 x 86
+    queries per step = 22 query tiles, the one-launch two-block presorted scan per shard).  Job 0
+    is the reference's own run; every job equals the unsharded batched run."""
+    from test_gpu_batch import _jobs_g32
+    z = load_e2e('g256')
+    kap = (0.5, 5.0, 25.0, 1.0, 2.0, 10.0, 15.0, 20.0)[:max(W, 2)]
+    jb = _jobs_g32(z, kappas=kap)
+    ju = [(k, [x.copy() for x in Bp]) for k, Bp in jb]
+    S, IM, st = _run_batch(ctx, z, jb, W, exchange)
+    Su, IMu, stu = _run_batch(ctx, z, ju, 1, 0)
+    for level in range(1, z['L']):
+        assert np.array_equal(S[0][level], z['s'][level]) and np.array_equal(IM[0][level], z['im'][level]), level
+        assert np.array_equal(jb[0][1][level], z['Bp_final'][level]), level
+        for j in range(len(jb)):
+            assert np.array_equal(S[j][level], Su[j][level]) and np.array_equal(IM[j][level], IMu[j][level]), (j, level)
+            assert np.array_equal(jb[j][1][level], ju[j][1][level]), (j, level)
+    assert st.bound_violations == 0 and st.kappa_ambiguous == 0 and st.pixels == stu.pixels
+    assert st.dist_launches > stu.dist_launches   # W shard scans per sharded step
+
+
+@pytest.mark.parametrize('W', [4])
+def test_emulated_shards_batched_1024(ctx, W):
+    """W cfg3 jobs (synth.make_jobs: job 0 = cfg3, others other B images) over a W-way sharded
+    1024^2 DB with the peer-write exchange == the same jobs batched unsharded, every level."""
+    from ia_amd import synth
+    jobs = synth.make_jobs(W, size=1024)
+    z = {'L': jobs[0].L, 'A_pyr': jobs[0].A_pyr, 'Ap_pyr': jobs[0].Ap_pyr_list, 'B_pyr': jobs[0].B_pyr,
+         'weights': jobs[0].weights}
+    out = []
+    for Wx, ex in ((W, 1), (1, 0)):
+        S, IM, Bps = [], [], []
+        from ia_amd import _native
+        st = _native.Stats()
+        ctx.set_option('shard_emulate', Wx)
+        ctx.set_option('exchange', ex)
+        Bp = [[x.copy() for x in j.Bp_init] for j in jobs]
+        try:
+            for level in range(1, z['L']):
+                specs = [dict(B=j.B_pyr[level], Bc=j.B_pyr[level - 1], Bpc=Bp[n][level - 1], Bp=Bp[n][level],
+                              weights=j.weights, kappa_factor=j.kappa_factor(level)) for n, j in enumerate(jobs)]
+                res = ctx.synthesize_levels(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
+                                            [p[level - 1] for p in z['Ap_pyr']], specs, st)
+                S.append([r[0] for r in res])
+                IM.append([r[1] for r in res])
+        finally:
+            ctx.set_option('shard_emulate', 1)
+            ctx.set_option('exchange', 0)
+        out.append((S, IM, Bp, st))
+    (S, IM, Bp, st), (Su, IMu, Bpu, stu) = out
+    for i in range(len(S)):
+        for n in range(W):
+            assert np.array_equal(S[i][n], Su[i][n]) and np.array_equal(IM[i][n], IMu[i][n]), (i, n)
+    for n in range(W):
+        for level in range(1, z['L']):
+            assert np.array_equal(Bp[n][level], Bpu[n][level]), (n, level)
+    assert st.pruned_levels == W and st.bound_violations == 0

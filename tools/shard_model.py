@@ -1,5 +1,7 @@
 """DESIGN.md §7 cost model of the DB-sharded path from a rocprofv3 kernel trace of
-`bench.py --shard-emulate W` (all W shards of every large level run back to back on one GPU).
+`bench.py --shard-emulate W [--shard-jobs J]` (all W shards of every large level run back to back
+on one GPU; with J jobs every scan and merge covers all J jobs' queries: bench.py's N > 1 shard
+mode at J = W, whose weak-scaling efficiency is the W = 1 single-job time / the modelled time).
 Per wavefront step of each level the trace holds: the query gather (K2), the W shard scans
 (K3h / K3p; + the query sort K2s on wide steps) and the W exchange merges (k_merge_xchg: W - 1
 publishing launches, then the finishing one) - or, on levels too small to shard, one scan and
@@ -72,8 +74,13 @@ for i, lv in enumerate(sel):
         meas += st['gather'] + st['sort'] + sum(st['scans']) + sum(st['merges'])
         nsh = len(st['merges'])
         sharded += nsh > 1
-        model += st['gather'] + st['sort'] + (max(st['scans']) if st['scans'] else 0.0) + \
-            (st['merges'][-1] if st['merges'] else 0.0) + (XLAT if nsh > 1 else 0.0)
+        # scans of one shard are consecutive launches (several query blocks of an unpruned or
+        # unsharded level run one after the other): a rank pays its shard's sum
+        sc = st['scans']
+        per = len(sc) // nsh if nsh > 1 and len(sc) % nsh == 0 else len(sc)
+        grp = [sum(sc[i:i + per]) for i in range(0, len(sc), per)] if sc else [0.0]
+        model += st['gather'] + st['sort'] + max(grp) + (st['merges'][-1] if st['merges'] else 0.0) + \
+            (XLAT if nsh > 1 else 0.0)
     meas += lv['other']
     model += lv['other']
     tot_meas += meas

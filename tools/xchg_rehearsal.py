@@ -73,6 +73,32 @@ def main():
     print('[rank %d] cfg3 1024^2, %d-way peer-write shards (pruned 1024^2 level): %s vs unsharded (%.2f s sharded, '
           'pruned levels %d, bound_violations %d)' % (rank, world, 'bit-identical' if same else 'DIFFERENT', t1 - t0,
                                                       st.pruned_levels, st.bound_violations), flush=True)
+    # bench.py's N > 1 shard mode: `world` jobs sharing A stepped together over the sharded DB
+    jobs = synth.make_jobs(world, size=1024)
+
+    def run_batch(c):
+        Bps = [[x.copy() for x in j.Bp_init] for j in jobs]
+        st = _native.Stats()
+        c.set_option('prune_min_rows', 524288)
+        res = []
+        for level in range(1, jobs[0].L):
+            specs = [dict(B=j.B_pyr[level], Bc=j.B_pyr[level - 1], Bpc=Bps[n][level - 1], Bp=Bps[n][level],
+                          weights=j.weights, kappa_factor=j.kappa_factor(level)) for n, j in enumerate(jobs)]
+            res.append(c.synthesize_levels(jobs[0].A_pyr[level], jobs[0].A_pyr[level - 1],
+                                           [p[level] for p in jobs[0].Ap_pyr_list],
+                                           [p[level - 1] for p in jobs[0].Ap_pyr_list], specs, st))
+        return res, Bps, st
+    dist.barrier()
+    t0 = time.time()
+    rb, Bpb, st = run_batch(ctx)
+    t1 = time.time()
+    ru, Bpu, _ = run_batch(plain)
+    same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for la, lb in zip(rb, ru) for a, b in zip(la, lb))
+    same &= all(np.array_equal(Bpb[n][l], Bpu[n][l]) for n in range(world) for l in range(1, jobs[0].L))
+    ok &= same
+    print('[rank %d] %d cfg3 jobs batched over %d-way peer-write shards: %s vs unsharded batched (%.2f s sharded, '
+          'bound_violations %d)' % (rank, world, world, 'bit-identical' if same else 'DIFFERENT', t1 - t0,
+                                    st.bound_violations), flush=True)
     plain.close()
     ctx.close()
     flag = torch.tensor([0 if ok else 1])
