@@ -13,12 +13,16 @@ the start of each step).  `value` = B' pixels of all ranks / wall time of K time
 Multi-GPU (N > 1): --mode shard (the default for cfg2/cfg3/cfg4: BASELINE config 3 as named)
 splits each pruned level's A database across the N ranks and steps N jobs sharing that A
 (synth.make_jobs: job 0 is the cfg job, the others other B images) through it together: every
-rank scans its 1/N of the DB for the queries of all N jobs, one winner exchange per wavefront
-step (--exchange peer = one-shot xGMI peer writes fused into the merge, rccl = ncclAllGather +
-finish), every rank holding every job's B-side replica.  Per-GPU scan work stays one job's
-("weak"); --shard-jobs 1 gives the one-job latency form ("strong").  The replicas aggregate (one
-independent job per GPU, no collective) rides along as value_replicas; --mode replicas makes that
-the value.
+rank scans its 1/N of the DB for the queries of all N jobs each wavefront step.
+  --exchange owner (default): rank r owns job r (its gather, query sort and merge); its sorted
+      queries go to every rank and every rank's scan records come back to it, both as one-shot
+      xGMI peer writes (include/ia.h exchange = 2); no per-query work is replicated;
+  --exchange peer / rccl: every rank holds every job's replica and runs every job's gather and
+      per-shard merge; the per-shard winners are exchanged by peer writes fused into the merge
+      (peer) or ncclAllGather + a finish kernel (rccl).
+Per-GPU scan work stays one job's ("weak"); --shard-jobs 1 with peer / rccl gives the one-job
+latency form ("strong").  The replicas aggregate (one independent job per GPU, no collective)
+rides along as value_replicas; --mode replicas makes that the value.
 cfg5 splits its 64-job sweep job j -> rank j mod N (no collective).
 
 Besides the contract fields the JSON line carries:
@@ -108,6 +112,8 @@ class DeviceBatch(object):
             ctx.synthesize_levels_device(self.ch, len(d0.job.Ap_pyr_list), d0.A[l].shape[:2], d0.B[l].shape[:2], ptrs,
                                          [d.job.kappa_factor(l) for d in self.dj], stats)
 
+
+EXCHANGE = {'rccl': 0, 'peer': 1, 'owner': 2}   # include/ia.h option "exchange"
 
 LSH_NOTE = ('n/a: the reference snapshot has no LSH path (algorithms.py:69 hard-codes the kdtree index) and '
             'pyflann / libflann are absent offline; the kd-tree path itself is approximate and unrunnable here, '
@@ -221,7 +227,7 @@ def make_context(args, local):
         cx.set_option('shard_unpruned', 1)
     if args.shard_emulate > 1:
         cx.set_option('shard_emulate', args.shard_emulate)
-        cx.set_option('exchange', 1 if args.exchange == 'peer' else 0)   # the emulated shards' exchange kernels
+        cx.set_option('exchange', EXCHANGE[args.exchange])   # the emulated shards' exchange kernels
     return cx
 
 
@@ -272,10 +278,11 @@ def main():
                     help='N > 1: shard (default for cfg2/cfg3/cfg4: BASELINE config 3 as named, one job whose DB '
                          'is sharded over the ranks, one winner exchange per wavefront step; the replicas aggregate '
                          'rides along as value_replicas) or replicas (one independent job per GPU)')
-    ap.add_argument('--exchange', default='peer', choices=['peer', 'rccl'],
-                    help='shard mode: winner exchange per wavefront step - peer = one-shot xGMI peer writes fused '
-                         'into the merge (HIP IPC buffers, include/ia.h ia_xchg_*), rccl = ncclAllGather + a finish '
-                         'kernel')
+    ap.add_argument('--exchange', default='owner', choices=['owner', 'peer', 'rccl'],
+                    help='shard mode: owner = rank r owns job r, sorted queries out and scan records back as one-shot '
+                         'xGMI peer writes (HIP IPC buffers, include/ia.h ia_xchg_*); peer = every rank holds every '
+                         'job, per-shard winners exchanged by peer writes fused into the merge; rccl = ncclAllGather '
+                         '+ a finish kernel')
     ap.add_argument('--shard-jobs', type=int, default=0,
                     help='jobs stepped together over the sharded DB (0 = N in --mode shard at N > 1, else 1): J '
                          'cfg jobs sharing A (synth.make_jobs), every rank scanning its 1/N of the DB for all of them '
@@ -346,6 +353,9 @@ def main():
     # GPUs, IA_BENCH_BACKEND=gloo: RCCL refuses two ranks on one device); never set by the driver
     if os.environ.get('IA_BENCH_SHARE_GPU') == '1':
         local = local % max(torch.cuda.device_count(), 1)
+        # exchanges wait on peers' kernels: ranks sharing a GPU get disjoint CU slices (libia
+        # streams), else a waiting kernel can hold the CUs the peer needs
+        os.environ['IA_CU_SPLIT'] = '%d/%d' % (rank, world)
     backend = os.environ.get('IA_BENCH_BACKEND', 'nccl')
     if world > 1:
         import torch.distributed as dist
@@ -390,7 +400,12 @@ def main():
                else cpu_baseline(job, args.cpu_seconds, args.cpu_procs))
         log('[bench] CPU baseline sampled in %.1fs: %.3g px/s' % (time.time() - t1, cpu['value']))
     ctx = make_context(args, local)
+    owner = args.mode == 'shard' and world > 1 and args.exchange == 'owner'
+    if owner and args.shard_jobs != world:
+        ap.error('--exchange owner: one job per rank (--shard-jobs N)')
     if args.mode == 'shard' and world > 1:
+        if owner:
+            ctx.set_option('exchange', 2)
         if args.exchange == 'rccl':
             uid = [_native.comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(uid, src=0)
@@ -408,6 +423,9 @@ def main():
         ctxs += [make_context(args, local) for _ in range(1, args.streams)]
         run = lambda st, cs=ctxs: dsw.run(cs, st, batched=not args.sequential, max_batch=args.max_batch)
         dj = dsw
+    elif owner:   # this rank's own job; the other ranks bring theirs
+        dj = DeviceJob(jobs_b[rank], torch, dev)
+        run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
     elif args.shard_jobs > 1:
         dj = DeviceBatch(jobs_b, torch, dev)
         run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)

@@ -7,6 +7,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -116,7 +117,9 @@ struct ia_ctx {
   // multi-GPU
   int rank = 0, world = 1;
   ncclComm_t comm = nullptr;
-  int exchange = 0;               // option "exchange": 0 = RCCL all-gather + finish, 1 = peer-write merge
+  int exchange = 0;               // option "exchange": 0 = RCCL all-gather + finish, 1 = peer-write merge,
+                                  // 2 = owner-computes (rank o owns job o; every rank scans its shard for all)
+  DevBuf xo_inv;                  // exchange = 2: the owners' query -> slot tables of the current step
   void *xbuf = nullptr;           // this process's exchange buffer (uncached, IPC-exportable)
   int xbuf_w = 0;                 // ranks the buffer was sized for
   XSlot *xpeer[IA_XCHG_MAXW] = {};  // every rank's buffer in this address space (ia_xchg_open)
@@ -300,7 +303,23 @@ int ia_init(int device, ia_ctx **out) {
   HIP_TRY(hipSetDevice(device));
   ia_ctx *c = new ia_ctx();
   c->dev = device;
-  if (hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking) != hipSuccess) {
+  // IA_CU_SPLIT=k/n (rehearsals of the multi-rank exchanges with n ranks sharing ONE GPU only):
+  // this context's stream runs on CU slice k of n, so a rank's kernel that waits for a peer's
+  // progress never holds the CUs the peer's kernels need (on separate GPUs nothing is shared)
+  int split_k = 0, split_n = 0;
+  if (const char *e = std::getenv("IA_CU_SPLIT")) {
+    if (std::sscanf(e, "%d/%d", &split_k, &split_n) != 2 || split_n < 1 || split_k < 0 || split_k >= split_n) split_n = 0;
+  }
+  hipError_t se;
+  if (split_n > 1) {
+    const int ncu = prop.multiProcessorCount;
+    std::vector<uint32_t> mask((ncu + 31) / 32, 0u);
+    for (int cu = ncu * split_k / split_n; cu < ncu * (split_k + 1) / split_n; cu++) mask[cu / 32] |= 1u << (cu % 32);
+    se = hipExtStreamCreateWithCUMask(&c->st, (uint32_t)mask.size(), mask.data());
+  } else {
+    se = hipStreamCreateWithFlags(&c->st, hipStreamNonBlocking);
+  }
+  if (se != hipSuccess) {
     delete c;
     return fail(IA_EHIP, "ia_init: hipStreamCreate failed");
   }
@@ -335,6 +354,7 @@ void ia_destroy(ia_ctx *c) {
     if (c->xmapped[p]) hipIpcCloseMemHandle(c->xpeer[p]);
   if (c->xbuf) hipFree(c->xbuf);
   c->xerr.release();
+  c->xo_inv.release();
   hipStreamDestroy(c->st);
   delete c;
 }
@@ -413,7 +433,8 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
   if (!std::strcmp(name, "exchange")) {
-    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: exchange must be 0 (RCCL) or 1 (peer write)");
+    if (value < 0 || value > 2)
+      return fail(IA_EINVAL, "ia_set_option: exchange must be 0 (RCCL), 1 (peer-write winners) or 2 (owner computes)");
     c->exchange = value;
     return IA_OK;
   }
@@ -451,7 +472,8 @@ static int xchg_alloc(ia_ctx *c, int world) {
   if (c->xbuf && c->xbuf_w >= world) return IA_OK;
   if (c->xbuf) hipFree(c->xbuf);
   c->xbuf = nullptr;
-  const size_t bytes = (size_t)2 * world * IA_XCHG_MAXQ * sizeof(XSlot);
+  // winner slots (exchange = 1) + two parities of the owner-computes area (exchange = 2)
+  const size_t bytes = ia_xslots_bytes(world) + 2 * XOLayout::PARITY;
   // uncached: peers' xGMI stores and this device's polling loads meet in memory, not in an L2
   HIP_TRY(hipExtMallocWithFlags(&c->xbuf, bytes, hipDeviceMallocUncached));
   HIP_TRY(hipMemset(c->xbuf, 0, bytes));
@@ -501,7 +523,7 @@ int ia_xchg_open(ia_ctx *c, int rank, int world, const unsigned char *handles) {
   c->comm = nullptr;
   c->rank = rank;
   c->world = world;
-  c->exchange = 1;
+  if (c->exchange == 0) c->exchange = 1;  // keep 2 (owner computes) when it was chosen before
   c->xseq = 0;
   return IA_OK;
 }
@@ -658,6 +680,19 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   const int Wsh = sharded ? c->world : emulated ? c->shard_emulate : 1;  // shards of this level
   const bool multi = Wsh > 1;
   const bool xchg = multi && c->exchange == 1;  // peer-write winner exchange (k_merge_xchg)
+  // owner-computes sharded step (exchange = 2, ia_internal.h XOLayout): a rank brings its own
+  // job (emulated: one job per shard); checked against the pruned scan below
+  const bool xo = multi && c->exchange == 2;
+  if (xo) {
+    if (sharded && !c->xpeer[0]) return fail(IA_EINVAL, "ia_synthesize_level: exchange = 2 needs ia_xchg_open");
+    if (Wsh > IA_XCHG_MAXW) return fail(IA_EINVAL, "ia_synthesize_level: the owner exchange takes <= 16 shards");
+    if (sharded && J != 1) return fail(IA_EINVAL, "ia_synthesize_level: exchange = 2 takes the rank's own job (n_jobs = 1)");
+    if (emulated && J != Wsh)
+      return fail(IA_EINVAL, "ia_synthesize_levels: emulated exchange = 2 takes one job per shard (n_jobs = shard_emulate)");
+    if (emulated && (rc = xchg_alloc(c, Wsh))) return rc;
+    if ((rc = c->xo_inv.ensure((size_t)IA_XO_MAXT * IA_TILE * 4))) return rc;
+    HIP_TRY(hipMemsetAsync(c->xerr.p, 0, 4, c->st));
+  }
   if (xchg) {
     if (sharded && !c->xpeer[0]) return fail(IA_EINVAL, "ia_synthesize_level: exchange = 1 needs ia_xchg_open");
     if (Wsh > IA_XCHG_MAXW) return fail(IA_EINVAL, "ia_synthesize_level: the peer-write exchange takes <= 16 shards");
@@ -755,9 +790,25 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   int64_t T, Mmax;
   ia_wavefront_shape(g.bh, g.bw, &T, &Mmax);
   const int64_t Mtmax = Mmax * J;  // queries of the widest step over all jobs
-  const int64_t Mpad_max = (Mtmax + IA_TILE - 1) / IA_TILE * IA_TILE;
+  // (exchange = 2 emulated: each owner's queries at its own tile-aligned offset j Mpad_j)
+  const int64_t Mpad_max = std::max((Mtmax + IA_TILE - 1) / IA_TILE * IA_TILE,
+                                    xo ? J * ((Mmax + IA_TILE - 1) / IA_TILE * IA_TILE) : 0);
   const bool prune = c->prune && use_h && g.ch == 1 && g.NA >= c->prune_min_rows && Mpad_max <= 4096 &&
                      (g.n_tiles + IA_NWG_H - 1) / IA_NWG_H <= IA_K3P_MAXK_LDS;
+  if (xo && !prune)
+    return fail(IA_EINVAL, "ia_synthesize_level: exchange = 2 shards pruned levels only (1 channel, split-f16, <= 4096 "
+                           "queries per step)");
+  // owner-computes geometry: per owner QTj query tiles in bpj blocks of QTx tiles, QTs = bpj QTx
+  // tiles per owner in the step layout (pads past QTj never contracted)
+  int xo_bpj = 1, xo_QTx = 1, xo_QTs = 1;
+  if (xo) {
+    const int QTj = (int)((Mmax + IA_TILE - 1) / IA_TILE);
+    xo_bpj = (QTj + ia_k3h_qtmax(g.KS) - 1) / ia_k3h_qtmax(g.KS);
+    xo_QTx = (QTj + xo_bpj - 1) / xo_bpj;
+    xo_QTs = xo_bpj * xo_QTx;
+    if (Wsh * xo_QTs > IA_XO_MAXT || Wsh * xo_bpj > IA_NWG_H)
+      return fail(IA_EINVAL, "ia_synthesize_level: exchange = 2: wavefront steps too wide for the exchange area");
+  }
   // Pruned levels: every rank holds the whole Morton-sorted DB, its tiles stored shard by shard
   // (ia_internal.h ia_shard_morton_tile: shard r = Morton tiles r, r + W, ...), and scans its own
   // contiguous storage range.  Unpruned levels: contiguous tile ranges (ia_shard_tiles).
@@ -940,6 +991,113 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       hipEventRecord(c->evg[2 * n_gm], c->st);
       gather_bytes_timed += gq_bytes * Mt;
     }
+    if (xo) {
+      // ---- owner-computes sharded step (exchange = 2, ia_internal.h XOLayout): every local owner
+      // (a rank: its own job; emulated: job j = owner j, each at its own tile-aligned offset)
+      // gathers its queries (K2p) and sorts them into every rank's area (K2s); this process's
+      // shard scans (K3p) run for all owners' queries and push their records to the owners; each
+      // local owner's fused merge (K4) runs over W nch records per query.  The emulated launches
+      // are exactly the ranks' launches, one after the other.
+      const unsigned seq = ++c->xseq;
+      const size_t par = (size_t)(seq & 1u) * XOLayout::PARITY;
+      auto area = [&](int p) -> char * {  // parity base of rank p's area in this address space
+        return (char *)(sharded ? (void *)c->xpeer[p] : c->xbuf) + ia_xslots_bytes(Wsh) + par;
+      };
+      char *loc = area(sharded ? c->rank : 0);
+      const int Mrec = Wsh * xo_QTs * IA_TILE;
+      const int Mpj = (sd.M + IA_TILE - 1) / IA_TILE * IA_TILE;  // one owner's padded queries
+      StepDesc s1 = sd;
+      s1.J = 1;
+      s1.Mpad = Mpj;
+      auto owner_of = [&](int jl) { return sharded ? c->rank : jl; };
+      for (int jl = 0; jl < J; jl++) {
+        const JobSet one{jp[jl], c->jobs.as<JobPtrs>() + jl, 1};
+        const size_t q0 = (size_t)jl * Mpj;
+        ia_launch_gather_p(g, s1, Bim, one, c->mu.as<double>(), c->q64.as<double>() + q0 * g.D, c->qn2.as<double>() + q0,
+                           (char *)c->qf.p + q0 * db_row_bytes, c->db64.as<double>(), c->pr_basis.as<double>(), ufac,
+                           c->qinfo.as<float4>() + 3 * q0, Aim, ma.img_rows, c->st);
+        XOSort xs{};
+        xs.inv = c->xo_inv.as<int>();
+        xs.W = sharded ? Wsh : 1;
+        for (int p = 0; p < xs.W; p++) xs.area[p] = area(p);
+        xs.q0 = 0;
+        xs.Mj = sd.M;
+        xs.tile0 = owner_of(jl) * xo_QTs;
+        xs.QTs = xo_QTs;
+        xs.seq = seq;
+        ia_launch_query_sort_xo(c->qinfo.as<float4>() + 3 * q0, (char *)c->qf.p + q0 * db_row_bytes, xs, c->st);
+      }
+      if (timed_gm) hipEventRecord(c->evg[2 * n_gm + 1], c->st);
+      const int nqb = Wsh * xo_bpj;
+      const bool timed = stride && t % stride == 0;
+      if (timed) hipEventRecord(c->evs[2 * n_rec], c->st);
+      int nch = IA_NWG_H;
+      for (size_t i = 0; i < shards.size(); i++) {
+        const Shard &x = shards[i];
+        const int n = x.t1 - x.t0;
+        nch = std::max(1, std::min(n, IA_NWG_H / nqb));
+        if (nch >= 64) nch &= ~7;
+        if ((n + nch - 1) / nch > IA_K3P_MAXK_LDS || (int64_t)Wsh * nch * Mrec > IA_XO_MAXREC)
+          return fail(IA_EINVAL, "ia_synthesize_level: exchange = 2: shard too large for the pruned scan's chunks");
+        XOScan xs{};
+        for (int p = 0; p < Wsh; p++) xs.area[p] = sharded ? area(p) : loc;
+        xs.flag = reinterpret_cast<const unsigned *>(loc + XOLayout::FLAG);
+        xs.on = 1;
+        xs.s = sharded ? c->rank : (int)i;
+        xs.bpj = xo_bpj;
+        xs.Mrec = Mrec;
+        xs.seq = seq;
+        xs.err = c->xerr.as<unsigned>();
+        xs.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
+        const char *dbp = (const char *)c->db.p + (size_t)(x.t0 - g.tile0) * tile_bytes;
+        const int kv = c->k3p_variant;
+        const int k3x = (kv == 14 || kv == 15) ? 15 : (kv == 18 || kv == 19) ? 19 : (kv == 7 || kv == 11) ? 11 : 21;
+        ia_launch_k3p(xo_QTx, dbp, loc + XOLayout::FRAG, reinterpret_cast<const float4 *>(loc + XOLayout::INFO), mas[i].boxes,
+                      mas[i].pos2row, n, 0, sd.M, Mrec, nch, nullptr, nullptr,
+                      c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
+                      c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3x, sd.t,
+                      reinterpret_cast<const int *>(loc + XOLayout::ORD), 0, sd.r0, nullptr,
+                      reinterpret_cast<const float4 *>(loc + XOLayout::TBOX), c->tnorm.as<float>() + x.t0, c->st, nqb,
+                      Wsh * xo_QTs, &xs);
+        pairs_full += (double)n * Wsh * xo_QTs;
+        tiles_full += (double)n * nqb;
+        dist_launches++;
+        if (timed) {
+          launches_timed++;
+          bytes_timed_fixed += (double)n * nqb * 32 + (double)Mrec * (16.0 * 16 * g.KS + 48) + (double)Mrec * nch * 24;
+        }
+      }
+      if (timed) hipEventRecord(c->evs[2 * n_rec++ + 1], c->st);
+      if (timed_gm) hipEventRecord(c->evm[2 * n_gm], c->st);
+      for (int jl = 0; jl < J; jl++) {
+        const JobSet one{jp[jl], c->jobs.as<JobPtrs>() + jl, 1};
+        const size_t q0 = (size_t)jl * Mpj;
+        MergeArgs mx = ma;
+        mx.q64 = c->q64.as<double>() + q0 * g.D;
+        mx.qn2 = c->qn2.as<double>() + q0;
+        mx.qinfo = c->qinfo.as<float4>() + 3 * q0;
+        mx.rec = reinterpret_cast<const float4 *>(loc + XOLayout::REC);
+        mx.xo_rts = reinterpret_cast<const unsigned long long *>(loc + XOLayout::RTS);
+        mx.nwg = Wsh * nch;
+        mx.rr = 1;
+        mx.NT = g.n_tiles;
+        mx.boxes = c->boxes.as<float4>();
+        mx.pos2row = g.pos2row;
+        mx.xo_inv = c->xo_inv.as<int>();
+        mx.xo_W = Wsh;
+        mx.xo_nch = nch;
+        mx.xo_Mrec = Mrec;
+        mx.xo_o0 = owner_of(jl);
+        mx.xo_M = sd.M;
+        mx.xo_QTs = xo_QTs;
+        mx.xo_seq = seq;
+        mx.xo_err = c->xerr.as<unsigned>();
+        mx.xo_timeout = 2000000000LL;
+        ia_launch_merge(g, s1, Aim, mx, c->win.as<Winner>(), one, true, c->st);
+      }
+      if (timed_gm) hipEventRecord(c->evm[2 * n_gm++ + 1], c->st);
+      continue;
+    }
 #ifdef IA_K3H_DIAG
     if (rot)
       ia_launch_gather_r(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
@@ -1094,10 +1252,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
 #if IA_PROBE & 16
   if (prune) ia_k3p_probe_dump();
 #endif
-  if (xchg) {
+  if (xchg || xo) {
     unsigned xe = 0;
     HIP_TRY(hipMemcpy(&xe, c->xerr.p, 4, hipMemcpyDeviceToHost));
-    if (xe) return fail(IA_ECOMM, "ia_synthesize_level: a peer's shard winner did not arrive within 20 s (peer-write exchange)");
+    if (xe)
+      return fail(IA_ECOMM, std::string("ia_synthesize_level: a peer's ") +
+                                (xe & 4 ? "sorted queries" : xe & 8 ? "scan records" : "shard winner") +
+                                " did not arrive within 20 s (peer-write exchange)");
   }
   if (stats) {
     unsigned long long ctr[5], prs[4], pfull = 0, prow[4] = {0, 0, 0, 0};

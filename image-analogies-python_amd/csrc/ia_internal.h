@@ -98,6 +98,15 @@ struct MergeArgs {
   int img_rows;                       // 1: exact rows gathered from the A-side images (1 channel)
   double eps_r = 0.;                  // rotated DB (k3p_variant 16/17): coefficient of (R + |q'|)^2
                                       // for the principal-axis rotation's deviation
+  // owner-computes sharded step (exchange = 2): records chunk-major in the exchange area (rec[w
+  // xo_Mrec + m], (T, seq) in xo_rts), record w = chunk w mod xo_nch of shard w / xo_nch (storage
+  // tiles ia_shard_off(NT, xo_W, s) + k + xo_nch i); boxes / pos2row are the whole level's
+  const unsigned long long *xo_rts = nullptr;
+  const int *xo_inv = nullptr;        // the owners' tables: query (o QTs 32 + local) -> slot
+  int xo_W = 0, xo_nch = 0, xo_Mrec = 0, xo_o0 = 0, xo_M = 0, xo_QTs = 0;  // query m: owner xo_o0 + m / xo_M
+  unsigned xo_seq = 0;
+  unsigned *xo_err = nullptr;         // bit 3: a record did not arrive in time
+  long long xo_timeout = 0;
 };
 
 // Rotated split-f16 DB of a pruned 1-channel level (k3p_variant 16 / 17): every
@@ -159,7 +168,7 @@ __host__ __device__ inline int64_t ia_shard_morton_tile_(int64_t ts, int64_t NT,
   }
   return r + (int64_t)W * k;
 }
-inline int64_t ia_shard_off(int64_t NT, int W, int r) { return r * (NT / W) + (r < NT % W ? r : NT % W); }
+__host__ __device__ inline int64_t ia_shard_off(int64_t NT, int W, int r) { return r * (NT / W) + (r < NT % W ? r : NT % W); }
 
 // certified pruning of the distance scan (ia_prune.hip): projection basis size, smallest DB
 // that prunes
@@ -253,6 +262,55 @@ struct XchgArgs {
 __host__ __device__ inline size_t ia_xslot(unsigned seq, int W, int rank, int m) {
   return ((size_t)(seq & 1u) * W + rank) * IA_XCHG_MAXQ + m;
 }
+
+// Owner-computes sharded steps (option "exchange" = 2): W ranks, rank o owns job o
+// (its gather K2p, query sort K2s and merge K4 run there only) and every rank scans ITS DB shard
+// for the queries of all W jobs.  Two one-shot exchanges per wavefront step through each rank's
+// exchange area (after the winner slots of the same IPC buffer; two parities, seq & 1):
+//   * owner o's K2s writes its job's sorted query tiles (fragments, pruning records, tile boxes,
+//     slot -> query map) at tiles [o QTs, o QTs + QTs) of EVERY rank's area, then per tile a
+//     flag = seq (after a system-scope fence); each K3p workgroup polls its block's tile flags;
+//   * K3p workgroup (block b, chunk k) of shard s writes the records of its block's queries into
+//     owner b's area, chunk-major in sorted-slot order (record w = s nch + k of slot x at w Mrec +
+//     x: one contiguous 1 KiB store per wave-instruction over xGMI), float4 (v1, row1, v2, row2)
+//     then, after a system-scope fence, (T, seq); the owner's fused merge K4 finds a query's slot
+//     in its own table (written by its K2s into local memory) and polls each record's seq.
+// No winner exchange and no finish: the owner's K4 is the single-GPU merge over W nch records
+// per query.  Every rank holds the whole DB (the fp64 rows a rerank or rescan needs), 0.7 GB per
+// 1024^2 level.
+#define IA_XO_MAXT 128            // query tiles of a step over all owners (4096 queries)
+#define IA_XO_MAXREC (1 << 20)    // records of a step over all owners' queries (W nch per query)
+struct XOLayout {                 // byte offsets inside one parity of an exchange area (KS = 4 fragments)
+  static constexpr size_t FRAG = 0;                                   // [tile][8][64] h16x8
+  static constexpr size_t INFO = FRAG + (size_t)IA_XO_MAXT * 8 * 64 * 16;  // [slot][3] float4
+  static constexpr size_t TBOX = INFO + (size_t)IA_XO_MAXT * 32 * 48;      // [tile][3] float4
+  static constexpr size_t ORD = TBOX + (size_t)IA_XO_MAXT * 48;            // [slot] int: query of the owner
+  static constexpr size_t FLAG = ORD + (size_t)IA_XO_MAXT * 32 * 4;        // [tile] unsigned seq
+  static constexpr size_t REC = FLAG + (size_t)IA_XO_MAXT * 4 + 256;       // [w][Mrec] float4
+  static constexpr size_t RTS = REC + (size_t)IA_XO_MAXREC * 16;           // [w][Mrec] (T bits, seq)
+  static constexpr size_t PARITY = RTS + (size_t)IA_XO_MAXREC * 8;
+};
+__host__ __device__ inline size_t ia_xslots_bytes(int world) { return (size_t)2 * world * IA_XCHG_MAXQ * sizeof(XSlot); }
+// what K2s of an owner writes: every rank's area of this parity (W of them; 1 when emulated:
+// one area serves every shard)
+struct XOSort {
+  char *area[IA_XCHG_MAXW];       // parity base of each rank's area
+  int *inv;                       // the owner's own table (local memory): inv[tile0 32 + query] = slot
+  int W;                          // areas written
+  int q0, Mj;                     // the owner's queries in the local K2p output: [q0, q0 + Mj)
+  int tile0, QTs;                 // its tiles in the step layout [tile0, tile0 + QTs)
+  unsigned seq;
+};
+// what K3p needs besides its PRE inputs (which point into the local area)
+struct XOScan {
+  char *area[IA_XCHG_MAXW];       // parity base of each owner's area (emulated: every entry local)
+  const unsigned *flag;           // local area's tile flags
+  int on, s, bpj;                 // owner of block b = b / bpj; this launch scans shard s
+  int Mrec;                       // record rows per chunk (slots of the step layout)
+  unsigned seq;
+  unsigned *err;                  // bit 2: a tile flag did not arrive in time
+  long long timeout_ticks;
+};
 
 __host__ __device__ inline int ia_reflect(int i, int n) {
   // np.pad(mode='symmetric') index map (img_preprocess.py:81-83).  Windows reach at most 2

@@ -565,7 +565,7 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
           float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
           unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
            int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox, const float *__restrict__ tnorm,
-           int /*nqb: one query block*/, int /*qt_end*/) {
+           int /*nqb: one query block*/, int /*qt_end*/, XOScan /*xo: PRE launches only*/) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   static_assert(QT <= 32, "need masks are 32-bit");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
@@ -927,7 +927,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
            float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
            unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
            int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox, const float *__restrict__ tnorm,
-           int nqb, int qt_end) {
+           int nqb, int qt_end, XOScan xo) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   constexpr int NE = PRE ? 1 : (IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE + WGT - 1) / WGT;  // unsorted fragments per thread
   static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
@@ -987,6 +987,21 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     ld_tile<KS>(a, db, tk(min(wave, K - 1)), lane);
   }
   if constexpr (PRE) {
+    if (xo.on) {
+      // owner-computes sharded step: this block's tiles come from their owner's K2s (another
+      // rank); wait for each tile's flag (bounded: a late peer sets xo.err, never a hang)
+      if (tid < qtb) {
+        const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(xo.flag + qt0 + tid, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != xo.seq) {
+          if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xo.timeout_ticks) {
+            atomicOr(xo.err, 4u);
+            break;
+          }
+          __builtin_amdgcn_s_sleep(1);
+        }
+      }
+      __syncthreads();
+    }
     // this launch's slice of the presorted queries, straight into LDS
     const h16x8 *qs = qf + (int64_t)qt0 * NP * IA_WAVE;
     for (int e = tid; e < QT * NP * IA_WAVE; e += WGT) ldsh[e] = e < qtb * NP * IA_WAVE ? qs[e] : h16x8{};
@@ -1575,8 +1590,21 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     if (mq < M) {
       const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
       const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
-      rec[(int64_t)mq * nwg + wg] = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
-      recT[(int64_t)mq * nwg + wg] = m.T;
+      const float4 rv = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
+      if (PRE && xo.on) {
+        // owner-computes sharded step: into the block's owner's area, record w = s nch + wg of
+        // sorted slot s0 + x (consecutive x: contiguous stores), then (T, seq) once it is visible
+        char *ar = xo.area[qblk / xo.bpj];
+        const int64_t ix = ((int64_t)xo.s * nwg + wg) * xo.Mrec + s0 + x;
+        reinterpret_cast<float4 *>(ar + XOLayout::REC)[ix] = rv;
+        __threadfence_system();
+        __hip_atomic_store(reinterpret_cast<unsigned long long *>(ar + XOLayout::RTS) + ix,
+                           ((unsigned long long)xo.seq << 32) | __float_as_uint(m.T), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+      } else {
+        rec[(int64_t)mq * nwg + wg] = rv;
+        recT[(int64_t)mq * nwg + wg] = m.T;
+      }
     }
   }
   if (tid == 0) {  // the workgroup's own counter slots (stream-ordered launches: no atomics)

@@ -1572,11 +1572,33 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   // ---- round 1: records (clamped, unconditional loads), coherence neighbours, query/weights
   float v1[RPL], v2[RPL], tt[RPL];
   int i1[RPL], i2[RPL];
+  int xslot = 0;  // owner-computes sharded step: the query's slot in the step layout
+  if (a.xo_W) {
+    const int o = m / a.xo_M;
+    xslot = a.xo_inv[(a.xo_o0 + o) * a.xo_QTs * IA_TILE + (m - o * a.xo_M)];
+  }
 #pragma unroll
   for (int j = 0; j < RPL; j++) {
     const int w = min(lane + IA_WAVE * j, a.nwg - 1);
-    const float4 x = rr[w];
-    const float t = rT[w];
+    float4 x;
+    float t;
+    if (a.xo_W) {  // records pushed by every shard's scan: wait for this step's (T, seq)
+      const int64_t ix = (int64_t)w * a.xo_Mrec + xslot;
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      unsigned long long ts;
+      while (((ts = __hip_atomic_load(a.xo_rts + ix, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) >> 32) != a.xo_seq) {
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.xo_timeout) {
+          atomicOr(a.xo_err, 8u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+      x = a.rec[ix];
+      t = __uint_as_float((unsigned)ts);
+    } else {
+      x = rr[w];
+      t = rT[w];
+    }
     const bool ok = lane + IA_WAVE * j < a.nwg;
     v1[j] = ok ? x.x : FLT_MAX;
     v2[j] = ok ? x.z : FLT_MAX;
@@ -1719,10 +1741,19 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
         // test (one tile per lane), two tiles per wave pass
         const float4 ql = a.qinfo[3 * m], qh = a.qinfo[3 * m + 1];
         const float ub = round_up_f(bd * a.ufac);
-        for (int64_t tb = 0; wgid + (int64_t)a.nwg * tb < a.NT; tb += IA_WAVE) {
-          const int64_t t = wgid + (int64_t)a.nwg * (tb + lane);
+        // the chunk's tiles t0 + tst k < tend (owner-computes step: chunk wgid mod nch of shard
+        // wgid / nch, in that shard's storage range of the whole level's table)
+        int64_t t0 = wgid, tst = a.nwg, tend = a.NT;
+        if (a.xo_W) {
+          const int sh = wgid / a.xo_nch;
+          t0 = ia_shard_off(a.NT, a.xo_W, sh) + (wgid - sh * a.xo_nch);
+          tst = a.xo_nch;
+          tend = ia_shard_off(a.NT, a.xo_W, sh + 1);
+        }
+        for (int64_t tb = 0; t0 + tst * tb < tend; tb += IA_WAVE) {
+          const int64_t t = t0 + tst * (tb + lane);
           bool nd = false;
-          if (t < a.NT) nd = prune_lb(a.boxes[2 * t], a.boxes[2 * t + 1], ql, qh) <= ub;
+          if (t < tend) nd = prune_lb(a.boxes[2 * t], a.boxes[2 * t + 1], ql, qh) <= ub;
           unsigned long long nm = __ballot(nd);
           while (nm) {
             const int j0 = __ffsll((long long)nm) - 1;
@@ -1734,7 +1765,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
             }
             const int j = lane < 32 ? j0 : j1;
             if (j >= 0) {
-              const int64_t i = a.pos2row[(wgid + (int64_t)a.nwg * (tb + j)) * IA_TILE + (lane & 31)];
+              const int64_t i = a.pos2row[(t0 + tst * (tb + j)) * IA_TILE + (lane & 31)];
               if (i < a.NA) {
                 const double d = exact_dist_level<CH>(a.db64, i, qs, IMG ? &A : nullptr);
                 if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
@@ -2535,7 +2566,7 @@ size_t ia_k3p_lds(int qt, int Mpad) {
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
-                   const float4 *tbox, const float *tnorm, hipStream_t st, int nqb, int qt_end) {
+                   const float4 *tbox, const float *tnorm, hipStream_t st, int nqb, int qt_end, const XOScan *xo) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
@@ -2566,7 +2597,9 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   // nqb > 1 (presorted variants only): one launch of nqb query blocks x nwg DB chunks
   if (!pre) nqb = 1;
   if (nqb == 1) qt_end = qt0 + qt;
+  XOScan x{};  // off unless an owner-computes step passes its exchange (presorted launches only)
+  if (xo && pre) x = *xo;
   allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nqb * nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row,
-                     NT, qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm, nqb, qt_end);
+                     NT, qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm, nqb, qt_end, x);
 }

@@ -55,6 +55,8 @@ void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
                         float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st);
 void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS, int *order, float4 *sq, void *qfs,
                           float4 *tbox, hipStream_t st);
+// owner-computes sharded step (exchange = 2): the owner's queries sorted into every rank's area
+void ia_launch_query_sort_xo(const float4 *qinfo, const void *qf, const XOSort &xs, hipStream_t st);
 // rotated DB + head-filtered scan (k3p_variant 16 / 17)
 void ia_launch_key_lut(const unsigned *skeys, int64_t NA, int n_tiles, int lb, int *lut, hipStream_t st);
 void ia_launch_db_build_rot(const double *db64, int64_t NA, int n_tiles, const int *pos2row, const double *mu_part,
@@ -66,7 +68,8 @@ size_t ia_k3p_lds(int qt, int Mpad);
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
-                   const float4 *tbox, const float *tnorm, hipStream_t st, int nqb = 1, int qt_end = 0);
+                   const float4 *tbox, const float *tnorm, hipStream_t st, int nqb = 1, int qt_end = 0,
+                   const XOScan *xo = nullptr);
 // GPU preprocessing (ia_pyramid.hip)
 void ia_launch_pyramid_reduce(const double *in, double *out, double *tmp, double *sm, double *mm, int h, int w, int ch,
                               const double *w7, hipStream_t st);

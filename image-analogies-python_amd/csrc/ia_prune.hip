@@ -192,16 +192,26 @@ __global__ void __launch_bounds__(PR_WG) k_tile_boxes(const int *__restrict__ po
 // is limited to 512).  (One workgroup for the whole step spent 20.7 us per cfg4 step, mostly
 // in the copies.)
 #define QS_WG 1024
+// XO (owner-computes sharded step, option "exchange" = 2, ia_internal.h XOSort): the owner's Mj
+// queries [q0, q0 + Mj) of the local K2p output are sorted alone (local index in the key's low
+// 12 bits), its QTs tiles go to tiles [tile0, tile0 + QTs) of every rank's exchange area (slots
+// past Mj: padding, U' = -inf, never contracted, no record), each followed by its flag = seq.
+template <bool XO>
 __global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__ qinfo, const h16x8 *__restrict__ qf,
                                                       int Mpad, int NS, int NP, int *__restrict__ order,
                                                       float4 *__restrict__ sq, h16x8 *__restrict__ qfs,
-                                                      float4 *__restrict__ tbox) {
+                                                      float4 *__restrict__ tbox, XOSort xs) {
   __shared__ unsigned key[4096];
   const int tid = threadIdx.x;
+  // sort key of sort slot i: unique (query index in the low 12 bits); padding last
+  auto key_of = [&](int i) -> unsigned {
+    if constexpr (XO) return i < xs.Mj ? ((__float_as_uint(qinfo[3 * (xs.q0 + i) + 2].y) & 0xFFFFF000u) | (unsigned)i) : 0xFFFFFFFFu;
+    else return i < Mpad ? ((__float_as_uint(qinfo[3 * i + 2].y) & 0xFFFFF000u) | (unsigned)i) : 0xFFFFFFFFu;
+  };
   if (NS <= QS_WG) {
     // one key per thread: exchanges below distance 64 are lane shuffles (no barrier), the wider
     // ones go through LDS
-    unsigned v = tid < Mpad ? ((__float_as_uint(qinfo[3 * tid + 2].y) & 0xFFFFF000u) | (unsigned)tid) : 0xFFFFFFFFu;
+    unsigned v = key_of(tid);
     for (int k = 2; k <= NS; k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
         unsigned o;
@@ -220,8 +230,7 @@ __global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__
     key[tid] = v;
     __syncthreads();
   } else {
-    for (int i = tid; i < NS; i += QS_WG)
-      key[i] = i < Mpad ? ((__float_as_uint(qinfo[3 * i + 2].y) & 0xFFFFF000u) | (unsigned)i) : 0xFFFFFFFFu;
+    for (int i = tid; i < NS; i += QS_WG) key[i] = key_of(i);
     __syncthreads();
     for (int k = 2; k <= NS; k <<= 1) {
       for (int j = k >> 1; j > 0; j >>= 1) {
@@ -239,24 +248,46 @@ __global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__
     }
   }
   const int xt0 = blockIdx.x;  // this workgroup's sorted query tile
+  const int nout = XO ? xs.W : 1;
+  // query (in qinfo / qf) of sorted slot x, -1 for XO padding
+  auto q_of = [&](int x) -> int {
+    const unsigned k = key[x];
+    if constexpr (XO) return k == 0xFFFFFFFFu ? -1 : xs.q0 + (int)(k & 0xFFFu);
+    else return (int)(k & 0xFFFu);
+  };
+  const int dt = XO ? xs.tile0 : 0;  // output tile offset
   for (int x = xt0 * IA_TILE + tid; x < (xt0 + 1) * IA_TILE && tid < IA_TILE; x += QS_WG) {
-    const int q = (int)(key[x] & 0xFFFu);
-    order[x] = q;
-    sq[3 * x] = qinfo[3 * q];
-    sq[3 * x + 1] = qinfo[3 * q + 1];
-    sq[3 * x + 2] = qinfo[3 * q + 2];
+    const int q = q_of(x);
+    const float4 i0 = q >= 0 ? qinfo[3 * q] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 i1 = q >= 0 ? qinfo[3 * q + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 i2 = q >= 0 ? qinfo[3 * q + 2] : make_float4(-INFINITY, 0.f, -INFINITY, 0.f);
+    const int ov = XO ? (q >= 0 ? q - xs.q0 : 0x7fffffff) : q;
+    if (XO && q >= 0) xs.inv[dt * IA_TILE + (q - xs.q0)] = dt * IA_TILE + x;  // the owner's query -> slot
+    for (int o = 0; o < nout; o++) {
+      const int xo = dt * IA_TILE + x;
+      int *ord = XO ? reinterpret_cast<int *>(xs.area[o] + XOLayout::ORD) : order;
+      float4 *si = XO ? reinterpret_cast<float4 *>(xs.area[o] + XOLayout::INFO) : sq;
+      ord[xo] = ov;
+      si[3 * xo] = i0;
+      si[3 * xo + 1] = i1;
+      si[3 * xo + 2] = i2;
+    }
   }
   // fragments of the tile: sorted slot x of tile xt, piece p, lane L (k-half L >> 5, row L & 31)
   for (int e = xt0 * NP * IA_WAVE + tid; e < (xt0 + 1) * NP * IA_WAVE; e += QS_WG) {
     const int L = e & 63, pq = e >> 6, xt = pq / NP, p = pq - xt * NP;
-    const int q = (int)(key[xt * IA_TILE + (L & 31)] & 0xFFFu);
-    qfs[e] = qf[((q >> 5) * NP + p) * IA_WAVE + (L & 32) + (q & 31)];
+    const int q = q_of(xt * IA_TILE + (L & 31));
+    const h16x8 v = q >= 0 ? qf[((q >> 5) * NP + p) * IA_WAVE + (L & 32) + (q & 31)] : h16x8{};
+    for (int o = 0; o < nout; o++) {
+      h16x8 *dst = XO ? reinterpret_cast<h16x8 *>(xs.area[o] + XOLayout::FRAG) : qfs;
+      dst[(int64_t)dt * NP * IA_WAVE + e] = v;
+    }
   }
   // the tile's box: one 32-lane half-wave
   const int lane = tid & 63;
   for (int t = xt0 + (tid >> 5); t < xt0 + 1; t += QS_WG / 32) {
-    const int q = (int)(key[t * IA_TILE + (lane & 31)] & 0xFFFu);
-    const float4 u = qinfo[3 * q + 2];
+    const int q = q_of(t * IA_TILE + (lane & 31));
+    const float4 u = q >= 0 ? qinfo[3 * q + 2] : make_float4(-INFINITY, 0.f, 0.f, 0.f);
     float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
     float um = -INFINITY;
     if (u.x != -INFINITY) {  // padding slots (U' = -inf) never widen a box
@@ -277,9 +308,22 @@ __global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__
       um = fmaxf(um, __shfl_xor(um, o, 64));
     }
     if ((lane & 31) == 0) {
-      tbox[3 * t] = lo;
-      tbox[3 * t + 1] = hi;
-      tbox[3 * t + 2] = make_float4(um, 0.f, 0.f, 0.f);
+      for (int o = 0; o < nout; o++) {
+        float4 *tb = XO ? reinterpret_cast<float4 *>(xs.area[o] + XOLayout::TBOX) : tbox;
+        tb[3 * (dt + t)] = lo;
+        tb[3 * (dt + t) + 1] = hi;
+        tb[3 * (dt + t) + 2] = make_float4(um, 0.f, 0.f, 0.f);
+      }
+    }
+  }
+  if constexpr (XO) {
+    // every store of this workgroup reaches every rank before the tile's flag: each thread fences
+    // its own stores at system scope, the barrier orders them before thread 0's flag stores
+    __threadfence_system();
+    __syncthreads();
+    if (tid < nout) {
+      unsigned *fl = reinterpret_cast<unsigned *>(xs.area[tid] + XOLayout::FLAG);
+      __hip_atomic_store(fl + dt + xt0, xs.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }
@@ -390,8 +434,14 @@ void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS,
                           float4 *tbox, hipStream_t st) {
   int NS = 32;
   while (NS < Mpad) NS <<= 1;
-  hipLaunchKernelGGL(k_query_sort, dim3(Mpad / IA_TILE), dim3(QS_WG), 0, st, qinfo, (const h16x8 *)qf, Mpad, NS, 2 * KS,
-                     order, sq, (h16x8 *)qfs, tbox);
+  hipLaunchKernelGGL(k_query_sort<false>, dim3(Mpad / IA_TILE), dim3(QS_WG), 0, st, qinfo, (const h16x8 *)qf, Mpad, NS,
+                     2 * KS, order, sq, (h16x8 *)qfs, tbox, XOSort{});
+}
+void ia_launch_query_sort_xo(const float4 *qinfo, const void *qf, const XOSort &xs, hipStream_t st) {
+  int NS = 32;
+  while (NS < xs.QTs * IA_TILE) NS <<= 1;
+  hipLaunchKernelGGL(k_query_sort<true>, dim3(xs.QTs), dim3(QS_WG), 0, st, qinfo, (const h16x8 *)qf, xs.QTs * IA_TILE, NS, 8,
+                     nullptr, nullptr, nullptr, nullptr, xs);
 }
 static inline unsigned pr_cdiv(int64_t a, int64_t b) { return (unsigned)((a + b - 1) / b); }
 

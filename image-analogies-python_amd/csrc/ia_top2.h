@@ -4,6 +4,8 @@
 #include <hip/hip_runtime.h>
 #include <float.h>
 
+#include "ia_internal.h"
+
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 h16x8 __attribute__((ext_vector_type(8)));
 
@@ -40,4 +42,4 @@ typedef void (*k3h_fn)(const h16x8 *, const h16x8 *, int, int, int, int, int, in
 // pruned split-f16 distance kernel entry (ia_k3h.hip, k3h_prune)
 typedef void (*k3p_fn)(const h16x8 *, const h16x8 *, const float4 *, const float4 *, const int *, int, int, int, int, int,
                        float4 *, float *, unsigned long long *, unsigned long long *, int, const int *, int, int,
-                       int *, const float4 *, const float *, int, int);
+                       int *, const float4 *, const float *, int, int, XOScan);

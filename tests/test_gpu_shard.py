@@ -80,7 +80,7 @@ def test_shard_emulate_option_bounds(ctx):
 def test_exchange_option_bounds(ctx):
     from ia_amd import _native
     with pytest.raises(_native.IAError):
-        ctx.set_option('exchange', 2)
+        ctx.set_option('exchange', 3)
     ctx.set_option('exchange', 1)
     ctx.set_option('shard_emulate', 32)   # more shards than exchange slots: refused per level
     ctx.set_option('prune_min_rows', 1)   # a pruned level shards (shard_unpruned = 0)
@@ -136,13 +136,14 @@ def _run_batch(ctx, z, jobs, W, exchange, prune_all=True):
     return S, IM, st
 
 
-@pytest.mark.parametrize('exchange', [0, 1], ids=['allgather', 'peerwrite'])
+@pytest.mark.parametrize('exchange', [0, 1, 2], ids=['allgather', 'peerwrite', 'owner'])
 @pytest.mark.parametrize('W', [2, 4, 8])
 def test_emulated_shards_batched_jobs_match_reference(ctx, W, exchange):
     """W jobs on the golden g256 run's A side stepped together over a W-way sharded DB (bench.py's
     N > 1 shard mode: every rank scans its shard for all jobs' queries; on the 256^2 level 8 x 86
     queries per step = 22 query tiles, the one-launch two-block presorted scan per shard).  Job 0
-    is the reference's own run; every job equals the unsharded batched run."""
+    is the reference's own run; every job equals the unsharded batched run.  exchange = 2: job j
+    owned by shard j (its sort and merge), records pushed to the owner (ia_internal.h XOLayout)."""
     from test_gpu_batch import _jobs_g32
     z = load_e2e('g256')
     kap = (0.5, 5.0, 25.0, 1.0, 2.0, 10.0, 15.0, 20.0)[:max(W, 2)]
@@ -160,16 +161,17 @@ def test_emulated_shards_batched_jobs_match_reference(ctx, W, exchange):
     assert st.dist_launches > stu.dist_launches   # W shard scans per sharded step
 
 
-@pytest.mark.parametrize('W', [4])
-def test_emulated_shards_batched_1024(ctx, W):
+@pytest.mark.parametrize('W,exchange', [(4, 1), (2, 2), (8, 2)])
+def test_emulated_shards_batched_1024(ctx, W, exchange):
     """W cfg3 jobs (synth.make_jobs: job 0 = cfg3, others other B images) over a W-way sharded
-    1024^2 DB with the peer-write exchange == the same jobs batched unsharded, every level."""
+    1024^2 DB with the peer-write winner exchange (1) or owner-computes steps (2, bench.py's N > 1
+    shard mode) == the same jobs batched unsharded, every level."""
     from ia_amd import synth
     jobs = synth.make_jobs(W, size=1024)
     z = {'L': jobs[0].L, 'A_pyr': jobs[0].A_pyr, 'Ap_pyr': jobs[0].Ap_pyr_list, 'B_pyr': jobs[0].B_pyr,
          'weights': jobs[0].weights}
     out = []
-    for Wx, ex in ((W, 1), (1, 0)):
+    for Wx, ex in ((W, exchange), (1, 0)):
         S, IM, Bps = [], [], []
         from ia_amd import _native
         st = _native.Stats()
@@ -196,3 +198,13 @@ def test_emulated_shards_batched_1024(ctx, W):
         for level in range(1, z['L']):
             assert np.array_equal(Bp[n][level], Bpu[n][level]), (n, level)
     assert st.pruned_levels == W and st.bound_violations == 0
+
+
+def test_owner_exchange_needs_one_job_per_shard(ctx):
+    """exchange = 2 emulated: one job per shard (n_jobs = shard_emulate), else IA_EINVAL."""
+    from ia_amd import _native
+    from test_gpu_batch import _jobs_g32
+    z = load_e2e('g256')
+    jb = _jobs_g32(z, kappas=(0.5, 5.0, 25.0))
+    with pytest.raises(_native.IAError):
+        _run_batch(ctx, z, jb, 2, 2)

@@ -9,6 +9,8 @@ one merge.  On W real ranks each rank runs K2, ITS shard's scan and one finishin
 step costs
     K2 + max over shards (scan) + finishing merge + x
 with x the exchange latency (an xGMI store + the peers' polling: a parameter, default 3 us).
+Owner-computes steps (exchange = 2: per step W gathers, W sorts, W scans, W merges, one per
+emulated rank) cost max(gather) + max(sort) + max(scan) + max(merge) + 2 x.
 Printed: measured kernel time per level (this one-GPU emulation) and the modelled per-rank time
 on W GPUs, per level and for the job; speedup and efficiency against the W = 1 model.
   python3 tools/shard_model.py <run_kernel_trace.csv> <W> [x_us] [baseline_job_ms]"""
@@ -37,31 +39,27 @@ def kind(name):
     return 'other'
 
 
-levels = []   # per level: list of steps, each {gather, sort, scans[], merges[]}
+levels = []   # per level: list of steps, each {gathers[], sorts[], scans[], merges[]}
 step = None
+last = None
 for r in rows:
     k = kind(r['Kernel_Name'])
     d = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
     if k == 'level':
         levels.append({'steps': [], 'other': 0.0})
-        step = None
+        step = last = None
         continue
     if not levels:
         continue
     lv = levels[-1]
-    if k == 'gather':
-        step = {'gather': d, 'sort': 0.0, 'scans': [], 'merges': []}
+    if k == 'gather' and last not in ('gather', 'sort'):   # a step starts with its gather(s)
+        step = {'gathers': [], 'sorts': [], 'scans': [], 'merges': []}
         lv['steps'].append(step)
-    elif step is None:
+    if step is None or k in ('other', 'level'):
         lv['other'] += d
-    elif k == 'sort':
-        step['sort'] += d
-    elif k == 'scan':
-        step['scans'].append(d)
-    elif k == 'merge':
-        step['merges'].append(d)
     else:
-        lv['other'] += d
+        step[k + 's'].append(d)
+    last = k
 
 # the bench's timed step is the last job of the trace: its levels are the last L - 1 entries
 L = 9 if len(levels) >= 9 else len(levels)
@@ -71,15 +69,22 @@ for i, lv in enumerate(sel):
     meas = model = 0.0
     sharded = 0
     for st in lv['steps']:
-        meas += st['gather'] + st['sort'] + sum(st['scans']) + sum(st['merges'])
+        meas += sum(st['gathers']) + sum(st['sorts']) + sum(st['scans']) + sum(st['merges'])
         nsh = len(st['merges'])
         sharded += nsh > 1
+        if len(st['gathers']) > 1:
+            # owner-computes step (exchange = 2): every emulated owner's gather, sort and merge
+            # are its rank's own launches; each rank pays the slowest of each plus its shard's
+            # scan and two exchange latencies (sorted queries out, records back)
+            model += max(st['gathers']) + max(st['sorts'] or [0.0]) + max(st['scans'] or [0.0]) + \
+                max(st['merges']) + 2 * XLAT
+            continue
         # scans of one shard are consecutive launches (several query blocks of an unpruned or
         # unsharded level run one after the other): a rank pays its shard's sum
         sc = st['scans']
         per = len(sc) // nsh if nsh > 1 and len(sc) % nsh == 0 else len(sc)
         grp = [sum(sc[i:i + per]) for i in range(0, len(sc), per)] if sc else [0.0]
-        model += st['gather'] + st['sort'] + max(grp) + (st['merges'][-1] if st['merges'] else 0.0) + \
+        model += sum(st['gathers']) + sum(st['sorts']) + max(grp) + (st['merges'][-1] if st['merges'] else 0.0) + \
             (XLAT if nsh > 1 else 0.0)
     meas += lv['other']
     model += lv['other']

@@ -38,6 +38,9 @@ def main():
     from ia_amd import _native, synth
     from golden_util import load_e2e
     rank, world = int(os.environ['RANK']), int(os.environ['WORLD_SIZE'])
+    # both ranks share ONE GPU here: each context's stream gets its own CU slice, so a kernel
+    # waiting for the peer's exchange never holds the CUs the peer's kernels need
+    os.environ['IA_CU_SPLIT'] = '%d/%d' % (rank, world)
     dist.init_process_group('gloo')
     ctx = _native.Context(0)
 
@@ -99,6 +102,35 @@ def main():
     print('[rank %d] %d cfg3 jobs batched over %d-way peer-write shards: %s vs unsharded batched (%.2f s sharded, '
           'bound_violations %d)' % (rank, world, world, 'bit-identical' if same else 'DIFFERENT', t1 - t0,
                                     st.bound_violations), flush=True)
+    # owner computes (exchange = 2, bench.py's N > 1 shard mode): rank r brings job r alone,
+    # every rank scans its shard for both jobs' queries; job r == its unsharded run
+    octx = _native.Context(0)
+    octx.set_option('exchange', 2)
+    octx.xchg_init(rank, world, all_gather)
+    mine = jobs[rank]
+
+    def run_one(c):
+        Bp1 = [x.copy() for x in mine.Bp_init]
+        st = _native.Stats()
+        res = []
+        for level in range(1, mine.L):
+            res.append(c.synthesize_level(mine.A_pyr[level], mine.A_pyr[level - 1], [p[level] for p in mine.Ap_pyr_list],
+                                          [p[level - 1] for p in mine.Ap_pyr_list], mine.B_pyr[level],
+                                          mine.B_pyr[level - 1], Bp1[level - 1], Bp1[level], mine.weights,
+                                          mine.kappa_factor(level), st))
+        return res, Bp1, st
+    dist.barrier()
+    t0 = time.time()
+    ro, Bpo, st = run_one(octx)
+    t1 = time.time()
+    rp, Bpp, _ = run_one(plain)
+    same = all(np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) for a, b in zip(ro, rp))
+    same &= all(np.array_equal(Bpo[l], Bpp[l]) for l in range(1, mine.L))
+    ok &= same
+    print('[rank %d] owner-computes: job %d over %d-way shards: %s vs its unsharded run (%.2f s, pruned levels %d, '
+          'bound_violations %d)' % (rank, rank, world, 'bit-identical' if same else 'DIFFERENT', t1 - t0,
+                                    st.pruned_levels, st.bound_violations), flush=True)
+    octx.close()
     plain.close()
     ctx.close()
     flag = torch.tensor([0 if ok else 1])
