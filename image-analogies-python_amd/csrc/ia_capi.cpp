@@ -120,6 +120,7 @@ struct ia_ctx {
   int exchange = 0;               // option "exchange": 0 = RCCL all-gather + finish, 1 = peer-write merge,
                                   // 2 = owner-computes (rank o owns job o; every rank scans its shard for all)
   DevBuf xo_inv;                  // exchange = 2: the owners' query -> slot tables of the current step
+  int xo_presort = 0;             // option "xo_presort": 1 = owners always sort with K2s (tests)
   void *xbuf = nullptr;           // this process's exchange buffer (uncached, IPC-exportable)
   int xbuf_w = 0;                 // ranks the buffer was sized for
   XSlot *xpeer[IA_XCHG_MAXW] = {};  // every rank's buffer in this address space (ia_xchg_open)
@@ -430,6 +431,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "k3p_blocks")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: k3p_blocks must be 0 or 1");
     c->k3p_blocks = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "xo_presort")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: xo_presort must be 0 or 1");
+    c->xo_presort = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "exchange")) {
@@ -1004,8 +1010,12 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         return (char *)(sharded ? (void *)c->xpeer[p] : c->xbuf) + ia_xslots_bytes(Wsh) + par;
       };
       char *loc = area(sharded ? c->rank : 0);
-      const int Mrec = Wsh * xo_QTs * IA_TILE;
       const int Mpj = (sd.M + IA_TILE - 1) / IA_TILE * IA_TILE;  // one owner's padded queries
+      // owners whose step fits one launch's query tiles skip K2s: K2p publishes the unsorted
+      // queries and each K3p block sorts its owner's queries itself (XOPub)
+      const bool ink = Mpj <= ia_k3h_qtmax(g.KS) * IA_TILE && !c->xo_presort;
+      const int QTs = ink ? Mpj / IA_TILE : xo_QTs;  // tiles per owner in this step's layout
+      const int Mrec = Wsh * QTs * IA_TILE;
       StepDesc s1 = sd;
       s1.J = 1;
       s1.Mpad = Mpj;
@@ -1013,22 +1023,30 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       for (int jl = 0; jl < J; jl++) {
         const JobSet one{jp[jl], c->jobs.as<JobPtrs>() + jl, 1};
         const size_t q0 = (size_t)jl * Mpj;
+        XOPub xp{};
+        if (ink) {
+          xp.W = sharded ? Wsh : 1;
+          for (int p = 0; p < xp.W; p++) xp.area[p] = area(p);
+          xp.slot0 = owner_of(jl) * Mpj;
+          xp.seq = seq;
+        }
         ia_launch_gather_p(g, s1, Bim, one, c->mu.as<double>(), c->q64.as<double>() + q0 * g.D, c->qn2.as<double>() + q0,
                            (char *)c->qf.p + q0 * db_row_bytes, c->db64.as<double>(), c->pr_basis.as<double>(), ufac,
-                           c->qinfo.as<float4>() + 3 * q0, Aim, ma.img_rows, c->st);
+                           c->qinfo.as<float4>() + 3 * q0, Aim, ma.img_rows, c->st, &xp);
+        if (ink) continue;
         XOSort xs{};
         xs.inv = c->xo_inv.as<int>();
         xs.W = sharded ? Wsh : 1;
         for (int p = 0; p < xs.W; p++) xs.area[p] = area(p);
         xs.q0 = 0;
         xs.Mj = sd.M;
-        xs.tile0 = owner_of(jl) * xo_QTs;
-        xs.QTs = xo_QTs;
+        xs.tile0 = owner_of(jl) * QTs;
+        xs.QTs = QTs;
         xs.seq = seq;
         ia_launch_query_sort_xo(c->qinfo.as<float4>() + 3 * q0, (char *)c->qf.p + q0 * db_row_bytes, xs, c->st);
       }
       if (timed_gm) hipEventRecord(c->evg[2 * n_gm + 1], c->st);
-      const int nqb = Wsh * xo_bpj;
+      const int nqb = ink ? Wsh : Wsh * xo_bpj;
       const bool timed = stride && t % stride == 0;
       if (timed) hipEventRecord(c->evs[2 * n_rec], c->st);
       int nch = IA_NWG_H;
@@ -1041,25 +1059,28 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           return fail(IA_EINVAL, "ia_synthesize_level: exchange = 2: shard too large for the pruned scan's chunks");
         XOScan xs{};
         for (int p = 0; p < Wsh; p++) xs.area[p] = sharded ? area(p) : loc;
-        xs.flag = reinterpret_cast<const unsigned *>(loc + XOLayout::FLAG);
+        xs.flag = reinterpret_cast<const unsigned *>(loc + (ink ? XOLayout::QSEQ : XOLayout::FLAG));
+        xs.inv = c->xo_inv.as<int>();
         xs.on = 1;
         xs.s = sharded ? c->rank : (int)i;
-        xs.bpj = xo_bpj;
+        xs.bpj = ink ? 1 : xo_bpj;
         xs.Mrec = Mrec;
         xs.seq = seq;
         xs.err = c->xerr.as<unsigned>();
         xs.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
         const char *dbp = (const char *)c->db.p + (size_t)(x.t0 - g.tile0) * tile_bytes;
         const int kv = c->k3p_variant;
-        const int k3x = (kv == 14 || kv == 15) ? 15 : (kv == 18 || kv == 19) ? 19 : (kv == 7 || kv == 11) ? 11 : 21;
-        ia_launch_k3p(xo_QTx, dbp, loc + XOLayout::FRAG, reinterpret_cast<const float4 *>(loc + XOLayout::INFO), mas[i].boxes,
-                      mas[i].pos2row, n, 0, sd.M, Mrec, nch, nullptr, nullptr,
+        // the in-kernel-sort variant (ink: 20 / 14 / 18 / 7) or its presorted form
+        const int k3x = ink ? ((kv == 14 || kv == 15) ? 14 : (kv == 18 || kv == 19) ? 18 : (kv == 7 || kv == 11) ? 7 : 20)
+                            : ((kv == 14 || kv == 15) ? 15 : (kv == 18 || kv == 19) ? 19 : (kv == 7 || kv == 11) ? 11 : 21);
+        ia_launch_k3p(ink ? QTs : xo_QTx, dbp, loc + XOLayout::FRAG, reinterpret_cast<const float4 *>(loc + XOLayout::INFO),
+                      mas[i].boxes, mas[i].pos2row, n, 0, sd.M, ink ? Mpj : Mrec, nch, nullptr, nullptr,
                       c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                       c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3x, sd.t,
                       reinterpret_cast<const int *>(loc + XOLayout::ORD), 0, sd.r0, nullptr,
                       reinterpret_cast<const float4 *>(loc + XOLayout::TBOX), c->tnorm.as<float>() + x.t0, c->st, nqb,
-                      Wsh * xo_QTs, &xs);
-        pairs_full += (double)n * Wsh * xo_QTs;
+                      Wsh * QTs, &xs);
+        pairs_full += (double)n * Wsh * QTs;
         tiles_full += (double)n * nqb;
         dist_launches++;
         if (timed) {
@@ -1089,7 +1110,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         mx.xo_Mrec = Mrec;
         mx.xo_o0 = owner_of(jl);
         mx.xo_M = sd.M;
-        mx.xo_QTs = xo_QTs;
+        mx.xo_QTs = QTs;
         mx.xo_seq = seq;
         mx.xo_err = c->xerr.as<unsigned>();
         mx.xo_timeout = 2000000000LL;

@@ -241,7 +241,7 @@ struct Winner {
 // One-shot peer-write winner exchange of a sharded level (option "exchange" = 1):
 // every rank's exchange buffer holds, per step parity (2) x rank (W) x query (IA_XCHG_MAXQ), a
 // 16-byte slot: the certified shard winner's exact distance, then (row | step sequence << 32)
-// written last with release semantics at system scope.  The merge of each rank writes its
+// written once the distance store has completed (ia_stores_done; the buffer is uncached).  The merge of each rank writes its
 // winner into the slot of every peer (xGMI stores into the peers' buffers, opened through HIP
 // IPC handles) and polls its own buffer for the W winners of the step.  Two parities suffice: a
 // rank can be at most one step ahead of any peer (its step t+1 needs every step-t winner).
@@ -278,6 +278,11 @@ __host__ __device__ inline size_t ia_xslot(unsigned seq, int W, int rank, int m)
 // No winner exchange and no finish: the owner's K4 is the single-GPU merge over W nch records
 // per query.  Every rank holds the whole DB (the fp64 rows a rerank or rescan needs), 0.7 GB per
 // 1024^2 level.
+// Ordering of an exchange hand-off: the payload goes to uncached memory (nothing in any L2 to
+// write back), so the writer waits for its own stores' completion (s_waitcnt vmcnt(0): a store
+// to uncached memory completes at the memory side) before the flag / seq store - no system-scope
+// release fence, whose L2 write-back of every dirty line costs microseconds per wave.
+__device__ __forceinline__ void ia_stores_done() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 #define IA_XO_MAXT 128            // query tiles of a step over all owners (4096 queries)
 #define IA_XO_MAXREC (1 << 20)    // records of a step over all owners' queries (W nch per query)
 struct XOLayout {                 // byte offsets inside one parity of an exchange area (KS = 4 fragments)
@@ -285,8 +290,9 @@ struct XOLayout {                 // byte offsets inside one parity of an exchan
   static constexpr size_t INFO = FRAG + (size_t)IA_XO_MAXT * 8 * 64 * 16;  // [slot][3] float4
   static constexpr size_t TBOX = INFO + (size_t)IA_XO_MAXT * 32 * 48;      // [tile][3] float4
   static constexpr size_t ORD = TBOX + (size_t)IA_XO_MAXT * 48;            // [slot] int: query of the owner
-  static constexpr size_t FLAG = ORD + (size_t)IA_XO_MAXT * 32 * 4;        // [tile] unsigned seq
-  static constexpr size_t REC = FLAG + (size_t)IA_XO_MAXT * 4 + 256;       // [w][Mrec] float4
+  static constexpr size_t FLAG = ORD + (size_t)IA_XO_MAXT * 32 * 4;        // [tile] unsigned seq (K2s path)
+  static constexpr size_t QSEQ = FLAG + (size_t)IA_XO_MAXT * 4;            // [slot] unsigned seq (K2p path)
+  static constexpr size_t REC = QSEQ + (size_t)IA_XO_MAXT * 32 * 4 + 256;  // [w][Mrec] float4
   static constexpr size_t RTS = REC + (size_t)IA_XO_MAXREC * 16;           // [w][Mrec] (T bits, seq)
   static constexpr size_t PARITY = RTS + (size_t)IA_XO_MAXREC * 8;
 };
@@ -301,10 +307,20 @@ struct XOSort {
   int tile0, QTs;                 // its tiles in the step layout [tile0, tile0 + QTs)
   unsigned seq;
 };
-// what K3p needs besides its PRE inputs (which point into the local area)
+// Owners whose step fits one launch's query tiles (<= 352 queries: cfg3) skip K2s: their K2p
+// publishes its unsorted queries (fragments, pruning records) at slots [slot0, slot0 + Mpad_j)
+// of every rank's area, each followed by its seq, and every K3p block sorts its owner's queries
+// itself (the single-GPU in-kernel sort); the scan of the owner's own shard writes its table.
+struct XOPub {
+  char *area[IA_XCHG_MAXW];       // parity base of each rank's area (emulated: 1, local)
+  int W, slot0;                   // areas written; the owner's first slot
+  unsigned seq;
+};
+// what K3p needs besides its query inputs (which point into the local area)
 struct XOScan {
   char *area[IA_XCHG_MAXW];       // parity base of each owner's area (emulated: every entry local)
-  const unsigned *flag;           // local area's tile flags
+  const unsigned *flag;           // local area's tile flags (PRE) or per-slot seqs (in-kernel sort)
+  int *inv;                       // in-kernel sort: the owner's table (written by the owner's shard)
   int on, s, bpj;                 // owner of block b = b / bpj; this launch scans shard s
   int Mrec;                       // record rows per chunk (slots of the step layout)
   unsigned seq;

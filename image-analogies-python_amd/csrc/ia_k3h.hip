@@ -951,7 +951,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   // one chunk get workgroup ids equal mod 8, i.e. the same XCD (round-robin dispatch): they read
   // the same tiles at about the same time through one L2.
   int wg = blockIdx.x, qblk = 0;
-  if (PRE && nqb > 1) {
+  if ((PRE || xo.on) && nqb > 1) {
     if ((nwg & 7) == 0) {
       const int grp = wg / (8 * nqb), r = wg - grp * 8 * nqb;
       qblk = r >> 3;
@@ -960,7 +960,11 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       qblk = wg / nwg;
       wg -= qblk * nwg;
     }
-    qt0 += qblk * QT;
+    if (PRE) qt0 += qblk * QT;
+  }
+  if (!PRE && xo.on) {  // owner-computes, in-kernel sort: block qblk = owner qblk's Mpad queries
+    qf += (int64_t)qblk * (Mpad / IA_TILE) * NP * IA_WAVE;
+    qinfo += 3 * (int64_t)qblk * Mpad;
   }
   const int qtb = PRE ? min(QT, qt_end - qt0) : QT;  // query tiles of this block (PRE: the last may hold fewer)
   const int K = (NT - wg + nwg - 1) / nwg;  // tiles wg + nwg*k, k < K (host: nwg <= NT, K <= IA_K3P_MAXK_LDS)
@@ -990,9 +994,13 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     if (xo.on) {
       // owner-computes sharded step: this block's tiles come from their owner's K2s (another
       // rank); wait for each tile's flag (bounded: a late peer sets xo.err, never a hang)
-      if (tid < qtb) {
+      // (after any earlier timeout of this context every wait is skipped: a lost peer costs one
+      // timeout, then the level runs to its end and reports IA_ECOMM)
+      if (tid < qtb && __hip_atomic_load(xo.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
         const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-        while (__hip_atomic_load(xo.flag + qt0 + tid, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != xo.seq) {
+        // relaxed: the area is uncached (no stale line to invalidate); the loads below issue
+        // after the barrier, i.e. after every flag was seen
+        while (__hip_atomic_load(xo.flag + qt0 + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != xo.seq) {
           if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xo.timeout_ticks) {
             atomicOr(xo.err, 4u);
             break;
@@ -1035,6 +1043,20 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   if (tid == 0) kctr = NW;
   if constexpr (PRE) __syncthreads();
   if constexpr (!PRE) {
+  if (xo.on) {  // owner-computes: wait for each of the block's queries (published by its owner's K2p)
+    const unsigned *qs = xo.flag + (int64_t)qblk * Mpad;
+    if (tid < Mpad && __hip_atomic_load(xo.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) {
+      const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(qs + tid, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != xo.seq) {
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xo.timeout_ticks) {
+          atomicOr(xo.err, 4u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+  }
   float4 mlo = make_float4(0.f, 0.f, 0.f, 0.f), mhi = mlo;
   float mU = -INFINITY, mzt = -INFINITY, mzw = 0.f;
   unsigned mkey = 0xFFFFFFFFu;
@@ -1591,13 +1613,15 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
       const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
       const float4 rv = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
-      if (PRE && xo.on) {
+      if (xo.on) {
         // owner-computes sharded step: into the block's owner's area, record w = s nch + wg of
         // sorted slot s0 + x (consecutive x: contiguous stores), then (T, seq) once it is visible
         char *ar = xo.area[qblk / xo.bpj];
-        const int64_t ix = ((int64_t)xo.s * nwg + wg) * xo.Mrec + s0 + x;
+        const int64_t slot = (PRE ? 0 : (int64_t)qblk * Mpad) + s0 + x;
+        const int64_t ix = ((int64_t)xo.s * nwg + wg) * xo.Mrec + slot;
+        if (!PRE && xo.s == qblk && wg == 0) xo.inv[(int64_t)qblk * Mpad + mq] = (int)slot;  // the owner's table
         reinterpret_cast<float4 *>(ar + XOLayout::REC)[ix] = rv;
-        __threadfence_system();
+        ia_stores_done();
         __hip_atomic_store(reinterpret_cast<unsigned long long *>(ar + XOLayout::RTS) + ix,
                            ((unsigned long long)xo.seq << 32) | __float_as_uint(m.T), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);

@@ -1297,19 +1297,45 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_gather_query_p(LevelGeo g, StepDes
                                                           double *__restrict__ q64, double *__restrict__ qn2,
                                                           _Float16 *__restrict__ qf, const double *__restrict__ db64,
                                                           const double *__restrict__ basis, double ufac,
-                                                          float4 *__restrict__ qinfo, Imgs A) {
+                                                          float4 *__restrict__ qinfo, Imgs A, XOPub xp) {
   constexpr int D = 55, KD = 16 * KS;
   static_assert(KD <= IA_WAVE, "one feature per lane");
   __shared__ double qsh[IA_PQ_WPB][Geo<1>::DS];
+  __shared__ __attribute__((aligned(16))) _Float16 xh[IA_PQ_WPB][2][KD];  // owner publish: the query's hi / lo columns
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m = blockIdx.x * IA_PQ_WPB + wv;
   if (m >= sd.Mpad) return;
+  // owner-computes sharded step (XOPub): the query's fragments (16 h16x8 pieces from LDS, one
+  // store instruction per area), its pruning record, then - once those stores completed - its
+  // seq, into every rank's area
+  auto publish = [&](float4 i0, float4 i1, float4 i2) {
+    __builtin_amdgcn_wave_barrier();  // xh written by this wave's lanes
+    const int qt = m / IA_TILE, j = m % IA_TILE;
+    const int c = lane, sp = c >> 2, part = (c >> 1) & 1, h = c & 1;  // chunk c < 2 KS * 2
+    h16x8 v{};
+    if (c < 4 * KS) v = *reinterpret_cast<const h16x8 *>(&xh[wv][part][16 * sp + 8 * h]);
+    const int64_t t0 = xp.slot0 / IA_TILE;
+    for (int o = 0; o < xp.W; o++) {
+      if (c < 4 * KS)
+        reinterpret_cast<h16x8 *>(xp.area[o] + XOLayout::FRAG)[((t0 + qt) * 2 * KS + 2 * sp + part) * IA_WAVE + h * IA_TILE + j] = v;
+      if (lane < 3) reinterpret_cast<float4 *>(xp.area[o] + XOLayout::INFO)[3 * (xp.slot0 + m) + lane] = lane == 0 ? i0 : lane == 1 ? i1 : i2;
+    }
+    ia_stores_done();
+    if (lane < xp.W)
+      __hip_atomic_store(reinterpret_cast<unsigned *>(xp.area[lane] + XOLayout::QSEQ) + xp.slot0 + m, xp.seq, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_SYSTEM);
+  };
   if (m >= sd.J * sd.M) {
     if (lane < KD) put_qh<KS>(qf, m, lane, 0.);
+    const float4 i0 = make_float4(0.f, 0.f, 0.f, 0.f), i2 = make_float4(-INFINITY, __uint_as_float(IA_PRUNE_KEY_PAD), -INFINITY, 0.f);
     if (lane == 0) {
-      qinfo[3 * m] = make_float4(0.f, 0.f, 0.f, 0.f);
-      qinfo[3 * m + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      qinfo[3 * m + 2] = make_float4(-INFINITY, __uint_as_float(IA_PRUNE_KEY_PAD), -INFINITY, 0.f);
+      qinfo[3 * m] = i0;
+      qinfo[3 * m + 1] = i0;
+      qinfo[3 * m + 2] = i2;
+    }
+    if (xp.W) {
+      if (lane < KD) xh[wv][0][lane] = xh[wv][1][lane] = (_Float16)0.f;
+      publish(i0, i0, i2);
     }
     return;
   }
@@ -1340,10 +1366,12 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_gather_query_p(LevelGeo g, StepDes
       const double qc = v - mu_part[feat_part<1>(f)];
       ss = qc * qc;
       put_qh<KS>(qf, m, f, -2.0 * qc);
+      if (xp.W) split_h(-2.0 * qc, xh[wv][0][f], xh[wv][1][f]);
 #pragma unroll
       for (int i = 0; i < IA_NPC; i++) p[i] = basis[i * D + f] * qc;
     } else {
       put_qh<KS>(qf, m, f, f == D ? IA_NORM_SCALE : 0.);
+      if (xp.W) split_h(f == D ? IA_NORM_SCALE : 0., xh[wv][0][f], xh[wv][1][f]);
     }
   }
   ss = wave_sum_d(ss);
@@ -1371,6 +1399,19 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_gather_query_p(LevelGeo g, StepDes
                         : INFINITY;
     const float w = round_up_f(0x1p-8 * qn * (1.0 + 0x1p-40));
     qinfo[3 * m + 2] = make_float4(up, __uint_as_float(key), z, w);
+  }
+  if (xp.W) {  // the record as lane 0 wrote it, on every lane (uniform values)
+    const double qn = sqrt(ss);
+    const bool fin = u < DBL_MAX;
+    const float up = fin ? round_up_f(u * ufac) : INFINITY;
+    const float z = fin ? round_up_f((double)up - ss + 0x1p-22 * (ss + (double)up) + 0x1p-24 * (16.0 * qn + 300.0)) : INFINITY;
+    const float w = round_up_f(0x1p-8 * qn * (1.0 + 0x1p-40));
+    const unsigned key = fin ? prune_key(p, basis + IA_NPC * D) : IA_PRUNE_KEY_INF;
+    publish(make_float4(round_down_f(p[0] - IA_PRUNE_MABS), round_down_f(p[1] - IA_PRUNE_MABS),
+                        round_down_f(p[2] - IA_PRUNE_MABS), round_down_f(p[3] - IA_PRUNE_MABS)),
+            make_float4(round_up_f(p[0] + IA_PRUNE_MABS), round_up_f(p[1] + IA_PRUNE_MABS),
+                        round_up_f(p[2] + IA_PRUNE_MABS), round_up_f(p[3] + IA_PRUNE_MABS)),
+            make_float4(up, __uint_as_float(key), z, w));
   }
 }
 
@@ -1585,9 +1626,14 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     if (a.xo_W) {  // records pushed by every shard's scan: wait for this step's (T, seq)
       const int64_t ix = (int64_t)w * a.xo_Mrec + xslot;
       const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+      // after an earlier timeout of this context: no waiting (one lost peer costs one timeout)
+      const long long lim = __hip_atomic_load(a.xo_err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? -1 : a.xo_timeout;
       unsigned long long ts;
-      while (((ts = __hip_atomic_load(a.xo_rts + ix, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM)) >> 32) != a.xo_seq) {
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > a.xo_timeout) {
+      // relaxed: the records are uncached (nothing stale to invalidate; an acquire would
+      // invalidate this CU's caches on every poll); the float4 load issues after the seq was seen
+      while (((ts = __hip_atomic_load(const_cast<unsigned long long *>(a.xo_rts) + ix, __ATOMIC_RELAXED,
+                                      __HIP_MEMORY_SCOPE_SYSTEM)) >> 32) != a.xo_seq) {
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > lim) {
           atomicOr(a.xo_err, 8u);
           break;
         }
@@ -1959,7 +2005,8 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd
     const unsigned row = wn.idx == INT64_MAX ? 0xffffffffu : (unsigned)wn.idx;
     __hip_atomic_store(reinterpret_cast<unsigned long long *>(&sl->d), (unsigned long long)__double_as_longlong(wn.d),
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    __hip_atomic_store(&sl->row_seq, (unsigned long long)row | ((unsigned long long)xa.seq << 32), __ATOMIC_RELEASE,
+    ia_stores_done();  // the distance has reached the (uncached) slot before its (row, seq) word
+    __hip_atomic_store(&sl->row_seq, (unsigned long long)row | ((unsigned long long)xa.seq << 32), __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
   }
   if constexpr (!FIN) {
@@ -1974,14 +2021,16 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd
     if (lane < xa.W) {  // lane p reads rank p's winner
       XSlot *sl = xa.local + ia_xslot(xa.seq, xa.W, lane, m);
       const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-      unsigned long long rs = __hip_atomic_load(&sl->row_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+      // after an earlier timeout of this context: no waiting (one lost peer costs one timeout)
+      const long long lim = __hip_atomic_load(xa.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ? -1 : xa.timeout_ticks;
+      unsigned long long rs = __hip_atomic_load(&sl->row_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       while ((unsigned)(rs >> 32) != xa.seq) {
-        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > xa.timeout_ticks) {
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > lim) {
           late = true;
           break;
         }
         __builtin_amdgcn_s_sleep(2);
-        rs = __hip_atomic_load(&sl->row_seq, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM);
+        rs = __hip_atomic_load(&sl->row_seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
       }
       if (!late) {
         const unsigned long long db =
@@ -2494,26 +2543,27 @@ void ia_launch_gather_h(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
 template <bool IMG>
 static void launch_gather_p_t(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                               double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
-                              float4 *qinfo, const Imgs &A, hipStream_t st) {
+                              float4 *qinfo, const Imgs &A, const XOPub &xp, hipStream_t st) {
   const dim3 grid(cdiv(sd.Mpad, IA_PQ_WPB));
   if (jobs.J == 1)
     hipLaunchKernelGGL((k_gather_query_p<4, IMG, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, job0_imgs(B, jobs), JobArg1{jobs.j0},
-                       mu, q64, qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A);
+                       mu, q64, qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A, xp);
   else
     hipLaunchKernelGGL((k_gather_query_p<4, IMG, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64,
-                       qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A);
+                       qn2, (_Float16 *)qf, db64, basis, ufac, qinfo, A, xp);
 }
 void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
-                        float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st) {
+                        float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st, const XOPub *xp) {
+  const XOPub x = xp ? *xp : XOPub{};
 #ifdef IA_K3H_DIAG
   if (img_rows) {
-    launch_gather_p_t<true>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, st);
+    launch_gather_p_t<true>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, x, st);
     return;
   }
 #endif
   (void)img_rows;
-  launch_gather_p_t<false>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, st);
+  launch_gather_p_t<false>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, x, st);
 }
 
 #ifdef IA_K3H_DIAG
@@ -2595,10 +2645,10 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
   lds = lds > red ? lds : red;
   // nqb > 1 (presorted variants only): one launch of nqb query blocks x nwg DB chunks
-  if (!pre) nqb = 1;
+  if (!pre && !(xo && xo->on)) nqb = 1;
   if (nqb == 1) qt_end = qt0 + qt;
-  XOScan x{};  // off unless an owner-computes step passes its exchange (presorted launches only)
-  if (xo && pre) x = *xo;
+  XOScan x{};  // off unless an owner-computes step passes its exchange
+  if (xo) x = *xo;
   allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nqb * nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row,
                      NT, qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm, nqb, qt_end, x);

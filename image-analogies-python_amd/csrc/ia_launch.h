@@ -52,7 +52,7 @@ void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t N
                            float *boxes, const float *rnorm, float *tnorm, hipStream_t st);
 void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
-                        float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st);
+                        float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st, const XOPub *xp = nullptr);
 void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS, int *order, float4 *sq, void *qfs,
                           float4 *tbox, hipStream_t st);
 // owner-computes sharded step (exchange = 2): the owner's queries sorted into every rank's area

@@ -317,13 +317,13 @@ __global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__
     }
   }
   if constexpr (XO) {
-    // every store of this workgroup reaches every rank before the tile's flag: each thread fences
-    // its own stores at system scope, the barrier orders them before thread 0's flag stores
-    __threadfence_system();
+    // every store of this workgroup reaches every rank before the tile's flag: each wave waits
+    // for its own (uncached) stores to complete, the barrier orders them before the flag stores
+    ia_stores_done();
     __syncthreads();
     if (tid < nout) {
       unsigned *fl = reinterpret_cast<unsigned *>(xs.area[tid] + XOLayout::FLAG);
-      __hip_atomic_store(fl + dt + xt0, xs.seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(fl + dt + xt0, xs.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
 }

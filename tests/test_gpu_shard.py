@@ -136,20 +136,26 @@ def _run_batch(ctx, z, jobs, W, exchange, prune_all=True):
     return S, IM, st
 
 
-@pytest.mark.parametrize('exchange', [0, 1, 2], ids=['allgather', 'peerwrite', 'owner'])
+@pytest.mark.parametrize('exchange', [0, 1, 2, 3], ids=['allgather', 'peerwrite', 'owner', 'owner_k2s'])
 @pytest.mark.parametrize('W', [2, 4, 8])
 def test_emulated_shards_batched_jobs_match_reference(ctx, W, exchange):
     """W jobs on the golden g256 run's A side stepped together over a W-way sharded DB (bench.py's
     N > 1 shard mode: every rank scans its shard for all jobs' queries; on the 256^2 level 8 x 86
     queries per step = 22 query tiles, the one-launch two-block presorted scan per shard).  Job 0
     is the reference's own run; every job equals the unsharded batched run.  exchange = 2: job j
-    owned by shard j (its sort and merge), records pushed to the owner (ia_internal.h XOLayout)."""
+    owned by shard j (its gather and merge), its queries published by its K2p and sorted inside
+    every shard's scan, records pushed to the owner (ia_internal.h XOLayout); owner_k2s: the same
+    with the owner's K2s sort + presorted scans (the path of steps wider than 352 queries)."""
     from test_gpu_batch import _jobs_g32
     z = load_e2e('g256')
     kap = (0.5, 5.0, 25.0, 1.0, 2.0, 10.0, 15.0, 20.0)[:max(W, 2)]
     jb = _jobs_g32(z, kappas=kap)
     ju = [(k, [x.copy() for x in Bp]) for k, Bp in jb]
-    S, IM, st = _run_batch(ctx, z, jb, W, exchange)
+    ctx.set_option('xo_presort', 1 if exchange == 3 else 0)
+    try:
+        S, IM, st = _run_batch(ctx, z, jb, W, min(exchange, 2))
+    finally:
+        ctx.set_option('xo_presort', 0)
     Su, IMu, stu = _run_batch(ctx, z, ju, 1, 0)
     for level in range(1, z['L']):
         assert np.array_equal(S[0][level], z['s'][level]) and np.array_equal(IM[0][level], z['im'][level]), level

@@ -13,11 +13,19 @@ Owner-computes steps (exchange = 2: per step W gathers, W sorts, W scans, W merg
 emulated rank) cost max(gather) + max(sort) + max(scan) + max(merge) + 2 x.
 Printed: measured kernel time per level (this one-GPU emulation) and the modelled per-rank time
 on W GPUs, per level and for the job; speedup and efficiency against the W = 1 model.
-  python3 tools/shard_model.py <run_kernel_trace.csv> <W> [x_us] [baseline_job_ms]"""
+  python3 tools/shard_model.py <run_kernel_trace.csv> <W> [x_us] [baseline_job_ms] [w1_model.txt]"""
 import csv
 import re
 import sys
 
+# optional 5th argument: the W = 1 run's model output; in owner-computes runs a level with no
+# sharded step runs only the rank's own job there, i.e. takes the one-job time
+BASE_LV = {}
+if len(sys.argv) > 5:
+    for ln in open(sys.argv[5]):
+        mm = re.match(r'level (\d+): .* modelled per rank ([\d.]+) ms', ln)
+        if mm:
+            BASE_LV[int(mm.group(1))] = float(mm.group(2)) * 1e3
 rows = list(csv.DictReader(open(sys.argv[1])))
 rows.sort(key=lambda r: int(r['Start_Timestamp']))
 W = int(sys.argv[2])
@@ -88,6 +96,9 @@ for i, lv in enumerate(sel):
             (XLAT if nsh > 1 else 0.0)
     meas += lv['other']
     model += lv['other']
+    owner = any(len(st['gathers']) > 1 for l2 in sel for st in l2['steps'])
+    if owner and sharded == 0 and (i + 1) in BASE_LV:
+        model = BASE_LV[i + 1]
     tot_meas += meas
     tot_model += model
     print('level %d: %d steps (%d sharded %d ways): emulated %.1f ms, modelled per rank %.1f ms'
@@ -95,4 +106,9 @@ for i, lv in enumerate(sel):
 print('job: emulated kernels %.1f ms on one GPU; modelled %.1f ms per rank on %d GPUs (exchange latency %.1f us/step)'
       % (tot_meas / 1e3, tot_model / 1e3, W, XLAT))
 if base:
-    print('speedup vs %.1f ms: %.2fx, efficiency %.0f %%' % (base, base / (tot_model / 1e3), 100 * base / (tot_model / 1e3) / W))
+    if any(len(st['gathers']) > 1 for lv in sel for st in lv['steps']):
+        # owner computes: W jobs on W ranks (weak scaling): efficiency = one job alone / per-rank time
+        print('weak scaling vs %.1f ms for one job on one GPU: efficiency %.0f %% (%d jobs in %.1f ms on %d GPUs)'
+              % (base, 100 * base / (tot_model / 1e3), W, tot_model / 1e3, W))
+    else:
+        print('speedup vs %.1f ms: %.2fx, efficiency %.0f %%' % (base, base / (tot_model / 1e3), 100 * base / (tot_model / 1e3) / W))
