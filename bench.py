@@ -403,19 +403,46 @@ def main():
     owner = args.mode == 'shard' and world > 1 and args.exchange == 'owner'
     if owner and args.shard_jobs != world:
         ap.error('--exchange owner: one job per rank (--shard-jobs N)')
+    shard_error = None
+
+    def agree(failed):
+        """True when any rank failed (every rank gets the same answer)"""
+        f = torch.tensor([1.0 if failed else 0.0], device=dev if backend == 'nccl' else 'cpu')
+        dist.all_reduce(f, op=dist.ReduceOp.MAX)
+        return float(f.item()) > 0
+
     if args.mode == 'shard' and world > 1:
-        if owner:
-            ctx.set_option('exchange', 2)
-        if args.exchange == 'rccl':
-            uid = [_native.comm_unique_id() if rank == 0 else None]
-            dist.broadcast_object_list(uid, src=0)
-            ctx.comm_init(rank, world, uid[0])
-        else:
-            def all_gather(b):
-                out = [None] * world
-                dist.all_gather_object(out, b)
-                return out
-            ctx.xchg_init(rank, world, all_gather)
+        try:
+            if owner:
+                ctx.set_option('exchange', 2)
+            if args.exchange == 'rccl':
+                uid = [_native.comm_unique_id() if rank == 0 else None]
+                dist.broadcast_object_list(uid, src=0)
+                ctx.comm_init(rank, world, uid[0])
+            else:
+                def all_gather(b):
+                    out = [None] * world
+                    dist.all_gather_object(out, b)
+                    return out
+                ctx.xchg_init(rank, world, all_gather)
+            if os.environ.get('IA_BENCH_FAIL_SHARD') == str(rank):   # rehearsal of the fallback only
+                raise RuntimeError('IA_BENCH_FAIL_SHARD')
+        except Exception as e:   # e.g. no peer access between the GPUs: measured as replicas, said so
+            shard_error = 'rank %d: %r' % (rank, e)
+            log('[bench] shard setup failed: %s' % shard_error)
+        if agree(shard_error is not None):
+            shard_error = shard_error or 'a peer rank failed the shard setup'
+
+    def fall_back():
+        """the shard exchange failed on some rank: every rank measures replicas instead (the line
+        says so in config.shard_error)"""
+        nonlocal ctx, owner
+        log('[bench] rank %d: shard mode unavailable (%s): measuring replicas' % (rank, shard_error))
+        ctx.close()
+        ctx = make_context(args, local)
+        args.mode, args.shard_jobs, owner = 'replicas', 1, False
+        d = DeviceJob(jobs_b[0], torch, dev)
+        return d, (lambda st, cs=None: d.run(ctx, torch, st))
     ctxs = [ctx]
     if sw is not None:
         from ia_amd import sweep
@@ -455,7 +482,22 @@ def main():
             el = float(tt.item())
         return el, stats
 
-    for _ in range(args.warmup):
+    if shard_error is not None:
+        dj, run = fall_back()
+        ctxs = [ctx]
+    for i in range(args.warmup):
+        if world > 1 and args.mode == 'shard' and i == 0:
+            try:
+                run(_native.Stats())
+            except Exception as e:   # e.g. IA_ECOMM: a peer's data never arrived
+                shard_error = 'rank %d: %r' % (rank, e)
+                log('[bench] sharded warmup failed: %s' % shard_error)
+            if agree(shard_error is not None):
+                shard_error = shard_error or 'a peer rank failed the sharded warmup'
+                dj, run = fall_back()
+                ctxs = [ctx]
+                run(_native.Stats())
+            continue
         run(_native.Stats())
     # with several streams (cfg5), HIP events around one stream's K3 launches also time the other
     # streams' kernels: the timed steps then run without events and the roofline comes from one
@@ -603,6 +645,8 @@ def main():
         out['config']['sweep'] = {'jobs': len(sw.jobs), 'batched': not args.sequential, 'max_batch': args.max_batch,
                                   'streams': args.streams,
                                   'kappas': sorted({j.k for j in sw.jobs}), 'depths': sorted(set(sw.L))}
+    if shard_error is not None:
+        out['config']['shard_error'] = shard_error
     if value_replicas is not None:
         out['value_replicas'] = value_replicas
         out['config']['replicas'] = ('value_replicas = %d independent cfg jobs, one per GPU, no collective '

@@ -246,10 +246,11 @@ class Context(object):
         all_gather(bytes) -> list of every rank's bytes in rank order (e.g. a torch.distributed
         all_gather_object wrapper).  Makes this context rank `rank` of a world-rank DB shard."""
         h = ctypes.create_string_buffer(64)
-        check(lib().ia_xchg_alloc(self._h, world, h), 'ia_xchg_alloc')
-        hs = all_gather(h.raw)
+        rc = lib().ia_xchg_alloc(self._h, world, h)
+        hs = all_gather(h.raw if rc == 0 else b'')   # every rank takes part, even after a failure
+        check(rc, 'ia_xchg_alloc')
         if len(hs) != world or any(len(x) != 64 for x in hs):
-            raise IAError('xchg_init: expected %d handles of 64 bytes' % world)
+            raise IAError('xchg_init: expected %d handles of 64 bytes (a peer failed ia_xchg_alloc)' % world)
         check(lib().ia_xchg_open(self._h, rank, world, b''.join(hs)), 'ia_xchg_open')
 
     def synthesize_level(self, A, Ac, Ap_list, Apc_list, B, Bc, Bpc, Bp, weights, kappa_factor, stats=None,

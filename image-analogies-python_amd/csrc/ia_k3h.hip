@@ -906,6 +906,9 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 //      between the loads: no need test left in the loop)
 //   5. per-query records exactly as V1
 // ------------------------------------------------------------------------------------------
+#ifndef IA_K3P_ROWS_EARLY  // 1: candidate rows looked up before the subset merge (0: after it)
+#define IA_K3P_ROWS_EARLY 1
+#endif
 #define IA_K3P3_MAXQ 512   // queries per step (one per thread)
 #define IA_K3P3_MAXK 512   // DB tiles per workgroup
 // steps of up to IA_K3P_RANK_MAX queries are sorted by rank counting, wider ones by the bitonic
@@ -1575,9 +1578,17 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   }  // !INTER
   K3P_T(ph[4]);
 #pragma unroll
-  for (int q = 0; q < QT; q++) {  // tile + packed in-tile index -> DB position
+  for (int q = 0; q < QT; q++) {  // tile + packed in-tile index -> DB position (-> DB row)
     const int r = (int)(__float_as_uint(b1[q]) & 15u);
-    i1[q] = b1[q] == FLT_MAX ? 0x7fffffff : i1[q] * IA_TILE + 4 * half + (r & 3) + 8 * (r >> 2);
+    const int pos = i1[q] * IA_TILE + 4 * half + (r & 3) + 8 * (r >> 2);
+#if IA_K3P_ROWS_EARLY
+    // the lane's candidate rows are looked up here, their loads in flight while the workgroup
+    // waits for its slowest wave and merges; the merge then orders ties by row instead of
+    // position (any order is exact: K4 reranks the listed rows and T bounds every other one)
+    i1[q] = b1[q] == FLT_MAX ? 0x7fffffff : pos2row[pos];
+#else
+    i1[q] = b1[q] == FLT_MAX ? 0x7fffffff : pos;
+#endif
   }
 
   // ---- 5. merge the 2*NW subsets of each query; records go to the original query slots
@@ -1585,6 +1596,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   // fragments for NW = 16, overwrites it)
   const int mq_pre = tid < NQ ? (PRE ? (int)skey[tid] : order[s0 + tid]) : 0;
   __syncthreads();
+  if constexpr (!HF) K3P_T(ph[6]);  // probe: the wait for the workgroup's slowest wave ends here
   if (lane == 0) {
     wpairs[wave] = cnt;
     wtiles[wave] = ntl;
@@ -1610,8 +1622,12 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
     const int mq = WGT >= NQ ? mq_pre : (PRE ? (int)skey[x] : order[s0 + x]);
     if (mq < M) {
+#if IA_K3P_ROWS_EARLY
+      const int r1 = m.i1, r2 = m.i2;
+#else
       const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
       const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
+#endif
       const float4 rv = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
       if (xo.on) {
         // owner-computes sharded step: into the block's owner's area, record w = s nch + wg of
@@ -1650,7 +1666,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     atomicAdd(&k3p_prof[2], ph[3] - ph[2]);
     atomicAdd(&k3p_prof[3], ph[4] - ph[3]);
     atomicAdd(&k3p_prof[7], ph[5] - ph[4]);
-    if (HF) atomicAdd(&k3p_prof[8], ph[6] - ph[3]);  // HF: phase 1 (heads); [3] - [8] = phase 2
+    atomicAdd(&k3p_prof[8], HF ? ph[6] - ph[3] : ph[6] - ph[4]);  // HF: phase 1 (heads); else: the tail's barrier wait
     atomicAdd(&k3p_prof[4], 1ull);
     atomicAdd(&k3p_prof[5], (unsigned long long)ntl);
     atomicAdd(&k3p_prof[6], (unsigned long long)cnt);
@@ -1666,7 +1682,7 @@ void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau w
     fprintf(stderr, "K3P_PROBE write phase: merge=%.0f pos2row=%.0f stores=%.0f atomics=%.0f\n", (double)v[7] / v[10],
             (double)v[8] / v[10], (double)v[9] / v[10], (double)v[11] / v[10]);
   fprintf(stderr, "K3P_PROBE v3 phases if variant>=3: load=setup, sort+scatter=need, need=loop, loop=tail, tail=[7]\n");
-  fprintf(stderr, "K3P_PROBE [7]=%.0f [8]=%.0f (HF: [8] = phase 1, loop - [8] = phase 2)\n", (double)v[7] / v[4],
+  fprintf(stderr, "K3P_PROBE [7]=%.0f [8]=%.0f (HF: [8] = phase 1, loop - [8] = phase 2; else [8] = the tail barrier wait)\n", (double)v[7] / v[4],
           (double)v[8] / v[4]);
   fprintf(stderr, "K3P_PROBE waves=%llu setup=%.0f need=%.0f loop=%.0f tail=%.0f tiles/wave=%.2f pairs/wave=%.2f (cycles/wave)\n",
           v[4], (double)v[0] / v[4], (double)v[1] / v[4], (double)v[2] / v[4], (double)v[3] / v[4], (double)v[5] / v[4],
