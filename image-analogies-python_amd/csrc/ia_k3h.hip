@@ -985,7 +985,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = qt0 * IA_TILE;
-  unsigned long long ph[7] = {0, 0, 0, 0, 0, 0, 0};
+  unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   K3P_T(ph[0]);
 
   // ---- 1. one global round
@@ -1605,21 +1605,23 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32], inside the query-fragment area
 #pragma unroll
   for (int q = 0; q < QT; q++) {
-    Top2 mine = {b1[q], FLT_MAX, b2[q], i1[q], 0x7fffffff};
-    Top2 other;
-    other.v1 = __shfl_xor(b1[q], 32, 64);
-    other.i1 = __shfl_xor(i1[q], 32, 64);
-    other.T = __shfl_xor(b2[q], 32, 64);
-    other.v2 = FLT_MAX;
-    other.i2 = 0x7fffffff;
-    Top2 mrg = half == 0 ? top2_merge(mine, other) : top2_merge(other, mine);
-    if (half == 0) red[(wave * QT + q) * IA_TILE + lane] = mrg;
+    // the two halves of the wave hold the same query's subsets: (b1, row) + runner-up value each;
+    // exchanged with v_permlane32_swap, merged with selects (half 0 stores)
+    const auto sb = __builtin_amdgcn_permlane32_swap(__float_as_uint(b1[q]), __float_as_uint(b1[q]), false, false);
+    const auto si = __builtin_amdgcn_permlane32_swap((unsigned)i1[q], (unsigned)i1[q], false, false);
+    const auto s2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(b2[q]), __float_as_uint(b2[q]), false, false);
+    const Top2 mine = {b1[q], FLT_MAX, b2[q], i1[q], 0x7fffffff};
+    const Top2 other = {__uint_as_float(half ? sb[0] : sb[1]), FLT_MAX, __uint_as_float(half ? s2[0] : s2[1]),
+                        (int)(half ? si[0] : si[1]), 0x7fffffff};
+    if (half == 0) red[(wave * QT + q) * IA_TILE + lane] = top2_merge_sel(mine, other);
   }
+  K3P_T(ph[7]);
   __syncthreads();
+  K3P_T(ph[8]);
   for (int x = tid; x < NQ; x += WGT) {
     Top2 m = red[x];
 #pragma unroll
-    for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
+    for (int w = 1; w < NW; w++) m = top2_merge_sel(m, red[(w * QT) * IA_TILE + x]);
     const int mq = WGT >= NQ ? mq_pre : (PRE ? (int)skey[x] : order[s0 + x]);
     if (mq < M) {
 #if IA_K3P_ROWS_EARLY
@@ -1647,6 +1649,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       }
     }
   }
+  K3P_T(ph[9]);
   if (tid == 0) {  // the workgroup's own counter slots (stream-ordered launches: no atomics)
     unsigned long long sp = 0, st = 0, sf = 0;
 #pragma unroll
@@ -1667,6 +1670,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     atomicAdd(&k3p_prof[3], ph[4] - ph[3]);
     atomicAdd(&k3p_prof[7], ph[5] - ph[4]);
     atomicAdd(&k3p_prof[8], HF ? ph[6] - ph[3] : ph[6] - ph[4]);  // HF: phase 1 (heads); else: the tail's barrier wait
+    atomicAdd(&k3p_prof[9], ph[7] - ph[6]);    // per-wave half merge + LDS writes
+    atomicAdd(&k3p_prof[10], ph[8] - ph[7]);   // second barrier
+    atomicAdd(&k3p_prof[11], ph[9] - ph[8]);   // subset merge + record stores
     atomicAdd(&k3p_prof[4], 1ull);
     atomicAdd(&k3p_prof[5], (unsigned long long)ntl);
     atomicAdd(&k3p_prof[6], (unsigned long long)cnt);
@@ -1678,9 +1684,8 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
 void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau wave, to stderr
   unsigned long long v[12];
   if (hipMemcpyFromSymbol(v, HIP_SYMBOL(k3p_prof), sizeof(v)) != hipSuccess || v[4] == 0) return;
-  if (v[10])
-    fprintf(stderr, "K3P_PROBE write phase: merge=%.0f pos2row=%.0f stores=%.0f atomics=%.0f\n", (double)v[7] / v[10],
-            (double)v[8] / v[10], (double)v[9] / v[10], (double)v[11] / v[10]);
+  fprintf(stderr, "K3P_PROBE tail split: half merge %.0f, barrier %.0f, subset merge + records %.0f\n", (double)v[9] / v[4],
+          (double)v[10] / v[4], (double)v[11] / v[4]);
   fprintf(stderr, "K3P_PROBE v3 phases if variant>=3: load=setup, sort+scatter=need, need=loop, loop=tail, tail=[7]\n");
   fprintf(stderr, "K3P_PROBE [7]=%.0f [8]=%.0f (HF: [8] = phase 1, loop - [8] = phase 2; else [8] = the tail barrier wait)\n", (double)v[7] / v[4],
           (double)v[8] / v[4]);

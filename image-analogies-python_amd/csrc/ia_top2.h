@@ -37,6 +37,23 @@ __device__ __forceinline__ Top2 top2_merge(Top2 a, const Top2 &b) {
   return a;
 }
 
+// top2_merge without branches (selects only): the two listed pairs of a and b are each sorted, so
+// the merged first is the smaller of the two heads, the second the smaller of the loser and the
+// winner's second, and the third value (into T) the smaller of what remains
+__device__ __forceinline__ Top2 top2_merge_sel(const Top2 &a, const Top2 &b) {
+  const bool x = lt(a.v1, a.i1, b.v1, b.i1);
+  const float fv = x ? a.v1 : b.v1, lv = x ? b.v1 : a.v1, nv = x ? a.v2 : b.v2, l2 = x ? b.v2 : a.v2;
+  const int fi = x ? a.i1 : b.i1, li = x ? b.i1 : a.i1, ni = x ? a.i2 : b.i2;
+  const bool y = lt(nv, ni, lv, li);
+  Top2 r;
+  r.v1 = fv;
+  r.i1 = fi;
+  r.v2 = y ? nv : lv;
+  r.i2 = y ? ni : li;
+  r.T = fminf(fminf(a.T, b.T), y ? lv : fminf(nv, l2));
+  return r;
+}
+
 // split-f16 distance kernel entry (ia_k3h.hip)
 typedef void (*k3h_fn)(const h16x8 *, const h16x8 *, int, int, int, int, int, int, int, float4 *, float *);
 // pruned split-f16 distance kernel entry (ia_k3h.hip, k3h_prune)
