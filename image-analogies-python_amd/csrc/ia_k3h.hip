@@ -1164,7 +1164,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
           o = sx[tid ^ jb];
           __syncthreads();
         } else {
-          o = (unsigned)__shfl_xor((int)v, jb, 64);
+          o = xlane_xor(v, jb);
         }
         const bool keep_min = ((tid & kb) == 0) == ((tid & jb) == 0);
         v = keep_min ? min(v, o) : max(v, o);
@@ -1228,15 +1228,15 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
 #pragma unroll
     for (int o = 1; o < 32; o <<= 1) {
-      lo.x = fminf(lo.x, __shfl_xor(lo.x, o, 64));
-      lo.y = fminf(lo.y, __shfl_xor(lo.y, o, 64));
-      lo.z = fminf(lo.z, __shfl_xor(lo.z, o, 64));
-      lo.w = fminf(lo.w, __shfl_xor(lo.w, o, 64));
-      hi.x = fmaxf(hi.x, __shfl_xor(hi.x, o, 64));
-      hi.y = fmaxf(hi.y, __shfl_xor(hi.y, o, 64));
-      hi.z = fmaxf(hi.z, __shfl_xor(hi.z, o, 64));
-      hi.w = fmaxf(hi.w, __shfl_xor(hi.w, o, 64));
-      u = fmaxf(u, __shfl_xor(u, o, 64));
+      lo.x = fminf(lo.x, xlane_xor_f(lo.x, o));
+      lo.y = fminf(lo.y, xlane_xor_f(lo.y, o));
+      lo.z = fminf(lo.z, xlane_xor_f(lo.z, o));
+      lo.w = fminf(lo.w, xlane_xor_f(lo.w, o));
+      hi.x = fmaxf(hi.x, xlane_xor_f(hi.x, o));
+      hi.y = fmaxf(hi.y, xlane_xor_f(hi.y, o));
+      hi.z = fmaxf(hi.z, xlane_xor_f(hi.z, o));
+      hi.w = fmaxf(hi.w, xlane_xor_f(hi.w, o));
+      u = fmaxf(u, xlane_xor_f(u, o));
     }
     if ((lane & 31) == 0 && j < QT) {
       tlo[j] = lo;

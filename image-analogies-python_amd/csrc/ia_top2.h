@@ -54,6 +54,27 @@ __device__ __forceinline__ Top2 top2_merge_sel(const Top2 &a, const Top2 &b) {
   return r;
 }
 
+// v from lane (lane ^ J) for J a power of two below 64, without the LDS crossbar where the
+// hardware has a register path: DPP quad_perm (J = 1, 2), ds_swizzle bit mode (4, 8),
+// v_permlane16_swap (16: rows 0 <-> 1, 2 <-> 3), v_permlane32_swap (32: the two halves)
+__device__ __forceinline__ unsigned xlane_xor(unsigned v, int J) {
+  switch (J) {
+    case 1: return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0xB1, 0xF, 0xF, false);
+    case 2: return (unsigned)__builtin_amdgcn_update_dpp((int)v, (int)v, 0x4E, 0xF, 0xF, false);
+    case 4: return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x101F);
+    case 8: return (unsigned)__builtin_amdgcn_ds_swizzle((int)v, 0x201F);
+    case 16: {
+      const auto r = __builtin_amdgcn_permlane16_swap(v, v, false, false);
+      return ((threadIdx.x >> 4) & 1) ? r[0] : r[1];
+    }
+    default: {
+      const auto r = __builtin_amdgcn_permlane32_swap(v, v, false, false);
+      return (threadIdx.x & 32) ? r[0] : r[1];
+    }
+  }
+}
+__device__ __forceinline__ float xlane_xor_f(float v, int J) { return __uint_as_float(xlane_xor(__float_as_uint(v), J)); }
+
 // split-f16 distance kernel entry (ia_k3h.hip)
 typedef void (*k3h_fn)(const h16x8 *, const h16x8 *, int, int, int, int, int, int, int, float4 *, float *);
 // pruned split-f16 distance kernel entry (ia_k3h.hip, k3h_prune)
