@@ -158,7 +158,12 @@ int ia_version(void);
  * runs as a W-way DB shard on this device (per-shard scans and certified winners, then the
  * multi-rank finish; no RCCL): the sharded code path, testable on one GPU.
  * "shard_unpruned" = 0 (default) / 1: shard only the levels that run the pruned scan / every
- * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge).
+ * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge)
+ * / 2 (owner computes: each rank brings its own job, every rank scans its shard for all of them,
+ * queries and scan records exchanged by peer writes; emulated: one job per shard).
+ * "xo_presort" = 1: owner-computes steps always sort in a K2s launch (tests; default 0: steps of
+ * <= 352 queries per owner are sorted inside the scan).  Environment IA_CU_SPLIT=k/n (rehearsals
+ * of n ranks on ONE GPU only): the context's stream runs on CU slice k of n.
  * Identical results for every setting. */
 #define IA_MATCH_F32 0
 #define IA_MATCH_F16X3 1
@@ -170,15 +175,16 @@ int ia_set_option(ia_ctx *ctx, const char *name, int value);
  * ia_comm_init on every rank. */
 int ia_comm_unique_id(unsigned char id_out[128]);
 int ia_comm_init(ia_ctx *ctx, int rank, int world, const unsigned char id[128]);
-/* One-shot peer-write winner exchange for sharded levels (replaces the RCCL
- * all-gather + finish of ia_comm_init with one fused merge per step).  Every rank calls
- * ia_xchg_alloc (an uncached device buffer of 2 x world x 4096 16-byte slots, zeroed) and
- * publishes the returned 64-byte HIP IPC handle; after gathering all world handles (rank order,
- * world x 64 bytes) it calls ia_xchg_open, which maps the peers' buffers and makes the context a
- * rank of a world-rank DB shard (option "exchange" = 1).  No RCCL communicator is needed.  A
- * peer that stops publishing makes the level fail with IA_ECOMM after 20 s instead of hanging.
- * With option "shard_emulate" = W and "exchange" = 1 a single process runs the same kernels
- * over a local buffer. */
+/* One-shot peer-write exchanges for sharded levels (replace the RCCL all-gather +
+ * finish of ia_comm_init).  Every rank calls ia_xchg_alloc (an uncached device buffer, zeroed:
+ * 2 x world x 4096 16-byte winner slots for "exchange" = 1, then two parities of the owner
+ * areas of "exchange" = 2, about 50 MiB) and publishes the returned 64-byte HIP IPC handle;
+ * after gathering all world handles (rank order, world x 64 bytes) it calls ia_xchg_open, which
+ * maps the peers' buffers and makes the context a rank of a world-rank DB shard (option
+ * "exchange" = 1 unless 2 was set before).  No RCCL communicator is needed.  A peer that stops
+ * publishing makes the level fail with IA_ECOMM after 20 s instead of hanging.  With option
+ * "shard_emulate" = W and "exchange" = 1 / 2 a single process runs the same kernels over a
+ * local buffer. */
 int ia_xchg_alloc(ia_ctx *ctx, int world, unsigned char handle_out[64]);
 int ia_xchg_open(ia_ctx *ctx, int rank, int world, const unsigned char *handles);
 
@@ -191,7 +197,8 @@ int ia_synthesize_level(ia_ctx *ctx, const ia_level_args *args, ia_stats *stats)
  * buffers are per job.  Every wavefront step gathers the queries of all jobs and runs ONE
  * distance scan over the DB for them (the DB is streamed once per step, not once per job), then
  * each job's coherence / kappa / writeback.  Results are those of n_jobs separate
- * ia_synthesize_level calls, bit for bit.  1 <= n_jobs <= 32; single-rank levels only. */
+ * ia_synthesize_level calls, bit for bit.  1 <= n_jobs <= 32.  Sharded levels take batches too
+ * ("exchange" 0 / 1: every rank holds every job; emulated "exchange" = 2: one job per shard). */
 int ia_synthesize_levels(ia_ctx *ctx, const ia_level_args *args, int n_jobs, ia_stats *stats);
 
 /* ---- FLANN-compatible exact index (algorithms.py:56,69,74) -------------------------------- */
