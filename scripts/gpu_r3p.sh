@@ -1,5 +1,5 @@
 #!/bin/bash
-# round 3, session P: K3p with register-path lane exchanges (sort, boxes) + branchless merges: parity tests,
+# round 3, session P: K3p lookahead tile choice: parity tests,
 # the v20 tail-split probe, same-box A/B against HEAD (diag/libia_head.so)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
