@@ -73,17 +73,27 @@ class DeviceJob(object):
         self.IM = [torch.empty(int(np.prod(x.shape[:2])), dtype=torch.int32, device=dev) for x in self.B]
         self.ch = 1 if job.A_pyr[0].ndim == 2 else job.A_pyr[0].shape[2]
 
-    def run(self, ctx, torch, stats):
+    def _level(self, ctx, l, stats):
+        ptrs = dict(A=self.A[l].data_ptr(), Ac=self.A[l - 1].data_ptr(), Ap=self.Ap[l].data_ptr(),
+                    Apc=self.Ap[l - 1].data_ptr(), B=self.B[l].data_ptr(), Bc=self.B[l - 1].data_ptr(),
+                    Bpc=self.Bp[l - 1].data_ptr(), Bp=self.Bp[l].data_ptr(), weights=self.W.data_ptr(),
+                    s_out=self.S[l].data_ptr(), im_out=self.IM[l].data_ptr())
+        ctx.synthesize_level_device(self.ch, len(self.job.Ap_pyr_list), self.A[l].shape[:2], self.B[l].shape[:2],
+                                    ptrs, self.job.kappa_factor(l), stats)
+
+    def run(self, ctx, torch, stats, pipe=None):
+        """pipe = a second context: levels alternate between the two, each level's steps waiting
+        only for the steps of the previous level they read (include/ia.h ia_pipeline_depend; two
+        host threads)"""
         for l in range(self.job.L):
             self.Bp[l].copy_(self.Bp0[l])
         torch.cuda.synchronize()   # libia runs on its own stream
-        for l in range(1, self.job.L):
-            ptrs = dict(A=self.A[l].data_ptr(), Ac=self.A[l - 1].data_ptr(), Ap=self.Ap[l].data_ptr(),
-                        Apc=self.Ap[l - 1].data_ptr(), B=self.B[l].data_ptr(), Bc=self.B[l - 1].data_ptr(),
-                        Bpc=self.Bp[l - 1].data_ptr(), Bp=self.Bp[l].data_ptr(), weights=self.W.data_ptr(),
-                        s_out=self.S[l].data_ptr(), im_out=self.IM[l].data_ptr())
-            ctx.synthesize_level_device(self.ch, len(self.job.Ap_pyr_list), self.A[l].shape[:2], self.B[l].shape[:2],
-                                        ptrs, self.job.kappa_factor(l), stats)
+        if pipe is None:
+            for l in range(1, self.job.L):
+                self._level(ctx, l, stats)
+            return
+        from ia_amd.pipeline import run_levels_pipelined
+        run_levels_pipelined(lambda c, l, st: self._level(c, l, st), [ctx, pipe], self.job.L, stats)
 
 
 class DeviceBatch(object):
@@ -306,6 +316,10 @@ def main():
                          'hi x hi accumulator (software-pipelined single chains), 20 (default) / 21 = the same on query-tile pairs '
                          '(two chains); '
                          'product builds hold 7, 11, 14, 15 and 18..21')
+    ap.add_argument('--pipeline', type=int, default=1, choices=[0, 1],
+                    help='1 (default; one-job configs and replicas): consecutive levels overlap (two libia '
+                         'contexts, each level\'s steps waiting only for the steps of the previous level they read; '
+                         'DESIGN.md §6b); 0: levels one after the other (always in the owner-computes shard mode)')
     ap.add_argument('--k3p-blocks', type=int, default=1, choices=[0, 1],
                     help='pruned scan of a step wider than 11 query tiles: 1 = one launch of (query block x DB '
                          'chunk) workgroups, 0 = one launch per query block')
@@ -442,7 +456,8 @@ def main():
         ctx = make_context(args, local)
         args.mode, args.shard_jobs, owner = 'replicas', 1, False
         d = DeviceJob(jobs_b[0], torch, dev)
-        return d, (lambda st, cs=None: d.run(ctx, torch, st))
+        p2 = make_context(args, local) if args.pipeline else None
+        return d, (lambda st, cs=None: d.run(ctx, torch, st, pipe=p2 if cs is None else None))
     ctxs = [ctx]
     if sw is not None:
         from ia_amd import sweep
@@ -451,11 +466,19 @@ def main():
         run = lambda st, cs=ctxs: dsw.run(cs, st, batched=not args.sequential, max_batch=args.max_batch)
         dj = dsw
     elif owner:   # this rank's own job; the other ranks bring theirs
+        # levels one after the other: pipelined, a rank's scan waiting on a peer's queries would
+        # hold the CUs its own next level needs (measured: 0.74 vs 4.5 M px/s for two ranks on one
+        # GPU, profiles/r03/pipeline/)
         dj = DeviceJob(jobs_b[rank], torch, dev)
         run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
     elif args.shard_jobs > 1:
         dj = DeviceBatch(jobs_b, torch, dev)
         run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
+    elif args.pipeline:
+        dj = DeviceJob(job, torch, dev)
+        pctx = make_context(args, local)
+        # the roofline's single-stream pass (run(st, [ctx])) runs the levels one after the other
+        run = lambda st, cs=None: dj.run(ctx, torch, st, pipe=pctx if cs is None else None)
     else:
         dj = DeviceJob(job, torch, dev)
         run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
@@ -502,7 +525,9 @@ def main():
     # with several streams (cfg5), HIP events around one stream's K3 launches also time the other
     # streams' kernels: the timed steps then run without events and the roofline comes from one
     # extra single-stream pass below
-    concurrent = len(ctxs) > 1
+    # pipelined levels (or several cfg5 streams): HIP events around one stream's K3 launches would
+    # also time the other stream's kernels, so the roofline comes from one extra sequential pass
+    concurrent = len(ctxs) > 1 or (args.pipeline and sw is None and not owner and args.shard_jobs <= 1)
     elapsed, stats = timed(args.steps, run, not concurrent)
     if concurrent:
         _, stats_rl = timed(1, lambda st: run(st, [ctx]), True)
@@ -591,8 +616,9 @@ def main():
                         'distance scan on MFMA; flops are the algorithmic 2*D*N_A*M per launch')
     if concurrent:
         roofline['k3_share_of_step'] = None   # single-stream pass vs concurrent timed steps: not comparable
-        roofline['timing'] = ('K3/K2/K4 device times from one extra single-stream pass (the timed steps ran %d '
-                              'concurrent streams, whose HIP events would overlap)' % len(ctxs))
+        roofline['timing'] = ('K3/K2/K4 device times from one extra single-stream pass (the timed steps ran %s, '
+                              'whose HIP events would overlap)' % ('%d concurrent streams' % len(ctxs) if len(ctxs) > 1
+                                                                  else 'pipelined levels on two streams'))
     roofline['gathers'] = gather_rooflines(st)
     roofline['fp32_mfma_equiv_tflops'] = fp32_equiv / 1e12
     roofline['fp32_mfma_equiv_frac'] = fp32_equiv / FP32_MFMA_PEAK
@@ -623,6 +649,8 @@ def main():
                                                            'dbshard%d_jobs%d' % (max(world, args.shard_emulate),
                                                                                  args.shard_jobs)),
                                            'jobs_per_step': jobs,
+                                           'level_pipeline': bool(args.pipeline and sw is None and not owner and
+                                                                  args.shard_jobs <= 1),
                                            'nn': 'exact: %s MFMA candidates + certified fp64 rerank'
                                                  % ('split-f16 (hi/lo x3)' if f16 else 'fp32'),
                                            'precision': ('f16x3 = every operand split into f16 hi + lo, 3 MFMA '

@@ -78,6 +78,8 @@ EXPORTS = {
     'ia_comm_init': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
     'ia_xchg_alloc': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_char_p]),
     'ia_xchg_open': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_char_p]),
+    'ia_pipeline_depend': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int]),
+    'ia_pipeline_generation': (ctypes.c_int, [ctypes.c_void_p]),
     'ia_synthesize_level': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LevelArgs), ctypes.POINTER(Stats)]),
     'ia_synthesize_levels': (ctypes.c_int, [ctypes.c_void_p, ctypes.POINTER(LevelArgs), ctypes.c_int,
                                             ctypes.POINTER(Stats)]),
@@ -252,6 +254,15 @@ class Context(object):
         if len(hs) != world or any(len(x) != 64 for x in hs):
             raise IAError('xchg_init: expected %d handles of 64 bytes (a peer failed ia_xchg_alloc)' % world)
         check(lib().ia_xchg_open(self._h, rank, world, b''.join(hs)), 'ia_xchg_open')
+
+    def pipeline_depend(self, prev, gen):
+        """The next level call on this context waits, step by step, for the level call number
+        `gen` of `prev` (a context with option pipeline_record = 1) - include/ia.h."""
+        check(lib().ia_pipeline_depend(self._h, prev.handle if prev is not None else None, int(gen)),
+              'ia_pipeline_depend')
+
+    def pipeline_generation(self):
+        return lib().ia_pipeline_generation(self._h)
 
     def synthesize_level(self, A, Ac, Ap_list, Apc_list, B, Bc, Bpc, Bp, weights, kappa_factor, stats=None,
                          debug=None):

@@ -5,6 +5,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <mutex>
+#include <thread>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -127,6 +131,17 @@ struct ia_ctx {
   bool xmapped[IA_XCHG_MAXW] = {};  // opened through hipIpcOpenMemHandle (closed on destroy)
   unsigned xseq = 0;              // exchange sequence number (one per sharded step, same on every rank)
   DevBuf xerr;
+  // level pipelining: a recording context publishes, per level call (a
+  // generation), the wavefront steps it has enqueued, each followed by an event; a context told
+  // to depend on it (ia_pipeline_depend) makes each of its steps wait for the steps of that
+  // generation it reads from (level l + 1 step t reads B' of level l steps <= t / 2 + 4)
+  int p_record = 0;                          // option "pipeline_record"
+  std::vector<hipEvent_t> p_ev[3];           // per generation mod 3: one event per step
+  std::atomic<long long> p_enq{-1};          // last step of the current generation enqueued
+  std::atomic<long long> p_T{0};             // steps of the current generation
+  std::atomic<int> p_gen{0}, p_done{0};      // current / last finished generation
+  ia_ctx *dep = nullptr;                     // the next level call waits on dep's generation dep_gen
+  int dep_gen = 0;
 };
 
 struct ia_index {
@@ -344,7 +359,7 @@ void ia_destroy(ia_ctx *c) {
                     &c->pr_rot, &c->pr_lut,
                     &c->py_in, &c->py_tmp, &c->py_sm, &c->py_mm, &c->py_out})
     b->release();
-  for (auto *v : {&c->evs, &c->evg, &c->evm})
+  for (auto *v : {&c->evs, &c->evg, &c->evm, &c->p_ev[0], &c->p_ev[1], &c->p_ev[2]})
     for (hipEvent_t e : *v) hipEventDestroy(e);
   for (hipEvent_t e : c->kb) hipEventDestroy(e);
   hipEventDestroy(c->lv0);
@@ -431,6 +446,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "k3p_blocks")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: k3p_blocks must be 0 or 1");
     c->k3p_blocks = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "pipeline_record")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: pipeline_record must be 0 or 1");
+    c->p_record = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "xo_presort")) {
@@ -533,6 +553,16 @@ int ia_xchg_open(ia_ctx *c, int rank, int world, const unsigned char *handles) {
   c->xseq = 0;
   return IA_OK;
 }
+
+int ia_pipeline_depend(ia_ctx *c, ia_ctx *prev, int prev_gen) {
+  if (!c || (prev && (prev == c || !prev->p_record || prev_gen < 1)))
+    return fail(IA_EINVAL, "ia_pipeline_depend: prev must be another context with pipeline_record = 1 and prev_gen >= 1");
+  c->dep = prev;
+  c->dep_gen = prev ? prev_gen : 0;
+  return IA_OK;
+}
+
+int ia_pipeline_generation(ia_ctx *c) { return c ? c->p_gen.load() : -1; }
 
 int ia_wavefront_shape(int h, int w, int64_t *steps, int64_t *max_queries) {
   if (h < 1 || w < 1) return fail(IA_EINVAL, "ia_wavefront_shape: empty level");
@@ -981,7 +1011,57 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   int64_t dist_launches = 0, launches_timed = 0, n_rec = 0;
   double dist_flops = 0., flops_timed = 0., pairs_full = 0., tiles_full = 0., bytes_timed_fixed = 0.;
   int ord_n = 0;  // pruned scan (k3p_variant 8): queries in the previous step's key order
-  for (int64_t t = 0; t < T; t++) {
+  // level pipelining: this level's per-step events (recording) / waits on the previous level
+  const int gen = c->p_record ? c->p_gen.load() + 1 : 0;
+  std::vector<hipEvent_t> *pev = nullptr;
+  if (gen) {
+    pev = &c->p_ev[gen % 3];
+    while ((int64_t)pev->size() < T) {
+      hipEvent_t e;
+      HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      pev->push_back(e);
+    }
+    c->p_enq.store(-1);
+    c->p_T.store(T);
+    c->p_gen.store(gen);  // published last: a dependent reads p_T / p_enq of this generation after it
+  }
+  struct PDone {  // every return from here on (errors too) releases the dependents' waits
+    ia_ctx *c;
+    int g;
+    ~PDone() {
+      if (g) c->p_done.store(g);
+    }
+  } pdone{c, gen};
+  ia_ctx *dp = c->dep;
+  const int dgen = c->dep_gen;
+  c->dep = nullptr;  // one level call per ia_pipeline_depend
+  c->dep_gen = 0;
+  int64_t waited = -1;
+  const auto t_start = std::chrono::steady_clock::now();
+  auto stalled = [&]() {  // the previous level's host thread stopped enqueueing (it failed)
+    return std::chrono::steady_clock::now() - t_start > std::chrono::seconds(120);
+  };
+  auto wait_dep = [&](int64_t t) -> int {
+    if (!dp) return IA_OK;
+    while (dp->p_gen.load() < dgen && dp->p_done.load() < dgen)  // it has started that level
+      if (stalled()) return fail(IA_ECOMM, "pipeline: the previous level did not start");
+      else std::this_thread::yield();
+    const int64_t need = std::min<int64_t>(t / 2 + 4, dp->p_T.load() - 1);
+    if (need <= waited) return IA_OK;
+    while (dp->p_done.load() < dgen && dp->p_enq.load() < need)
+      if (stalled()) return fail(IA_ECOMM, "pipeline: the previous level stopped enqueueing");
+      else std::this_thread::yield();
+    if (dp->p_done.load() < dgen) HIP_TRY(hipStreamWaitEvent(c->st, dp->p_ev[dgen % 3][need], 0));
+    waited = need;
+    return IA_OK;
+  };
+  auto mark_step = [&](int64_t t) {
+    if (!gen) return;
+    hipEventRecord((*pev)[t], c->st);
+    c->p_enq.store(t);
+  };
+  for (int64_t t = 0; t < T; mark_step(t), t++) {
+    if ((rc = wait_dep(t))) return rc;
     StepDesc sd;
     sd.t = (int)t;
     sd.J = J;

@@ -201,6 +201,18 @@ int ia_synthesize_level(ia_ctx *ctx, const ia_level_args *args, ia_stats *stats)
  * ("exchange" 0 / 1: every rank holds every job; emulated "exchange" = 2: one job per shard). */
 int ia_synthesize_levels(ia_ctx *ctx, const ia_level_args *args, int n_jobs, ia_stats *stats);
 
+/* Level pipelining: level l + 1 of a job only reads B' of level l near
+ * (r / 2, c / 2), so its wavefront step t needs level l's steps <= t / 2 + 4, not the whole level.
+ * Two contexts driven from two host threads run alternate levels concurrently: the context of
+ * level l has option "pipeline_record" = 1 (its level calls are numbered 1, 2, ...: generations,
+ * ia_pipeline_generation = the last one started) and before the level l + 1 call the other
+ * context calls ia_pipeline_depend(ctx, prev_ctx, generation of level l): each of its steps then
+ * waits (a stream event wait, no host sync) for the steps of level l it reads.  Results are those
+ * of the sequential order, bit for bit.  A previous level that stops for 120 s makes the
+ * dependent call fail with IA_ECOMM. */
+int ia_pipeline_depend(ia_ctx *ctx, ia_ctx *prev, int prev_gen);
+int ia_pipeline_generation(ia_ctx *ctx);
+
 /* ---- FLANN-compatible exact index (algorithms.py:56,69,74) -------------------------------- */
 /* build_index(pts): pts is n x d fp64 (row-major), d <= 167. */
 int ia_index_build(ia_ctx *ctx, const double *pts, int64_t n, int d, ia_index **out);
