@@ -82,9 +82,9 @@ class DeviceJob(object):
                                     ptrs, self.job.kappa_factor(l), stats)
 
     def run(self, ctx, torch, stats, pipe=None):
-        """pipe = a second context: levels alternate between the two, each level's steps waiting
-        only for the steps of the previous level they read (include/ia.h ia_pipeline_depend; two
-        host threads)"""
+        """pipe = more contexts (one or a list): levels rotate over ctx + them, each level's steps
+        waiting only for the steps of the previous level they read (include/ia.h
+        ia_pipeline_depend; one host thread per context)"""
         for l in range(self.job.L):
             self.Bp[l].copy_(self.Bp0[l])
         torch.cuda.synchronize()   # libia runs on its own stream
@@ -93,7 +93,8 @@ class DeviceJob(object):
                 self._level(ctx, l, stats)
             return
         from ia_amd.pipeline import run_levels_pipelined
-        run_levels_pipelined(lambda c, l, st: self._level(c, l, st), [ctx, pipe], self.job.L, stats)
+        run_levels_pipelined(lambda c, l, st: self._level(c, l, st), [ctx] + (pipe if isinstance(pipe, list) else [pipe]),
+                             self.job.L, stats)
 
 
 class DeviceBatch(object):
@@ -231,6 +232,8 @@ def make_context(args, local):
         cx.set_option('k3p_blocks', args.k3p_blocks)
     if args.prune_group != 1:
         cx.set_option('prune_group', args.prune_group)
+    if args.fuse_gather != 1:
+        cx.set_option('fuse_gather', args.fuse_gather)
     if args.row_source:
         cx.set_option('row_source', args.row_source)
     if args.shard_unpruned:
@@ -239,6 +242,17 @@ def make_context(args, local):
         cx.set_option('shard_emulate', args.shard_emulate)
         cx.set_option('exchange', EXCHANGE[args.exchange])   # the emulated shards' exchange kernels
     return cx
+
+
+def pipe_contexts(args, local, ctx):
+    """the extra contexts of level pipelining (--pipe-ctx - 1 of them); with --pipe-priority the
+    finest level's context (ctx) gets the high stream priority, the others the low one"""
+    extra = [make_context(args, local) for _ in range(args.pipe_ctx - 1)]
+    if args.pipe_priority:
+        ctx.set_option('stream_priority', 1)
+        for cx in extra:
+            cx.set_option('stream_priority', 2)
+    return extra
 
 
 def gather_rooflines(st):
@@ -320,6 +334,15 @@ def main():
                     help='1 (default; one-job configs and replicas): consecutive levels overlap (two libia '
                          'contexts, each level\'s steps waiting only for the steps of the previous level they read; '
                          'DESIGN.md §6b); 0: levels one after the other (always in the owner-computes shard mode)')
+    ap.add_argument('--fuse-gather', type=int, default=1, choices=[0, 1],
+                    help='1 (default): on pruned one-job levels the merge of step t and the gather of step t + 1 run '
+                         'as one launch (ia_kernels.hip k_merge_gather); 0: separate launches')
+    ap.add_argument('--pipe-ctx', type=int, default=4, choices=[2, 3, 4, 5],
+                    help='contexts the pipelined levels rotate over (default 4: the finest level\'s stream is free '
+                         'once level L - 5 ends; 2: level l + 2 follows level l on one stream; 5: above the box\'s '
+                         '4 hardware queues per process, measured slower, DESIGN.md §6b)')
+    ap.add_argument('--pipe-priority', type=int, default=1, choices=[0, 1],
+                    help='1: the finest level\'s stream at high priority, the coarser levels\' at low')
     ap.add_argument('--k3p-blocks', type=int, default=1, choices=[0, 1],
                     help='pruned scan of a step wider than 11 query tiles: 1 = one launch of (query block x DB '
                          'chunk) workgroups, 0 = one launch per query block')
@@ -456,7 +479,7 @@ def main():
         ctx = make_context(args, local)
         args.mode, args.shard_jobs, owner = 'replicas', 1, False
         d = DeviceJob(jobs_b[0], torch, dev)
-        p2 = make_context(args, local) if args.pipeline else None
+        p2 = pipe_contexts(args, local, ctx) if args.pipeline else None
         return d, (lambda st, cs=None: d.run(ctx, torch, st, pipe=p2 if cs is None else None))
     ctxs = [ctx]
     if sw is not None:
@@ -476,7 +499,7 @@ def main():
         run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
     elif args.pipeline:
         dj = DeviceJob(job, torch, dev)
-        pctx = make_context(args, local)
+        pctx = pipe_contexts(args, local, ctx)
         # the roofline's single-stream pass (run(st, [ctx])) runs the levels one after the other
         run = lambda st, cs=None: dj.run(ctx, torch, st, pipe=pctx if cs is None else None)
     else:
@@ -649,8 +672,10 @@ def main():
                                                            'dbshard%d_jobs%d' % (max(world, args.shard_emulate),
                                                                                  args.shard_jobs)),
                                            'jobs_per_step': jobs,
-                                           'level_pipeline': bool(args.pipeline and sw is None and not owner and
-                                                                  args.shard_jobs <= 1),
+                                           'level_pipeline': (('%d contexts%s' % (args.pipe_ctx, ', finest level high priority'
+                                                                                  if args.pipe_priority else ''))
+                                                              if args.pipeline and sw is None and not owner and
+                                                              args.shard_jobs <= 1 else None),
                                            'nn': 'exact: %s MFMA candidates + certified fp64 rerank'
                                                  % ('split-f16 (hi/lo x3)' if f16 else 'fp32'),
                                            'precision': ('f16x3 = every operand split into f16 hi + lo, 3 MFMA '

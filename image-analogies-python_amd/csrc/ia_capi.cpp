@@ -113,6 +113,10 @@ struct ia_ctx {
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   int k3p_blocks = 1;            // option "k3p_blocks": 1 = a wide step's presorted pruned scan is one launch over
                                  // all its query blocks (2-D grid); 0 = one launch per block
+  int fuse_gather = 1;           // option "fuse_gather": 1 = K4 of step t and K2p of step t + 1 in one launch
+  HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
+  int hand_rows = 0;
+  unsigned hseq = 0;
   // per-step K3 timing (optional)
   int time_dist = 0;
   std::vector<hipEvent_t> evs, evg, evm;  // sampled steps: K3, K2 and K4 brackets
@@ -369,6 +373,7 @@ void ia_destroy(ia_ctx *c) {
   for (int p = 0; p < IA_XCHG_MAXW; p++)
     if (c->xmapped[p]) hipIpcCloseMemHandle(c->xpeer[p]);
   if (c->xbuf) hipFree(c->xbuf);
+  if (c->hand) hipFree(c->hand);
   c->xerr.release();
   c->xo_inv.release();
   hipStreamDestroy(c->st);
@@ -448,9 +453,30 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     c->k3p_blocks = value;
     return IA_OK;
   }
+  if (!std::strcmp(name, "fuse_gather")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_gather must be 0 or 1");
+    c->fuse_gather = value;
+    return IA_OK;
+  }
   if (!std::strcmp(name, "pipeline_record")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: pipeline_record must be 0 or 1");
     c->p_record = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "stream_priority")) {
+    // 0 = default, 1 = high, 2 = low: the stream is recreated (idle contexts only); level
+    // pipelining gives the finest level's context the high priority so the
+    // coarser levels' kernels fill its gaps instead of delaying its steps
+    if (value < 0 || value > 2) return fail(IA_EINVAL, "ia_set_option: stream_priority must be 0, 1 (high) or 2 (low)");
+    if (std::getenv("IA_CU_SPLIT")) return fail(IA_EINVAL, "ia_set_option: stream_priority with IA_CU_SPLIT");
+    HIP_TRY(hipSetDevice(c->dev));
+    int least = 0, greatest = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIP_TRY(hipStreamSynchronize(c->st));
+    hipStream_t ns = nullptr;
+    HIP_TRY(hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, value == 0 ? 0 : value == 1 ? greatest : least));
+    hipStreamDestroy(c->st);
+    c->st = ns;
     return IA_OK;
   }
   if (!std::strcmp(name, "xo_presort")) {
@@ -892,13 +918,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   // per-level scratch
   if ((rc = c->db.ensure((size_t)std::max(ns, 1) * IA_TILE * db_row_bytes)) || (rc = c->mu.ensure((16 + 4 * 3 * 128) * 8)) ||
       (rc = c->db64.ensure((size_t)g.NA * ia_db64_stride(g.ch) * 8)) ||
-      (rc = c->Rbits.ensure(4)) || (rc = c->q64.ensure((size_t)Mpad_max * g.D * 8)) ||
-      (rc = c->qn2.ensure((size_t)Mpad_max * 8)) || (rc = c->qf.ensure((size_t)Mpad_max * db_row_bytes)) ||
+      (rc = c->Rbits.ensure(4)) || (rc = c->q64.ensure((size_t)Mpad_max * g.D * 8 * 2)) ||
+      (rc = c->qn2.ensure((size_t)Mpad_max * 8 * 2)) || (rc = c->qf.ensure((size_t)Mpad_max * db_row_bytes)) ||
       (rc = c->rec.ensure(rec_stride * shards.size() * 16)) || (rc = c->recT.ensure(rec_stride * shards.size() * 4)) ||
       (rc = c->win.ensure((size_t)Mtmax * 16)) || (rc = c->allwin.ensure((size_t)Mtmax * 16 * Wsh)) ||
       (rc = c->counters.ensure(5 * 8)) ||
       (rc = c->pairs.ensure(4 * IA_NWG_H * 8)) || (rc = c->ord.ensure(2 * 4096 * 4)) ||
-      (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 : 16)))
+      (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 * 2 : 16)))
     return rc;
   if (prune && ((rc = c->qs_order.ensure((size_t)Mpad_max * 4)) || (rc = c->qs_info.ensure((size_t)Mpad_max * 3 * 16)) ||
                 (rc = c->qs_frag.ensure((size_t)Mpad_max * db_row_bytes)) ||
@@ -994,6 +1020,35 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
 
   const int qtmax = use_h ? ia_k3h_qtmax(g.KS) : ia_k3_qtmax(g.KH);
   const int stride = c->time_dist > 0 ? c->time_dist : 0;
+  // fused K4(t) + K2p(t + 1) (option "fuse_gather", ia_kernels.hip k_merge_gather): one-job
+  // unsharded pruned levels whose every step takes the in-kernel-sort scan (<= 256 records per
+  // query); the query buffers alternate by step parity
+  const int kv0 = c->k3p_variant;
+  const bool chain = c->fuse_gather && prune && !multi && !xo && J == 1 && !rot && ma.img_rows == 0 && g.bw >= 3 &&
+                     Mpad_max <= std::min(512, qtmax * IA_TILE) && mas[0].nwg <= 4 * IA_WAVE &&
+                     !(kv0 == 11 || kv0 == 12 || kv0 == 15 || kv0 == 17 || kv0 == 19 || kv0 == 21);
+  if (chain) {
+    if (c->hand_rows < g.bh) {
+      HIP_TRY(hipStreamSynchronize(c->st));
+      if (c->hand) hipFree(c->hand);
+      c->hand = nullptr;
+      c->hand_rows = 0;
+      HIP_TRY(hipExtMallocWithFlags((void **)&c->hand, (size_t)g.bh * sizeof(HandSlot), hipDeviceMallocUncached));
+      HIP_TRY(hipMemset(c->hand, 0, (size_t)g.bh * sizeof(HandSlot)));
+      HIP_TRY(hipDeviceSynchronize());
+      c->hand_rows = g.bh;
+    }
+    if ((rc = c->xerr.ensure(4))) return rc;
+    HIP_TRY(hipMemsetAsync(c->xerr.p, 0, 4, c->st));
+  }
+  // query buffers of step t (chain: parity half t & 1)
+  auto qhalf = [&](int64_t t, double *&q64, double *&qn2, float4 *&qinfo) {
+    const size_t h = chain && (t & 1) ? 1 : 0;
+    q64 = c->q64.as<double>() + h * Mpad_max * g.D;
+    qn2 = c->qn2.as<double>() + h * Mpad_max;
+    qinfo = prune ? c->qinfo.as<float4>() + h * 3 * Mpad_max : nullptr;
+  };
+  int64_t gathered = -1;  // the step whose gather the previous fused launch ran
   const int64_t n_timed = stride ? (T + stride - 1) / stride : 0;
   for (auto *v : {&c->evs, &c->evg, &c->evm})
     if ((int64_t)v->size() < 2 * n_timed) {
@@ -1199,16 +1254,25 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       if (timed_gm) hipEventRecord(c->evm[2 * n_gm++ + 1], c->st);
       continue;
     }
+    double *q64t, *qn2t;
+    float4 *qinfot;
+    qhalf(t, q64t, qn2t, qinfot);
+    if (chain) {
+      mas[0].q64 = q64t;
+      mas[0].qn2 = qn2t;
+      mas[0].qinfo = qinfot;
+    }
 #ifdef IA_K3H_DIAG
     if (rot)
       ia_launch_gather_r(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
                          c->db64.as<double>(), c->pr_basis.as<double>(), ufac, ra, c->qinfo.as<float4>(), Aim, c->st);
     else
 #endif
-    if (prune)
-      ia_launch_gather_p(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
-                         c->db64.as<double>(), c->pr_basis.as<double>(), ufac, c->qinfo.as<float4>(), Aim, ma.img_rows,
-                         c->st);
+    if (prune && gathered == t)
+      ;  // K2p of this step ran in the previous step's fused merge
+    else if (prune)
+      ia_launch_gather_p(g, sd, Bim, djobs, c->mu.as<double>(), q64t, qn2t, c->qf.p, c->db64.as<double>(),
+                         c->pr_basis.as<double>(), ufac, qinfot, Aim, ma.img_rows, c->st);
     else if (use_h)
       ia_launch_gather_h(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p, c->st);
     else
@@ -1274,7 +1338,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t,
                           c->qs_order.as<int>(), 0, sd.r0, nullptr, c->qs_tbox.as<float4>(), tn, c->st);
           else if (prune)
-            ia_launch_k3p(qt, dbp, c->qf.p, c->qinfo.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
+            ia_launch_k3p(qt, dbp, c->qf.p, qinfot, m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
                           k3v, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
@@ -1305,7 +1369,26 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       ord_n = prune && J == 1 && !multi && sd.Mpad <= 4096 ? sd.M : 0;
     }
     if (timed_gm) hipEventRecord(c->evm[2 * n_gm], c->st);
-    if (!multi) {
+    if (!multi && chain && t + 1 < T && !(stride && (t % stride == 0 || (t + 1) % stride == 0))) {
+      // this step's merge + the next step's gather (not on sampled steps: their K2 / K4 brackets)
+      if ((rc = wait_dep(t + 1))) return rc;  // the next step's gather reads the previous level
+      NextStep nx{};
+      nx.sn.t = (int)(t + 1);
+      nx.sn.J = 1;
+      ia_wavefront_step(g.bh, g.bw, t + 1, &nx.sn.r0, &nx.sn.M);
+      nx.sn.Mpad = (nx.sn.M + IA_TILE - 1) / IA_TILE * IA_TILE;
+      qhalf(t + 1, nx.q64, nx.qn2, nx.qinfo);
+      nx.mu = c->mu.as<double>();
+      nx.basis = c->pr_basis.as<double>();
+      nx.qf = c->qf.p;
+      nx.ufac = ufac;
+      nx.hand = c->hand;
+      nx.seq = ++c->hseq;
+      nx.err = c->xerr.as<unsigned>();
+      nx.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
+      ia_launch_merge_gather(g, sd, Aim, mas[0], djobs, Bim, nx, c->st);
+      gathered = t + 1;
+    } else if (!multi) {
       ia_launch_merge(g, sd, Aim, mas[0], c->win.as<Winner>(), djobs, true, c->st);
     } else if (xchg) {
       // one-shot peer-write exchange fused into the merge: each shard's winner goes into every
@@ -1353,6 +1436,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
 #if IA_PROBE & 16
   if (prune) ia_k3p_probe_dump();
 #endif
+  if (chain) {
+    unsigned xe = 0;
+    HIP_TRY(hipMemcpy(&xe, c->xerr.p, 4, hipMemcpyDeviceToHost));
+    if (xe & 16) return fail(IA_EHIP, "ia_synthesize_level: a fused gather's handoff did not arrive within 20 s");
+  }
   if (xchg || xo) {
     unsigned xe = 0;
     HIP_TRY(hipMemcpy(&xe, c->xerr.p, 4, hipMemcpyDeviceToHost));

@@ -328,6 +328,27 @@ struct XOScan {
   long long timeout_ticks;
 };
 
+// fused K4(t) + K2p(t + 1) (k_merge_gather, option "fuse_gather"): the next step's gather
+// outputs (the other parity half of the query buffers) and the per-row handoff slots
+struct HandSlot {          // uncached: row r's step-t result for row r + 1's step-(t + 1) query
+  double v;                // B' value
+  int sr, sc, im;          // source pixel, A' image
+  unsigned seq;            // the step's seq, stored after the fields above completed
+  unsigned pad[2];
+};
+struct NextStep {
+  StepDesc sn;             // step t + 1
+  const double *mu, *basis;
+  double *q64, *qn2;
+  void *qf;
+  float4 *qinfo;
+  double ufac;
+  HandSlot *hand;          // one slot per B row
+  unsigned seq;
+  unsigned *err;           // bit 4: a handoff did not arrive in time
+  long long timeout_ticks;
+};
+
 __host__ __device__ inline int ia_reflect(int i, int n) {
   // np.pad(mode='symmetric') index map (img_preprocess.py:81-83).  Windows reach at most 2
   // pixels past an edge, so two folds suffice unless the image is narrower than the window;

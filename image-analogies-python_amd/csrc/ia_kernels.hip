@@ -1282,6 +1282,125 @@ __device__ __forceinline__ double wave_sum_d_x(double v) {  // fixed butterfly o
   else return v;
 }
 
+// The two pixels of step t whose results a fused K4(t) + K2p(t + 1) wave (k_merge_gather) hands
+// to its next query: its own (r0, c0) and the row above's (r1, c1), both written in the same
+// launch, so their B', s and im come from registers / the handoff slot, never from memory.
+struct QHand {
+  int r0 = -1, c0 = -1, r1 = -1, c1 = -1;
+  double v0 = 0., v1 = 0.;
+  int s0r = 0, s0c = 0, i0 = 0, s1r = 0, s1c = 0, i1 = 0;
+};
+template <bool FUSE>
+__device__ __forceinline__ double feat_q1(const Imgs &B, int f, int r, int c, const QHand &h) {
+  if constexpr (FUSE) {
+    if (f >= 43) {  // the B' part (causal 5x5 at (r, c), k < 12)
+      const int k = f - 43, y = ia_reflect(r + k / 5 - 2, B.h), x = ia_reflect(c + k % 5 - 2, B.w);
+      if (y == h.r0 && x == h.c0) return h.v0;
+      if (y == h.r1 && x == h.c1) return h.v1;
+      return B.p3[(int64_t)y * B.w + x];
+    }
+  }
+  return feat<1>(B, f, r, c, 0);
+}
+
+// K2p's pad query m >= J M: zero fragments, an empty pruning record
+template <int KS>
+__device__ __forceinline__ void gather_p_pad(int m, int lane, _Float16 *qf, float4 *qinfo, float4 &o0, float4 &o1,
+                                             float4 &o2) {
+  if (lane < 16 * KS) put_qh<KS>(qf, m, lane, 0.);
+  o0 = o1 = make_float4(0.f, 0.f, 0.f, 0.f);
+  o2 = make_float4(-INFINITY, __uint_as_float(IA_PRUNE_KEY_PAD), -INFINITY, 0.f);
+  if (lane == 0) {
+    qinfo[3 * m] = o0;
+    qinfo[3 * m + 1] = o1;
+    qinfo[3 * m + 2] = o2;
+  }
+}
+
+// K2p's work for one query m of step sd (one wave): q64, qn2, fragments, pruning record (also
+// returned, uniform, for the owner-computes publish); xh0 / xh1 (optional) receive the query's
+// hi / lo columns
+template <int KS, bool IMG, bool FUSE>
+__device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobPtrs &jp, int m,
+                                               int lane, const double *__restrict__ mu_part, double *__restrict__ q64,
+                                               double *__restrict__ qn2, _Float16 *__restrict__ qf,
+                                               const double *__restrict__ db64, const double *__restrict__ basis, double ufac,
+                                               float4 *__restrict__ qinfo, const Imgs &A, double *qsh, _Float16 *xh0,
+                                               _Float16 *xh1, const QHand &h, float4 &o0, float4 &o1, float4 &o2) {
+  constexpr int D = 55, KD = 16 * KS;
+  static_assert(KD <= IA_WAVE, "one feature per lane");
+  const QPix px = ia_qpix(sd, g.bw, m);
+  const int32_t *__restrict__ s = jp.s, *__restrict__ im = jp.im;
+  const int r = px.r, c = px.c, qi = px.qi;
+  // coherence candidate of this lane (lanes 0..14, product(rows, cols) order as merge_fused)
+  int crow = -1;
+  if (qi > 0 && lane < 15) {
+    const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
+    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
+      const int nb = nr * g.bw + nc;
+      int sr, sc, si;
+      if (FUSE && nr == h.r0 && nc == h.c0) {
+        sr = h.s0r; sc = h.s0c; si = h.i0;
+      } else if (FUSE && nr == h.r1 && nc == h.c1) {
+        sr = h.s1r; sc = h.s1c; si = h.i1;
+      } else {
+        sr = s[2 * nb]; sc = s[2 * nb + 1]; si = im[nb];
+      }
+      const int tr = sr + r - nr, tc = sc + c - nc;
+      if (tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) crow = (si * g.ah + tr) * g.aw + tc;
+    }
+  }
+  double ss = 0., p[IA_NPC];
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) p[i] = 0.;
+  if (lane < KD) {
+    const int f = lane;
+    if (f < D) {
+      const double v = feat_q1<FUSE>(B, f, r, c, h);
+      q64[(int64_t)m * D + f] = v;
+      qsh[f] = v;
+      const double qc = v - mu_part[feat_part<1>(f)];
+      ss = qc * qc;
+      put_qh<KS>(qf, m, f, -2.0 * qc);
+      if (xh0) split_h(-2.0 * qc, xh0[f], xh1[f]);
+#pragma unroll
+      for (int i = 0; i < IA_NPC; i++) p[i] = basis[i * D + f] * qc;
+    } else {
+      put_qh<KS>(qf, m, f, f == D ? IA_NORM_SCALE : 0.);
+      if (xh0) split_h(f == D ? IA_NORM_SCALE : 0., xh0[f], xh1[f]);
+    }
+  }
+  ss = wave_sum_d(ss);
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) p[i] = wave_sum_d_x(p[i]);
+  __builtin_amdgcn_wave_barrier();  // qsh written by this wave's lanes, read below
+  double u = DBL_MAX;
+  if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh, IMG ? &A : nullptr);
+  u = wave_min_d_x(u);
+  // the pruning record (uniform values): projection interval, U' and the Morton key, and K3p's
+  // hi x hi block filter bound (k3p_variant 14/15, ia_k3h.hip k3p_filtered): value bound
+  // z >= U' - |q'|^2 with the f32 rounding of z and of the kernel's lim = z + R_t (...)
+  // (2^-22 (|q'|^2 + U')) and the subnormal / norm-column terms (2^-24 (16 |q'| + 300));
+  // w = 2^-8 |q'| (twice the relative error term's |q'| part)
+  const double qn = sqrt(ss);
+  const bool fin = u < DBL_MAX;
+  const unsigned key = fin ? prune_key(p, basis + IA_NPC * D) : IA_PRUNE_KEY_INF;
+  const float up = fin ? round_up_f(u * ufac) : INFINITY;
+  const float z = fin ? round_up_f((double)up - ss + 0x1p-22 * (ss + (double)up) + 0x1p-24 * (16.0 * qn + 300.0)) : INFINITY;
+  const float w = round_up_f(0x1p-8 * qn * (1.0 + 0x1p-40));
+  o0 = make_float4(round_down_f(p[0] - IA_PRUNE_MABS), round_down_f(p[1] - IA_PRUNE_MABS), round_down_f(p[2] - IA_PRUNE_MABS),
+                   round_down_f(p[3] - IA_PRUNE_MABS));
+  o1 = make_float4(round_up_f(p[0] + IA_PRUNE_MABS), round_up_f(p[1] + IA_PRUNE_MABS), round_up_f(p[2] + IA_PRUNE_MABS),
+                   round_up_f(p[3] + IA_PRUNE_MABS));
+  o2 = make_float4(up, __uint_as_float(key), z, w);
+  if (lane == 0) {
+    qn2[m] = ss;
+    qinfo[3 * m] = o0;
+    qinfo[3 * m + 1] = o1;
+    qinfo[3 * m + 2] = o2;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // K2p: K2h for the pruned scan (1 channel) — one wave per query.  Besides the split-f16 query
 // fragments it writes the query's pruning record (ia_prune.h), qinfo[3m .. 3m+2]:
@@ -1298,121 +1417,42 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_gather_query_p(LevelGeo g, StepDes
                                                           _Float16 *__restrict__ qf, const double *__restrict__ db64,
                                                           const double *__restrict__ basis, double ufac,
                                                           float4 *__restrict__ qinfo, Imgs A, XOPub xp) {
-  constexpr int D = 55, KD = 16 * KS;
-  static_assert(KD <= IA_WAVE, "one feature per lane");
+  constexpr int KD = 16 * KS;
   __shared__ double qsh[IA_PQ_WPB][Geo<1>::DS];
   __shared__ __attribute__((aligned(16))) _Float16 xh[IA_PQ_WPB][2][KD];  // owner publish: the query's hi / lo columns
   const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int m = blockIdx.x * IA_PQ_WPB + wv;
   if (m >= sd.Mpad) return;
+  float4 i0, i1, i2;
+  if (m >= sd.J * sd.M) {
+    gather_p_pad<KS>(m, lane, qf, qinfo, i0, i1, i2);
+    if (xp.W && lane < KD) xh[wv][0][lane] = xh[wv][1][lane] = (_Float16)0.f;
+  } else {
+    const QPix px = ia_qpix(sd, g.bw, m);
+    const JobPtrs jp = jobs.get(px.job);
+    if constexpr (!JS::single) B = job_imgs(B, jp);  // single job: B already holds its images
+    gather_p_query<KS, IMG, false>(g, sd, B, jp, m, lane, mu_part, q64, qn2, qf, db64, basis, ufac, qinfo, A, qsh[wv],
+                                   xp.W ? xh[wv][0] : nullptr, xh[wv][1], QHand{}, i0, i1, i2);
+  }
+  if (!xp.W) return;
   // owner-computes sharded step (XOPub): the query's fragments (16 h16x8 pieces from LDS, one
   // store instruction per area), its pruning record, then - once those stores completed - its
   // seq, into every rank's area
-  auto publish = [&](float4 i0, float4 i1, float4 i2) {
-    __builtin_amdgcn_wave_barrier();  // xh written by this wave's lanes
-    const int qt = m / IA_TILE, j = m % IA_TILE;
-    const int c = lane, sp = c >> 2, part = (c >> 1) & 1, h = c & 1;  // chunk c < 2 KS * 2
-    h16x8 v{};
-    if (c < 4 * KS) v = *reinterpret_cast<const h16x8 *>(&xh[wv][part][16 * sp + 8 * h]);
-    const int64_t t0 = xp.slot0 / IA_TILE;
-    for (int o = 0; o < xp.W; o++) {
-      if (c < 4 * KS)
-        reinterpret_cast<h16x8 *>(xp.area[o] + XOLayout::FRAG)[((t0 + qt) * 2 * KS + 2 * sp + part) * IA_WAVE + h * IA_TILE + j] = v;
-      if (lane < 3) reinterpret_cast<float4 *>(xp.area[o] + XOLayout::INFO)[3 * (xp.slot0 + m) + lane] = lane == 0 ? i0 : lane == 1 ? i1 : i2;
-    }
-    ia_stores_done();
-    if (lane < xp.W)
-      __hip_atomic_store(reinterpret_cast<unsigned *>(xp.area[lane] + XOLayout::QSEQ) + xp.slot0 + m, xp.seq, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_SYSTEM);
-  };
-  if (m >= sd.J * sd.M) {
-    if (lane < KD) put_qh<KS>(qf, m, lane, 0.);
-    const float4 i0 = make_float4(0.f, 0.f, 0.f, 0.f), i2 = make_float4(-INFINITY, __uint_as_float(IA_PRUNE_KEY_PAD), -INFINITY, 0.f);
-    if (lane == 0) {
-      qinfo[3 * m] = i0;
-      qinfo[3 * m + 1] = i0;
-      qinfo[3 * m + 2] = i2;
-    }
-    if (xp.W) {
-      if (lane < KD) xh[wv][0][lane] = xh[wv][1][lane] = (_Float16)0.f;
-      publish(i0, i0, i2);
-    }
-    return;
+  __builtin_amdgcn_wave_barrier();  // xh written by this wave's lanes
+  const int qt = m / IA_TILE, j = m % IA_TILE;
+  const int c = lane, sp = c >> 2, part = (c >> 1) & 1, h = c & 1;  // chunk c < 2 KS * 2
+  h16x8 v{};
+  if (c < 4 * KS) v = *reinterpret_cast<const h16x8 *>(&xh[wv][part][16 * sp + 8 * h]);
+  const int64_t t0 = xp.slot0 / IA_TILE;
+  for (int o = 0; o < xp.W; o++) {
+    if (c < 4 * KS)
+      reinterpret_cast<h16x8 *>(xp.area[o] + XOLayout::FRAG)[((t0 + qt) * 2 * KS + 2 * sp + part) * IA_WAVE + h * IA_TILE + j] = v;
+    if (lane < 3) reinterpret_cast<float4 *>(xp.area[o] + XOLayout::INFO)[3 * (xp.slot0 + m) + lane] = lane == 0 ? i0 : lane == 1 ? i1 : i2;
   }
-  const QPix px = ia_qpix(sd, g.bw, m);
-  const JobPtrs jp = jobs.get(px.job);
-  if constexpr (!JS::single) B = job_imgs(B, jp);  // single job: B already holds its images
-  const int32_t *__restrict__ s = jp.s, *__restrict__ im = jp.im;
-  const int r = px.r, c = px.c, qi = px.qi;
-  // coherence candidate of this lane (lanes 0..14, product(rows, cols) order as merge_fused)
-  int crow = -1;
-  if (qi > 0 && lane < 15) {
-    const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
-    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
-      const int nb = nr * g.bw + nc;
-      const int tr = s[2 * nb] + r - nr, tc = s[2 * nb + 1] + c - nc;
-      if (tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) crow = (im[nb] * g.ah + tr) * g.aw + tc;
-    }
-  }
-  double ss = 0., p[IA_NPC];
-#pragma unroll
-  for (int i = 0; i < IA_NPC; i++) p[i] = 0.;
-  if (lane < KD) {
-    const int f = lane;
-    if (f < D) {
-      const double v = feat<1>(B, f, r, c, 0);
-      q64[(int64_t)m * D + f] = v;
-      qsh[wv][f] = v;
-      const double qc = v - mu_part[feat_part<1>(f)];
-      ss = qc * qc;
-      put_qh<KS>(qf, m, f, -2.0 * qc);
-      if (xp.W) split_h(-2.0 * qc, xh[wv][0][f], xh[wv][1][f]);
-#pragma unroll
-      for (int i = 0; i < IA_NPC; i++) p[i] = basis[i * D + f] * qc;
-    } else {
-      put_qh<KS>(qf, m, f, f == D ? IA_NORM_SCALE : 0.);
-      if (xp.W) split_h(f == D ? IA_NORM_SCALE : 0., xh[wv][0][f], xh[wv][1][f]);
-    }
-  }
-  ss = wave_sum_d(ss);
-#pragma unroll
-  for (int i = 0; i < IA_NPC; i++) p[i] = wave_sum_d_x(p[i]);
-  __builtin_amdgcn_wave_barrier();  // qsh written by this wave's lanes, read below
-  double u = DBL_MAX;
-  if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh[wv], IMG ? &A : nullptr);
-  u = wave_min_d_x(u);
-  if (lane == 0) {
-    qn2[m] = ss;
-    qinfo[3 * m] = make_float4(round_down_f(p[0] - IA_PRUNE_MABS), round_down_f(p[1] - IA_PRUNE_MABS),
-                               round_down_f(p[2] - IA_PRUNE_MABS), round_down_f(p[3] - IA_PRUNE_MABS));
-    qinfo[3 * m + 1] = make_float4(round_up_f(p[0] + IA_PRUNE_MABS), round_up_f(p[1] + IA_PRUNE_MABS),
-                                   round_up_f(p[2] + IA_PRUNE_MABS), round_up_f(p[3] + IA_PRUNE_MABS));
-    const bool fin = u < DBL_MAX;
-    const unsigned key = fin ? prune_key(p, basis + IA_NPC * D) : IA_PRUNE_KEY_INF;
-    const float up = fin ? round_up_f(u * ufac) : INFINITY;
-    // K3p's hi x hi block filter (k3p_variant 14/15, ia_k3h.hip k3p_filtered): value bound
-    // z >= U' - |q'|^2 with the f32 rounding of z and of the kernel's lim = z + R_t (...)
-    // (2^-22 (|q'|^2 + U')) and the subnormal / norm-column terms (2^-24 (16 |q'| + 300));
-    // w = 2^-8 |q'| (twice the relative error term's |q'| part)
-    const double qn = sqrt(ss);
-    const float z = fin ? round_up_f((double)up - ss + 0x1p-22 * (ss + (double)up) + 0x1p-24 * (16.0 * qn + 300.0))
-                        : INFINITY;
-    const float w = round_up_f(0x1p-8 * qn * (1.0 + 0x1p-40));
-    qinfo[3 * m + 2] = make_float4(up, __uint_as_float(key), z, w);
-  }
-  if (xp.W) {  // the record as lane 0 wrote it, on every lane (uniform values)
-    const double qn = sqrt(ss);
-    const bool fin = u < DBL_MAX;
-    const float up = fin ? round_up_f(u * ufac) : INFINITY;
-    const float z = fin ? round_up_f((double)up - ss + 0x1p-22 * (ss + (double)up) + 0x1p-24 * (16.0 * qn + 300.0)) : INFINITY;
-    const float w = round_up_f(0x1p-8 * qn * (1.0 + 0x1p-40));
-    const unsigned key = fin ? prune_key(p, basis + IA_NPC * D) : IA_PRUNE_KEY_INF;
-    publish(make_float4(round_down_f(p[0] - IA_PRUNE_MABS), round_down_f(p[1] - IA_PRUNE_MABS),
-                        round_down_f(p[2] - IA_PRUNE_MABS), round_down_f(p[3] - IA_PRUNE_MABS)),
-            make_float4(round_up_f(p[0] + IA_PRUNE_MABS), round_up_f(p[1] + IA_PRUNE_MABS),
-                        round_up_f(p[2] + IA_PRUNE_MABS), round_up_f(p[3] + IA_PRUNE_MABS)),
-            make_float4(up, __uint_as_float(key), z, w));
-  }
+  ia_stores_done();
+  if (lane < xp.W)
+    __hip_atomic_store(reinterpret_cast<unsigned *>(xp.area[lane] + XOLayout::QSEQ) + xp.slot0 + m, xp.seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
 #ifdef IA_K3H_DIAG  // k3p_variant 16 / 17: DIAG=1 builds only
@@ -1581,6 +1621,11 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_r(LevelGeo g, StepDesc s
 
 #endif  // IA_K3H_DIAG
 
+struct MergeOut {  // one pixel's result: B' value (first channel), source pixel and A' image
+  double v;
+  int pr, pc, img;
+};
+
 // Fused single-rank merge of query m: certified exact NN + coherence + kappa + writeback.
 // Memory is touched in two dependent rounds: (1) the K3 records, the coherence neighbours'
 // s/im and the query/weights (staged in LDS), (2) ONE fp64-DB row per lane, in which lane
@@ -1592,7 +1637,8 @@ __global__ void __launch_bounds__(IA_WG) k_gather_query_r(LevelGeo g, StepDesc s
 template <int CH, bool IMG, int RPL>
 __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &a,
                                             int m, const JobPtrs &jp, const QPix &px,
-                                            double *qs, double *ws, int *cand_row, float *cand_v) {
+                                            double *qs, double *ws, int *cand_row, float *cand_v,
+                                            MergeOut *out = nullptr) {
 #if IA_PROBE & 8
   unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1905,6 +1951,12 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
       jp.dbg_dist[2 * qi + 1] = dbg_coh;
     }
   }
+  if (out) {  // the pixel's result (wave-uniform) for a fused next-step gather (k_merge_gather)
+    out->v = val[0];
+    out->pr = pr;
+    out->pc = pc;
+    out->img = img;
+  }
 #if IA_PROBE & 8
   if (lane == 0 && m == sd.M / 2 && (sd.t % 256) == 128) {
     __builtin_amdgcn_s_waitcnt(0);
@@ -1958,6 +2010,89 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_level(LevelGeo g, StepDesc s
       if (jp.pstat) jp.pstat[px.qi] = stat;  // finish adds the coherence bit
     }
   }
+}
+
+// ------------------------------------------------------------------------------------------
+// K4 + K2p fused (option "fuse_gather"): K4 of step t, then K2p of step t + 1, one launch.
+// Pixel (r, c + 1) of step t + 1 reads two results of step t: its own row's (r, c) and the row
+// above's (r - 1, c + 3) (skew 3: both lie on step t); everything else it reads is older.  So
+// wave w (query w of step t, row r = r0 + w) merges (r, c), hands its result to row r + 1
+// through an uncached slot (fields, store completion, then the step's seq), and gathers
+// (r, c + 1), waiting for the slot of row r - 1: a wave of the same launch with a LOWER index
+// (rows ascend with the query index), dispatched before it, so the waits always drain.  Wave
+// M gathers the row entering at step t + 1 (column 0; its row above is wave M - 1), the waves
+// after it the step's pad queries.  The query buffers alternate by step parity (this launch's
+// merge reads step t's half while its gathers write step t + 1's).
+// ------------------------------------------------------------------------------------------
+template <int RPL>
+__global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, JobArg1 jobs,
+                                                         Imgs B, NextStep nx) {
+  constexpr int KS = 4;
+  const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * IA_PQ_WPB + (threadIdx.x >> 6));
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const JobPtrs jp = jobs.j0;
+  __shared__ double qsh[IA_PQ_WPB][Geo<1>::DS], wsh[IA_PQ_WPB][Geo<1>::DS];
+  __shared__ int crsh[IA_PQ_WPB][IA_WAVE];
+  __shared__ float cvsh[IA_PQ_WPB][IA_WAVE];
+  QHand h;
+  int mn = -1;  // this wave's query of step t + 1
+  if (w < sd.M) {
+    const QPix px = ia_qpix(sd, g.bw, w);
+    MergeOut o;
+    merge_fused<1, false, RPL>(g, sd, A, ma, w, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv], &o);
+    if (px.r + 1 < g.bh && px.c >= 2) {  // row r + 1 gathers (r + 1, c - 2) at step t + 1
+      HandSlot *hs = nx.hand + px.r;
+      if (lane == 0) {
+        hs->v = o.v;
+        hs->sr = o.pr;
+        hs->sc = o.pc;
+        hs->im = o.img;
+      }
+      ia_stores_done();
+      if (lane == 0) __hip_atomic_store(&hs->seq, nx.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    h.r0 = px.r;
+    h.c0 = px.c;
+    h.v0 = o.v;
+    h.s0r = o.pr;
+    h.s0c = o.pc;
+    h.i0 = o.img;
+    if (px.c + 1 < g.bw) mn = px.r - nx.sn.r0;
+  } else if (w == sd.M) {
+    if (nx.sn.t - 3 * (nx.sn.r0 + nx.sn.M - 1) == 0) mn = nx.sn.M - 1;  // a row enters at column 0
+  } else {
+    mn = nx.sn.M + (w - sd.M - 1);
+  }
+  if (mn < 0 || mn >= nx.sn.Mpad) return;
+  _Float16 *qf = (_Float16 *)nx.qf;
+  float4 o0, o1, o2;
+  if (mn >= nx.sn.M) {
+    gather_p_pad<KS>(mn, lane, qf, nx.qinfo, o0, o1, o2);
+    return;
+  }
+  const QPix pn = ia_qpix(nx.sn, g.bw, mn);
+  if (pn.r >= 1 && pn.c + 2 < g.bw) {  // (r - 1, c + 2) of step t: the row above's handoff
+    const HandSlot *hs = nx.hand + (pn.r - 1);
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    // relaxed: the slot is uncached (nothing stale to invalidate); its fields load after the
+    // seq was seen
+    while (__hip_atomic_load(&hs->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != nx.seq) {
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > nx.timeout_ticks) {
+        atomicOr(nx.err, 16u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    h.r1 = pn.r - 1;
+    h.c1 = pn.c + 2;
+    h.v1 = hs->v;
+    h.s1r = hs->sr;
+    h.s1c = hs->sc;
+    h.i1 = hs->im;
+  }
+  __builtin_amdgcn_wave_barrier();  // the merge's LDS rows are done with
+  gather_p_query<KS, false, true>(g, nx.sn, B, jp, mn, lane, nx.mu, nx.q64, nx.qn2, qf, ma.db64, nx.basis, nx.ufac,
+                                  nx.qinfo, A, qsh[wv], nullptr, nullptr, h, o0, o1, o2);
 }
 
 // multi-rank finish: global winner over the all-gathered per-rank winners, then coherence
@@ -2343,6 +2478,13 @@ static void launch_merge_j(const LevelGeo &g, const StepDesc &sd, const Imgs &A,
       hipLaunchKernelGGL((k_merge_level<CH, FUSED, IMG, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, win,
                          JobArgN{jobs.rest});
   }
+}
+void ia_launch_merge_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const JobSet &jobs,
+                            const Imgs &B, const NextStep &nx, hipStream_t st) {
+  // waves: the step's merges, the entering row's gather, the next step's pad queries
+  const int nw = sd.M + 1 + (nx.sn.Mpad - nx.sn.M);
+  hipLaunchKernelGGL((k_merge_gather<4>), dim3(cdiv(nw, IA_PQ_WPB)), dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArg1{jobs.j0},
+                     job0_imgs(B, jobs), nx);
 }
 template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,

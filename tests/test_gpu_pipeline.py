@@ -1,5 +1,6 @@
 """Level pipelining (include/ia.h ia_pipeline_depend, ia_amd.pipeline): levels
-alternate between two contexts run from two host threads, each step of level l + 1 waiting only
+rotate over two (or four, the finest level's stream at high priority) contexts run from one host
+thread each, each step of level l + 1 waiting only
 for the steps of level l it reads.  Every level's s, im and B' must equal the sequential run's
 (and the reference's, for golden cases) bit for bit."""
 import numpy as np
@@ -66,25 +67,40 @@ def ctx2():
     c.close()
 
 
+@pytest.fixture(scope='module')
+def ctx4():
+    """four contexts as bench.py --pipe-ctx 4 --pipe-priority 1 makes them"""
+    from ia_amd import _native
+    cs = [_native.Context(0) for _ in range(4)]
+    cs[0].set_option('stream_priority', 1)
+    for c in cs[1:]:
+        c.set_option('stream_priority', 2)
+    yield cs
+    for c in cs:
+        c.close()
+
+
+@pytest.mark.parametrize('nctx', [2, 4])
 @pytest.mark.parametrize('prune_all', [False, True], ids=['default', 'pruned'])
 @pytest.mark.parametrize('name', ['g64', 'k25', 'ties128'] + [c for c in ('g256',) if c in BIG_CASES])
-def test_pipelined_levels_match_reference(ctx, ctx2, name, prune_all):
+def test_pipelined_levels_match_reference(ctx, ctx2, ctx4, name, prune_all, nctx):
     z = load_e2e(name)
-    S, IM, Bp, st = _run([ctx, ctx2], z, True, prune_all)
+    S, IM, Bp, st = _run([ctx, ctx2] if nctx == 2 else ctx4, z, True, prune_all)
     for l in range(1, z['L']):
         assert np.array_equal(S[l], z['s'][l]) and np.array_equal(IM[l], z['im'][l]), l
         assert np.array_equal(Bp[l], z['Bp_final'][l]), l
     assert st.bound_violations == 0 and st.pixels == sum(int(np.prod(z['B_pyr'][l].shape[:2])) for l in range(1, z['L']))
 
 
-def test_pipelined_cfg3_matches_sequential(ctx, ctx2):
+@pytest.mark.parametrize('nctx', [2, 3, 4])
+def test_pipelined_cfg3_matches_sequential(ctx, ctx2, ctx4, nctx):
     """cfg3 (1024^2, 10 levels: the pruned 1024^2 level overlapping the 512^2 one)"""
     from ia_amd import synth
     job = synth.make_job(1024)
     z = {'L': job.L, 'k': job.k, 'A_pyr': job.A_pyr, 'Ap_pyr': job.Ap_pyr_list, 'B_pyr': job.B_pyr,
          'Bp_init': job.Bp_init, 'weights': job.weights}
     S1, IM1, Bp1, _ = _run([ctx], z, False)
-    S2, IM2, Bp2, st = _run([ctx, ctx2], z, True)
+    S2, IM2, Bp2, st = _run([ctx, ctx2] if nctx == 2 else ctx4[:nctx], z, True)
     for l in range(1, job.L):
         assert np.array_equal(S1[l], S2[l]) and np.array_equal(IM1[l], IM2[l]) and np.array_equal(Bp1[l], Bp2[l]), l
     assert st.pruned_levels == 1 and st.bound_violations == 0
