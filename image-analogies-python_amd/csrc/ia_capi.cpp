@@ -1021,12 +1021,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   const int qtmax = use_h ? ia_k3h_qtmax(g.KS) : ia_k3_qtmax(g.KH);
   const int stride = c->time_dist > 0 ? c->time_dist : 0;
   // fused K4(t) + K2p(t + 1) (option "fuse_gather", ia_kernels.hip k_merge_gather): one-job
-  // unsharded pruned levels whose every step takes the in-kernel-sort scan (<= 256 records per
-  // query); the query buffers alternate by step parity
-  const int kv0 = c->k3p_variant;
+  // unsharded pruned levels (<= 256 records per query: one launch's chunks, or nch <= 256 of a
+  // wide step's 2-D launch); the query buffers alternate by step parity
+  static_assert(IA_NWG_H <= 4 * IA_WAVE, "k_merge_gather reads 4 records per lane");
   const bool chain = c->fuse_gather && prune && !multi && !xo && J == 1 && !rot && ma.img_rows == 0 && g.bw >= 3 &&
-                     Mpad_max <= std::min(512, qtmax * IA_TILE) && mas[0].nwg <= 4 * IA_WAVE &&
-                     !(kv0 == 11 || kv0 == 12 || kv0 == 15 || kv0 == 17 || kv0 == 19 || kv0 == 21);
+                     mas[0].nwg <= 4 * IA_WAVE;
   if (chain) {
     if (c->hand_rows < g.bh) {
       HIP_TRY(hipStreamSynchronize(c->st));
@@ -1292,7 +1291,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                            : kv);
     const bool presorted = k3v == 11 || k3v == 12 || k3v == 15 || k3v == 17 || k3v == 19 || k3v == 21;
     if (prune && presorted)
-      ia_launch_query_sort(c->qinfo.as<float4>(), c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
+      ia_launch_query_sort(qinfot, c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
                            c->qs_frag.p, c->qs_tbox.as<float4>(), c->st);
     if (ns > 0) {
       const int qtt = sd.Mpad / IA_TILE, nqb = (qtt + qtmax - 1) / qtmax;

@@ -87,6 +87,33 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
              st1.fallbacks))
 
 
+@pytest.mark.parametrize('variant', [20, 21])
+def test_fused_gather_equals_separate_launches(ctx, variant):
+    """option fuse_gather (ia_kernels.hip k_merge_gather): the merge of step t and the gather of
+    step t + 1 in one launch, the step's results handed row to row; with K3 timing every third
+    step (time_dist 3: sampled steps run the separate launches) the fused and separate forms
+    alternate within a level.  All three runs bit-identical (21: presorted wide-step scan)."""
+    from ia_amd import synth
+    job = synth.make_job(1024)
+    runs = []
+    for fuse, stride in ((0, 0), (1, 0), (1, 3)):
+        ctx.set_option('fuse_gather', fuse)
+        ctx.set_option('time_dist', stride)
+        try:
+            runs.append(_run(ctx, job, 1, variant))
+        finally:
+            ctx.set_option('fuse_gather', 1)
+            ctx.set_option('time_dist', 0)
+    for Bp, S, IM, st in runs[1:]:
+        for level in range(1, job.L):
+            assert np.array_equal(S[level], runs[0][1][level]), level
+            assert np.array_equal(IM[level], runs[0][2][level]), level
+            assert np.array_equal(Bp[level], runs[0][0][level]), level
+        assert st.bound_violations == 0 and st.pruned_levels == 2
+        # rescans depend on which wave took which tile (dynamic hand-out): close, not equal
+        assert abs(st.fallbacks - runs[0][3].fallbacks) <= 0.05 * runs[0][3].fallbacks + 10
+
+
 @pytest.mark.parametrize('size,group', [(512, 2), (1024, 4), (1024, 8)])
 def test_pruned_groups_equal_unpruned(ctx, size, group):
     """option prune_group: Morton tiles interleaved in groups of G (sort neighbours in different

@@ -16,9 +16,17 @@ sk = 'Stream_Id' if 'Stream_Id' in rows[0] else 'Queue_Id'
 fin = [r for r in rows if 'k3h_prune' in r['Kernel_Name']]
 st = fin[-1][sk]
 mine = [r for r in rows if r[sk] == st]
-g = [i for i, r in enumerate(mine) if 'k_gather_query_p' in r['Kernel_Name']]
-first = g[-T]
-lev = [r for r in mine[first:] if any(k in r['Kernel_Name'] for k in ('k_gather_query_p', 'k3h_prune', 'k_merge_level'))]
+pr = [i for i, r in enumerate(mine) if 'k3h_prune' in r['Kernel_Name']]
+# the last finest-level instance that other streams overlap (a pipelined job; bench.py's
+# roofline pass at the end runs the levels on one stream)
+other_end = max((r['e'] for r in rows if r[sk] != st and r[sk] != rows[0][sk]), default=0)
+k = len(pr) // T
+while k > 1 and mine[pr[(k - 1) * T]]['s'] > other_end:
+    k -= 1
+first = max(pr[(k - 1) * T] - 1, 0)   # the step-0 gather precedes the level's first scan
+last = pr[k * T - 1] + 1               # its last merge follows the last scan
+KINDS = ('k_gather_query_p', 'k3h_prune', 'k_merge_level', 'k_merge_gather')
+lev = [r for r in mine[first:last + 1] if any(kd in r['Kernel_Name'] for kd in KINDS)]
 t0, t1 = lev[0]['s'], lev[-1]['e']
 by = defaultdict(float)
 for r in lev:
@@ -30,7 +38,7 @@ for k, v in sorted(by.items(), key=lambda kv: -kv[1]):
     n = sum(1 for r in lev if r['Kernel_Name'].split('(')[0][:40] == k)
     print('  %-40s %5d x %6.1f us = %6.1f ms' % (k, n, v * 1e3 / n, v))
 # the job: its kernels on every (queue, stream) since the previous job's last finest-level merge
-prev_end = max((r['e'] for r in mine[:first] if 'k_merge_level' in r['Kernel_Name']), default=0)
+prev_end = max((r['e'] for r in mine[:first] if 'k_merge' in r['Kernel_Name']), default=0)
 job = [r for r in rows if r['s'] > prev_end and r['s'] < t1 + 1]
 j0 = min(r['s'] for r in job)
 print('job: first kernel %.1f ms before the finest level, last one %.1f ms after its start'
