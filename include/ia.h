@@ -149,6 +149,11 @@ int ia_version(void);
  * head filter before the full rows; unsharded levels, else 14 / 15).
  * "k3p_blocks" = 1 (default) / 0: a presorted pruned scan wider than one launch's 11 query tiles
  * runs as ONE launch of (query block x DB chunk) workgroups instead of one launch per block.
+ * "fuse_gather" = 1 (default) / 0: on one-job unsharded pruned levels the merge of step t and the
+ * gather of step t + 1 run as one launch (the step's results handed row to row through uncached
+ * slots); 0 = separate launches.
+ * "stream_priority" = 0 (default) / 1 (high) / 2 (low): recreate the context's stream with that
+ * priority (idle contexts; level pipelining puts the finest level's stream high).
  * "prune_group" = G in {1 (default), 2, 4, 8}: pruned levels store each group of G Morton tiles
  * interleaved (sort neighbours in different tiles and scan chunks: fewer certification rescans,
  * looser tile boxes).
