@@ -641,7 +641,11 @@ def main():
         roofline['k3_share_of_step'] = None   # single-stream pass vs concurrent timed steps: not comparable
         roofline['timing'] = ('K3/K2/K4 device times from one extra single-stream pass (the timed steps ran %s, '
                               'whose HIP events would overlap)' % ('%d concurrent streams' % len(ctxs) if len(ctxs) > 1
-                                                                  else 'pipelined levels on two streams'))
+                                                                  else 'pipelined levels on %d streams' % args.pipe_ctx))
+    if args.fuse_gather and st['prune_launches_timed'] > 0:
+        roofline['fused_gather'] = ('the unsampled steps of a pruned level run K4 of step t and K2p of step t + 1 as one '
+                                    'launch (k_merge_gather, DESIGN.md §6c); the sampled steps keep separate K2 / K4 '
+                                    'launches, which the gather / merge timings above are')
     roofline['gathers'] = gather_rooflines(st)
     roofline['fp32_mfma_equiv_tflops'] = fp32_equiv / 1e12
     roofline['fp32_mfma_equiv_frac'] = fp32_equiv / FP32_MFMA_PEAK

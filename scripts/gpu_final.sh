@@ -5,7 +5,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-F=gpurun_out/final
+F=gpurun_out/${FINAL_DIR:-final}
 mkdir -p $F
 timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > $F/pytest_gpu.log 2>&1 || { echo "pytest failed"; tail -40 $F/pytest_gpu.log; exit 1; }
 tail -1 $F/pytest_gpu.log
