@@ -248,7 +248,7 @@ def pipe_contexts(args, local, ctx):
     """the extra contexts of level pipelining (--pipe-ctx - 1 of them); with --pipe-priority the
     finest level's context (ctx) gets the high stream priority, the others the low one"""
     extra = [make_context(args, local) for _ in range(args.pipe_ctx - 1)]
-    if args.pipe_priority:
+    if args.pipe_priority and not os.environ.get('IA_CU_SPLIT'):   # CU-masked rehearsal streams keep theirs
         ctx.set_option('stream_priority', 1)
         for cx in extra:
             cx.set_option('stream_priority', 2)
@@ -337,6 +337,8 @@ def main():
     ap.add_argument('--fuse-gather', type=int, default=1, choices=[0, 1],
                     help='1 (default): on pruned one-job levels the merge of step t and the gather of step t + 1 run '
                          'as one launch (ia_kernels.hip k_merge_gather); 0: separate launches')
+    ap.add_argument('--owner-pipeline', type=int, default=0, choices=[0, 1],
+                    help='1: pipelined levels in the owner-computes shard mode too (N > 1)')
     ap.add_argument('--pipe-ctx', type=int, default=4, choices=[2, 3, 4, 5],
                     help='contexts the pipelined levels rotate over (default 4: the finest level\'s stream is free '
                          'once level L - 5 ends; 2: level l + 2 follows level l on one stream; 5: above the box\'s '
@@ -438,6 +440,7 @@ def main():
         log('[bench] CPU baseline sampled in %.1fs: %.3g px/s' % (time.time() - t1, cpu['value']))
     ctx = make_context(args, local)
     owner = args.mode == 'shard' and world > 1 and args.exchange == 'owner'
+    pipe_owner = owner and args.pipeline and args.owner_pipeline
     if owner and args.shard_jobs != world:
         ap.error('--exchange owner: one job per rank (--shard-jobs N)')
     shard_error = None
@@ -473,11 +476,11 @@ def main():
     def fall_back():
         """the shard exchange failed on some rank: every rank measures replicas instead (the line
         says so in config.shard_error)"""
-        nonlocal ctx, owner
+        nonlocal ctx, owner, pipe_owner
         log('[bench] rank %d: shard mode unavailable (%s): measuring replicas' % (rank, shard_error))
         ctx.close()
         ctx = make_context(args, local)
-        args.mode, args.shard_jobs, owner = 'replicas', 1, False
+        args.mode, args.shard_jobs, owner, pipe_owner = 'replicas', 1, False, False
         d = DeviceJob(jobs_b[0], torch, dev)
         p2 = pipe_contexts(args, local, ctx) if args.pipeline else None
         return d, (lambda st, cs=None: d.run(ctx, torch, st, pipe=p2 if cs is None else None))
@@ -489,11 +492,16 @@ def main():
         run = lambda st, cs=ctxs: dsw.run(cs, st, batched=not args.sequential, max_batch=args.max_batch)
         dj = dsw
     elif owner:   # this rank's own job; the other ranks bring theirs
-        # levels one after the other: pipelined, a rank's scan waiting on a peer's queries would
-        # hold the CUs its own next level needs (measured: 0.74 vs 4.5 M px/s for two ranks on one
-        # GPU, profiles/r03/pipeline/)
         dj = DeviceJob(jobs_b[rank], torch, dev)
-        run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
+        if pipe_owner:
+            # pipelined levels: the fused merge's waiter wave holds one SIMD until every owner's next
+            # queries arrived, so the scans no longer spin on all CUs.  Measured
+            # with two ranks on one GPU only (CU halves): 0.51 vs 4.63 M px/s, hence off by default
+            ctx.set_option('xo_wait', 1)
+            pctx = pipe_contexts(args, local, ctx)
+            run = lambda st, cs=None: dj.run(ctx, torch, st, pipe=pctx if cs is None else None)
+        else:
+            run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
     elif args.shard_jobs > 1:
         dj = DeviceBatch(jobs_b, torch, dev)
         run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
@@ -550,7 +558,7 @@ def main():
     # extra single-stream pass below
     # pipelined levels (or several cfg5 streams): HIP events around one stream's K3 launches would
     # also time the other stream's kernels, so the roofline comes from one extra sequential pass
-    concurrent = len(ctxs) > 1 or (args.pipeline and sw is None and not owner and args.shard_jobs <= 1)
+    concurrent = len(ctxs) > 1 or (args.pipeline and sw is None and (not owner or pipe_owner) and args.shard_jobs <= 1)
     elapsed, stats = timed(args.steps, run, not concurrent)
     if concurrent:
         _, stats_rl = timed(1, lambda st: run(st, [ctx]), True)
@@ -678,8 +686,8 @@ def main():
                                            'jobs_per_step': jobs,
                                            'level_pipeline': (('%d contexts%s' % (args.pipe_ctx, ', finest level high priority'
                                                                                   if args.pipe_priority else ''))
-                                                              if args.pipeline and sw is None and not owner and
-                                                              args.shard_jobs <= 1 else None),
+                                                              if args.pipeline and sw is None and (not owner or pipe_owner)
+                                                              and args.shard_jobs <= 1 else None),
                                            'nn': 'exact: %s MFMA candidates + certified fp64 rerank'
                                                  % ('split-f16 (hi/lo x3)' if f16 else 'fp32'),
                                            'precision': ('f16x3 = every operand split into f16 hi + lo, 3 MFMA '

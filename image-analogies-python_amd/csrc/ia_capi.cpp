@@ -129,6 +129,8 @@ struct ia_ctx {
                                   // 2 = owner-computes (rank o owns job o; every rank scans its shard for all)
   DevBuf xo_inv;                  // exchange = 2: the owners' query -> slot tables of the current step
   int xo_presort = 0;             // option "xo_presort": 1 = owners always sort with K2s (tests)
+  int xo_wait = 0;                // option "xo_wait": 1 = the fused merge waits for every owner's next
+                                  // queries (one wave), so the next scan does not spin on all CUs
   void *xbuf = nullptr;           // this process's exchange buffer (uncached, IPC-exportable)
   int xbuf_w = 0;                 // ranks the buffer was sized for
   XSlot *xpeer[IA_XCHG_MAXW] = {};  // every rank's buffer in this address space (ia_xchg_open)
@@ -479,6 +481,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     c->st = ns;
     return IA_OK;
   }
+  if (!std::strcmp(name, "xo_wait")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: xo_wait must be 0 or 1");
+    c->xo_wait = value;
+    return IA_OK;
+  }
   if (!std::strcmp(name, "xo_presort")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: xo_presort must be 0 or 1");
     c->xo_presort = value;
@@ -518,6 +525,23 @@ int ia_comm_init(ia_ctx *c, int rank, int world, const unsigned char id[128]) {
   std::memcpy(&uid, id, 128);
   NCCL_TRY(ncclCommInitRank(&c->comm, world, uid, rank));
   return IA_OK;
+}
+
+// owner o's K2s of an owner-computes step: its queries sorted into every rank's area (area(p))
+extern "C++" template <class AreaFn>
+static void ia_launch_query_sort_xo_owner(ia_ctx *c, const LevelGeo &g, const float4 *qinfo, const void *qf,
+                                          const StepDesc &sd, int owner, int QTs, unsigned seq, int W, AreaFn area) {
+  (void)g;
+  XOSort xs{};
+  xs.inv = c->xo_inv.as<int>();
+  xs.W = W;
+  for (int p = 0; p < xs.W; p++) xs.area[p] = area(p);
+  xs.q0 = 0;
+  xs.Mj = sd.M;
+  xs.tile0 = owner * QTs;
+  xs.QTs = QTs;
+  xs.seq = seq;
+  ia_launch_query_sort_xo(qinfo, qf, xs, c->st);
 }
 
 static int xchg_alloc(ia_ctx *c, int world) {
@@ -1024,18 +1048,20 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   // unsharded pruned levels (<= 256 records per query: one launch's chunks, or nch <= 256 of a
   // wide step's 2-D launch); the query buffers alternate by step parity
   static_assert(IA_NWG_H <= 4 * IA_WAVE, "k_merge_gather reads 4 records per lane");
-  const bool chain = c->fuse_gather && prune && !multi && !xo && J == 1 && !rot && ma.img_rows == 0 && g.bw >= 3 &&
-                     mas[0].nwg <= 4 * IA_WAVE;
+  // (owner-computes steps too: each local owner's merge + its next gather, which publishes)
+  const bool chain = c->fuse_gather && prune && ((!multi && J == 1 && mas[0].nwg <= 4 * IA_WAVE) || xo) && !rot &&
+                     ma.img_rows == 0 && g.bw >= 3;
   if (chain) {
-    if (c->hand_rows < g.bh) {
+    const int hrows = g.bh * (xo ? J : 1);  // per local owner
+    if (c->hand_rows < hrows) {
       HIP_TRY(hipStreamSynchronize(c->st));
       if (c->hand) hipFree(c->hand);
       c->hand = nullptr;
       c->hand_rows = 0;
-      HIP_TRY(hipExtMallocWithFlags((void **)&c->hand, (size_t)g.bh * sizeof(HandSlot), hipDeviceMallocUncached));
-      HIP_TRY(hipMemset(c->hand, 0, (size_t)g.bh * sizeof(HandSlot)));
+      HIP_TRY(hipExtMallocWithFlags((void **)&c->hand, (size_t)hrows * sizeof(HandSlot), hipDeviceMallocUncached));
+      HIP_TRY(hipMemset(c->hand, 0, (size_t)hrows * sizeof(HandSlot)));
       HIP_TRY(hipDeviceSynchronize());
-      c->hand_rows = g.bh;
+      c->hand_rows = hrows;
     }
     if ((rc = c->xerr.ensure(4))) return rc;
     HIP_TRY(hipMemsetAsync(c->xerr.p, 0, 4, c->st));
@@ -1139,10 +1165,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       // local owner's fused merge (K4) runs over W nch records per query.  The emulated launches
       // are exactly the ranks' launches, one after the other.
       const unsigned seq = ++c->xseq;
-      const size_t par = (size_t)(seq & 1u) * XOLayout::PARITY;
-      auto area = [&](int p) -> char * {  // parity base of rank p's area in this address space
-        return (char *)(sharded ? (void *)c->xpeer[p] : c->xbuf) + ia_xslots_bytes(Wsh) + par;
+      auto area_s = [&](int p, unsigned sq) -> char * {  // parity base of rank p's area for step seq sq
+        return (char *)(sharded ? (void *)c->xpeer[p] : c->xbuf) + ia_xslots_bytes(Wsh) + (size_t)(sq & 1u) * XOLayout::PARITY;
       };
+      auto area = [&](int p) -> char * { return area_s(p, seq); };
       char *loc = area(sharded ? c->rank : 0);
       const int Mpj = (sd.M + IA_TILE - 1) / IA_TILE * IA_TILE;  // one owner's padded queries
       // owners whose step fits one launch's query tiles skip K2s: K2p publishes the unsorted
@@ -1154,9 +1180,18 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       s1.J = 1;
       s1.Mpad = Mpj;
       auto owner_of = [&](int jl) { return sharded ? c->rank : jl; };
+      double *q64t, *qn2t;
+      float4 *qinfot;
+      qhalf(t, q64t, qn2t, qinfot);
       for (int jl = 0; jl < J; jl++) {
         const JobSet one{jp[jl], c->jobs.as<JobPtrs>() + jl, 1};
         const size_t q0 = (size_t)jl * Mpj;
+        if (chain && gathered == t) {  // K2p (+ publish) ran in the previous step's fused merge
+          if (!ink)
+            ia_launch_query_sort_xo_owner(c, g, qinfot + 3 * q0, (char *)c->qf.p + q0 * db_row_bytes, sd, owner_of(jl),
+                                          QTs, seq, sharded ? Wsh : 1, area);
+          continue;
+        }
         XOPub xp{};
         if (ink) {
           xp.W = sharded ? Wsh : 1;
@@ -1164,20 +1199,12 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           xp.slot0 = owner_of(jl) * Mpj;
           xp.seq = seq;
         }
-        ia_launch_gather_p(g, s1, Bim, one, c->mu.as<double>(), c->q64.as<double>() + q0 * g.D, c->qn2.as<double>() + q0,
+        ia_launch_gather_p(g, s1, Bim, one, c->mu.as<double>(), q64t + q0 * g.D, qn2t + q0,
                            (char *)c->qf.p + q0 * db_row_bytes, c->db64.as<double>(), c->pr_basis.as<double>(), ufac,
-                           c->qinfo.as<float4>() + 3 * q0, Aim, ma.img_rows, c->st, &xp);
+                           qinfot + 3 * q0, Aim, ma.img_rows, c->st, &xp);
         if (ink) continue;
-        XOSort xs{};
-        xs.inv = c->xo_inv.as<int>();
-        xs.W = sharded ? Wsh : 1;
-        for (int p = 0; p < xs.W; p++) xs.area[p] = area(p);
-        xs.q0 = 0;
-        xs.Mj = sd.M;
-        xs.tile0 = owner_of(jl) * QTs;
-        xs.QTs = QTs;
-        xs.seq = seq;
-        ia_launch_query_sort_xo(c->qinfo.as<float4>() + 3 * q0, (char *)c->qf.p + q0 * db_row_bytes, xs, c->st);
+        ia_launch_query_sort_xo_owner(c, g, qinfot + 3 * q0, (char *)c->qf.p + q0 * db_row_bytes, sd, owner_of(jl), QTs,
+                                      seq, sharded ? Wsh : 1, area);
       }
       if (timed_gm) hipEventRecord(c->evg[2 * n_gm + 1], c->st);
       const int nqb = ink ? Wsh : Wsh * xo_bpj;
@@ -1224,13 +1251,30 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       }
       if (timed) hipEventRecord(c->evs[2 * n_rec++ + 1], c->st);
       if (timed_gm) hipEventRecord(c->evm[2 * n_gm], c->st);
+      // the next step's layout (fused merge + gather: each owner publishes its next queries)
+      const bool fuse_next = chain && t + 1 < T && !(stride && (t % stride == 0 || (t + 1) % stride == 0));
+      StepDesc sn{};
+      int Mpj_n = 0;
+      bool ink_n = false;
+      double *q64n = nullptr, *qn2n = nullptr;
+      float4 *qinfon = nullptr;
+      if (fuse_next) {
+        if ((rc = wait_dep(t + 1))) return rc;
+        sn.t = (int)(t + 1);
+        sn.J = 1;
+        ia_wavefront_step(g.bh, g.bw, t + 1, &sn.r0, &sn.M);
+        Mpj_n = (sn.M + IA_TILE - 1) / IA_TILE * IA_TILE;
+        sn.Mpad = Mpj_n;
+        ink_n = Mpj_n <= ia_k3h_qtmax(g.KS) * IA_TILE && !c->xo_presort;
+        qhalf(t + 1, q64n, qn2n, qinfon);
+      }
       for (int jl = 0; jl < J; jl++) {
         const JobSet one{jp[jl], c->jobs.as<JobPtrs>() + jl, 1};
         const size_t q0 = (size_t)jl * Mpj;
         MergeArgs mx = ma;
-        mx.q64 = c->q64.as<double>() + q0 * g.D;
-        mx.qn2 = c->qn2.as<double>() + q0;
-        mx.qinfo = c->qinfo.as<float4>() + 3 * q0;
+        mx.q64 = q64t + q0 * g.D;
+        mx.qn2 = qn2t + q0;
+        mx.qinfo = qinfot + 3 * q0;
         mx.rec = reinterpret_cast<const float4 *>(loc + XOLayout::REC);
         mx.xo_rts = reinterpret_cast<const unsigned long long *>(loc + XOLayout::RTS);
         mx.nwg = Wsh * nch;
@@ -1248,8 +1292,37 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         mx.xo_seq = seq;
         mx.xo_err = c->xerr.as<unsigned>();
         mx.xo_timeout = 2000000000LL;
-        ia_launch_merge(g, s1, Aim, mx, c->win.as<Winner>(), one, true, c->st);
+        if (!fuse_next) {
+          ia_launch_merge(g, s1, Aim, mx, c->win.as<Winner>(), one, true, c->st);
+          continue;
+        }
+        const size_t q0n = (size_t)jl * Mpj_n;
+        NextStep nx{};
+        nx.sn = sn;
+        nx.q64 = q64n + q0n * g.D;
+        nx.qn2 = qn2n + q0n;
+        nx.qinfo = qinfon + 3 * q0n;
+        nx.qf = (char *)c->qf.p + q0n * db_row_bytes;
+        nx.mu = c->mu.as<double>();
+        nx.basis = c->pr_basis.as<double>();
+        nx.ufac = ufac;
+        nx.hand = c->hand + (size_t)jl * g.bh;
+        nx.seq = ++c->hseq;
+        nx.err = c->xerr.as<unsigned>();
+        nx.timeout_ticks = 2000000000LL;
+        if (ink_n) {  // the next step's queries go straight to every rank's area (else its K2s sorts them)
+          nx.xp.W = sharded ? Wsh : 1;
+          for (int p = 0; p < nx.xp.W; p++) nx.xp.area[p] = area_s(p, seq + 1);
+          nx.xp.slot0 = owner_of(jl) * Mpj_n;
+          nx.xp.seq = seq + 1;
+          if (sharded && c->xo_wait && jl == J - 1) {  // ranks: wait here for every owner's next queries
+            nx.wait_seq = reinterpret_cast<const unsigned *>(area_s(c->rank, seq + 1) + XOLayout::QSEQ);
+            nx.wait_n = Wsh * Mpj_n;
+          }
+        }
+        ia_launch_merge_gather(g, s1, Aim, mx, one, Bim, nx, c->st);
       }
+      if (fuse_next) gathered = t + 1;
       if (timed_gm) hipEventRecord(c->evm[2 * n_gm++ + 1], c->st);
       continue;
     }

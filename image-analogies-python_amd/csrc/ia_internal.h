@@ -347,6 +347,10 @@ struct NextStep {
   unsigned seq;
   unsigned *err;           // bit 4: a handoff did not arrive in time
   long long timeout_ticks;
+  XOPub xp;                // owner-computes step t + 1: publish its queries (xp.W = 0: off)
+  const unsigned *wait_seq;  // owner-computes ranks: one extra wave waits until all wait_n query
+  int wait_n;                // seqs of step t + 1 (this rank's area) arrived, so the next scan
+                             // starts with its queries in place instead of spinning on every CU
 };
 
 __host__ __device__ inline int ia_reflect(int i, int n) {

@@ -1303,6 +1303,29 @@ __device__ __forceinline__ double feat_q1(const Imgs &B, int f, int r, int c, co
   return feat<1>(B, f, r, c, 0);
 }
 
+// owner-computes sharded step (XOPub): query m's fragments (16 h16x8 pieces from LDS, one store
+// instruction per area), its pruning record, then - once those stores completed - its seq, into
+// every rank's area
+template <int KS>
+__device__ __forceinline__ void xo_publish(const XOPub &xp, int m, int lane, const _Float16 *xh0, const _Float16 *xh1,
+                                           float4 i0, float4 i1, float4 i2) {
+  __builtin_amdgcn_wave_barrier();  // xh written by this wave's lanes
+  const int qt = m / IA_TILE, j = m % IA_TILE;
+  const int c = lane, sp = c >> 2, part = (c >> 1) & 1, h = c & 1;  // chunk c < 2 KS * 2
+  h16x8 v{};
+  if (c < 4 * KS) v = *reinterpret_cast<const h16x8 *>(&(part ? xh1 : xh0)[16 * sp + 8 * h]);
+  const int64_t t0 = xp.slot0 / IA_TILE;
+  for (int o = 0; o < xp.W; o++) {
+    if (c < 4 * KS)
+      reinterpret_cast<h16x8 *>(xp.area[o] + XOLayout::FRAG)[((t0 + qt) * 2 * KS + 2 * sp + part) * IA_WAVE + h * IA_TILE + j] = v;
+    if (lane < 3) reinterpret_cast<float4 *>(xp.area[o] + XOLayout::INFO)[3 * (xp.slot0 + m) + lane] = lane == 0 ? i0 : lane == 1 ? i1 : i2;
+  }
+  ia_stores_done();
+  if (lane < xp.W)
+    __hip_atomic_store(reinterpret_cast<unsigned *>(xp.area[lane] + XOLayout::QSEQ) + xp.slot0 + m, xp.seq, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // K2p's pad query m >= J M: zero fragments, an empty pruning record
 template <int KS>
 __device__ __forceinline__ void gather_p_pad(int m, int lane, _Float16 *qf, float4 *qinfo, float4 &o0, float4 &o1,
@@ -1434,25 +1457,7 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_gather_query_p(LevelGeo g, StepDes
     gather_p_query<KS, IMG, false>(g, sd, B, jp, m, lane, mu_part, q64, qn2, qf, db64, basis, ufac, qinfo, A, qsh[wv],
                                    xp.W ? xh[wv][0] : nullptr, xh[wv][1], QHand{}, i0, i1, i2);
   }
-  if (!xp.W) return;
-  // owner-computes sharded step (XOPub): the query's fragments (16 h16x8 pieces from LDS, one
-  // store instruction per area), its pruning record, then - once those stores completed - its
-  // seq, into every rank's area
-  __builtin_amdgcn_wave_barrier();  // xh written by this wave's lanes
-  const int qt = m / IA_TILE, j = m % IA_TILE;
-  const int c = lane, sp = c >> 2, part = (c >> 1) & 1, h = c & 1;  // chunk c < 2 KS * 2
-  h16x8 v{};
-  if (c < 4 * KS) v = *reinterpret_cast<const h16x8 *>(&xh[wv][part][16 * sp + 8 * h]);
-  const int64_t t0 = xp.slot0 / IA_TILE;
-  for (int o = 0; o < xp.W; o++) {
-    if (c < 4 * KS)
-      reinterpret_cast<h16x8 *>(xp.area[o] + XOLayout::FRAG)[((t0 + qt) * 2 * KS + 2 * sp + part) * IA_WAVE + h * IA_TILE + j] = v;
-    if (lane < 3) reinterpret_cast<float4 *>(xp.area[o] + XOLayout::INFO)[3 * (xp.slot0 + m) + lane] = lane == 0 ? i0 : lane == 1 ? i1 : i2;
-  }
-  ia_stores_done();
-  if (lane < xp.W)
-    __hip_atomic_store(reinterpret_cast<unsigned *>(xp.area[lane] + XOLayout::QSEQ) + xp.slot0 + m, xp.seq, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
+  if (xp.W) xo_publish<KS>(xp, m, lane, xh[wv][0], xh[wv][1], i0, i1, i2);
 }
 
 #ifdef IA_K3H_DIAG  // k3p_variant 16 / 17: DIAG=1 builds only
@@ -2034,6 +2039,21 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc 
   __shared__ double qsh[IA_PQ_WPB][Geo<1>::DS], wsh[IA_PQ_WPB][Geo<1>::DS];
   __shared__ int crsh[IA_PQ_WPB][IA_WAVE];
   __shared__ float cvsh[IA_PQ_WPB][IA_WAVE];
+  __shared__ __attribute__((aligned(16))) _Float16 xh[IA_PQ_WPB][2][16 * KS];  // owner publish: hi / lo columns
+  if (w >= sd.M + 1 + (nx.sn.Mpad - nx.sn.M)) {  // the waiter (nx.wait_n > 0 only)
+    // after an earlier timeout of this context: no waiting (one lost peer costs one timeout)
+    if (__hip_atomic_load(nx.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    for (int i = lane; i < nx.wait_n; i += IA_WAVE)
+      while (__hip_atomic_load(nx.wait_seq + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != nx.xp.seq) {
+        if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > nx.timeout_ticks) {
+          atomicOr(nx.err, 4u);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    return;
+  }
   QHand h;
   int mn = -1;  // this wave's query of step t + 1
   if (w < sd.M) {
@@ -2068,6 +2088,10 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc 
   float4 o0, o1, o2;
   if (mn >= nx.sn.M) {
     gather_p_pad<KS>(mn, lane, qf, nx.qinfo, o0, o1, o2);
+    if (nx.xp.W) {
+      if (lane < 16 * KS) xh[wv][0][lane] = xh[wv][1][lane] = (_Float16)0.f;
+      xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
+    }
     return;
   }
   const QPix pn = ia_qpix(nx.sn, g.bw, mn);
@@ -2092,7 +2116,8 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc 
   }
   __builtin_amdgcn_wave_barrier();  // the merge's LDS rows are done with
   gather_p_query<KS, false, true>(g, nx.sn, B, jp, mn, lane, nx.mu, nx.q64, nx.qn2, qf, ma.db64, nx.basis, nx.ufac,
-                                  nx.qinfo, A, qsh[wv], nullptr, nullptr, h, o0, o1, o2);
+                                  nx.qinfo, A, qsh[wv], nx.xp.W ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2);
+  if (nx.xp.W) xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
 }
 
 // multi-rank finish: global winner over the all-gathered per-rank winners, then coherence
@@ -2482,7 +2507,7 @@ static void launch_merge_j(const LevelGeo &g, const StepDesc &sd, const Imgs &A,
 void ia_launch_merge_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const JobSet &jobs,
                             const Imgs &B, const NextStep &nx, hipStream_t st) {
   // waves: the step's merges, the entering row's gather, the next step's pad queries
-  const int nw = sd.M + 1 + (nx.sn.Mpad - nx.sn.M);
+  const int nw = sd.M + 1 + (nx.sn.Mpad - nx.sn.M) + (nx.wait_n > 0 ? 1 : 0);
   hipLaunchKernelGGL((k_merge_gather<4>), dim3(cdiv(nw, IA_PQ_WPB)), dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArg1{jobs.j0},
                      job0_imgs(B, jobs), nx);
 }

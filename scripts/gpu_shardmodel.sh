@@ -12,7 +12,9 @@ for W in ${WS:-1 2 4 8}; do
   cp /tmp/sh$W/run_kernel_stats.csv gpurun_out/shard/w${W}_stats.csv
   python3 tools/trace_breakdown.py /tmp/sh$W/run_kernel_trace.csv 1 > gpurun_out/shard/w$W.txt 2>&1
   B1=profiles/r03/shard_jobs/w1_model.txt; [ -f gpurun_out/shard/w1_model.txt ] && B1=gpurun_out/shard/w1_model.txt
-  python3 tools/shard_model.py /tmp/sh$W/run_kernel_trace.csv $W 3.0 382 $B1 > gpurun_out/shard/w${W}_model.txt 2>&1 || true
+  # baseline: the W = 1 run's modelled job time (one job alone, same kernels)
+  B0=$(grep -oP 'modelled \K[0-9.]+' gpurun_out/shard/w1_model.txt 2>/dev/null || echo 382)
+  python3 tools/shard_model.py /tmp/sh$W/run_kernel_trace.csv $W 3.0 $B0 $B1 > gpurun_out/shard/w${W}_model.txt 2>&1 || true
   rm -rf /tmp/sh$W
   grep -E "^level 9|^total" gpurun_out/shard/w$W.txt | cut -c1-400
   cat gpurun_out/shard/w${W}_model.txt

@@ -42,7 +42,7 @@ def kind(name):
         return 'scan'
     if 'k_query_sort' in name:
         return 'sort'
-    if 'k_merge_xchg' in name or 'k_merge_level' in name or 'k_finish_level' in name:
+    if 'k_merge_xchg' in name or 'k_merge_level' in name or 'k_finish_level' in name or 'k_merge_gather' in name:
         return 'merge'
     return 'other'
 
@@ -60,9 +60,16 @@ for r in rows:
     if not levels:
         continue
     lv = levels[-1]
-    if k == 'gather' and last not in ('gather', 'sort'):   # a step starts with its gather(s)
-        step = {'gathers': [], 'sorts': [], 'scans': [], 'merges': []}
+    # a step starts with its gather(s), or - when the previous step's fused merge + gather
+    # (k_merge_gather) ran them - with its sort / scan right after a merge
+    if (k == 'gather' and last not in ('gather', 'sort')) or (k in ('sort', 'scan') and last in ('merge', None)):
+        step = {'gathers': [], 'sorts': [], 'scans': [], 'merges': [], 'owner': False}
         lv['steps'].append(step)
+    # owner-computes steps: one fused merge per owner (k_merge_level<CH, true, ...> or k_merge_gather);
+    # the RCCL exchange's per-shard merges are k_merge_level<CH, false, ...>
+    if k == 'merge' and step is not None and ('k_merge_gather' in r['Kernel_Name'] or
+                                              re.search(r'k_merge_level<\d+, true', r['Kernel_Name'])):
+        step['nown'] = step.get('nown', 0) + 1
     if step is None or k in ('other', 'level'):
         lv['other'] += d
     else:
@@ -80,11 +87,11 @@ for i, lv in enumerate(sel):
         meas += sum(st['gathers']) + sum(st['sorts']) + sum(st['scans']) + sum(st['merges'])
         nsh = len(st['merges'])
         sharded += nsh > 1
-        if len(st['gathers']) > 1:
+        if len(st['gathers']) > 1 or st.get('nown', 0) > 1:
             # owner-computes step (exchange = 2): every emulated owner's gather, sort and merge
             # are its rank's own launches; each rank pays the slowest of each plus its shard's
             # scan and two exchange latencies (sorted queries out, records back)
-            model += max(st['gathers']) + max(st['sorts'] or [0.0]) + max(st['scans'] or [0.0]) + \
+            model += max(st['gathers'] or [0.0]) + max(st['sorts'] or [0.0]) + max(st['scans'] or [0.0]) + \
                 max(st['merges']) + 2 * XLAT
             continue
         # scans of one shard are consecutive launches (several query blocks of an unpruned or
@@ -96,7 +103,7 @@ for i, lv in enumerate(sel):
             (XLAT if nsh > 1 else 0.0)
     meas += lv['other']
     model += lv['other']
-    owner = any(len(st['gathers']) > 1 for l2 in sel for st in l2['steps'])
+    owner = any(len(st['gathers']) > 1 or st.get('nown', 0) > 1 for l2 in sel for st in l2['steps'])
     if owner and sharded == 0 and (i + 1) in BASE_LV:
         model = BASE_LV[i + 1]
     tot_meas += meas
@@ -106,7 +113,7 @@ for i, lv in enumerate(sel):
 print('job: emulated kernels %.1f ms on one GPU; modelled %.1f ms per rank on %d GPUs (exchange latency %.1f us/step)'
       % (tot_meas / 1e3, tot_model / 1e3, W, XLAT))
 if base:
-    if any(len(st['gathers']) > 1 for lv in sel for st in lv['steps']):
+    if any(len(st['gathers']) > 1 or st.get('nown', 0) > 1 for lv in sel for st in lv['steps']):
         # owner computes: W jobs on W ranks (weak scaling): efficiency = one job alone / per-rank time
         print('weak scaling vs %.1f ms for one job on one GPU: efficiency %.0f %% (%d jobs in %.1f ms on %d GPUs)'
               % (base, 100 * base / (tot_model / 1e3), W, tot_model / 1e3, W))
