@@ -234,6 +234,8 @@ def make_context(args, local):
         cx.set_option('prune_group', args.prune_group)
     if args.fuse_gather != 1:
         cx.set_option('fuse_gather', args.fuse_gather)
+    if args.fuse_unpruned:
+        cx.set_option('fuse_unpruned', 1)
     if args.row_source:
         cx.set_option('row_source', args.row_source)
     if args.shard_unpruned:
@@ -339,6 +341,8 @@ def main():
                          'as one launch (ia_kernels.hip k_merge_gather); 0: separate launches')
     ap.add_argument('--owner-pipeline', type=int, default=0, choices=[0, 1],
                     help='1: pipelined levels in the owner-computes shard mode too (N > 1)')
+    ap.add_argument('--fuse-unpruned', type=int, default=0, choices=[0, 1],
+                    help='1: the fused merge + gather on unpruned levels too (measured slower, DESIGN.md §6c)')
     ap.add_argument('--pipe-ctx', type=int, default=4, choices=[2, 3, 4, 5],
                     help='contexts the pipelined levels rotate over (default 4: the finest level\'s stream is free '
                          'once level L - 5 ends; 2: level l + 2 follows level l on one stream; 5: above the box\'s '

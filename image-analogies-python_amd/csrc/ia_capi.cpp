@@ -114,6 +114,7 @@ struct ia_ctx {
   int k3p_blocks = 1;            // option "k3p_blocks": 1 = a wide step's presorted pruned scan is one launch over
                                  // all its query blocks (2-D grid); 0 = one launch per block
   int fuse_gather = 1;           // option "fuse_gather": 1 = K4 of step t and K2p of step t + 1 in one launch
+  int fuse_unpruned = 0;         // option "fuse_unpruned": 1 = also on unpruned levels (K4 + K2h)
   HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
   int hand_rows = 0;
   unsigned hseq = 0;
@@ -458,6 +459,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "fuse_gather")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_gather must be 0 or 1");
     c->fuse_gather = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "fuse_unpruned")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_unpruned must be 0 or 1");
+    c->fuse_unpruned = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "pipeline_record")) {
@@ -1049,10 +1055,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   // wide step's 2-D launch); the query buffers alternate by step parity
   static_assert(IA_NWG_H <= 4 * IA_WAVE, "k_merge_gather reads 4 records per lane");
   // (owner-computes steps too: each local owner's merge + its next gather, which publishes)
-  const bool chain = c->fuse_gather && prune && ((!multi && J == 1 && mas[0].nwg <= 4 * IA_WAVE) || xo) && !rot &&
-                     ma.img_rows == 0 && g.bw >= 3;
+  // (batched jobs: one handoff row set per job.  Unpruned levels - K2h fused, option
+  // "fuse_unpruned" - measured slower: their longer fused launches delay the pipelined finest
+  // level's scans, and cfg5's batched 512^2 steps lose 1-2 %)
+  const bool chain = c->fuse_gather && use_h && g.ch == 1 && !rot && ma.img_rows == 0 && g.bw >= 3 &&
+                     (prune || c->fuse_unpruned) && ((!multi && !xo && mas[0].nwg <= 4 * IA_WAVE) || (xo && prune));
   if (chain) {
-    const int hrows = g.bh * (xo ? J : 1);  // per local owner
+    const int hrows = g.bh * J;  // per job (local owner)
     if (c->hand_rows < hrows) {
       HIP_TRY(hipStreamSynchronize(c->st));
       if (c->hand) hipFree(c->hand);
@@ -1320,7 +1329,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
             nx.wait_n = Wsh * Mpj_n;
           }
         }
-        ia_launch_merge_gather(g, s1, Aim, mx, one, Bim, nx, c->st);
+        ia_launch_merge_gather(g, s1, Aim, mx, one, Bim, nx, true, c->st);
       }
       if (fuse_next) gathered = t + 1;
       if (timed_gm) hipEventRecord(c->evm[2 * n_gm++ + 1], c->st);
@@ -1340,13 +1349,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                          c->db64.as<double>(), c->pr_basis.as<double>(), ufac, ra, c->qinfo.as<float4>(), Aim, c->st);
     else
 #endif
-    if (prune && gathered == t)
-      ;  // K2p of this step ran in the previous step's fused merge
+    if (chain && gathered == t)
+      ;  // this step's gather ran in the previous step's fused merge
     else if (prune)
       ia_launch_gather_p(g, sd, Bim, djobs, c->mu.as<double>(), q64t, qn2t, c->qf.p, c->db64.as<double>(),
                          c->pr_basis.as<double>(), ufac, qinfot, Aim, ma.img_rows, c->st);
     else if (use_h)
-      ia_launch_gather_h(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p, c->st);
+      ia_launch_gather_h(g, sd, Bim, djobs, c->mu.as<double>(), q64t, qn2t, c->qf.p, c->st);
     else
       ia_launch_gather(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.as<float>(),
                        c->st);
@@ -1446,9 +1455,9 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       if ((rc = wait_dep(t + 1))) return rc;  // the next step's gather reads the previous level
       NextStep nx{};
       nx.sn.t = (int)(t + 1);
-      nx.sn.J = 1;
+      nx.sn.J = J;
       ia_wavefront_step(g.bh, g.bw, t + 1, &nx.sn.r0, &nx.sn.M);
-      nx.sn.Mpad = (nx.sn.M + IA_TILE - 1) / IA_TILE * IA_TILE;
+      nx.sn.Mpad = (J * nx.sn.M + IA_TILE - 1) / IA_TILE * IA_TILE;
       qhalf(t + 1, nx.q64, nx.qn2, nx.qinfo);
       nx.mu = c->mu.as<double>();
       nx.basis = c->pr_basis.as<double>();
@@ -1458,7 +1467,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       nx.seq = ++c->hseq;
       nx.err = c->xerr.as<unsigned>();
       nx.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
-      ia_launch_merge_gather(g, sd, Aim, mas[0], djobs, Bim, nx, c->st);
+      ia_launch_merge_gather(g, sd, Aim, mas[0], djobs, Bim, nx, prune, c->st);
       gathered = t + 1;
     } else if (!multi) {
       ia_launch_merge(g, sd, Aim, mas[0], c->win.as<Winner>(), djobs, true, c->st);

@@ -2029,18 +2029,65 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_level(LevelGeo g, StepDesc s
 // after it the step's pad queries.  The query buffers alternate by step parity (this launch's
 // merge reads step t's half while its gathers write step t + 1's).
 // ------------------------------------------------------------------------------------------
-template <int RPL>
-__global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, JobArg1 jobs,
+// K2h's work for one query m of step sd (unpruned split-f16 levels), with the fused gather's
+// two step-t pixels substituted (QHand) in the B' part
+template <int KS>
+__device__ __forceinline__ void gather_h_query_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &B, int m, int lane,
+                                                     const double *__restrict__ mu_part, double *__restrict__ q64,
+                                                     double *__restrict__ qn2, _Float16 *__restrict__ qf, const QHand &h) {
+  constexpr int D = 55, KD = 16 * KS;
+  static_assert(KD <= IA_WAVE, "one feature per lane");
+  const QPix px = ia_qpix(sd, g.bw, m);
+  const int r = px.r, c = px.c;
+  double ss = 0.;
+  if (lane < KD) {
+    const int f = lane;
+    if (f < D) {
+      double v;
+      if (f >= 43) {  // the B' part (causal 5x5 at (r, c), k < 12)
+        const int k = f - 43, y = ia_reflect(r + k / 5 - 2, B.h), x = ia_reflect(c + k % 5 - 2, B.w);
+        v = (y == h.r0 && x == h.c0) ? h.v0 : (y == h.r1 && x == h.c1) ? h.v1 : B.p3[(int64_t)y * B.w + x];
+      } else {
+        v = feat<1>(B, f, r, c, 0);
+      }
+      q64[(int64_t)m * D + f] = v;
+      const double qc = v - mu_part[feat_part<1>(f)];
+      ss = qc * qc;
+      put_qh<KS>(qf, m, f, -2.0 * qc);
+    } else {
+      put_qh<KS>(qf, m, f, f == D ? IA_NORM_SCALE : 0.);
+    }
+  }
+  ss = wave_sum_d(ss);
+  if (lane == 0) qn2[m] = ss;
+}
+
+// ------------------------------------------------------------------------------------------
+// K4 + K2 fused (option "fuse_gather"): K4 of step t, then the gather (K2p on pruned levels,
+// K2h on the others) of step t + 1, one launch.  Pixel (r, c + 1) of step t + 1 reads two
+// results of step t: its own row's (r, c) and the row above's (r - 1, c + 3) (skew 3: both lie
+// on step t); everything else it reads is older.  So the wave of query (job j, row r) merges
+// (r, c), hands its result to row r + 1 through an uncached slot (fields, store completion, then
+// the step's seq), and gathers (r, c + 1), waiting for the slot of row r - 1: a wave of the same
+// launch with a LOWER index (rows ascend with the query index within a job), dispatched before
+// it, so the waits always drain.  Waves J M .. J M + J - 1 gather each job's row entering at
+// step t + 1 (column 0; its row above is that job's last merge wave), the waves after them the
+// step's pad queries (and, owner-computes ranks with xo_wait, one waiter).  The query buffers
+// alternate by step parity (this launch's merges read step t's half while its gathers write
+// step t + 1's).
+// ------------------------------------------------------------------------------------------
+template <int RPL, bool PR, class JS>
+__global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, JS jobs,
                                                          Imgs B, NextStep nx) {
   constexpr int KS = 4;
   const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * IA_PQ_WPB + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const JobPtrs jp = jobs.j0;
+  const int J = sd.J, JM = J * sd.M;
   __shared__ double qsh[IA_PQ_WPB][Geo<1>::DS], wsh[IA_PQ_WPB][Geo<1>::DS];
   __shared__ int crsh[IA_PQ_WPB][IA_WAVE];
   __shared__ float cvsh[IA_PQ_WPB][IA_WAVE];
   __shared__ __attribute__((aligned(16))) _Float16 xh[IA_PQ_WPB][2][16 * KS];  // owner publish: hi / lo columns
-  if (w >= sd.M + 1 + (nx.sn.Mpad - nx.sn.M)) {  // the waiter (nx.wait_n > 0 only)
+  if (w >= JM + J + (nx.sn.Mpad - J * nx.sn.M)) {  // the waiter (nx.wait_n > 0 only)
     // after an earlier timeout of this context: no waiting (one lost peer costs one timeout)
     if (__hip_atomic_load(nx.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
@@ -2055,13 +2102,16 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc 
     return;
   }
   QHand h;
-  int mn = -1;  // this wave's query of step t + 1
-  if (w < sd.M) {
+  int mn = -1;   // this wave's query of step t + 1
+  int job = 0;
+  if (w < JM) {
     const QPix px = ia_qpix(sd, g.bw, w);
+    job = px.job;
+    const JobPtrs jp = jobs.get(job);
     MergeOut o;
     merge_fused<1, false, RPL>(g, sd, A, ma, w, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv], &o);
     if (px.r + 1 < g.bh && px.c >= 2) {  // row r + 1 gathers (r + 1, c - 2) at step t + 1
-      HandSlot *hs = nx.hand + px.r;
+      HandSlot *hs = nx.hand + (int64_t)job * g.bh + px.r;
       if (lane == 0) {
         hs->v = o.v;
         hs->sr = o.pr;
@@ -2077,26 +2127,33 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc 
     h.s0r = o.pr;
     h.s0c = o.pc;
     h.i0 = o.img;
-    if (px.c + 1 < g.bw) mn = px.r - nx.sn.r0;
-  } else if (w == sd.M) {
-    if (nx.sn.t - 3 * (nx.sn.r0 + nx.sn.M - 1) == 0) mn = nx.sn.M - 1;  // a row enters at column 0
+    if (px.c + 1 < g.bw) mn = job * nx.sn.M + (px.r - nx.sn.r0);
+  } else if (w < JM + J) {
+    job = w - JM;
+    if (nx.sn.t - 3 * (nx.sn.r0 + nx.sn.M - 1) == 0) mn = job * nx.sn.M + nx.sn.M - 1;  // a row enters at column 0
   } else {
-    mn = nx.sn.M + (w - sd.M - 1);
+    mn = J * nx.sn.M + (w - JM - J);
   }
   if (mn < 0 || mn >= nx.sn.Mpad) return;
   _Float16 *qf = (_Float16 *)nx.qf;
   float4 o0, o1, o2;
-  if (mn >= nx.sn.M) {
-    gather_p_pad<KS>(mn, lane, qf, nx.qinfo, o0, o1, o2);
-    if (nx.xp.W) {
-      if (lane < 16 * KS) xh[wv][0][lane] = xh[wv][1][lane] = (_Float16)0.f;
-      xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
+  if (mn >= J * nx.sn.M) {
+    if constexpr (PR) {
+      gather_p_pad<KS>(mn, lane, qf, nx.qinfo, o0, o1, o2);
+      if (nx.xp.W) {
+        if (lane < 16 * KS) xh[wv][0][lane] = xh[wv][1][lane] = (_Float16)0.f;
+        xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
+      }
+    } else {
+      if (lane < 16 * KS) put_qh<KS>(qf, mn, lane, 0.);
     }
     return;
   }
+  const JobPtrs jp = jobs.get(job);
+  if constexpr (!JS::single) B = job_imgs(B, jp);  // single job: B already holds its images
   const QPix pn = ia_qpix(nx.sn, g.bw, mn);
   if (pn.r >= 1 && pn.c + 2 < g.bw) {  // (r - 1, c + 2) of step t: the row above's handoff
-    const HandSlot *hs = nx.hand + (pn.r - 1);
+    const HandSlot *hs = nx.hand + (int64_t)job * g.bh + (pn.r - 1);
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
     // relaxed: the slot is uncached (nothing stale to invalidate); its fields load after the
     // seq was seen
@@ -2115,9 +2172,13 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc 
     h.i1 = hs->im;
   }
   __builtin_amdgcn_wave_barrier();  // the merge's LDS rows are done with
-  gather_p_query<KS, false, true>(g, nx.sn, B, jp, mn, lane, nx.mu, nx.q64, nx.qn2, qf, ma.db64, nx.basis, nx.ufac,
-                                  nx.qinfo, A, qsh[wv], nx.xp.W ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2);
-  if (nx.xp.W) xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
+  if constexpr (PR) {
+    gather_p_query<KS, false, true>(g, nx.sn, B, jp, mn, lane, nx.mu, nx.q64, nx.qn2, qf, ma.db64, nx.basis, nx.ufac,
+                                    nx.qinfo, A, qsh[wv], nx.xp.W ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2);
+    if (nx.xp.W) xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
+  } else {
+    gather_h_query_fused<KS>(g, nx.sn, B, mn, lane, nx.mu, nx.q64, nx.qn2, qf, h);
+  }
 }
 
 // multi-rank finish: global winner over the all-gathered per-rank winners, then coherence
@@ -2505,11 +2566,25 @@ static void launch_merge_j(const LevelGeo &g, const StepDesc &sd, const Imgs &A,
   }
 }
 void ia_launch_merge_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const JobSet &jobs,
-                            const Imgs &B, const NextStep &nx, hipStream_t st) {
-  // waves: the step's merges, the entering row's gather, the next step's pad queries
-  const int nw = sd.M + 1 + (nx.sn.Mpad - nx.sn.M) + (nx.wait_n > 0 ? 1 : 0);
-  hipLaunchKernelGGL((k_merge_gather<4>), dim3(cdiv(nw, IA_PQ_WPB)), dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArg1{jobs.j0},
-                     job0_imgs(B, jobs), nx);
+                            const Imgs &B, const NextStep &nx, bool pruned, hipStream_t st) {
+  // waves: the step's merges, each job's entering row, the next step's pad queries (+ the waiter)
+  const int nw = sd.J * sd.M + sd.J + (nx.sn.Mpad - sd.J * nx.sn.M) + (nx.wait_n > 0 ? 1 : 0);
+  const dim3 grid(cdiv(nw, IA_PQ_WPB));
+  if (jobs.J == 1) {
+    if (pruned)
+      hipLaunchKernelGGL((k_merge_gather<4, true, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArg1{jobs.j0},
+                         job0_imgs(B, jobs), nx);
+    else
+      hipLaunchKernelGGL((k_merge_gather<4, false, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArg1{jobs.j0},
+                         job0_imgs(B, jobs), nx);
+  } else {
+    if (pruned)
+      hipLaunchKernelGGL((k_merge_gather<4, true, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArgN{jobs.rest},
+                         B, nx);
+    else
+      hipLaunchKernelGGL((k_merge_gather<4, false, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArgN{jobs.rest},
+                         B, nx);
+  }
 }
 template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,

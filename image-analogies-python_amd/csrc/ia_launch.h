@@ -13,9 +13,10 @@ void ia_launch_k3(int KH, int qt, const float4 *db, const float4 *qf, int n_tile
                   int row0, int NT, float4 *rec, float *recT, hipStream_t st);
 void ia_launch_merge(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
                      const JobSet &jobs, bool fused, hipStream_t st);
-// fused K4 of step sd + K2p of step nx.sn (single job, pruned 1-channel level, <= 256 records per query)
+// fused K4 of step sd + the gather of step nx.sn (K2p when pruned, else K2h; 1-channel levels,
+// <= 256 records per query)
 void ia_launch_merge_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, const JobSet &jobs,
-                            const Imgs &B, const NextStep &nx, hipStream_t st);
+                            const Imgs &B, const NextStep &nx, bool pruned, hipStream_t st);
 void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const double *db64, const double *q64,
                       const Winner *allwin, int world, int Mstride, const JobSet &jobs, hipStream_t st);
 void ia_launch_db64_build(const LevelGeo &g, const Imgs &A, double *db64, hipStream_t st);

@@ -40,13 +40,18 @@ def _run(ctx, z, jobs, batched):
     return S, IM, st
 
 
-@pytest.mark.parametrize('mode', ['default', 'pruned', 'f32'])
+@pytest.mark.parametrize('mode', ['default', 'pruned', 'f32', 'fuse_unpruned'])
 @pytest.mark.parametrize('name', ['g32', 'multiap', 'ties'])
 def test_batched_levels_match_separate_and_reference(ctx, name, mode):
+    """pruned: every level pruned, the batched steps run the fused merge + gather per job
+    (k_merge_gather with one handoff row set per job); fuse_unpruned: the fused launch on the
+    unpruned levels too"""
     from ia_amd import _native
     z = load_e2e(name)
     if mode == 'pruned':
         ctx.set_option('prune_min_rows', 1)
+    if mode == 'fuse_unpruned':
+        ctx.set_option('fuse_unpruned', 1)
     if mode == 'f32':
         ctx.set_option('matcher', _native.IA_MATCH_F32)
     try:
@@ -57,6 +62,7 @@ def test_batched_levels_match_separate_and_reference(ctx, name, mode):
     finally:
         ctx.set_option('prune_min_rows', 524288)
         ctx.set_option('matcher', _native.IA_MATCH_F16X3)
+        ctx.set_option('fuse_unpruned', 0)
     for j in range(len(jb)):
         for level in range(1, z['L']):
             assert np.array_equal(Sb[j][level], Ss[j][level]) and np.array_equal(IMb[j][level], IMs[j][level])
