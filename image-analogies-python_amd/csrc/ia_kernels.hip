@@ -2076,18 +2076,18 @@ __device__ __forceinline__ void gather_h_query_fused(const LevelGeo &g, const St
 // alternate by step parity (this launch's merges read step t's half while its gathers write
 // step t + 1's).
 // ------------------------------------------------------------------------------------------
-template <int RPL, bool PR, class JS>
+template <int RPL, bool PR, bool XO, class JS>
 __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, JS jobs,
                                                          Imgs B, NextStep nx) {
   constexpr int KS = 4;
   const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * IA_PQ_WPB + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int J = sd.J, JM = J * sd.M;
+  const int J = JS::single ? 1 : sd.J, JM = J * sd.M;
   __shared__ double qsh[IA_PQ_WPB][Geo<1>::DS], wsh[IA_PQ_WPB][Geo<1>::DS];
   __shared__ int crsh[IA_PQ_WPB][IA_WAVE];
   __shared__ float cvsh[IA_PQ_WPB][IA_WAVE];
   __shared__ __attribute__((aligned(16))) _Float16 xh[IA_PQ_WPB][2][16 * KS];  // owner publish: hi / lo columns
-  if (w >= JM + J + (nx.sn.Mpad - J * nx.sn.M)) {  // the waiter (nx.wait_n > 0 only)
+  if (XO && w >= JM + J + (nx.sn.Mpad - J * nx.sn.M)) {  // the waiter (nx.wait_n > 0 only)
     // after an earlier timeout of this context: no waiting (one lost peer costs one timeout)
     if (__hip_atomic_load(nx.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
     const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
@@ -2140,7 +2140,7 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc 
   if (mn >= J * nx.sn.M) {
     if constexpr (PR) {
       gather_p_pad<KS>(mn, lane, qf, nx.qinfo, o0, o1, o2);
-      if (nx.xp.W) {
+      if (XO && nx.xp.W) {
         if (lane < 16 * KS) xh[wv][0][lane] = xh[wv][1][lane] = (_Float16)0.f;
         xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
       }
@@ -2174,8 +2174,8 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc 
   __builtin_amdgcn_wave_barrier();  // the merge's LDS rows are done with
   if constexpr (PR) {
     gather_p_query<KS, false, true>(g, nx.sn, B, jp, mn, lane, nx.mu, nx.q64, nx.qn2, qf, ma.db64, nx.basis, nx.ufac,
-                                    nx.qinfo, A, qsh[wv], nx.xp.W ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2);
-    if (nx.xp.W) xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
+                                    nx.qinfo, A, qsh[wv], XO && nx.xp.W ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2);
+    if (XO && nx.xp.W) xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
   } else {
     gather_h_query_fused<KS>(g, nx.sn, B, mn, lane, nx.mu, nx.q64, nx.qn2, qf, h);
   }
@@ -2570,21 +2570,22 @@ void ia_launch_merge_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &A
   // waves: the step's merges, each job's entering row, the next step's pad queries (+ the waiter)
   const int nw = sd.J * sd.M + sd.J + (nx.sn.Mpad - sd.J * nx.sn.M) + (nx.wait_n > 0 ? 1 : 0);
   const dim3 grid(cdiv(nw, IA_PQ_WPB));
-  if (jobs.J == 1) {
-    if (pruned)
-      hipLaunchKernelGGL((k_merge_gather<4, true, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArg1{jobs.j0},
-                         job0_imgs(B, jobs), nx);
-    else
-      hipLaunchKernelGGL((k_merge_gather<4, false, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArg1{jobs.j0},
-                         job0_imgs(B, jobs), nx);
-  } else {
-    if (pruned)
-      hipLaunchKernelGGL((k_merge_gather<4, true, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArgN{jobs.rest},
-                         B, nx);
-    else
-      hipLaunchKernelGGL((k_merge_gather<4, false, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArgN{jobs.rest},
-                         B, nx);
-  }
+  const bool xo = nx.xp.W > 0 || nx.wait_n > 0;
+  if (jobs.J == 1 && pruned && xo)
+    hipLaunchKernelGGL((k_merge_gather<4, true, true, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArg1{jobs.j0},
+                       job0_imgs(B, jobs), nx);
+  else if (jobs.J == 1 && pruned)
+    hipLaunchKernelGGL((k_merge_gather<4, true, false, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArg1{jobs.j0},
+                       job0_imgs(B, jobs), nx);
+  else if (jobs.J == 1)
+    hipLaunchKernelGGL((k_merge_gather<4, false, false, JobArg1>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArg1{jobs.j0},
+                       job0_imgs(B, jobs), nx);
+  else if (pruned)
+    hipLaunchKernelGGL((k_merge_gather<4, true, false, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArgN{jobs.rest},
+                       B, nx);
+  else
+    hipLaunchKernelGGL((k_merge_gather<4, false, false, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArgN{jobs.rest},
+                       B, nx);
 }
 template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
