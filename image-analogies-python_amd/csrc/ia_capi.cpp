@@ -143,6 +143,8 @@ struct ia_ctx {
   // to depend on it (ia_pipeline_depend) makes each of its steps wait for the steps of that
   // generation it reads from (level l + 1 step t reads B' of level l steps <= t / 2 + 4)
   int p_record = 0;                          // option "pipeline_record"
+  int p_last = 0;                            // option "pipeline_last": the next level call has no
+                                             // dependents (no per-step events; one call only)
   std::vector<hipEvent_t> p_ev[3];           // per generation mod 3: one event per step
   std::atomic<long long> p_enq{-1};          // last step of the current generation enqueued
   std::atomic<long long> p_T{0};             // steps of the current generation
@@ -464,6 +466,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "fuse_unpruned")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_unpruned must be 0 or 1");
     c->fuse_unpruned = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "pipeline_last")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: pipeline_last must be 0 or 1");
+    c->p_last = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "pipeline_record")) {
@@ -1140,13 +1147,20 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     while (dp->p_done.load() < dgen && dp->p_enq.load() < need)
       if (stalled()) return fail(IA_ECOMM, "pipeline: the previous level stopped enqueueing");
       else std::this_thread::yield();
-    if (dp->p_done.load() < dgen) HIP_TRY(hipStreamWaitEvent(c->st, dp->p_ev[dgen % 3][need], 0));
+    if (dp->p_done.load() < dgen) {
+      hipEvent_t ev = dp->p_ev[dgen % 3][need];
+      // the previous level usually runs far ahead: an event that already completed needs no
+      // barrier packet on this stream
+      if (hipEventQuery(ev) != hipSuccess) HIP_TRY(hipStreamWaitEvent(c->st, ev, 0));
+    }
     waited = need;
     return IA_OK;
   };
+  const bool no_events = c->p_last != 0;  // nothing waits on this call's steps
+  c->p_last = 0;
   auto mark_step = [&](int64_t t) {
     if (!gen) return;
-    hipEventRecord((*pev)[t], c->st);
+    if (!no_events) hipEventRecord((*pev)[t], c->st);
     c->p_enq.store(t);
   };
   for (int64_t t = 0; t < T; mark_step(t), t++) {

@@ -8,6 +8,7 @@ step wait (a stream event wait) for exactly the steps it reads.  Results equal t
 order bit for bit; device-resident levels only (a host-buffer level returns its B' at the end of
 its call, too late for the next level's first steps).
 """
+import os
 import threading
 
 
@@ -36,6 +37,8 @@ def run_levels_pipelined(level_fn, ctxs, L, stats):
                     continue
                 if l > 1:
                     ctxs[w].pipeline_depend(ctxs[side(l - 1)], gen[l - 1])
+                if l == L - 1 and not os.environ.get('IA_PIPE_RECORD_ALL'):
+                    ctxs[w].set_option('pipeline_last', 1)   # nothing depends on the finest level: no per-step events
                 level_fn(ctxs[w], l, sts[w])
         except Exception as e:   # the other thread's waits end by timeout (IA_ECOMM)
             errs.append(e)

@@ -152,6 +152,8 @@ int ia_version(void);
  * "fuse_gather" = 1 (default) / 0: on one-job unsharded pruned levels the merge of step t and the
  * gather of step t + 1 run as one launch (the step's results handed row to row through uncached
  * slots); 0 = separate launches.
+ * "pipeline_last" = 1: the next level call has no dependents, so it records no per-step events
+ * (level pipelining's finest level; applies to one call).
  * "stream_priority" = 0 (default) / 1 (high) / 2 (low): recreate the context's stream with that
  * priority (idle contexts; level pipelining puts the finest level's stream high).
  * "prune_group" = G in {1 (default), 2, 4, 8}: pruned levels store each group of G Morton tiles
