@@ -345,8 +345,8 @@ def main():
                     help='1: the fused merge + gather on unpruned levels too (measured slower, DESIGN.md §6c)')
     ap.add_argument('--pipe-ctx', type=int, default=4, choices=[2, 3, 4, 5],
                     help='contexts the pipelined levels rotate over (default 4: the finest level\'s stream is free '
-                         'once level L - 5 ends; 2: level l + 2 follows level l on one stream; 5: above the box\'s '
-                         '4 hardware queues per process, measured slower, DESIGN.md §6b)')
+                         'once level L - 5 ends; 2: level l + 2 follows level l on one stream; 5: measured slower, '
+                         'DESIGN.md §6b)')
     ap.add_argument('--pipe-priority', type=int, default=1, choices=[0, 1],
                     help='1: the finest level\'s stream at high priority, the coarser levels\' at low')
     ap.add_argument('--k3p-blocks', type=int, default=1, choices=[0, 1],
