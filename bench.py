@@ -251,9 +251,10 @@ def pipe_contexts(args, local, ctx):
     finest level's context (ctx) gets the high stream priority, the others the low one"""
     extra = [make_context(args, local) for _ in range(args.pipe_ctx - 1)]
     if args.pipe_priority and not os.environ.get('IA_CU_SPLIT'):   # CU-masked rehearsal streams keep theirs
-        ctx.set_option('stream_priority', 1)
+        hi, lo = (1, 2) if args.pipe_priority == 1 else (2, 1)      # 2: reversed (experiment)
+        ctx.set_option('stream_priority', hi)
         for cx in extra:
-            cx.set_option('stream_priority', 2)
+            cx.set_option('stream_priority', lo)
     return extra
 
 
@@ -347,8 +348,8 @@ def main():
                     help='contexts the pipelined levels rotate over (default 4: the finest level\'s stream is free '
                          'once level L - 5 ends; 2: level l + 2 follows level l on one stream; 5: measured slower, '
                          'DESIGN.md §6b)')
-    ap.add_argument('--pipe-priority', type=int, default=1, choices=[0, 1],
-                    help='1: the finest level\'s stream at high priority, the coarser levels\' at low')
+    ap.add_argument('--pipe-priority', type=int, default=1, choices=[0, 1, 2],
+                    help='1: the finest level\'s stream at high priority, the coarser levels\' at low; 2: reversed')
     ap.add_argument('--k3p-blocks', type=int, default=1, choices=[0, 1],
                     help='pruned scan of a step wider than 11 query tiles: 1 = one launch of (query block x DB '
                          'chunk) workgroups, 0 = one launch per query block')
