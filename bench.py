@@ -658,7 +658,7 @@ def main():
     if args.fuse_gather and st['prune_launches_timed'] > 0:
         roofline['fused_gather'] = ('the unsampled steps of a pruned level run K4 of step t and K2p of step t + 1 as one '
                                     'launch (k_merge_gather, DESIGN.md §6c); the sampled steps keep separate K2 / K4 '
-                                    'launches, which the gather / merge timings above are')
+                                    'launches, which the gather / merge timings in roofline.gathers measure')
     roofline['gathers'] = gather_rooflines(st)
     roofline['fp32_mfma_equiv_tflops'] = fp32_equiv / 1e12
     roofline['fp32_mfma_equiv_frac'] = fp32_equiv / FP32_MFMA_PEAK
