@@ -81,6 +81,10 @@ class DeviceJob(object):
         ctx.synthesize_level_device(self.ch, len(self.job.Ap_pyr_list), self.A[l].shape[:2], self.B[l].shape[:2],
                                     ptrs, self.job.kappa_factor(l), stats)
 
+    def outputs(self):
+        """the job's results: B', s and im of every synthesised level (device tensors)"""
+        return [x for l in range(1, self.job.L) for x in (self.Bp[l], self.S[l], self.IM[l])]
+
     def run(self, ctx, torch, stats, pipe=None):
         """pipe = more contexts (one or a list): levels rotate over ctx + them, each level's steps
         waiting only for the steps of the previous level they read (include/ia.h
@@ -109,6 +113,9 @@ class DeviceBatch(object):
         self.dj += [DeviceJob(j, torch, dev, a_from=self.dj[0]) for j in jobs[1:]]
         self.ch = self.dj[0].ch
 
+    def outputs(self):
+        return [x for d in self.dj for x in d.outputs()]
+
     def run(self, ctx, torch, stats):
         for d in self.dj:
             for l in range(d.job.L):
@@ -122,6 +129,33 @@ class DeviceBatch(object):
                          s_out=d.S[l].data_ptr(), im_out=d.IM[l].data_ptr()) for d in self.dj]
             ctx.synthesize_levels_device(self.ch, len(d0.job.Ap_pyr_list), d0.A[l].shape[:2], d0.B[l].shape[:2], ptrs,
                                          [d.job.kappa_factor(l) for d in self.dj], stats)
+
+
+class HostCopy(object):
+    """Pinned host buffers for a set of device result tensors: fetch() is the D2H copy that ends a
+    timed step back on the host (B', s, im of every level, as image_analogies_main returns them);
+    digest() hashes the fetched bytes (bit-exact parity checks between runs and ranks)."""
+
+    def __init__(self, tensors, torch):
+        self.torch = torch
+        self.dev = list(tensors)
+        self.host = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in self.dev]
+
+    def fetch(self):
+        for d, h in zip(self.dev, self.host):
+            h.copy_(d, non_blocking=True)
+
+    @property
+    def nbytes(self):
+        return sum(t.numel() * t.element_size() for t in self.dev)
+
+    def digest(self):
+        import hashlib
+        self.torch.cuda.synchronize()
+        hs = hashlib.sha1()
+        for h in self.host:
+            hs.update(h.numpy().tobytes())
+        return hs.hexdigest()
 
 
 EXCHANGE = {'rccl': 0, 'peer': 1, 'owner': 2}   # include/ia.h option "exchange"
@@ -216,11 +250,15 @@ def cpu_baseline_sweep(sw, seconds, procs=4):
                      'per level', procs, total)
 
 
+ALL_CTX = []   # every libia context this process made (timed steps switch option "stamps" on all)
+
+
 def make_context(args, local):
     """One libia context with every option of the command line (each context of a multi-stream
     cfg5 run gets the same settings)."""
     from ia_amd import _native
     cx = _native.Context(local)
+    ALL_CTX.append(cx)
     cx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
     if args.k3_variant != 1:
         cx.set_option('k3_variant', args.k3_variant)       # DIAG=1 builds only
@@ -315,7 +353,15 @@ def main():
                          'cfg jobs sharing A (synth.make_jobs), every rank scanning its 1/N of the DB for all of them '
                          '(with --shard-emulate W on one GPU: the W-rank step for the cost model)')
     ap.add_argument('--no-replicas-extra', action='store_true',
-                    help='N > 1 shard mode: skip the extra replicas measurement (value_replicas)')
+                    help='N > 1 shard mode: skip the extra replicas measurement (value_replicas; the single-GPU '
+                         'run of the rank\'s job that shard_parity compares against still runs once)')
+    ap.add_argument('--strong', type=int, default=1, choices=[0, 1],
+                    help='N > 1 shard mode: also time ONE cfg job whose DB is sharded over the N ranks '
+                         '(value_strong, the single-analogy reading of BASELINE config 3) and check it bit for '
+                         'bit against the single-GPU run (strong_parity)')
+    ap.add_argument('--strong-exchange', default='peer', choices=['peer', 'rccl'],
+                    help='exchange of the value_strong run: per-shard winners by peer writes fused into the merge '
+                         '(peer) or ncclAllGather + a finish kernel (rccl)')
     ap.add_argument('--cpu-procs', type=int, default=4,
                     help='worker processes the CPU-baseline sample is split over (each single-threaded)')
     ap.add_argument('--matcher', default='f16x3', choices=['f16x3', 'f32'],
@@ -519,10 +565,15 @@ def main():
         dj = DeviceJob(job, torch, dev)
         run = lambda st, cs=ctxs: dj.run(cs[0], torch, st)
 
-    def timed(steps, fn, sample_events):
-        """steps x fn between barriers + device syncs; max over ranks"""
+    def timed(steps, fn, sample_events, hc=None):
+        """steps x fn between barriers + device syncs; max over ranks.  hc (HostCopy): each step
+        ends with the D2H copy of its results, inside the timed region"""
         if sample_events and args.time_stride > 0:
             ctx.set_option('time_dist', args.time_stride)
+        # kernel-written stamps: the device time of every K3p / merge launch of these steps
+        for cx in ALL_CTX:
+            if cx.handle:
+                cx.set_option('stamps', 1)
         stats = _native.Stats()
         torch.cuda.synchronize()
         if dist:
@@ -530,11 +581,16 @@ def main():
         t_start = time.perf_counter()
         for _ in range(steps):
             fn(stats)
+            if hc is not None:
+                hc.fetch()
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
         el = time.perf_counter() - t_start
         ctx.set_option('time_dist', 0)
+        for cx in ALL_CTX:
+            if cx.handle:
+                cx.set_option('stamps', 0)
         if dist:
             tt = torch.tensor([el], dtype=torch.float64, device=dev if backend == 'nccl' else 'cpu')
             dist.all_reduce(tt, op=dist.ReduceOp.MAX)
@@ -544,6 +600,24 @@ def main():
     if shard_error is not None:
         dj, run = fall_back()
         ctxs = [ctx]
+    if owner and shard_error is None:
+        # exchange = 2 lays every rank's slots out from its own job's geometry (include/ia.h): the
+        # ranks' jobs must have identical level shapes, checked here instead of timing out
+        geo = [tuple(x.shape) for x in dj.job.B_pyr[:dj.job.L]] + [tuple(x.shape) for x in dj.job.A_pyr[:dj.job.L]]
+        allgeo = [None] * world
+        dist.all_gather_object(allgeo, geo)
+        if any(gx != allgeo[0] for gx in allgeo):
+            shard_error = 'the ranks\' jobs differ in level shapes (exchange = 2 needs identical shapes)'
+            dj, run = fall_back()
+            ctxs = [ctx]
+
+    def host_copy():
+        """pinned host buffers for the timed job(s)' results (the D2H that ends every timed step)"""
+        if sw is not None:
+            return HostCopy([x for j in mine for l in range(1, sw.L[j])
+                             for x in (dj.Bp[j][l], dj.S[j][l], dj.IM[j][l])], torch)
+        return HostCopy(dj.outputs(), torch)
+    hc = host_copy()
     for i in range(args.warmup):
         if world > 1 and args.mode == 'shard' and i == 0:
             try:
@@ -555,6 +629,7 @@ def main():
                 shard_error = shard_error or 'a peer rank failed the sharded warmup'
                 dj, run = fall_back()
                 ctxs = [ctx]
+                hc = host_copy()
                 run(_native.Stats())
             continue
         run(_native.Stats())
@@ -564,20 +639,82 @@ def main():
     # pipelined levels (or several cfg5 streams): HIP events around one stream's K3 launches would
     # also time the other stream's kernels, so the roofline comes from one extra sequential pass
     concurrent = len(ctxs) > 1 or (args.pipeline and sw is None and (not owner or pipe_owner) and args.shard_jobs <= 1)
-    elapsed, stats = timed(args.steps, run, not concurrent)
+    elapsed, stats = timed(args.steps, run, not concurrent, hc)
+    dj1 = h_shard = None
+    if world > 1 and args.mode == 'shard':
+        # this rank's own job (owner mode: job `rank`; every rank holds every job otherwise: job
+        # rank mod J) as the sharded run left it
+        dj1 = dj.dj[rank % len(dj.dj)] if isinstance(dj, DeviceBatch) else dj
+        hx = HostCopy(dj1.outputs(), torch)
+        hx.fetch()
+        h_shard = hx.digest()
     if concurrent:
         _, stats_rl = timed(1, lambda st: run(st, [ctx]), True)
     else:
         stats_rl = stats
-    value_replicas = None
-    if world > 1 and args.mode == 'shard' and not args.no_replicas_extra:
-        # the other multi-GPU reading: one independent job per GPU (no collective), the aggregate
-        # carried as value_replicas (never `value`: BASELINE config 3 is the sharded job)
+    value_replicas = value_strong = shard_parity = strong_parity = None
+    strong_info = None
+    if world > 1 and args.mode == 'shard':
+        # (1) the single-GPU run of this rank's own job (owner mode: job `rank`; every rank holds
+        # every job otherwise: job rank mod J), which the sharded result must equal bit for bit;
+        # timed, it is the other multi-GPU reading: one independent job per GPU, no collective
+        # (value_replicas; never `value`: BASELINE config 3 is the sharded job)
+        hc1 = HostCopy(dj1.outputs(), torch)
         rctx = make_context(args, local)
-        dj1 = dj.dj[0] if isinstance(dj, DeviceBatch) else dj
-        el_r, _ = timed(args.steps, lambda st: dj1.run(rctx, torch, st), False)
-        value_replicas = job_pixels * args.steps * world / el_r
+        if args.no_replicas_extra:
+            dj1.run(rctx, torch, _native.Stats())
+            hc1.fetch()
+        else:
+            el_r, _ = timed(args.steps, lambda st: dj1.run(rctx, torch, st), False, hc1)
+            value_replicas = job_pixels * args.steps * world / el_r
         rctx.close()
+        h_single = hc1.digest()
+        ok = h_shard == h_single
+        shard_parity = not agree(not ok)
+        log('[bench] rank %d: sharded run of job %d %s its single-GPU run'
+            % (rank, rank if owner else rank % args.shard_jobs, 'equals' if ok else 'DIFFERS FROM'))
+        # (2) value_strong: ONE cfg job, its DB sharded over the N ranks (every rank holds the job,
+        # scans its 1/N of each pruned level, per-step winner exchange), equal bit for bit to the
+        # single-GPU run of that job (rank 0's job 0 above)
+        if args.strong:
+            strong_error, h_strong = None, None
+            sctx = None
+            try:
+                sctx = make_context(args, local)
+                if args.strong_exchange == 'rccl':
+                    uid = [_native.comm_unique_id() if rank == 0 else None]
+                    dist.broadcast_object_list(uid, src=0)
+                    sctx.comm_init(rank, world, uid[0])
+                else:
+                    def all_gather_s(b):
+                        o = [None] * world
+                        dist.all_gather_object(o, b)
+                        return o
+                    sctx.xchg_init(rank, world, all_gather_s)
+                ds = DeviceJob(jobs_b[0], torch, dev, a_from=dj1)
+                hcs = HostCopy(ds.outputs(), torch)
+                ds.run(sctx, torch, _native.Stats())   # warmup
+                el_s, st_s = timed(args.steps, lambda st: ds.run(sctx, torch, st), False, hcs)
+                value_strong = job_pixels * args.steps / el_s
+                h_strong = hcs.digest()
+            except Exception as e:
+                strong_error = 'rank %d: %r' % (rank, e)
+                log('[bench] strong (one-job) run failed: %s' % strong_error)
+            if agree(strong_error is not None):
+                value_strong = None
+                strong_info = {'error': strong_error or 'a peer rank failed the one-job sharded run'}
+            else:
+                allh = [None] * world
+                dist.all_gather_object(allh, (h_strong, h_single))
+                ref = allh[0][1]          # rank 0's single-GPU run of job 0
+                strong_parity = all(x[0] == ref for x in allh)
+                strong_info = {'jobs': 1, 'exchange': args.strong_exchange, 'ms_per_step': el_s * 1e3 / args.steps,
+                               'scaling': 'strong', 'parallelism': 'dbshard%d_jobs1' % world,
+                               'note': 'one %s job (job 0), every pruned level\'s DB sharded %d ways, per-step '
+                                       'certified winner exchange; value_strong = that job\'s B\' px / wall time'
+                                       % (args.config, world)}
+            if sctx is not None:
+                sctx.close()
 
     # jobs whose pixels the timed steps produced: replicas one per rank; shard mode J jobs (every
     # rank holds all J: counted once); cfg5: the ranks split one sweep
@@ -659,6 +796,22 @@ def main():
         roofline['fused_gather'] = ('the unsampled steps of a pruned level run K4 of step t and K2p of step t + 1 as one '
                                     'launch (k_merge_gather, DESIGN.md §6c); the sampled steps keep separate K2 / K4 '
                                     'launches, which the gather / merge timings in roofline.gathers measure')
+    if st_all['k3p_stamp_launches'] > 0:
+        # the timed steps' own launches (kernel-written s_memrealtime stamps, no events): every
+        # pruned-scan launch of every timed step, in the configuration that is timed (pipelined
+        # levels, concurrent streams)
+        k3t = st_all['k3p_stamp_ms'] * 1e-3
+        roofline['frac_timed'] = st_all['k3p_bytes_all'] / k3t / HBM_PEAK
+        roofline['achieved_timed'] = st_all['k3p_bytes_all'] / k3t / 1e9
+        roofline['k3_us_per_launch_timed'] = st_all['k3p_stamp_ms'] * 1e3 / st_all['k3p_stamp_launches']
+        roofline['k3_launches_timed'] = st_all['k3p_stamp_launches']
+        roofline['algorithmic_bytes_per_launch_timed'] = st_all['k3p_bytes_all'] / st_all['k3p_stamp_launches']
+        if st_all['merge_stamp_launches'] > 0:
+            roofline['merge_us_per_launch_timed'] = st_all['merge_stamp_ms'] * 1e3 / st_all['merge_stamp_launches']
+            roofline['merge_launches_timed'] = st_all['merge_stamp_launches']
+        roofline['timing_timed'] = ('frac_timed / *_timed: every pruned-scan (and fused merge) launch of the %d timed '
+                                    'steps, device time = max(workgroup end) - min(workgroup start) from s_memrealtime '
+                                    'stamps the kernels write (include/ia.h option "stamps")' % args.steps)
     roofline['gathers'] = gather_rooflines(st)
     roofline['fp32_mfma_equiv_tflops'] = fp32_equiv / 1e12
     roofline['fp32_mfma_equiv_frac'] = fp32_equiv / FP32_MFMA_PEAK
@@ -702,10 +855,9 @@ def main():
                                                          "reference's fp64 brute-force decisions"
                                                          if f16 else 'fp32 MFMA candidates + certified fp64 rerank'),
                                            'timed_region': ('per step: every level 1..L-1 (DB build, wavefront '
-                                                            'synthesis) from device-resident pyramids to device '
-                                                            "completion of B'/s/im; the D2H copy of B'/s/im (about "
-                                                            '%.0f MB, <1%% of the step) is excluded'
-                                                            % (job_pixels * 20 / 1e6))},
+                                                            'synthesis) from device-resident pyramids, ending with '
+                                                            "the D2H copy of every level's B'/s/im (%.1f MB) into "
+                                                            'pinned host memory, back on the host' % (hc.nbytes / 1e6))},
            'roofline': roofline,
            'stats': {k: st_all[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
                                         'synth_ms', 'bound_violations', 'kappa_ambiguous', 'f16_levels', 'pruned_levels',
@@ -717,6 +869,15 @@ def main():
                                   'kappas': sorted({j.k for j in sw.jobs}), 'depths': sorted(set(sw.L))}
     if shard_error is not None:
         out['config']['shard_error'] = shard_error
+    if world > 1 and args.mode == 'shard':
+        out['shard_parity'] = shard_parity
+        out['config']['exchange_used'] = args.exchange
+        out['config']['shard_parity'] = ("each rank's own job of the timed sharded run (B', s, im of every level, "
+                                         'sha1 of the D2H bytes) == the same job run alone on that GPU')
+    if args.strong and world > 1 and args.mode == 'shard':
+        out['value_strong'] = value_strong
+        out['strong_parity'] = strong_parity
+        out['config']['strong'] = strong_info
     if value_replicas is not None:
         out['value_replicas'] = value_replicas
         out['config']['replicas'] = ('value_replicas = %d independent cfg jobs, one per GPU, no collective '
@@ -729,6 +890,10 @@ def main():
         cx.close()
     if dist:
         dist.destroy_process_group()
+    if shard_parity is False or strong_parity is False:
+        log('[bench] PARITY FAILURE: a sharded run differs from the single-GPU run (shard_parity %s, strong_parity %s)'
+            % (shard_parity, strong_parity))
+        sys.exit(3)
 
 
 if __name__ == '__main__':

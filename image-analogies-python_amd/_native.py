@@ -49,7 +49,10 @@ class Stats(ctypes.Structure):
                 ('k1_bytes', ctypes.c_double), ('build_levels', ctypes.c_int64),
                 ('gather_ms_timed', ctypes.c_double), ('gather_launches_timed', ctypes.c_int64),
                 ('gather_bytes_timed', ctypes.c_double), ('merge_ms_timed', ctypes.c_double),
-                ('merge_launches_timed', ctypes.c_int64), ('build_rows', ctypes.c_int64)]
+                ('merge_launches_timed', ctypes.c_int64), ('build_rows', ctypes.c_int64),
+                ('k3p_stamp_ms', ctypes.c_double), ('k3p_stamp_launches', ctypes.c_int64),
+                ('k3p_bytes_all', ctypes.c_double), ('merge_stamp_ms', ctypes.c_double),
+                ('merge_stamp_launches', ctypes.c_int64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

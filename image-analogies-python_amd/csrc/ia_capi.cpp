@@ -117,9 +117,14 @@ struct ia_ctx {
   int fuse_unpruned = 0;         // option "fuse_unpruned": 1 = also on unpruned levels (K4 + K2h)
   HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
   int hand_rows = 0;
+  int fuse_sort = 1;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot)
+  unsigned long long *kslot = nullptr;  // their per-query key slots (uncached)
+  int kslot_n = 0;
   unsigned hseq = 0;
   // per-step K3 timing (optional)
   int time_dist = 0;
+  int stamps = 0;                 // option "stamps": per-launch device time from kernel stamps
+  DevBuf stamp_k3, stamp_mg, stamp_dur;
   std::vector<hipEvent_t> evs, evg, evm;  // sampled steps: K3, K2 and K4 brackets
   hipEvent_t lv0 = nullptr, lv1 = nullptr, lv2 = nullptr;
   hipEvent_t kb[4] = {nullptr, nullptr, nullptr, nullptr};  // per level: K1b start / end, K1 start / end
@@ -137,6 +142,7 @@ struct ia_ctx {
   XSlot *xpeer[IA_XCHG_MAXW] = {};  // every rank's buffer in this address space (ia_xchg_open)
   bool xmapped[IA_XCHG_MAXW] = {};  // opened through hipIpcOpenMemHandle (closed on destroy)
   unsigned xseq = 0;              // exchange sequence number (one per sharded step, same on every rank)
+  bool xfresh = false;            // the buffer was zeroed by ia_xchg_alloc and not opened since
   DevBuf xerr;
   // level pipelining: a recording context publishes, per level call (a
   // generation), the wavefront steps it has enqueued, each followed by an event; a context told
@@ -365,7 +371,7 @@ void ia_destroy(ia_ctx *c) {
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
                     &c->boxes, &c->qinfo, &c->pairs, &c->ord, &c->qs_order, &c->qs_info, &c->qs_frag, &c->qs_tbox, &c->tnorm,
-                    &c->pr_rot, &c->pr_lut,
+                    &c->pr_rot, &c->pr_lut, &c->stamp_k3, &c->stamp_mg, &c->stamp_dur,
                     &c->py_in, &c->py_tmp, &c->py_sm, &c->py_mm, &c->py_out})
     b->release();
   for (auto *v : {&c->evs, &c->evg, &c->evm, &c->p_ev[0], &c->p_ev[1], &c->p_ev[2]})
@@ -379,6 +385,7 @@ void ia_destroy(ia_ctx *c) {
     if (c->xmapped[p]) hipIpcCloseMemHandle(c->xpeer[p]);
   if (c->xbuf) hipFree(c->xbuf);
   if (c->hand) hipFree(c->hand);
+  if (c->kslot) hipFree(c->kslot);
   c->xerr.release();
   c->xo_inv.release();
   hipStreamDestroy(c->st);
@@ -389,6 +396,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!c || !name) return fail(IA_EINVAL, "ia_set_option: NULL argument");
   if (!std::strcmp(name, "time_dist")) {
     c->time_dist = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "stamps")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: stamps must be 0 or 1");
+    c->stamps = value;
     return IA_OK;
   }
 #ifdef IA_K3H_DIAG  // DIAG=1 builds: every kernel version of DESIGN.md §4b's progression
@@ -463,6 +475,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     c->fuse_gather = value;
     return IA_OK;
   }
+  if (!std::strcmp(name, "fuse_sort")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_sort must be 0 or 1");
+    c->fuse_sort = value;
+    return IA_OK;
+  }
   if (!std::strcmp(name, "fuse_unpruned")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_unpruned must be 0 or 1");
     c->fuse_unpruned = value;
@@ -531,6 +548,13 @@ int ia_comm_init(ia_ctx *c, int rank, int world, const unsigned char id[128]) {
   HIP_TRY(hipSetDevice(c->dev));
   if (c->comm) ncclCommDestroy(c->comm);
   c->comm = nullptr;
+  // the RCCL all-gather replaces any peer-write exchange opened before (ia_xchg_open)
+  for (int p = 0; p < IA_XCHG_MAXW; p++) {
+    if (c->xmapped[p]) hipIpcCloseMemHandle(c->xpeer[p]);
+    c->xmapped[p] = false;
+    c->xpeer[p] = nullptr;
+  }
+  c->exchange = 0;
   c->rank = rank;
   c->world = world;
   if (world == 1) return IA_OK;
@@ -557,18 +581,33 @@ static void ia_launch_query_sort_xo_owner(ia_ctx *c, const LevelGeo &g, const fl
   ia_launch_query_sort_xo(qinfo, qf, xs, c->st);
 }
 
-static int xchg_alloc(ia_ctx *c, int world) {
-  if (c->xbuf && c->xbuf_w >= world) return IA_OK;
+// fresh = true (ia_xchg_alloc, before the ranks swap handles): a reused buffer is zeroed too and
+// the sequence restarts, so no seq word left from an earlier exchange (or an emulated run on this
+// context) can match the restarted sequence; the handle swap orders every rank's zeroing before
+// any peer's first store
+static int xchg_alloc(ia_ctx *c, int world, bool fresh = false) {
+  const size_t bytes = ia_xslots_bytes(world) + 2 * XOLayout::PARITY;
+  if (c->xbuf && c->xbuf_w >= world) {
+    if (fresh) {
+      HIP_TRY(hipStreamSynchronize(c->st));
+      HIP_TRY(hipMemset(c->xbuf, 0, ia_xslots_bytes(c->xbuf_w) + 2 * XOLayout::PARITY));
+      HIP_TRY(hipDeviceSynchronize());
+      c->xbuf_w = world;
+      c->xseq = 0;
+      c->xfresh = true;
+    }
+    return IA_OK;
+  }
   if (c->xbuf) hipFree(c->xbuf);
   c->xbuf = nullptr;
   // winner slots (exchange = 1) + two parities of the owner-computes area (exchange = 2)
-  const size_t bytes = ia_xslots_bytes(world) + 2 * XOLayout::PARITY;
   // uncached: peers' xGMI stores and this device's polling loads meet in memory, not in an L2
   HIP_TRY(hipExtMallocWithFlags(&c->xbuf, bytes, hipDeviceMallocUncached));
   HIP_TRY(hipMemset(c->xbuf, 0, bytes));
   HIP_TRY(hipDeviceSynchronize());
   c->xbuf_w = world;
   c->xseq = 0;
+  c->xfresh = fresh;
   int rc;
   if ((rc = c->xerr.ensure(4))) return rc;
   return IA_OK;
@@ -579,7 +618,7 @@ int ia_xchg_alloc(ia_ctx *c, int world, unsigned char handle_out[64]) {
   static_assert(sizeof(hipIpcMemHandle_t) == 64, "hipIpcMemHandle_t size");
   HIP_TRY(hipSetDevice(c->dev));
   int rc;
-  if ((rc = xchg_alloc(c, world))) return rc;
+  if ((rc = xchg_alloc(c, world, true))) return rc;
   hipIpcMemHandle_t h;
   HIP_TRY(hipIpcGetMemHandle(&h, c->xbuf));
   std::memcpy(handle_out, &h, 64);
@@ -589,7 +628,8 @@ int ia_xchg_alloc(ia_ctx *c, int world, unsigned char handle_out[64]) {
 int ia_xchg_open(ia_ctx *c, int rank, int world, const unsigned char *handles) {
   if (!c || !handles || world < 1 || world > IA_XCHG_MAXW || rank < 0 || rank >= world)
     return fail(IA_EINVAL, "ia_xchg_open: bad rank / world");
-  if (!c->xbuf || c->xbuf_w != world) return fail(IA_EINVAL, "ia_xchg_open: call ia_xchg_alloc with this world first");
+  if (!c->xbuf || c->xbuf_w != world || !c->xfresh)
+    return fail(IA_EINVAL, "ia_xchg_open: call ia_xchg_alloc with this world first (once per ia_xchg_open)");
   HIP_TRY(hipSetDevice(c->dev));
   for (int p = 0; p < IA_XCHG_MAXW; p++)
     if (c->xmapped[p]) {
@@ -613,7 +653,8 @@ int ia_xchg_open(ia_ctx *c, int rank, int world, const unsigned char *handles) {
   c->rank = rank;
   c->world = world;
   if (c->exchange == 0) c->exchange = 1;  // keep 2 (owner computes) when it was chosen before
-  c->xseq = 0;
+  c->xseq = 0;  // the buffer was zeroed by ia_xchg_alloc: no stale seq word matches the new sequence
+  c->xfresh = false;
   return IA_OK;
 }
 
@@ -967,6 +1008,27 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                 (rc = c->qs_frag.ensure((size_t)Mpad_max * db_row_bytes)) ||
                 (rc = c->qs_tbox.ensure((size_t)Mpad_max / IA_TILE * 3 * 16))))
     return rc;
+  // option "stamps" (pruned levels): per-launch workgroup stamps of every K3p launch (<= IA_NWG_H
+  // workgroups each) and every fused merge launch (<= Mpad_max + J + 1 workgroups)
+  const bool stamped = c->stamps && prune;
+  const int64_t k3_cap = T * (int64_t)shards.size() * (c->k3p_blocks ? 1 : 8);
+  const int mg_stride = (int)Mpad_max + J + 64;
+  const int64_t mg_cap = T * J;
+  int64_t k3_n = 0, mg_n = 0;
+  if (stamped) {
+    if ((rc = c->stamp_k3.ensure((size_t)k3_cap * IA_NWG_H * 16)) || (rc = c->stamp_mg.ensure((size_t)mg_cap * mg_stride * 16)) ||
+        (rc = c->stamp_dur.ensure((size_t)(k3_cap + mg_cap) * 4)))
+      return rc;
+    HIP_TRY(hipMemsetAsync(c->stamp_k3.p, 0, (size_t)k3_cap * IA_NWG_H * 16, c->st));
+    HIP_TRY(hipMemsetAsync(c->stamp_mg.p, 0, (size_t)mg_cap * mg_stride * 16, c->st));
+  }
+  auto k3_stamp = [&]() -> unsigned long long * {
+    return stamped && k3_n < k3_cap ? c->stamp_k3.as<unsigned long long>() + (size_t)2 * IA_NWG_H * k3_n++ : nullptr;
+  };
+  auto mg_stamp = [&]() -> unsigned long long * {
+    return stamped && mg_n < mg_cap ? c->stamp_mg.as<unsigned long long>() + (size_t)2 * mg_stride * mg_n++ : nullptr;
+  };
+  double bytes_all_fixed = 0.;  // algorithmic bytes of every pruned launch besides its DB tiles
   // per-workgroup counters of the pruned scan: [pairs | pairs (timed steps) | tiles | tiles (timed)][wg]
   HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 4 * IA_NWG_H * 8, c->st));
   HIP_TRY(hipMemsetAsync(c->Rbits.p, 0, 4, c->st));
@@ -1079,6 +1141,16 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       HIP_TRY(hipDeviceSynchronize());
       c->hand_rows = hrows;
     }
+    if (c->kslot_n < Mpad_max) {  // key slots of the gathers' sort (option "fuse_sort")
+      HIP_TRY(hipStreamSynchronize(c->st));
+      if (c->kslot) hipFree(c->kslot);
+      c->kslot = nullptr;
+      c->kslot_n = 0;
+      HIP_TRY(hipExtMallocWithFlags((void **)&c->kslot, (size_t)Mpad_max * 8, hipDeviceMallocUncached));
+      HIP_TRY(hipMemset(c->kslot, 0, (size_t)Mpad_max * 8));
+      HIP_TRY(hipDeviceSynchronize());
+      c->kslot_n = (int)Mpad_max;
+    }
     if ((rc = c->xerr.ensure(4))) return rc;
     HIP_TRY(hipMemsetAsync(c->xerr.p, 0, 4, c->st));
   }
@@ -1090,6 +1162,8 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     qinfo = prune ? c->qinfo.as<float4>() + h * 3 * Mpad_max : nullptr;
   };
   int64_t gathered = -1;  // the step whose gather the previous fused launch ran
+  bool gsort = false;     // ... and that launch also sorted it (option "fuse_sort": no K2s, no in-scan sort)
+  const bool fsort = chain && prune && c->fuse_sort && !rot && !xo;
   const int64_t n_timed = stride ? (T + stride - 1) / stride : 0;
   for (auto *v : {&c->evs, &c->evg, &c->evm})
     if ((int64_t)v->size() < 2 * n_timed) {
@@ -1133,9 +1207,22 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   c->dep = nullptr;  // one level call per ia_pipeline_depend
   c->dep_gen = 0;
   int64_t waited = -1;
-  const auto t_start = std::chrono::steady_clock::now();
-  auto stalled = [&]() {  // the previous level's host thread stopped enqueueing (it failed)
-    return std::chrono::steady_clock::now() - t_start > std::chrono::seconds(120);
+  // the previous level's host thread stopped enqueueing (it failed): 120 s without progress of
+  // its generation or its enqueued steps (a long but healthy predecessor keeps resetting this)
+  auto t_prog = std::chrono::steady_clock::now();
+  long long seen_enq = -2;
+  int seen_gen = -1;
+  auto stalled = [&]() {
+    const auto now = std::chrono::steady_clock::now();
+    const long long e = dp->p_enq.load();
+    const int gn = dp->p_gen.load();
+    if (e != seen_enq || gn != seen_gen) {
+      seen_enq = e;
+      seen_gen = gn;
+      t_prog = now;
+      return false;
+    }
+    return now - t_prog > std::chrono::seconds(120);
   };
   auto wait_dep = [&](int64_t t) -> int {
     if (!dp) return IA_OK;
@@ -1233,12 +1320,14 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       const int nqb = ink ? Wsh : Wsh * xo_bpj;
       const bool timed = stride && t % stride == 0;
       if (timed) hipEventRecord(c->evs[2 * n_rec], c->st);
-      int nch = IA_NWG_H;
+      // one chunk count for every shard (the owners' merges index records as shard * nch + chunk
+      // and map a chunk back to its tiles with it): from the smallest shard, which every rank
+      // computes alike (shards differ by at most one tile, ia_shard_off)
+      int nch = std::max(1, std::min((int)(g.n_tiles / Wsh), IA_NWG_H / nqb));
+      if (nch >= 64) nch &= ~7;
       for (size_t i = 0; i < shards.size(); i++) {
         const Shard &x = shards[i];
         const int n = x.t1 - x.t0;
-        nch = std::max(1, std::min(n, IA_NWG_H / nqb));
-        if (nch >= 64) nch &= ~7;
         if ((n + nch - 1) / nch > IA_K3P_MAXK_LDS || (int64_t)Wsh * nch * Mrec > IA_XO_MAXREC)
           return fail(IA_EINVAL, "ia_synthesize_level: exchange = 2: shard too large for the pruned scan's chunks");
         XOScan xs{};
@@ -1263,10 +1352,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                       c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3x, sd.t,
                       reinterpret_cast<const int *>(loc + XOLayout::ORD), 0, sd.r0, nullptr,
                       reinterpret_cast<const float4 *>(loc + XOLayout::TBOX), c->tnorm.as<float>() + x.t0, c->st, nqb,
-                      Wsh * QTs, &xs);
+                      Wsh * QTs, &xs, k3_stamp());
         pairs_full += (double)n * Wsh * QTs;
         tiles_full += (double)n * nqb;
         dist_launches++;
+        bytes_all_fixed += (double)n * nqb * 32 + (double)Mrec * (16.0 * 16 * g.KS + 48) + (double)Mrec * nch * 24;
         if (timed) {
           launches_timed++;
           bytes_timed_fixed += (double)n * nqb * 32 + (double)Mrec * (16.0 * 16 * g.KS + 48) + (double)Mrec * nch * 24;
@@ -1315,6 +1405,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         mx.xo_seq = seq;
         mx.xo_err = c->xerr.as<unsigned>();
         mx.xo_timeout = 2000000000LL;
+        mx.stamp = mg_stamp();
         if (!fuse_next) {
           ia_launch_merge(g, s1, Aim, mx, c->win.as<Winner>(), one, true, c->st);
           continue;
@@ -1381,12 +1472,15 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     // steps wider than one launch's query tiles take the presorted form too when their blocks
     // run as one launch (k3p_blocks): one K2s launch instead of a second scan launch
     const bool wide = sd.Mpad > 512 || (c->k3p_blocks && sd.Mpad > qtmax * IA_TILE && !rot);
+    // sorted by the previous launch's gathers: the presorted form of the variant, no K2s
+    const bool gsorted = fsort && gathered == t && gsort;
     const int k3v = (kv == 11 || kv == 12 || kv == 15 || kv == 17 || kv == 19 || kv == 21) ? kv
-                    : (prune && wide
+                    : (prune && (wide || gsorted)
                            ? (kv == 13 ? 12 : kv == 14 ? 15 : kv == 18 ? 19 : kv == 20 ? 21 : kv == 16 ? 17 : 11)
                            : kv);
     const bool presorted = k3v == 11 || k3v == 12 || k3v == 15 || k3v == 17 || k3v == 19 || k3v == 21;
-    if (prune && presorted)
+    const float4 *tboxp = gsorted ? nullptr : c->qs_tbox.as<float4>();  // nullptr: boxes from the slice
+    if (prune && presorted && !gsorted)
       ia_launch_query_sort(qinfot, c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
                            c->qs_frag.p, c->qs_tbox.as<float4>(), c->st);
     if (ns > 0) {
@@ -1411,11 +1505,12 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
             ia_launch_k3p(qtb, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, 0, Mt, sd.Mpad, nch,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t, c->qs_order.as<int>(),
-                          0, sd.r0, nullptr, c->qs_tbox.as<float4>(), tn, c->st, nqb, qtt);
+                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp());
             m.nwg = nch;
             pairs_full += (double)n * qtt;
             tiles_full += (double)n * nqb;
             dist_launches++;
+            bytes_all_fixed += (double)n * nqb * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) + (double)Mt * nch * 20;
             if (timed) {
               launches_timed++;
               bytes_timed_fixed += (double)n * nqb * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) + (double)Mt * nch * 20;
@@ -1431,13 +1526,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
             ia_launch_k3p(qt, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t,
-                          c->qs_order.as<int>(), 0, sd.r0, nullptr, c->qs_tbox.as<float4>(), tn, c->st);
+                          c->qs_order.as<int>(), 0, sd.r0, nullptr, tboxp, tn, c->st, 1, 0, nullptr, k3_stamp());
           else if (prune)
             ia_launch_k3p(qt, dbp, c->qf.p, qinfot, m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
                           k3v, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
-                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st);
+                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, nullptr, k3_stamp());
           else if (use_h)
             ia_launch_k3h(g.KS, qt, dbp, c->qf.p, n, x.tpw, qt0, Mt, x.nwg, m.pos0, g.n_tiles, (float4 *)m.rec,
                           (float *)m.recT, c->k3_variant, c->st);
@@ -1450,6 +1545,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           pairs_full += (double)n * qt;
           tiles_full += (double)n;
           dist_launches++;
+          if (prune) bytes_all_fixed += (double)n * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) + (double)mq * x.nwg * 20;
           if (timed) {
             flops_timed += fl;
             launches_timed++;
@@ -1481,9 +1577,18 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       nx.seq = ++c->hseq;
       nx.err = c->xerr.as<unsigned>();
       nx.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
+      if (fsort) {  // the gathers also sort step t + 1 into k_query_sort's outputs
+        nx.kslot = c->kslot;
+        nx.sorder = c->qs_order.as<int>();
+        nx.sinfo = c->qs_info.as<float4>();
+        nx.sfrag = c->qs_frag.p;
+      }
+      mas[0].stamp = mg_stamp();
       ia_launch_merge_gather(g, sd, Aim, mas[0], djobs, Bim, nx, prune, c->st);
       gathered = t + 1;
+      gsort = fsort;
     } else if (!multi) {
+      mas[0].stamp = mg_stamp();
       ia_launch_merge(g, sd, Aim, mas[0], c->win.as<Winner>(), djobs, true, c->st);
     } else if (xchg) {
       // one-shot peer-write exchange fused into the merge: each shard's winner goes into every
@@ -1514,6 +1619,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   }
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipEventRecord(c->lv2, c->st));
+  if (stamped) {  // per-launch device ticks: K3p launches first, then the merges
+    ia_launch_stamp_durations(c->stamp_k3.as<unsigned long long>(), (int)k3_n, IA_NWG_H, c->stamp_dur.as<unsigned>(), c->st);
+    ia_launch_stamp_durations(c->stamp_mg.as<unsigned long long>(), (int)mg_n, mg_stride, c->stamp_dur.as<unsigned>() + k3_n,
+                              c->st);
+  }
   if (stats)
     for (int j = 0; j < J; j++) ia_launch_reduce_stats(jp[j].pstat, NB, c->counters.as<unsigned long long>(), c->st);
   for (int j = 0; j < J; j++) {
@@ -1621,6 +1731,18 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     stats->synth_ms += ms_syn;
     stats->dist_launches += dist_launches;
     stats->dist_flops += dist_flops;
+    if (stamped && k3_n + mg_n > 0) {
+      std::vector<unsigned> dur((size_t)(k3_n + mg_n));
+      HIP_TRY(hipMemcpy(dur.data(), c->stamp_dur.p, dur.size() * 4, hipMemcpyDeviceToHost));
+      double tk = 0., tm = 0.;
+      for (int64_t i = 0; i < k3_n; i++) tk += dur[i];
+      for (int64_t i = k3_n; i < k3_n + mg_n; i++) tm += dur[i];
+      stats->k3p_stamp_ms += tk * 1e-5;  // 100 MHz ticks
+      stats->k3p_stamp_launches += k3_n;
+      stats->merge_stamp_ms += tm * 1e-5;
+      stats->merge_stamp_launches += mg_n;
+      stats->k3p_bytes_all += (double)(prs[2] + prs[3]) * ia_k3h_tile_bytes(g.KS) + bytes_all_fixed;
+    }
     if (stride && ns > 0) {
       double tot = 0.;
       for (int64_t i = 0; i < n_rec; i++) {

@@ -107,7 +107,20 @@ struct MergeArgs {
   unsigned xo_seq = 0;
   unsigned *xo_err = nullptr;         // bit 3: a record did not arrive in time
   long long xo_timeout = 0;
+  unsigned long long *stamp = nullptr;  // option "stamps": this launch's per-workgroup (start, end)
 };
+
+// Per-launch device timing without HIP events (option "stamps"): every workgroup of a stamped
+// launch stores its (start, end) s_memrealtime ticks (100 MHz) at stamp[2 blockIdx], with vector
+// stores from one lane; k_stamp_durations turns each launch's slots into max(end) - min(start).
+// The timed, concurrent (pipelined) bench steps thereby report the device time of the kernels
+// they actually ran.
+__device__ __forceinline__ unsigned long long ia_clock() { return __builtin_amdgcn_s_memrealtime(); }
+__device__ __forceinline__ void ia_stamp_wg(unsigned long long *stamp, unsigned long long t0) {
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  stamp[2 * blockIdx.x] = t0 | 1ull;  // nonzero: a slot that was written (one tick of slack)
+  stamp[2 * blockIdx.x + 1] = t1;
+}
 
 // Rotated split-f16 DB of a pruned 1-channel level (k3p_variant 16 / 17): every
 // centred row a' is rotated onto the level's 55 principal axes, a'' = R a' (fp64), and stored
@@ -326,6 +339,7 @@ struct XOScan {
   unsigned seq;
   unsigned *err;                  // bit 2: a tile flag did not arrive in time
   long long timeout_ticks;
+  unsigned long long *stamp;      // option "stamps" (any K3p launch, owner-computes or not): per-WG ticks
 };
 
 // fused K4(t) + K2p(t + 1) (k_merge_gather, option "fuse_gather"): the next step's gather
@@ -351,6 +365,16 @@ struct NextStep {
   const unsigned *wait_seq;  // owner-computes ranks: one extra wave waits until all wait_n query
   int wait_n;                // seqs of step t + 1 (this rank's area) arrived, so the next scan
                              // starts with its queries in place instead of spinning on every CU
+  // option "fuse_sort" (pruned one-rank levels): the gathers of step t + 1 also sort it for the
+  // presorted scan.  Every gather wave publishes its query's sort key with the step's seq
+  // (kslot[m], uncached), waits until all sn.Mpad keys of the step are there, counts the keys
+  // below its own (its sorted slot x) and writes its pruning record, fragments and query index
+  // at slot x (sinfo / sfrag / sorder: k_query_sort's outputs); the scan then skips its
+  // per-workgroup sort (kslot = nullptr: off)
+  unsigned long long *kslot;
+  int *sorder;
+  float4 *sinfo;
+  void *sfrag;
 };
 
 __host__ __device__ inline int ia_reflect(int i, int n) {

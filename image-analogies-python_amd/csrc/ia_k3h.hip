@@ -987,6 +987,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   const int s0 = qt0 * IA_TILE;
   unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   K3P_T(ph[0]);
+  const unsigned long long stamp0 = xo.stamp ? ia_clock() : 0ull;
 
   // ---- 1. one global round
   h16x8 a[NP], an[NP], an2[NP];
@@ -1029,7 +1030,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       }
       skey[x] = ok ? ord_in[sl] : 0x7fffffff;  // slot -> query of this slice
     }
-    if (tid < QT) {
+    if (tid < QT && tbox) {  // (tbox = nullptr: the boxes are taken from the slice below)
       const bool ok = tid < qtb;
       tlo[tid] = ok ? tbox[3 * (qt0 + tid)] : make_float4(0.f, 0.f, 0.f, 0.f);
       thi[tid] = ok ? tbox[3 * (qt0 + tid) + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1045,6 +1046,40 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   __shared__ int kctr;  // DYN: next tile index to hand out
   if (tid == 0) kctr = NW;
   if constexpr (PRE) __syncthreads();
+  // the query-tile boxes (min lo, max hi, max U' over the tile's real queries) by 32-lane
+  // butterflies over the sorted slots in LDS: the in-kernel-sort path, and the presorted path
+  // when the step was sorted by its gathers (option "fuse_sort": no k_query_sort, tbox = nullptr)
+  auto tile_boxes = [&]() {
+    const int j = 2 * wave + half, x = j * IA_TILE + (lane & 31);
+    float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+    float u = -INFINITY;
+    if (j < QT && qU[x] != -INFINITY) {  // padding slots (U' = -inf) never widen a box
+      lo = qlo[x];
+      hi = qhi[x];
+      u = qU[x];
+    }
+#pragma unroll
+    for (int o = 1; o < 32; o <<= 1) {
+      lo.x = fminf(lo.x, xlane_xor_f(lo.x, o));
+      lo.y = fminf(lo.y, xlane_xor_f(lo.y, o));
+      lo.z = fminf(lo.z, xlane_xor_f(lo.z, o));
+      lo.w = fminf(lo.w, xlane_xor_f(lo.w, o));
+      hi.x = fmaxf(hi.x, xlane_xor_f(hi.x, o));
+      hi.y = fmaxf(hi.y, xlane_xor_f(hi.y, o));
+      hi.z = fmaxf(hi.z, xlane_xor_f(hi.z, o));
+      hi.w = fmaxf(hi.w, xlane_xor_f(hi.w, o));
+      u = fmaxf(u, xlane_xor_f(u, o));
+    }
+    if ((lane & 31) == 0 && j < QT) {
+      tlo[j] = lo;
+      thi[j] = hi;
+      tU[j] = u;
+    }
+  };
+  if (PRE && !tbox) {
+    tile_boxes();
+    __syncthreads();
+  }
   if constexpr (!PRE) {
   if (xo.on) {  // owner-computes: wait for each of the block's queries (published by its owner's K2p)
     const unsigned *qs = xo.flag + (int64_t)qblk * Mpad;
@@ -1217,33 +1252,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       if (x >= 0 && x < NQ) ldsh[((x >> 5) * NP + p) * IA_WAVE + (L & 32) + (x & 31)] = qe[i];
     }
   }
-  {
-    const int j = 2 * wave + half, x = j * IA_TILE + (lane & 31);
-    float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-    float u = -INFINITY;
-    if (j < QT && qU[x] != -INFINITY) {  // padding slots (U' = -inf) never widen a box
-      lo = qlo[x];
-      hi = qhi[x];
-      u = qU[x];
-    }
-#pragma unroll
-    for (int o = 1; o < 32; o <<= 1) {
-      lo.x = fminf(lo.x, xlane_xor_f(lo.x, o));
-      lo.y = fminf(lo.y, xlane_xor_f(lo.y, o));
-      lo.z = fminf(lo.z, xlane_xor_f(lo.z, o));
-      lo.w = fminf(lo.w, xlane_xor_f(lo.w, o));
-      hi.x = fmaxf(hi.x, xlane_xor_f(hi.x, o));
-      hi.y = fmaxf(hi.y, xlane_xor_f(hi.y, o));
-      hi.z = fmaxf(hi.z, xlane_xor_f(hi.z, o));
-      hi.w = fmaxf(hi.w, xlane_xor_f(hi.w, o));
-      u = fmaxf(u, xlane_xor_f(u, o));
-    }
-    if ((lane & 31) == 0 && j < QT) {
-      tlo[j] = lo;
-      thi[j] = hi;
-      tU[j] = u;
-    }
-  }
+  tile_boxes();
   __syncthreads();
   }  // !PRE
   K3P_T(ph[2]);
@@ -1660,6 +1669,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
     pairs[blockIdx.x] += sp + (HHF || HF ? sf << 32 : 0ull);
     tiles[blockIdx.x] += st + (HF ? (unsigned long long)nitems_wg << 32 : 0ull);
+  }
+  if (xo.stamp) {  // (uniform) option "stamps": the workgroup's first and last tick
+    __syncthreads();
+    if (tid == 0) ia_stamp_wg(xo.stamp, stamp0);
   }
 #if IA_PROBE & 16
   K3P_T(ph[5]);

@@ -955,6 +955,22 @@ __device__ __forceinline__ double exact_dist_level(const double *__restrict__ db
   });
 }
 
+// MFMA error bound of a row with |a'| <= Rx (ia_internal.h ia_eps_c_h / DESIGN.md §5)
+__device__ __forceinline__ double merge_eps(const MergeArgs &a, double Rx, double qn) {
+  return a.eps_c * (Rx * Rx + 2.0 * Rx * qn) + a.eps_a * (Rx * Rx + 14.0 * Rx + 28.0 * qn + 260.0) +
+         a.eps_r * (Rx + qn) * (Rx + qn);
+}
+// Certification threshold of the best exact distance bd: a chunk whose unlisted rows all have
+// MFMA value >= T can hide a row that beats or ties bd only if T <= theta.  Only rows with exact
+// distance <= bd matter, and such a row has |a'| <= |q'| + sqrt(bd) (|a' - q'|^2 = its distance;
+// 1e-12 covers the fp64 roundings of qn and bd), so its error bound uses that radius instead of
+// the DB-wide R when smaller (at 1024^2 about ten times tighter at the median query: far fewer
+// near-duplicate chunks rescanned, the same certified decisions).
+__device__ __forceinline__ double cert_theta(const MergeArgs &a, double R, double qn, double qn2, double bd) {
+  const double Rl = fmin(R, (qn + sqrt(bd)) * (1.0 + 1e-12) + 1e-12);
+  return bd - qn2 + merge_eps(a, Rl, qn) + 1e-13 * (bd + 1.0);
+}
+
 // the certified single-rank winner of query m (exact NN over this rank's shard); RPL records per
 // lane (nwg <= 64 RPL)
 template <int RPL = IA_WG_TARGET / IA_WAVE, class DistFn>
@@ -981,8 +997,7 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
   for (int j = 0; j < RPL; j++) a1 = fminf(a1, v1[j]);
   a1 = wave_min_f(a1);
   const double qn = sqrt(qn2);
-  const double eps = a.eps_c * (R * R + 2.0 * R * qn) + a.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0) +
-                     a.eps_r * (R + qn) * (R + qn);
+  const double eps = merge_eps(a, R, qn);
   const double thr = (double)a1 + 2.0 * eps;
 
   // rerank every listed candidate that could be the exact winner
@@ -1017,7 +1032,7 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
 
   // certification: every unlisted row of chunk w has MFMA value >= T_w, hence true distance
   // >= T_w + |q'|^2 - eps.  Chunks with T_w <= theta may hide a row that beats or ties bd.
-  const double theta = bd - qn2 + eps + 1e-13 * (bd + 1.0);
+  const double theta = cert_theta(a, R, qn, qn2, bd);
   unsigned long long nfb = 0;
 #pragma unroll
   for (int jb = 0; jb < RPL; jb++) {
@@ -1324,6 +1339,47 @@ __device__ __forceinline__ void xo_publish(const XOPub &xp, int m, int lane, con
   if (lane < xp.W)
     __hip_atomic_store(reinterpret_cast<unsigned *>(xp.area[lane] + XOLayout::QSEQ) + xp.slot0 + m, xp.seq, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// option "fuse_sort" (NextStep::kslot): query m of step nx.sn publishes its sort key (the Morton
+// key's top 20 bits above the 12-bit query index, k_query_sort's order), waits for every key of
+// the step, takes its rank x among them and writes its pruning record, query index and split-f16
+// fragments (hi / lo columns from xh0 / xh1) at sorted slot x.  Every query of the step is
+// gathered by exactly one wave of this launch, all of them resident together (one wave per
+// workgroup), so the wait drains; a key that never arrives (bounded, 20 s) sets err bit 4.
+template <int KS>
+__device__ __forceinline__ void sorted_publish(const NextStep &nx, int m, int lane, const _Float16 *xh0, const _Float16 *xh1,
+                                               float4 i0, float4 i1, float4 i2) {
+  const unsigned key = (__float_as_uint(i2.y) & 0xFFFFF000u) | (unsigned)m;
+  if (lane == 0)
+    __hip_atomic_store(nx.kslot + m, ((unsigned long long)nx.seq << 32) | key, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  __builtin_amdgcn_wave_barrier();  // xh written by this wave's lanes
+  // the fragments to registers while the other keys arrive
+  const int c = lane, sp = c >> 2, part = (c >> 1) & 1, h = c & 1;  // chunk c < 4 KS
+  h16x8 v{};
+  if (c < 4 * KS) v = *reinterpret_cast<const h16x8 *>(&(part ? xh1 : xh0)[16 * sp + 8 * h]);
+  int below = 0;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  const bool late = __hip_atomic_load(nx.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0u;
+  for (int i = lane; i < nx.sn.Mpad; i += IA_WAVE) {
+    unsigned long long x;
+    // relaxed: the slots are uncached (no stale line to invalidate)
+    while (((x = __hip_atomic_load(nx.kslot + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)) >> 32) != nx.seq && !late) {
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > nx.timeout_ticks) {
+        atomicOr(nx.err, 16u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    below += (unsigned)x < key ? 1 : 0;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) below += __shfl_xor(below, o, 64);
+  const int x = __builtin_amdgcn_readfirstlane(below);
+  const int qt = x / IA_TILE, j = x % IA_TILE;
+  if (c < 4 * KS) reinterpret_cast<h16x8 *>(nx.sfrag)[((int64_t)qt * 2 * KS + 2 * sp + part) * IA_WAVE + h * IA_TILE + j] = v;
+  if (lane < 3) nx.sinfo[3 * x + lane] = lane == 0 ? i0 : lane == 1 ? i1 : i2;
+  if (lane == 3) nx.sorder[x] = m;
 }
 
 // K2p's pad query m >= J M: zero fragments, an empty pruning record
@@ -1735,8 +1791,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   for (int j = 0; j < RPL; j++) a1 = fminf(a1, v1[j]);
   a1 = wave_min_f_x(a1);
   const double qn = sqrt(qn2);
-  const double eps = a.eps_c * (R * R + 2.0 * R * qn) + a.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0) +
-                     a.eps_r * (R + qn) * (R + qn);
+  const double eps = merge_eps(a, R, qn);
   const double thr = (double)a1 + 2.0 * eps;
   unsigned cmask = 0;
 #pragma unroll
@@ -1820,7 +1875,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   IA_STAMP(4);
 
   // certification (see certified_winner): rescan chunks whose threshold does not clear bd
-  const double theta = bd - qn2 + eps + 1e-13 * (bd + 1.0);
+  const double theta = cert_theta(a, R, qn, qn2, bd);
   unsigned long long nfb = 0;
 #pragma unroll
   for (int jb = 0; jb < RPL; jb++) {
@@ -1986,7 +2041,9 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_level(LevelGeo g, StepDesc s
     __shared__ int crsh[IA_PQ_WPB][IA_WAVE];
     __shared__ float cvsh[IA_PQ_WPB][IA_WAVE];
     const int wv = threadIdx.x >> 6;
+    const unsigned long long t0 = ma.stamp ? ia_clock() : 0ull;  // option "stamps"
     merge_fused<CH, IMG, RPL>(g, sd, A, ma, m, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv]);
+    if (ma.stamp && (threadIdx.x & 63) == 0) ia_stamp_wg(ma.stamp, t0);
     return;
   }
 #endif
@@ -2077,8 +2134,8 @@ __device__ __forceinline__ void gather_h_query_fused(const LevelGeo &g, const St
 // step t + 1's).
 // ------------------------------------------------------------------------------------------
 template <int RPL, bool PR, bool XO, class JS>
-__global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, JS jobs,
-                                                         Imgs B, NextStep nx) {
+__device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma,
+                                                  const JS &jobs, Imgs B, const NextStep &nx) {
   constexpr int KS = 4;
   const int w = __builtin_amdgcn_readfirstlane(blockIdx.x * IA_PQ_WPB + (threadIdx.x >> 6));
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -2140,9 +2197,10 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc 
   if (mn >= J * nx.sn.M) {
     if constexpr (PR) {
       gather_p_pad<KS>(mn, lane, qf, nx.qinfo, o0, o1, o2);
-      if (XO && nx.xp.W) {
+      if ((XO && nx.xp.W) || (!XO && nx.kslot)) {
         if (lane < 16 * KS) xh[wv][0][lane] = xh[wv][1][lane] = (_Float16)0.f;
-        xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
+        if (XO) xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
+        else sorted_publish<KS>(nx, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
       }
     } else {
       if (lane < 16 * KS) put_qh<KS>(qf, mn, lane, 0.);
@@ -2173,12 +2231,21 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc 
   }
   __builtin_amdgcn_wave_barrier();  // the merge's LDS rows are done with
   if constexpr (PR) {
+    const bool pub = (XO && nx.xp.W) || (!XO && nx.kslot);
     gather_p_query<KS, false, true>(g, nx.sn, B, jp, mn, lane, nx.mu, nx.q64, nx.qn2, qf, ma.db64, nx.basis, nx.ufac,
-                                    nx.qinfo, A, qsh[wv], XO && nx.xp.W ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2);
+                                    nx.qinfo, A, qsh[wv], pub ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2);
     if (XO && nx.xp.W) xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
+    if (!XO && nx.kslot) sorted_publish<KS>(nx, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
   } else {
     gather_h_query_fused<KS>(g, nx.sn, B, mn, lane, nx.mu, nx.q64, nx.qn2, qf, h);
   }
+}
+template <int RPL, bool PR, bool XO, class JS>
+__global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, JS jobs,
+                                                         Imgs B, NextStep nx) {
+  const unsigned long long t0 = ma.stamp ? ia_clock() : 0ull;  // option "stamps"
+  merge_gather_body<RPL, PR, XO, JS>(g, sd, A, ma, jobs, B, nx);
+  if (ma.stamp && (threadIdx.x & 63) == 0) ia_stamp_wg(ma.stamp, t0);
 }
 
 // multi-rank finish: global winner over the all-gathered per-rank winners, then coherence
@@ -2276,6 +2343,31 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd
 // per-level statistics: sum the per-pixel stats words.  Grid-stride loop over up to 256
 // workgroups; each workgroup reduces in LDS and adds its five integer sums with one u64
 // atomicAdd per counter (integer sums are order-free; counters are zeroed per level)
+// option "stamps": launch i's device time = max(end) - min(start) over the `stride` workgroup
+// slots (unwritten slots are zero), in s_memrealtime ticks; one wave per launch
+__global__ void __launch_bounds__(IA_WAVE) k_stamp_durations(const unsigned long long *__restrict__ stamps, int stride,
+                                                            unsigned *__restrict__ dur) {
+  const int i = blockIdx.x, lane = threadIdx.x;
+  unsigned long long lo = ~0ull, hi = 0ull;
+  for (int j = lane; j < stride; j += IA_WAVE) {
+    const unsigned long long a = stamps[2 * ((int64_t)i * stride + j)], b = stamps[2 * ((int64_t)i * stride + j) + 1];
+    if (a) {
+      lo = a < lo ? a : lo;
+      hi = b > hi ? b : hi;
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned long long l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
+    lo = l2 < lo ? l2 : lo;
+    hi = h2 > hi ? h2 : hi;
+  }
+  if (lane == 0) dur[i] = hi >= lo && hi ? (unsigned)(hi - lo) : 0u;
+}
+void ia_launch_stamp_durations(const unsigned long long *stamps, int n, int stride, unsigned *dur, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(k_stamp_durations, dim3(n), dim3(IA_WAVE), 0, st, stamps, stride, dur);
+}
+
 __global__ void __launch_bounds__(IA_WG) k_reduce_stats(const unsigned *__restrict__ pstat, int64_t n,
                                                          unsigned long long *__restrict__ counters) {
   unsigned long long rr = 0, fb = 0, cw = 0, bv = 0, ka = 0;
@@ -2859,7 +2951,8 @@ size_t ia_k3p_lds(int qt, int Mpad) {
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
-                   const float4 *tbox, const float *tnorm, hipStream_t st, int nqb, int qt_end, const XOScan *xo) {
+                   const float4 *tbox, const float *tnorm, hipStream_t st, int nqb, int qt_end, const XOScan *xo,
+                   unsigned long long *stamp) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
@@ -2892,6 +2985,7 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   if (nqb == 1) qt_end = qt0 + qt;
   XOScan x{};  // off unless an owner-computes step passes its exchange
   if (xo) x = *xo;
+  x.stamp = stamp;
   allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nqb * nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row,
                      NT, qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm, nqb, qt_end, x);

@@ -22,6 +22,8 @@ void ia_launch_finish(const LevelGeo &g, const StepDesc &sd, const Imgs &A, cons
 void ia_launch_db64_build(const LevelGeo &g, const Imgs &A, double *db64, hipStream_t st);
 int ia_db64_stride(int ch);
 void ia_launch_reduce_stats(const unsigned *pstat, int64_t n, unsigned long long *counters, hipStream_t st);
+// option "stamps": per-launch device ticks (max end - min start over each launch's stride slots)
+void ia_launch_stamp_durations(const unsigned long long *stamps, int n, int stride, unsigned *dur, hipStream_t st);
 void ia_launch_dense_db(int KH, const double *pts, int64_t n, int d, int n_tiles, const double *mu, float4 *db,
                         unsigned *Rbits, hipStream_t st);
 void ia_launch_dense_query(int KH, const double *q, int64_t nq, int d, int Mpad, const double *mu, double *qn2, float *qf,
@@ -73,7 +75,7 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
                    const float4 *tbox, const float *tnorm, hipStream_t st, int nqb = 1, int qt_end = 0,
-                   const XOScan *xo = nullptr);
+                   const XOScan *xo = nullptr, unsigned long long *stamp = nullptr);
 // GPU preprocessing (ia_pyramid.hip)
 void ia_launch_pyramid_reduce(const double *in, double *out, double *tmp, double *sm, double *mm, int h, int w, int ch,
                               const double *w7, hipStream_t st);

@@ -108,4 +108,5 @@ CONFIGS = {
     'cfg5': (dict(size=512), "multi_script-style sweep: 64 jobs, kappa {0.5,1,2,5,10,15,20,25} x pyramid "
                              "depth 2..9 on 512x512 A/A'/B, job j on GPU j mod N, jobs sharing a GPU batched"),
     'small': (dict(size=128), "128x128 smoke size"),
+    's256': (dict(size=256), "256x256 synthetic A/A'/B (multi-rank parity tests)"),
 }

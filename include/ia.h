@@ -92,6 +92,14 @@ typedef struct {
   double merge_ms_timed;    /* K4 (k_merge_level) of the sampled steps: device ms */
   int64_t merge_launches_timed;
   int64_t build_rows;       /* DB rows of the levels in k1*_ms (the largest seen) */
+  /* option "stamps" = 1: device time of EVERY pruned-scan launch and every fused merge launch of
+   * the pruned levels, from per-workgroup s_memrealtime stamps written by the kernels themselves
+   * (no HIP events, nothing on the stream between kernels: valid in pipelined / concurrent runs) */
+  double k3p_stamp_ms;      /* summed over the launches: max(WG end) - min(WG start) each */
+  int64_t k3p_stamp_launches;
+  double k3p_bytes_all;     /* algorithmic bytes of those launches (tiles loaded, boxes, queries, records) */
+  double merge_stamp_ms;    /* the merges (k_merge_gather / fused k_merge_level) of the same levels */
+  int64_t merge_stamp_launches;
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
@@ -168,6 +176,9 @@ int ia_version(void);
  * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge)
  * / 2 (owner computes: each rank brings its own job, every rank scans its shard for all of them,
  * queries and scan records exchanged by peer writes; emulated: one job per shard).
+ * "stamps" = 1: every pruned-scan and fused-merge launch of a pruned level stamps its
+ * workgroups' first / last s_memrealtime tick; ia_stats.k3p_stamp_ms / merge_stamp_ms sum the
+ * per-launch device times (bench.py roofline.frac_timed: the timed, pipelined steps' own kernels).
  * "xo_presort" = 1: owner-computes steps always sort in a K2s launch (tests; default 0: steps of
  * <= 352 queries per owner are sorted inside the scan).  Environment IA_CU_SPLIT=k/n (rehearsals
  * of n ranks on ONE GPU only): the context's stream runs on CU slice k of n.
@@ -191,7 +202,12 @@ int ia_comm_init(ia_ctx *ctx, int rank, int world, const unsigned char id[128]);
  * "exchange" = 1 unless 2 was set before).  No RCCL communicator is needed.  A peer that stops
  * publishing makes the level fail with IA_ECOMM after 20 s instead of hanging.  With option
  * "shard_emulate" = W and "exchange" = 1 / 2 a single process runs the same kernels over a
- * local buffer. */
+ * local buffer.  Every ia_xchg_open needs its own ia_xchg_alloc before the handle swap (a reused
+ * buffer is zeroed there and the step sequence restarts on every rank alike; ia_comm_init
+ * afterwards drops the peer mappings and returns to "exchange" = 0).  The ranks of one
+ * exchange run the same sequence of level calls with identical A levels and identical B shapes
+ * (per level): slots and sequence numbers are laid out from the local geometry, so ranks that
+ * disagree time out (IA_ECOMM after 20 s) - check the shapes on the host first. */
 int ia_xchg_alloc(ia_ctx *ctx, int world, unsigned char handle_out[64]);
 int ia_xchg_open(ia_ctx *ctx, int rank, int world, const unsigned char *handles);
 

@@ -214,3 +214,46 @@ def test_owner_exchange_needs_one_job_per_shard(ctx):
     jb = _jobs_g32(z, kappas=(0.5, 5.0, 25.0))
     with pytest.raises(_native.IAError):
         _run_batch(ctx, z, jb, 2, 2)
+
+
+@pytest.mark.parametrize('presort', [0, 1], ids=['inkernel', 'k2s'])
+def test_owner_shards_with_unequal_tile_counts(ctx, presort):
+    """owner-computes shards whose tile counts differ by one across a multiple of 8
+    (A 66 x 69 = 4,554 rows -> 143 tiles: shards of 72 and 71 tiles, W = 2).  Every shard's scan
+    must use the one chunk count the owners' merges assume (from the smaller shard), else records
+    overlap or DB chunks drop out; every level pruned, both jobs == their unsharded batched run."""
+    from ia_amd import _native, synth
+    jobs = synth.make_jobs(2, size=(66, 69))
+    assert (66 * 69 + 31) // 32 == 143
+    z = {'L': jobs[0].L, 'A_pyr': jobs[0].A_pyr, 'Ap_pyr': jobs[0].Ap_pyr_list}
+    out = []
+    ctx.set_option('xo_presort', presort)
+    ctx.set_option('prune_min_rows', 1)
+    try:
+        for Wx, ex in ((2, 2), (1, 0)):
+            S, IM = [], []
+            st = _native.Stats()
+            ctx.set_option('shard_emulate', Wx)
+            ctx.set_option('exchange', ex)
+            Bp = [[x.copy() for x in j.Bp_init] for j in jobs]
+            for level in range(1, z['L']):
+                specs = [dict(B=j.B_pyr[level], Bc=j.B_pyr[level - 1], Bpc=Bp[n][level - 1], Bp=Bp[n][level],
+                              weights=j.weights, kappa_factor=j.kappa_factor(level)) for n, j in enumerate(jobs)]
+                res = ctx.synthesize_levels(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
+                                            [p[level - 1] for p in z['Ap_pyr']], specs, st)
+                S.append([r[0] for r in res])
+                IM.append([r[1] for r in res])
+            out.append((S, IM, Bp, st))
+    finally:
+        ctx.set_option('shard_emulate', 1)
+        ctx.set_option('exchange', 0)
+        ctx.set_option('xo_presort', 0)
+        ctx.set_option('prune_min_rows', 524288)
+    (S, IM, Bp, st), (Su, IMu, Bpu, stu) = out
+    for i in range(len(S)):
+        for n in range(2):
+            assert np.array_equal(S[i][n], Su[i][n]) and np.array_equal(IM[i][n], IMu[i][n]), (i, n)
+    for n in range(2):
+        for level in range(1, z['L']):
+            assert np.array_equal(Bp[n][level], Bpu[n][level]), (n, level)
+    assert st.bound_violations == 0 and st.dist_launches > stu.dist_launches
