@@ -260,11 +260,9 @@ def make_context(args, local):
     cx = _native.Context(local)
     ALL_CTX.append(cx)
     cx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
-    if args.k3_variant != 1:
-        cx.set_option('k3_variant', args.k3_variant)       # DIAG=1 builds only
     cx.set_option('prune', args.prune)
     if args.k3p_variant != 20:
-        cx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15, 18..21; the rest DIAG=1 builds only
+        cx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15, 18..21
     cx.set_option('prune_min_rows', args.prune_min_rows)
     if args.k3p_blocks != 1:
         cx.set_option('k3p_blocks', args.k3p_blocks)
@@ -274,8 +272,8 @@ def make_context(args, local):
         cx.set_option('fuse_gather', args.fuse_gather)
     if args.fuse_unpruned:
         cx.set_option('fuse_unpruned', 1)
-    if args.row_source:
-        cx.set_option('row_source', args.row_source)
+    if args.fuse_sort != 1:
+        cx.set_option('fuse_sort', args.fuse_sort)
     if args.shard_unpruned:
         cx.set_option('shard_unpruned', 1)
     if args.shard_emulate > 1:
@@ -366,19 +364,14 @@ def main():
                     help='worker processes the CPU-baseline sample is split over (each single-threaded)')
     ap.add_argument('--matcher', default='f16x3', choices=['f16x3', 'f32'],
                     help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
-    ap.add_argument('--k3-variant', type=int, default=1, choices=[0, 1],
-                    help='split-f16 K3 epilogue (ia_k3h.hip): 1 = packed row index (default), 0 = compare/select (DIAG=1 builds)')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
-    ap.add_argument('--k3p-variant', type=int, default=20, choices=list(range(22)),
-                    help='pruned-scan kernel version (ia_k3h.hip k3h_prune*): 0 = first version, 1 = boxes in '
-                         'registers, 2 = coarse query-tile test only (diagnostic), 3 = phased (batched need masks, '
-                         'balanced tile list, two tiles in flight), 4 = as 3 with one tile in flight, 5 = need tests interleaved with the contraction, 6 = as 5 with a bitonic sort and tiles handed out dynamically, 7 = as 6 walking alternate steps in reverse, 8 = as 7 with the previous step\'s query order (no sort), 9 = 6 with software-pipelined single chains, 10 = 9 + reverse walks, 11 = 7 on queries presorted once per step, '
-                         '14 / 15 = 7 / 11 with the hi x hi block filter, 16 / 17 = rotated DB with the '
-                         'principal-axis head filter (DESIGN.md §4f), 18 / 19 = 14 / 15 with the correction products fused onto the '
-                         'hi x hi accumulator (software-pipelined single chains), 20 (default) / 21 = the same on query-tile pairs '
-                         '(two chains); '
-                         'product builds hold 7, 11, 14, 15 and 18..21')
+    ap.add_argument('--k3p-variant', type=int, default=20, choices=[7, 11, 14, 15, 18, 19, 20, 21],
+                    help='pruned-scan kernel version (ia_k3h.hip k3h_prune3, DESIGN.md §4b): 7 = need tests interleaved '
+                         'with the contraction, bitonic in-kernel query sort, reverse walks on alternate steps; 11 = 7 on '
+                         'queries presorted once per step; 14 / 15 = 7 / 11 with the hi x hi block filter; 18 / 19 = 14 / '
+                         '15 with the correction products fused onto the hi x hi accumulator (single chains); 20 '
+                         '(default) / 21 = the same on query-tile pairs (two chains)')
     ap.add_argument('--pipeline', type=int, default=1, choices=[0, 1],
                     help='1 (default; one-job configs and replicas): consecutive levels overlap (two libia '
                          'contexts, each level\'s steps waiting only for the steps of the previous level they read; '
@@ -386,6 +379,9 @@ def main():
     ap.add_argument('--fuse-gather', type=int, default=1, choices=[0, 1],
                     help='1 (default): on pruned one-job levels the merge of step t and the gather of step t + 1 run '
                          'as one launch (ia_kernels.hip k_merge_gather); 0: separate launches')
+    ap.add_argument('--fuse-sort', type=int, default=1, choices=[0, 1],
+                    help='1 (default): the fused gathers of step t + 1 also sort its queries for the presorted scan '
+                         '(include/ia.h option fuse_sort); 0: the scan sorts them in every workgroup (or K2s)')
     ap.add_argument('--owner-pipeline', type=int, default=0, choices=[0, 1],
                     help='1: pipelined levels in the owner-computes shard mode too (N > 1)')
     ap.add_argument('--fuse-unpruned', type=int, default=0, choices=[0, 1],
@@ -403,9 +399,6 @@ def main():
                     help='pruned levels: Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)')
     ap.add_argument('--prune-min-rows', type=int, default=524288,
                     help='smallest DB (rows) the pruned scan is used on (default: the 1024^2 level)')
-    ap.add_argument('--row-source', type=int, default=0, choices=[0, 1],
-                    help='exact rows of the rerank / coherence / pruning bound: 0 = fp64 row DB, 1 = gathered from '
-                         'the A-side images (identical results)')
     ap.add_argument('--shard-unpruned', action='store_true',
                     help='shard (or emulate shards of) levels that scan unpruned too (default: only pruned levels, '
                          'DESIGN.md §7)')
@@ -752,12 +745,7 @@ def main():
         roofline = {'bound': 'hbm', 'achieved': p_gbs, 'peak': HBM_PEAK / 1e9, 'unit': 'GB/s',
                     'frac': p_gbs * 1e9 / HBM_PEAK, 'traffic': traffic,
                     'algorithmic_bytes_per_launch': p_bytes,
-                    'kernel': ('k3h_prune3 HF (certified pruned scan on the rotated DB: PCA-box need tests, '
-                               'principal-axis head filter = 3 x v_mfma_f32_32x32x16_f16 over 16 k per box-needed '
-                               'block, full split-f16 chain + packed-index top-2 for the passing blocks; bytes = 2 KiB '
-                               'heads + 8 KiB full-row tiles + boxes, queries, records)'
-                               if st.get('dist_tiles_rows', 0) > 0 else
-                               'k3h_prune3 (certified pruned scan: PCA-box need tests, split-f16 '
+                    'kernel': ('k3h_prune3 (certified pruned scan: PCA-box need tests, hi x hi block filter, split-f16 '
                                '3 x v_mfma_f32_32x32x16_f16, fused packed-index top-2)'),
                     'k3_us_per_launch': st['prune_ms_timed'] * 1e3 / st['prune_launches_timed'],
                     'k3_launches_sampled': st['prune_launches_timed'],
@@ -817,13 +805,9 @@ def main():
     roofline['fp32_mfma_equiv_frac'] = fp32_equiv / FP32_MFMA_PEAK
     roofline['pairs_frac'] = st['dist_pairs'] / max(st['dist_pairs_full'], 1.)
     if st['dist_pairs_corrected'] > 0:
-        # k3p_variant 14/15: every box-needed pair runs the hi x hi product; only this share also
-        # runs the two correction products and the top-2 epilogue (mfma_* above count 3 products).
-        # 16/17: every box-needed pair runs the 3-product head chain (16 of 64 k); only this share
-        # runs the full chain + epilogue, and only dist_tiles_rows of the heads' tiles load full rows
+        # the hi x hi block filter: every box-needed pair runs the hi x hi product; only this share
+        # also runs the two correction products and the top-2 epilogue (mfma_* above count 3)
         roofline['pairs_corrected_frac'] = st['dist_pairs_corrected'] / max(st['dist_pairs'], 1.)
-    if st.get('dist_tiles_rows', 0) > 0:
-        roofline['tiles_rows_frac'] = st['dist_tiles_rows'] / max(st['dist_tiles'], 1.)
     out = {'metric': METRIC, 'value': value, 'unit': "B' px/s", 'n_gpus': world, 'steps': args.steps,
            'warmup': args.warmup, 'ms_per_step': elapsed * 1e3 / args.steps, 'higher_is_better': True,
            'scaling': 'strong' if (sw is not None or (args.mode == 'shard' and jobs < max(world, args.shard_emulate)))
@@ -834,7 +818,7 @@ def main():
                                            'pyramid_levels': job.L,
                                            'px_per_step': job_pixels, 'nn_flops_per_step': job_flops,
                                            'mode': 'sweep' if sw is not None else args.mode,
-                                           'shard_emulate': args.shard_emulate, 'row_source': args.row_source,
+                                           'shard_emulate': args.shard_emulate,
                                            'exchange': args.exchange if (args.mode == 'shard' and world > 1) else None,
                                            'parallelism': (('jobs%d' % world) if sw is not None else
                                                            ('replicas%d' % world) if args.mode == 'replicas' and
@@ -862,7 +846,7 @@ def main():
            'stats': {k: st_all[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
                                         'synth_ms', 'bound_violations', 'kappa_ambiguous', 'f16_levels', 'pruned_levels',
                                         'dist_pairs', 'dist_pairs_full', 'dist_tiles', 'dist_tiles_full',
-                                        'dist_pairs_corrected', 'dist_tiles_rows')}}
+                                        'dist_pairs_corrected')}}
     if sw is not None:
         out['config']['sweep'] = {'jobs': len(sw.jobs), 'batched': not args.sequential, 'max_batch': args.max_batch,
                                   'streams': args.streams,

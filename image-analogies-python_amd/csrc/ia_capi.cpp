@@ -97,11 +97,9 @@ struct ia_ctx {
   // certified pruned scan (option "prune"): per-level basis, sorted DB table, tile boxes
   DevBuf pr_part, pr_cov, pr_basis, pr_proj, pr_keys, pr_rows, pr_tmp, pos2row, boxes, qinfo, pairs, ord;
   DevBuf qs_order, qs_info, qs_frag, qs_tbox;
-  DevBuf pr_rot, pr_lut;  // rotated DB (k3p_variant 16 / 17): R^T (56 x 56) and the home-tile table
   DevBuf tnorm;  // per DB tile of a pruned level: R_t >= max |a'| over its rows (k3p_variant 14/15)  // presorted queries of a step (k3p_variant 11, K2s)
   DevBuf py_in, py_tmp, py_sm, py_mm, py_out;  // GPU preprocessing (ia_gaussian_pyramid, ia_color_matrix)
   std::vector<double> basis_h;   // staging of the basis upload (lives until the copy ran)
-  std::vector<double> rot_h;     // staging of R^T (rotated DB levels)
   int64_t prune_min_rows = IA_PRUNE_MIN_ROWS;  // option "prune_min_rows": smallest DB that prunes
   int prune = 1;
   int row_source = 0;            // option "row_source": exact rows from 0 = the fp64 row DB, 1 = the A images
@@ -215,11 +213,7 @@ void jacobi_eig(int n, std::vector<double> &A, std::vector<double> &V, std::vect
 // the centred fp64 DB (sampled) -> top IA_NPC eigenvectors (host Jacobi) -> projections and
 // Morton keys of every row -> radix sort -> position -> row table + per-tile projection boxes.
 // Sets g.pos2row; *ufac = the U' factor of ia_prune.h.  One host sync (the covariance).
-// rot (k3p_variant 16 / 17): also R^T of all 55 axes (c->pr_rot), *eps_r (its
-// deviation from an orthogonal matrix + the fp64 rotation's rounding) and the
-// home-tile table of the sorted keys (c->pr_lut, 2^*lut_bits entries).
-int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac, bool rot = false, double *eps_r = nullptr,
-                  int *lut_bits = nullptr) {
+int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac) {
   constexpr int D = 55, NPAIR = D * (D + 1) / 2, NWG_COV = 256;
   const int64_t NA = g.NA, NT = g.n_tiles;
   const int64_t stride = std::max<int64_t>(1, NA / 65536), nsamp = (NA + stride - 1) / stride;
@@ -262,33 +256,6 @@ int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac,
     }
   *ufac = (1.0 + 2.0 * (double)delta + 1e-15) * (1.0 + std::ldexp(1.0, -17)) * (1.0 + std::ldexp(1.0, -19));
   HIP_TRY(hipMemcpyAsync(c->pr_basis.p, c->basis_h.data(), c->basis_h.size() * 8, hipMemcpyHostToDevice, c->st));
-  if (rot) {
-    // R: row f = axis f (eigenvalues descending; rows 0..3 are the basis above, bit for bit),
-    // uploaded transposed with stride 56: rt[g * 56 + f] = R[f][g]
-    constexpr int DS = 56;
-    if ((rc = c->pr_rot.ensure((size_t)DS * DS * 8))) return rc;
-    c->rot_h.assign((size_t)DS * DS, 0.);
-    std::vector<double> Rm((size_t)D * D);
-    for (int f = 0; f < D; f++) {
-      double nrm = 0.;
-      for (int k = 0; k < D; k++) nrm += V[(size_t)k * D + idx[f]] * V[(size_t)k * D + idx[f]];
-      nrm = std::sqrt(nrm);
-      for (int k = 0; k < D; k++) Rm[(size_t)f * D + k] = V[(size_t)k * D + idx[f]] / nrm;
-    }
-    long double dr = 0.L;  // sum |R R^T - I| >= the spectral deviation of R^T R from I
-    for (int i = 0; i < D; i++)
-      for (int j = 0; j < D; j++) {
-        long double gij = 0.L;
-        for (int k = 0; k < D; k++) gij += (long double)Rm[(size_t)i * D + k] * Rm[(size_t)j * D + k];
-        dr += std::fabs((double)(gij - (i == j ? 1.L : 0.L)));
-      }
-    for (int f = 0; f < D; f++)
-      for (int k = 0; k < D; k++) c->rot_h[(size_t)k * DS + f] = Rm[(size_t)f * D + k];
-    // | |a'' - q''|^2 - |a - q|^2 | <= (delta + the fp64 rotation's rounding) (|a'| + |q'|)^2, and the
-    // same for |q''|^2 vs |q'|^2: twice (delta + 1e-12) covers both (55-term fp64 sums: < 1e-13)
-    *eps_r = 2.0 * ((double)dr + 1e-12);
-    HIP_TRY(hipMemcpyAsync(c->pr_rot.p, c->rot_h.data(), c->rot_h.size() * 8, hipMemcpyHostToDevice, c->st));
-  }
   unsigned *keys = c->pr_keys.as<unsigned>();
   int *rows = c->pr_rows.as<int>();
   float *rnorm = reinterpret_cast<float *>(c->pr_proj.as<double>() + NA * IA_NPC);  // |a'| per row, rounded up
@@ -296,20 +263,9 @@ int prepare_prune(ia_ctx *c, LevelGeo &g, const double *mu, int W, double *ufac,
                       c->st);
   if (ia_sort_pairs(c->pr_tmp.p, sort_bytes, keys, keys + NA, rows, rows + NA, NA, c->st) != 0)
     return fail(IA_EHIP, "prepare_prune: radix sort failed");
-  ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, W, rot ? 1 : c->prune_group, c->pos2row.as<int>(),
+  ia_launch_table_boxes(rows + NA, c->pr_proj.as<double>(), NA, (int)NT, W, c->prune_group, c->pos2row.as<int>(),
                         c->boxes.as<float>(), rnorm,
                         c->tnorm.as<float>(), c->st);
-#ifdef IA_K3H_DIAG
-  if (rot) {
-    int lb = 8;
-    while (lb < 20 && ((int64_t)1 << lb) < 4 * NA) lb++;
-    if ((rc = c->pr_lut.ensure(((size_t)1 << lb) * 4))) return rc;
-    ia_launch_key_lut(keys + NA, NA, (int)NT, lb, c->pr_lut.as<int>(), c->st);
-    *lut_bits = lb;
-  }
-#else
-  (void)lut_bits;
-#endif
   HIP_TRY(hipGetLastError());
   g.pos2row = c->pos2row.as<int>();
   return IA_OK;
@@ -371,7 +327,7 @@ void ia_destroy(ia_ctx *c) {
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
                     &c->boxes, &c->qinfo, &c->pairs, &c->ord, &c->qs_order, &c->qs_info, &c->qs_frag, &c->qs_tbox, &c->tnorm,
-                    &c->pr_rot, &c->pr_lut, &c->stamp_k3, &c->stamp_mg, &c->stamp_dur,
+                    &c->stamp_k3, &c->stamp_mg, &c->stamp_dur,
                     &c->py_in, &c->py_tmp, &c->py_sm, &c->py_mm, &c->py_out})
     b->release();
   for (auto *v : {&c->evs, &c->evg, &c->evm, &c->p_ev[0], &c->p_ev[1], &c->p_ev[2]})
@@ -403,33 +359,20 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     c->stamps = value;
     return IA_OK;
   }
-#ifdef IA_K3H_DIAG  // DIAG=1 builds: every kernel version of DESIGN.md §4b's progression
-  if (!std::strcmp(name, "k3p_variant")) {
-    if (value < 0 || value > 21) return fail(IA_EINVAL, "ia_set_option: k3p_variant must be 0..21");
-    c->k3p_variant = value;
-    return IA_OK;
-  }
-  if (!std::strcmp(name, "k3_variant")) {
-    if (value < 0 || value > 3) return fail(IA_EINVAL, "ia_set_option: k3_variant must be 0..3");
-    c->k3_variant = value;
-    return IA_OK;
-  }
-#else  // product build: the default kernels only (7: pruned scan, 1: packed-index K3h)
   if (!std::strcmp(name, "k3p_variant")) {  // 20 (default) / 21: hi x hi block filter with the correction
                                             // products fused on query-tile pairs (in-kernel sort up to 512
                                             // queries, presorted 21 above); 14 / 15: the filter, then full
                                             // chains; 18 / 19: fused, single chains; 7 / 11: v7 (DESIGN.md
-                                            // §4b); 16 / 17 (rotated DB, §4f) are in DIAG=1 builds
+                                            // §4b); the other versions of §4b / §4f are in git history
     if (value != 7 && value != 11 && value != 14 && value != 15 && value != 18 && value != 19 && value != 20 && value != 21)
-      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14, 15 or 18..21 (other versions are in DIAG=1 builds only)");
+      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14, 15 or 18..21");
     c->k3p_variant = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "k3_variant")) {
-    if (value != 1) return fail(IA_EINVAL, "ia_set_option: k3_variant other than 1 is in DIAG=1 builds only");
+    if (value != 1) return fail(IA_EINVAL, "ia_set_option: k3_variant is 1 (the packed-index epilogue; the others are in git history)");
     return IA_OK;
   }
-#endif
   if (!std::strcmp(name, "prune_group")) {
     if (value != 1 && value != 2 && value != 4 && value != 8)
       return fail(IA_EINVAL, "ia_set_option: prune_group must be 1, 2, 4 or 8");
@@ -442,11 +385,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
   if (!std::strcmp(name, "row_source")) {
-#ifdef IA_K3H_DIAG
-    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: row_source must be 0 (row DB) or 1 (images)");
-#else  // the image-gather rows measured slower: DIAG=1 builds only
     if (value != 0) return fail(IA_EINVAL, "ia_set_option: row_source 1 is built with DIAG=1 only (measured slower)");
-#endif
     c->row_source = value;
     return IA_OK;
   }
@@ -683,6 +622,8 @@ int ia_wavefront_step(int h, int w, int64_t t, int *r0, int *M) {
   *M = (int)(r_hi - r_lo + 1);
   return IA_OK;
 }
+
+#define IA_FUSE_SORT_MAXW 768  // waves of a k_merge_gather launch whose gathers sort the next step
 
 static bool shard_level(int64_t n_tiles, int world) { return world > 1 && n_tiles >= 64 * (int64_t)world; }
 
@@ -1043,27 +984,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   HIP_TRY(hipEventRecord(c->kb[0], c->st));
   ia_launch_db64_build(g, Aim, c->db64.as<double>(), c->st);  // every row: coherence reads any row
   HIP_TRY(hipEventRecord(c->kb[1], c->st));
-  double ufac = 0., eps_r = 0.;
-  int lut_bits = 0;
-  // rotated DB + head-filtered scan (k3p_variant 16 / 17): unsharded pruned levels whose
-  // workgroups hold <= 512 tiles (the in-kernel tile lists)
-#ifdef IA_K3H_DIAG
-  constexpr bool kRotBuilt = true;   // k3p_variant 16 / 17: DIAG=1 builds only
-#else
-  constexpr bool kRotBuilt = false;
-#endif
-  const bool rot = kRotBuilt && prune && !multi && (c->k3p_variant == 16 || c->k3p_variant == 17) &&
-                   (g.n_tiles + IA_NWG_H - 1) / IA_NWG_H <= 512;
-  if (prune && (rc = prepare_prune(c, g, c->mu.as<double>(), Wsh, &ufac, rot, &eps_r, &lut_bits)))
+  double ufac = 0.;
+  if (prune && (rc = prepare_prune(c, g, c->mu.as<double>(), Wsh, &ufac)))
     return rc;  // sets g.pos2row
   HIP_TRY(hipEventRecord(c->kb[2], c->st));
   if (ns > 0) {
-#ifdef IA_K3H_DIAG
-    if (rot)
-      ia_launch_db_build_rot(c->db64.as<double>(), g.NA, g.n_tiles, g.pos2row, c->mu.as<double>(), c->pr_rot.as<double>(),
-                             c->db.p, c->Rbits.as<unsigned>(), c->st);
-    else
-#endif
     if (use_h) ia_launch_db_build_h(g, Aim, c->db64.as<double>(), c->mu.as<double>(), c->db.p, c->Rbits.as<unsigned>(), c->st);
     else ia_launch_db_build(g, Aim, c->mu.as<double>(), c->db.as<float4>(), c->Rbits.as<unsigned>(), c->st);
   }
@@ -1090,10 +1015,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   ma.ufac = ufac;
   ma.img_rows = (c->row_source == 1 && g.ch == 1) ? 1 : 0;
   ma.eps_c = use_h ? ia_eps_c_h(g.KS, prune || c->k3_variant == 1) : ia_eps_c(DP);
-  ma.eps_a = use_h ? ia_eps_a_h() * (rot ? 2.0 : 1.0) : 0.;  // rot: two norm columns
-  ma.eps_r = eps_r;
-  [[maybe_unused]] RotArgs ra{c->pr_rot.as<double>(), c->db.p, c->pr_lut.as<int>(), lut_bits, g.n_tiles, c->Rbits.as<unsigned>(),
-             ma.eps_c, ma.eps_a, eps_r};
+  ma.eps_a = use_h ? ia_eps_a_h() : 0.;
   // per shard: its records, decomposition, DB positions (and table / boxes of a pruned level)
   std::vector<MergeArgs> mas(shards.size(), ma);
   std::vector<int64_t> shard_rows(shards.size(), 0);  // real DB rows in each shard (unpruned flops)
@@ -1127,7 +1049,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   // (batched jobs: one handoff row set per job.  Unpruned levels - K2h fused, option
   // "fuse_unpruned" - measured slower: their longer fused launches delay the pipelined finest
   // level's scans, and cfg5's batched 512^2 steps lose 1-2 %)
-  const bool chain = c->fuse_gather && use_h && g.ch == 1 && !rot && ma.img_rows == 0 && g.bw >= 3 &&
+  const bool chain = c->fuse_gather && use_h && g.ch == 1 && ma.img_rows == 0 && g.bw >= 3 &&
                      (prune || c->fuse_unpruned) && ((!multi && !xo && mas[0].nwg <= 4 * IA_WAVE) || (xo && prune));
   if (chain) {
     const int hrows = g.bh * J;  // per job (local owner)
@@ -1163,7 +1085,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   };
   int64_t gathered = -1;  // the step whose gather the previous fused launch ran
   bool gsort = false;     // ... and that launch also sorted it (option "fuse_sort": no K2s, no in-scan sort)
-  const bool fsort = chain && prune && c->fuse_sort && !rot && !xo;
+  const bool fsort = chain && prune && c->fuse_sort && !xo;
   const int64_t n_timed = stride ? (T + stride - 1) / stride : 0;
   for (auto *v : {&c->evs, &c->evg, &c->evm})
     if ((int64_t)v->size() < 2 * n_timed) {
@@ -1448,12 +1370,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       mas[0].qn2 = qn2t;
       mas[0].qinfo = qinfot;
     }
-#ifdef IA_K3H_DIAG
-    if (rot)
-      ia_launch_gather_r(g, sd, Bim, djobs, c->mu.as<double>(), c->q64.as<double>(), c->qn2.as<double>(), c->qf.p,
-                         c->db64.as<double>(), c->pr_basis.as<double>(), ufac, ra, c->qinfo.as<float4>(), Aim, c->st);
-    else
-#endif
     if (chain && gathered == t)
       ;  // this step's gather ran in the previous step's fused merge
     else if (prune)
@@ -1468,17 +1384,17 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     // pruned scan: queries sorted once per step (K2s) when the step is wider than the in-kernel
     // sort of v6/v7 (512) or variant 11 is selected
     // (variants 11, 12: presorted; 7, 13: in-kernel sort up to 512 queries, presorted v11 / v12 above)
-    const int kv = rot ? c->k3p_variant : (c->k3p_variant == 16 ? 14 : c->k3p_variant == 17 ? 15 : c->k3p_variant);
+    const int kv = c->k3p_variant;
     // steps wider than one launch's query tiles take the presorted form too when their blocks
     // run as one launch (k3p_blocks): one K2s launch instead of a second scan launch
-    const bool wide = sd.Mpad > 512 || (c->k3p_blocks && sd.Mpad > qtmax * IA_TILE && !rot);
+    const bool wide = sd.Mpad > 512 || (c->k3p_blocks && sd.Mpad > qtmax * IA_TILE);
     // sorted by the previous launch's gathers: the presorted form of the variant, no K2s
     const bool gsorted = fsort && gathered == t && gsort;
-    const int k3v = (kv == 11 || kv == 12 || kv == 15 || kv == 17 || kv == 19 || kv == 21) ? kv
+    const int k3v = (kv == 11 || kv == 15 || kv == 19 || kv == 21) ? kv
                     : (prune && (wide || gsorted)
-                           ? (kv == 13 ? 12 : kv == 14 ? 15 : kv == 18 ? 19 : kv == 20 ? 21 : kv == 16 ? 17 : 11)
+                           ? (kv == 14 ? 15 : kv == 18 ? 19 : kv == 20 ? 21 : 11)
                            : kv);
-    const bool presorted = k3v == 11 || k3v == 12 || k3v == 15 || k3v == 17 || k3v == 19 || k3v == 21;
+    const bool presorted = k3v == 11 || k3v == 15 || k3v == 19 || k3v == 21;
     const float4 *tboxp = gsorted ? nullptr : c->qs_tbox.as<float4>();  // nullptr: boxes from the slice
     if (prune && presorted && !gsorted)
       ia_launch_query_sort(qinfot, c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
@@ -1577,7 +1493,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       nx.seq = ++c->hseq;
       nx.err = c->xerr.as<unsigned>();
       nx.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
-      if (fsort) {  // the gathers also sort step t + 1 into k_query_sort's outputs
+      // the gathers also sort step t + 1 into k_query_sort's outputs when every wave of the launch
+      // can be resident at once (each gather waits for all of the step's keys): k_merge_gather
+      // holds one wave per SIMD (264 VGPRs), 1,024 on the chip; 768 leaves room for the kernels of
+      // concurrent (pipelined) levels, which never wait on this one
+      const int nw = J * sd.M + J + (nx.sn.Mpad - J * nx.sn.M);
+      const bool srt = fsort && nw <= IA_FUSE_SORT_MAXW;
+      if (srt) {
         nx.kslot = c->kslot;
         nx.sorder = c->qs_order.as<int>();
         nx.sinfo = c->qs_info.as<float4>();
@@ -1586,7 +1508,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       mas[0].stamp = mg_stamp();
       ia_launch_merge_gather(g, sd, Aim, mas[0], djobs, Bim, nx, prune, c->st);
       gathered = t + 1;
-      gsort = fsort;
+      gsort = srt;
     } else if (!multi) {
       mas[0].stamp = mg_stamp();
       ia_launch_merge(g, sd, Aim, mas[0], c->win.as<Winner>(), djobs, true, c->st);
@@ -1655,7 +1577,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                                 " did not arrive within 20 s (peer-write exchange)");
   }
   if (stats) {
-    unsigned long long ctr[5], prs[4], pfull = 0, prow[4] = {0, 0, 0, 0};
+    unsigned long long ctr[5], prs[4], pfull = 0;
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
     {  // per-workgroup counter slots (no same-address atomics in the distance kernel)
       std::vector<unsigned long long> slots(4 * IA_NWG_H);
@@ -1667,9 +1589,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           if (j < 2) {  // pair slots: (pairs with corrections << 32) + pairs (k3p_variant 14/15)
             prs[j] += v & 0xffffffffull;
             pfull += v >> 32;
-          } else if (rot) {  // tile slots of the rotated scan: (full-row tiles << 32) + heads
-            prs[j] += v & 0xffffffffull;
-            prow[j] += v >> 32;
           } else {
             prs[j] += v;
           }
@@ -1687,7 +1606,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     stats->dist_tiles += prune ? (double)(prs[2] + prs[3]) : tiles_full;
     stats->dist_tiles_full += tiles_full;
     stats->dist_pairs_corrected += (double)pfull;
-    stats->dist_tiles_rows += (double)(prow[2] + prow[3]);
     float ms_db = 0.f, ms_syn = 0.f, ms_k1b = 0.f, ms_k1 = 0.f;
     hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
     hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);
@@ -1703,7 +1621,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       const int DSb = ia_db64_stride(g.ch);
       stats->k1b_ms += ms_k1b;
       stats->k1b_bytes += (double)(nA + nAc) * (1 + g.n_ap) * 8 + (double)g.NA * DSb * 8;
-      if (ns > 0 && use_h && !rot) {
+      if (ns > 0 && use_h) {
         stats->k1_ms += ms_k1;
         stats->k1_bytes += (double)std::min<int64_t>((int64_t)ns * IA_TILE, g.NA) * DSb * 8 + (double)ns * tile_bytes;
       }
@@ -1757,10 +1675,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         stats->prune_ms_timed += tot;
         stats->prune_launches_timed += launches_timed;
         stats->prune_flops_timed += flops_timed;
-        // rotated scan: 2 KiB heads + 8 KiB (head + tail) of the full-row tiles
-        stats->prune_bytes_timed += (rot ? 2048.0 * (double)prs[3] + 8192.0 * (double)prow[3]
-                                         : (double)prs[3] * ia_k3h_tile_bytes(g.KS)) +
-                                    bytes_timed_fixed;
+        stats->prune_bytes_timed += (double)prs[3] * ia_k3h_tile_bytes(g.KS) + bytes_timed_fixed;
       }
     }
   }

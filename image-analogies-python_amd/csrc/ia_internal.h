@@ -96,8 +96,6 @@ struct MergeArgs {
   const float4 *boxes;                // pruned levels: per-tile projection boxes (ia_prune.hip)
   double ufac;                        // pruned levels: bound factor of ia_prune.h
   int img_rows;                       // 1: exact rows gathered from the A-side images (1 channel)
-  double eps_r = 0.;                  // rotated DB (k3p_variant 16/17): coefficient of (R + |q'|)^2
-                                      // for the principal-axis rotation's deviation
   // owner-computes sharded step (exchange = 2): records chunk-major in the exchange area (rec[w
   // xo_Mrec + m], (T, seq) in xo_rts), record w = chunk w mod xo_nch of shard w / xo_nch (storage
   // tiles ia_shard_off(NT, xo_W, s) + k + xo_nch i); boxes / pos2row are the whole level's
@@ -121,27 +119,6 @@ __device__ __forceinline__ void ia_stamp_wg(unsigned long long *stamp, unsigned 
   stamp[2 * blockIdx.x] = t0 | 1ull;  // nonzero: a slot that was written (one tick of slack)
   stamp[2 * blockIdx.x + 1] = t1;
 }
-
-// Rotated split-f16 DB of a pruned 1-channel level (k3p_variant 16 / 17): every
-// centred row a' is rotated onto the level's 55 principal axes, a'' = R a' (fp64), and stored
-// in two arrays of v_mfma_f32_32x32x16_f16 operand pieces (TileFmt order, KS = 4, 8 pieces):
-//   head [NT][2][64]: k-step 0 = columns 0..14: a''_0..14, column 15: |a''_0..14|^2 / 256
-//   tail [NT][6][64]: k-steps 1..3 = columns 16..55: a''_15..54, column 56: |a''_15..54|^2 / 256
-// The query holds -2 q'' with 256 in both norm columns, so the k-step-0 MFMA value is the
-// 15-axis partial distance |a''_h - q''_h|^2 - |q''_h|^2 (a lower bound of the full one) and the
-// whole chain is |a''|^2 - 2 q''.a'' as in the unrotated DB.
-#define IA_ROT_HNORM 15   // head norm column
-#define IA_ROT_TNORM 56   // tail norm column
-__host__ __device__ inline int ia_rot_col(int f) { return f < IA_ROT_HNORM ? f : f + 1; }  // axis f -> column
-struct RotArgs {             // K2r's inputs besides K2p's
-  const double *rt;          // R transposed, rt[g * 56 + f] (56 x 56, zero padded)
-  const void *db;            // the rotated DB (head + tail arrays)
-  const int *lut;            // home-tile table (k_key_lut), 2^lb entries
-  int lb, NT;
-  const unsigned *Rbits;     // R = max |a''| (K1r)
-  double eps_c, eps_a, eps_r;  // K4's certification coefficients (the head filter's threshold)
-};
-
 
 // DB positions are tile-strided and tile-scattered: slot j of tile t holds row j*NT + perm(t)
 // with perm(t) = t * (IA_TILE_MUL mod NT) mod NT (a bijection: IA_TILE_MUL is a prime above any

@@ -281,37 +281,6 @@ __device__ __forceinline__ void k3p_epi1(const f32x16 &e, int t, float &b1, floa
 // query-tile pairs QP.. of one DB tile t; m2 = the pair's two need bits (wave-uniform).  A pair
 // with one needed tile runs one chain on it; its query state is selected with v_cndmask (never
 // a dynamically indexed register array, which would live in scratch)
-// software-pipelined alternative (PIPE): one chain per needed query tile, into accumulators
-// alternating by the tile's parity (static indices, no copies); the epilogue of tile q - 1 is
-// issued after the MFMAs of tile q, so the VALU work overlaps the matrix core
-template <int KS, int QT, int Q>
-__device__ __forceinline__ void k3p_pipe(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, int t, float (&b1)[QT],
-                                         float (&b2)[QT], int (&i1)[QT], f32x16 (&acc)[2]) {
-  if constexpr (Q <= QT) {
-    constexpr int NP = 2 * KS;
-    if constexpr (Q < QT) {
-      if ((msk >> Q) & 1u) acc[Q & 1] = k3p_chain<KS>(a, lq + Q * NP * IA_WAVE);
-    }
-    if constexpr (Q >= 1) {
-      if ((msk >> (Q - 1)) & 1u) k3p_epi1(acc[(Q - 1) & 1], t, b1[Q - 1], b2[Q - 1], i1[Q - 1]);
-    }
-    k3p_pipe<KS, QT, Q + 1>(a, lq, msk, t, b1, b2, i1, acc);
-  }
-}
-
-// one accumulator at a time (k3h_prune3 with NBUF = 1: 4 waves per SIMD interleave the chains)
-template <int KS, int QT, int Q>
-__device__ __forceinline__ void k3p_singles(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, int t, float (&b1)[QT],
-                                            float (&b2)[QT], int (&i1)[QT]) {
-  if constexpr (Q < QT) {
-    if ((msk >> Q) & 1u) {
-      const f32x16 c = k3p_chain<KS>(a, lq + Q * 2 * KS * IA_WAVE);
-      k3p_epi1(c, t, b1[Q], b2[Q], i1[Q]);
-    }
-    k3p_singles<KS, QT, Q + 1>(a, lq, msk, t, b1, b2, i1);
-  }
-}
-
 template <int KS, int QT, int QP>
 __device__ __forceinline__ void k3p_pairs(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, int t, float (&b1)[QT],
                                           float (&b2)[QT], int (&i1)[QT]) {
@@ -515,42 +484,6 @@ __device__ __forceinline__ void k3p_hhpairs(const h16x8 (&a)[2 * KS], const h16x
       }
     }
     k3p_hhpairs<KS, QT, QP + 1>(a, lq, msk, rt, qzt, qzw, t, b1, b2, i1, pass);
-  }
-}
-
-// HF (k3p_variant 16 / 17): the rotated DB (ia_internal.h).  A tile's head is
-// its k-step 0 (2 pieces, 2 KiB), its tail the other 6 (6 KiB, a separate array after the NT
-// heads).  The head chain (3 MFMAs) of a (DB tile, query tile) block yields the 15-axis partial
-// distance minus |q''_h|^2; a lane's 16 values belong to its query (lane & 31), whose z0 (K2r)
-// bounds every value a row within the query's U' can have.
-__device__ __forceinline__ void ld_head(h16x8 (&h)[2], const h16x8 *__restrict__ db, int64_t tile, int lane) {
-  const h16x8 *src = db + tile * 2 * IA_WAVE;
-  h[0] = src[lane];
-  h[1] = src[IA_WAVE + lane];
-}
-template <int KS>
-__device__ __forceinline__ void ld_rtile(h16x8 (&a)[2 * KS], const h16x8 *__restrict__ db, int64_t NT, int64_t tile, int lane) {
-  static_assert(KS == 4, "rotated DB: 1 channel");
-  const h16x8 *hs = db + tile * 2 * IA_WAVE;
-  const h16x8 *ts = db + NT * 2 * IA_WAVE + tile * 6 * IA_WAVE;
-  a[0] = hs[lane];
-  a[1] = hs[IA_WAVE + lane];
-#pragma unroll
-  for (int p = 2; p < 2 * KS; p++) a[p] = ts[(p - 2) * IA_WAVE + lane];
-}
-template <int KS, int QT, int Q>
-__device__ __forceinline__ void k3f_headpipe(const h16x8 (&hd)[2], const h16x8 *lq, unsigned msk, const float *qz0,
-                                             f32x16 (&acc)[2], unsigned &pass) {
-  if constexpr (Q <= QT) {
-    constexpr int NP = 2 * KS;
-    if constexpr (Q < QT) {
-      if ((msk >> Q) & 1u) acc[Q & 1] = k3p_chain<1>(hd, lq + Q * NP * IA_WAVE);
-    }
-    if constexpr (Q >= 1) {
-      if ((msk >> (Q - 1)) & 1u)
-        pass |= __ballot(k3p_min16(acc[(Q - 1) & 1]) <= qz0[(Q - 1) * IA_TILE]) != 0ull ? 1u << (Q - 1) : 0u;
-    }
-    k3f_headpipe<KS, QT, Q + 1>(hd, lq, msk, qz0, acc, pass);
   }
 }
 
@@ -877,40 +810,32 @@ k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const floa
 // The product library holds only the packed-index epilogue (variant 1); the compare/select
 // epilogue (0) and the probes (2, 3) are experiments, built with DIAG=1 only.
 k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
-#ifdef IA_K3H_DIAG
-  if (variant == 0) return k3h_scan<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, false>;
-  if constexpr (IA_K3H_KS == 4 && IA_K3H_QT == 11) {  // diagnostic variants (plateau instance only)
-    if (variant == 2) return k3h_scan<IA_K3H_KS, IA_K3H_QT, 4, true>;
-    if (variant == 3) return k3h_scan<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, true, 1>;
-  }
-#endif
   (void)variant;
   return k3h_scan<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, true>;
 }
 #endif
 
 // ------------------------------------------------------------------------------------------
-// K3p v3 (k3p_variant 3, the default where it applies: Mpad <= 512, <= 512 tiles per
-// workgroup).  Same pairs, same records semantics as V1, organised in phases so no phase waits
-// on another's memory latency:
+// K3p (k3p_variants 7, 11, 14, 15, 18..21).  Same pairs, same records semantics
+// as V1, organised so no phase waits on another's memory latency:
 //   1. ONE global round: every query's pruning record (thread = query, registers), the step's
 //      unsorted split-f16 query fragments (coalesced, registers), the workgroup's tile boxes
-//      (to LDS) and each wave's speculative first DB tile
-//   2. rank sort by unique key (as V1); fragments and records scattered to their sorted LDS
-//      slots; query-tile boxes by 32-lane butterflies
-//   3. need masks of ALL the workgroup's tiles (wave v: tiles k = v mod NW), with the lane's
-//      per-pair query intervals held in registers; the needed tiles compacted into one list
-//      in tile order (ballot + mbcnt)
-//   4. list item j -> wave j mod NW (deterministic, balanced by tile count); the DB tiles of
-//      items j + NW and j + 2 NW are in flight while item j is contracted (nothing else
-//      between the loads: no need test left in the loop)
-//   5. per-query records exactly as V1
+//      (to LDS) and each wave's speculative first DB tile (PRE: this launch's presorted slice
+//      straight into LDS)
+//   2. bitonic sort by unique key; fragments and records scattered to their sorted LDS slots;
+//      query-tile boxes by 32-lane butterflies (PRE: skipped, or only the boxes)
+//   3. tiles handed out through an LDS counter; per tile the coarse (query-tile box) and fine
+//      (per query) need tests, the needed tile's load in flight while the previous one is
+//      contracted (two register buffers in rotation)
+//   4. per-query records exactly as V1
+// (The other versions of DESIGN.md §4b's progression - no interleaving, one or three tile
+// buffers, software-pipelined single chains, the previous step's order, the rotated-DB head
+// filter - are in the history of this file up to round 3.)
 // ------------------------------------------------------------------------------------------
 #ifndef IA_K3P_ROWS_EARLY  // 1: candidate rows looked up before the subset merge (0: after it)
 #define IA_K3P_ROWS_EARLY 1
 #endif
 #define IA_K3P3_MAXQ 512   // queries per step (one per thread)
-#define IA_K3P3_MAXK 512   // DB tiles per workgroup
 // steps of up to IA_K3P_RANK_MAX queries are sorted by rank counting, wider ones by the bitonic
 // network (at 342 queries the network measured faster: profiles/r02/ab3)
 #ifndef IA_K3P_RANK_MAX
@@ -921,9 +846,10 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // ord_in maps a sorted slot to its query and tbox holds the sorted query tiles' boxes, so phase
 // 1 loads only this launch's slice and phase 2 (sort, scatter, tile boxes) is skipped.
 // HHF (k3p_variant 14 / 15): the hi x hi block filter above (k3p_hhpipe); the per-WG pair
-// counter slot then holds (pairs with corrections << 32) + box-needed pairs.
-template <int KS, int QT, int NW, int NBUF, bool INTER, bool DYN = false, bool ORD = false, bool PIPE = false,
-          bool PRE = false, bool HHF = false, bool HF = false, int HHX = 0>
+// counter slot then holds (pairs with corrections << 32) + box-needed pairs.  HHX: how the
+// correction products follow the filter (0: full chains, 1: fused single chains, 2: fused on
+// query-tile pairs, k3p_hhpairs).
+template <int KS, int QT, int NW, bool PRE = false, bool HHF = false, int HHX = 0>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
@@ -934,9 +860,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
   constexpr int NE = PRE ? 1 : (IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE + WGT - 1) / WGT;  // unsorted fragments per thread
   static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
-  // the in-kernel sort holds one query per thread; the tile lists of the !INTER and HF paths one
-  // tile per thread (the launcher keeps K <= IA_K3P3_MAXK there); INTER walks any K
-  static_assert(WGT >= IA_K3P3_MAXQ && WGT >= IA_K3P3_MAXK, "one query / one tile per thread");
+  // the in-kernel sort holds one query per thread; the tile walk takes any K (the launcher keeps
+  // K <= IA_K3P_MAXK_LDS: the boxes, need masks and R_t of the WG's tiles live in LDS)
+  static_assert(WGT >= IA_K3P3_MAXQ, "one query per thread");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
   float4 *qlo = reinterpret_cast<float4 *>(ldsh + QT * NP * IA_WAVE);  // [NQ]
   float4 *qhi = qlo + NQ;                                               // [NQ]
@@ -991,7 +917,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
 
   // ---- 1. one global round
   h16x8 a[NP], an[NP], an2[NP];
-  if constexpr (!(INTER && NBUF == 1) && !HF) {
+  {
     ld_tile<KS>(a, db, tk(min(wave, K - 1)), lane);
   }
   if constexpr (PRE) {
@@ -1024,7 +950,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       qhi[x] = ok ? qinfo[3 * sl + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
       const float4 u = ok ? qinfo[3 * sl + 2] : make_float4(-INFINITY, 0.f, -INFINITY, 0.f);
       qU[x] = u.x;
-      if constexpr (HHF || HF) {
+      if constexpr (HHF) {
         qzt[x] = u.z;
         qzw[x] = u.w;
       }
@@ -1036,14 +962,14 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       thi[tid] = ok ? tbox[3 * (qt0 + tid) + 1] : make_float4(0.f, 0.f, 0.f, 0.f);
       tU[tid] = ok ? tbox[3 * (qt0 + tid) + 2].x : -INFINITY;
     }
-    for (int x = tid; x < K; x += WGT) {  // K may exceed WGT (INTER variants: up to IA_K3P_MAXK_LDS)
+    for (int x = tid; x < K; x += WGT) {  // K may exceed WGT (up to IA_K3P_MAXK_LDS)
       const int t = tk(x);
       wbox[2 * x] = boxes[2 * t];
       wbox[2 * x + 1] = boxes[2 * t + 1];
       if constexpr (HHF) wR[x] = tnorm[t];
     }
   }
-  __shared__ int kctr;  // DYN: next tile index to hand out
+  __shared__ int kctr;  // next tile index to hand out
   if (tid == 0) kctr = NW;
   if constexpr (PRE) __syncthreads();
   // the query-tile boxes (min lo, max hi, max U' over the tile's real queries) by 32-lane
@@ -1124,65 +1050,11 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     skey[tid] = mkey;
     rankof[tid] = -1;
   }
-  const int prow = ORD && tid < n_in ? ord_in[tid] : -1;
   __syncthreads();
   K3P_T(ph[1]);
-  if (ORD && qt0 == 0 && wave == 0) {
-    // ORD: this step's exact key order, for the NEXT step (its queries are these pixels' right
-    // neighbours, whose features are close): workgroup w ranks queries w, w + nwg, ... and
-    // writes their rows at their ranks, so the grid writes the whole order once
-    for (int q = wg; q < M; q += nwg) {
-      const unsigned kq = skey[q];
-      int c = 0;
-      for (int j = lane; j < Mpad; j += IA_WAVE) c += (int)(skey[j] < kq);
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o, 64);
-      if (lane == 0) ord_out[c] = r0 + q;
-    }
-  }
 
   // ---- 2. sort, scatter to sorted slots, query-tile boxes
-  if (ORD && n_in > 0) {  // (uniform) the previous step's order: no sort on the critical path
-    // rows of the previous order still in this step keep their relative order; then the new
-    // rows, then padding, by index (any grouping is exact: it only steers the pruning)
-    const int pm = prow - r0;
-    const bool v1 = tid < n_in && pm >= 0 && pm < M;
-    unsigned long long b = __ballot(v1);
-    int pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
-    if (lane == 0) wcnt[wave] = __popcll(b);
-    __syncthreads();
-    int base = 0, nvalid = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-      base += w < wave ? wcnt[w] : 0;
-      nvalid += wcnt[w];
-    }
-    if (v1) rankof[pm] = base + pre;
-    __syncthreads();
-    const bool un = tid < Mpad && rankof[tid] < 0;
-    b = __ballot(un);
-    pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
-    if (lane == 0) wcnt[wave] = __popcll(b);
-    __syncthreads();
-    base = nvalid;
-#pragma unroll
-    for (int w = 0; w < NW; w++) base += w < wave ? wcnt[w] : 0;
-    if (un) rankof[tid] = base + pre;
-    if (tid < Mpad) {
-      const int rk = rankof[tid];
-      order[rk] = tid;
-      const int x = rk - s0;
-      if (x >= 0 && x < NQ) {
-        qlo[x] = mlo;
-        qhi[x] = mhi;
-        qU[x] = mU;
-        if constexpr (HHF || HF) {
-          qzt[x] = mzt;
-          qzw[x] = mzw;
-        }
-      }
-    }
-  } else if (DYN && Mpad > IA_K3P_RANK_MAX) {  // (uniform) up to IA_K3P_RANK_MAX queries the rank count
+  if (Mpad > IA_K3P_RANK_MAX) {  // (uniform) up to IA_K3P_RANK_MAX queries the rank count
     // bitonic network over the first 512 threads' unique keys (padding: 0xFFFFFFFF, last):
     // exchanges at distance < 64 are lane swaps, the 6 at distance >= 64 go through LDS (the
     // query-fragment area, free until the scatter below)
@@ -1217,7 +1089,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         qlo[x] = mlo;
         qhi[x] = mhi;
         qU[x] = mU;
-        if constexpr (HHF || HF) {
+        if constexpr (HHF) {
           qzt[x] = mzt;
           qzw[x] = mzw;
         }
@@ -1236,7 +1108,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       qlo[x] = mlo;
       qhi[x] = mhi;
       qU[x] = mU;
-      if constexpr (HHF || HF) {
+      if constexpr (HHF) {
         qzt[x] = mzt;
         qzw[x] = mzw;
       }
@@ -1266,146 +1138,18 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     i1[q] = 0x7fffffff;
   }
   unsigned cnt = 0, ntl = 0, nfull = 0;
-  int nitems_wg = 0;  // HF: tiles whose full rows were loaded
-  if constexpr (HF) {
-    // ---- HF (k3p_variant 16 / 17), three list phases with deterministic item ->
-    // wave assignment (item j -> wave j mod NW), so no phase waits on a dependent load:
-    //   0. box need masks of all the workgroup's tiles (wave v: tiles v, v + NW, ...), the needed
-    //      tiles compacted in tile order;
-    //   1. their heads (2 KiB) streamed three items ahead; per needed block the 3-MFMA head
-    //      chain and the z0 test -> pass mask per tile; the passing tiles compacted in order;
-    //   2. their full rows (head + tail, 8 KiB) two items ahead; the full 12-MFMA chains and the
-    //      packed top-2 epilogue of the passing blocks.
-    unsigned *kpass = reinterpret_cast<unsigned *>(wR);  // [K] pass mask per tile
-    int *items2 = reinterpret_cast<int *>(wR + K);        // [K] passing tiles, in order
-    {
-      // box need masks as the !INTER path: the query-tile box test (lane q < QT), then per
-      // needed pair of query tiles the per-query test with the lane's query intervals held in
-      // registers (no LDS reads in the loop)
-      float4 fl[NPAIR], fh[NPAIR];
-      float fu[NPAIR];
-#pragma unroll
-      for (int pr = 0; pr < NPAIR; pr++) {
-        const int jq = 2 * pr + half, x = jq * IA_TILE + (lane & 31);
-        fl[pr] = jq < QT ? qlo[x] : make_float4(0.f, 0.f, 0.f, 0.f);
-        fh[pr] = jq < QT ? qhi[x] : make_float4(0.f, 0.f, 0.f, 0.f);
-        fu[pr] = jq < QT ? qU[x] : -INFINITY;
-      }
-      const bool cl = lane < QT;
-      const float4 ctl = cl ? tlo[lane] : make_float4(0.f, 0.f, 0.f, 0.f), cth = cl ? thi[lane] : ctl;
-      const float ctu = cl ? tU[lane] : -INFINITY;
-      for (int k = wave; k < K; k += NW) {
-        const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
-        const unsigned coarse = (unsigned)__ballot(cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
-        unsigned msk = 0;
-#pragma unroll
-        for (int pr = 0; pr < NPAIR; pr++) {
-          if ((coarse >> (2 * pr)) & 3u) {
-            const unsigned long long b = __ballot(prune_lb(blo, bhi, fl[pr], fh[pr]) <= fu[pr]);
-            msk |= (((unsigned)b != 0u ? 1u : 0u) | ((unsigned)(b >> 32) != 0u ? 2u : 0u)) << (2 * pr);
-          }
-        }
-        if (lane == 0) {
-          kmask[k] = msk & coarse;
-          kpass[k] = 0u;
-        }
-      }
-    }
-    // ordered compaction of the tiles k < K with pred(k) into list[]: returns the count
-    auto compact = [&](auto pred, int *list) -> int {
-      __syncthreads();
-      const bool nd = tid < K && pred(tid);
-      const unsigned long long b = __ballot(nd);
-      const int pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
-      if (lane == 0) wcnt[wave] = __popcll(b);
-      __syncthreads();
-      int base = 0, n = 0;
-#pragma unroll
-      for (int w = 0; w < NW; w++) {
-        base += w < wave ? wcnt[w] : 0;
-        n += wcnt[w];
-      }
-      if (nd) list[base + pre] = tid;
-      __syncthreads();
-      return n;
-    };
-    const int n1 = compact([&](int k) { return kmask[k] != 0u; }, items);
-    K3P_T(ph[3]);
-    int j = wave;
-    if (j < n1) {
-      auto itm = [&](int jj) { return tk(items[jj < n1 ? jj : n1 - 1]); };  // past the end: the last item again
-      // six head buffers in rotation, five items ahead (the compiler's wait at the loop's top
-      // is one item conservative, so the effective depth is four)
-      h16x8 g0[2], g1[2], g2[2], g3[2], g4[2], g5[2];
-      ld_head(g0, db, itm(j), lane);
-      ld_head(g1, db, itm(j + NW), lane);
-      ld_head(g2, db, itm(j + 2 * NW), lane);
-      ld_head(g3, db, itm(j + 3 * NW), lane);
-      ld_head(g4, db, itm(j + 4 * NW), lane);
-      auto hs = [&](const h16x8(&cur)[2], h16x8(&nx5)[2], int jj) {
-        ld_head(nx5, db, itm(jj + 5 * NW), lane);  // unconditional: equal vmcnt on every path
-        asm volatile("" ::: "memory");
-        const int k = items[jj];
-        const unsigned m = kmask[k];
-        f32x16 acc[2];
-        unsigned pass = 0;
-        k3f_headpipe<KS, QT, 0>(cur, ldsh + lane, m, qzt + (lane & 31), acc, pass);
-        if (lane == 0) kpass[k] = pass;
-        cnt += __popc(m);
-        nfull += __popc(pass);
-        ntl++;
-      };
-      for (; j < n1; j += 6 * NW) {
-        hs(g0, g5, j);
-        if (j + NW >= n1) break;
-        hs(g1, g0, j + NW);
-        if (j + 2 * NW >= n1) break;
-        hs(g2, g1, j + 2 * NW);
-        if (j + 3 * NW >= n1) break;
-        hs(g3, g2, j + 3 * NW);
-        if (j + 4 * NW >= n1) break;
-        hs(g4, g3, j + 4 * NW);
-        if (j + 5 * NW >= n1) break;
-        hs(g5, g4, j + 5 * NW);
-      }
-    }
-    K3P_T(ph[6]);
-    const int n2 = compact([&](int k) { return kpass[k] != 0u; }, items2);
-    nitems_wg = n2;
-    j = wave;
-    if (j < n2) {
-      auto itm2 = [&](int jj) { return tk(items2[jj < n2 ? jj : n2 - 1]); };
-      ld_rtile<KS>(a, db, NT, itm2(j), lane);
-      ld_rtile<KS>(an, db, NT, itm2(j + NW), lane);
-      auto fs = [&](const h16x8(&cur)[NP], h16x8(&nx2)[NP], int jj) {
-        ld_rtile<KS>(nx2, db, NT, itm2(jj + 2 * NW), lane);
-        asm volatile("" ::: "memory");
-        const int k = items2[jj];
-        k3p_pairs<KS, QT, 0>(cur, ldsh + lane, kpass[k], tk(k), b1, b2, i1);
-      };
-      for (; j < n2; j += 3 * NW) {
-        fs(a, an2, j);
-        if (j + NW >= n2) break;
-        fs(an, a, j + NW);
-        if (j + 2 * NW >= n2) break;
-        fs(an2, an, j + 2 * NW);
-      }
-    }
-  } else if constexpr (INTER) {
+  {
     K3P_T(ph[3]);
     // ---- 3'/4'. need tests interleaved with the contraction: wave v walks tiles k = v mod NW;
     // while tile k is contracted, the next needed tile's load is in flight and the need tests
     // after it run on the VALU (two buffers in rotation)
     const bool cl = lane < QT;
-    // NBUF = 1 (128 VGPRs): the query-tile boxes are re-read from LDS per test, not held
-    const float4 ctl = cl && NBUF != 1 ? tlo[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float4 cth = cl && NBUF != 1 ? thi[lane] : ctl;
-    const float ctu = cl && NBUF != 1 ? tU[lane] : -INFINITY;
+    const float4 ctl = cl ? tlo[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float4 cth = cl ? thi[lane] : ctl;
+    const float ctu = cl ? tU[lane] : -INFINITY;
     auto need_k = [&](int k) -> unsigned {
       const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
-      const bool cpass = NBUF == 1 ? (cl && prune_lb(blo, bhi, tlo[lane < QT ? lane : 0], thi[lane < QT ? lane : 0]) <=
-                                                tU[lane < QT ? lane : 0])
-                                   : (cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
+      const bool cpass = cl && prune_lb(blo, bhi, ctl, cth) <= ctu;
       const unsigned coarse = (unsigned)__ballot(cpass);
       unsigned msk = 0;
 #pragma unroll
@@ -1420,15 +1164,15 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       }
       return msk & coarse;
     };
-    // DYN: tiles handed out through an LDS counter (balances the waves' pair counts; the
-    // records stay exact, only which subset holds which row varies)
+    // tiles handed out through an LDS counter (balances the waves' pair counts; the records stay
+    // exact, only which subset holds which row varies)
     auto grab = [&]() -> int {
       int g = 0;
       if (lane == 0) g = atomicAdd(&kctr, 1);
       return __builtin_amdgcn_readfirstlane(g);
     };
     auto next_k = [&](int k, unsigned &m) -> int {
-      for (; k < K; k = DYN ? grab() : k + NW) {
+      for (; k < K; k = grab()) {
         m = need_k(k);
         if (m) return k;
       }
@@ -1437,28 +1181,12 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     };
     unsigned m;
     int k = next_k(wave, m);
-    if constexpr (NBUF == 1) {
-      // one tile buffer (NW = 16: 4 waves per SIMD within 128 VGPRs): the tile's load is in
-      // flight while the need tests of the next tile run; the other waves of the SIMD cover
-      // the rest of the latency
-      while (k < K) {
-        ld_tile<KS>(a, db, tk(k), lane);
-        unsigned mn;
-        const int kn = next_k(DYN ? grab() : k + NW, mn);
-        asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-        k3p_singles<KS, QT, 0>(a, ldsh + lane, m, tk(k), b1, b2, i1);
-        cnt += __popc(m);
-        ntl++;
-        k = kn;
-        m = mn;
-      }
-    } else {
     // (re)load the first needed tile unconditionally (usually the speculative one again: a
     // cache hit), so the loop is entered with the same outstanding loads on every path
     ld_tile<KS>(a, db, tk(k < K ? k : min(wave, K - 1)), lane);
     auto step = [&](const h16x8(&cur)[NP], h16x8(&nxt)[NP]) {
       unsigned mn;
-      const int kn = next_k(DYN ? grab() : k + NW, mn);
+      const int kn = next_k(grab(), mn);
       // always issue the 8 loads (past the last tile: the current tile again, an L2 hit): with a
       // conditional prefetch the compiler's vmcnt at the join covers the no-load path, which
       // makes the MFMAs below wait for the prefetch itself
@@ -1480,9 +1208,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         k3p_hhpipe<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
         if (pass) k3p_pairs<KS, QT, 0>(cur, ldsh + lane, pass, tk(k), b1, b2, i1);
         nfull += __popc(pass);
-      } else if constexpr (PIPE) {
-        f32x16 acc[2];
-        k3p_pipe<KS, QT, 0>(cur, ldsh + lane, m, tk(k), b1, b2, i1, acc);
       } else {
         k3p_pairs<KS, QT, 0>(cur, ldsh + lane, m, tk(k), b1, b2, i1);
       }
@@ -1496,95 +1221,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       if (k >= K) break;
       step(an, a);
     }
-    }  // NBUF != 1
-  } else {
-  // ---- 3. need masks of the workgroup's tiles
-  {
-    float4 fl[NPAIR], fh[NPAIR];
-    float fu[NPAIR];
-#pragma unroll
-    for (int pr = 0; pr < NPAIR; pr++) {
-      const int j = 2 * pr + half, x = j * IA_TILE + (lane & 31);
-      fl[pr] = j < QT ? qlo[x] : make_float4(0.f, 0.f, 0.f, 0.f);
-      fh[pr] = j < QT ? qhi[x] : make_float4(0.f, 0.f, 0.f, 0.f);
-      fu[pr] = j < QT ? qU[x] : -INFINITY;
-    }
-    const bool cl = lane < QT;
-    const float4 ctl = cl ? tlo[lane] : make_float4(0.f, 0.f, 0.f, 0.f), cth = cl ? thi[lane] : ctl;
-    const float ctu = cl ? tU[lane] : -INFINITY;
-    for (int k = wave; k < K; k += NW) {
-      const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
-      const unsigned coarse = (unsigned)__ballot(cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
-      unsigned msk = 0;
-#pragma unroll
-      for (int pr = 0; pr < NPAIR; pr++) {
-        if ((coarse >> (2 * pr)) & 3u) {
-          const unsigned long long b = __ballot(prune_lb(blo, bhi, fl[pr], fh[pr]) <= fu[pr]);
-          msk |= (((unsigned)b != 0u ? 1u : 0u) | ((unsigned)(b >> 32) != 0u ? 2u : 0u)) << (2 * pr);
-        }
-      }
-      if (lane == 0) kmask[k] = msk & coarse;
-    }
   }
-  __syncthreads();
-  int n = 0;  // needed tiles of the workgroup
-  {  // compaction in tile order (thread k = tile k)
-    const bool nd = tid < K && kmask[tid] != 0u;
-    const unsigned long long b = __ballot(nd);
-    const int pre = __builtin_amdgcn_mbcnt_hi((unsigned)(b >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)b, 0u));
-    if (lane == 0) wcnt[wave] = __popcll(b);
-    __syncthreads();
-    int base = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-      base += w < wave ? wcnt[w] : 0;
-      n += wcnt[w];
-    }
-    if (nd) items[base + pre] = tid;
-    __syncthreads();
-  }
-  K3P_T(ph[3]);
-
-  // ---- 4. contract the needed pairs: item j -> wave j mod NW, two tiles in flight
-  auto tile_of = [&](int j) { return tk(items[j]); };
-  int j = wave;
-  if (j < n) {
-    if (items[j] != min(wave, K - 1)) {  // the speculative tile is not this wave's first item
-      ld_tile<KS>(a, db, tile_of(j), lane);
-    }
-    if (NBUF == 3 && j + NW < n) {
-      ld_tile<KS>(an, db, tile_of(j + NW), lane);
-    }
-  }
-  // three tile buffers in rotation (no register copies: a copy of a loaded register waits for
-  // its load, which would collapse the prefetch depth to zero)
-  constexpr int AHEAD = (NBUF - 1) * NW;  // items in flight ahead of the one contracted
-  auto step = [&](const h16x8(&cur)[NP], h16x8(&nx2)[NP], int jj) {
-    if (jj + AHEAD < n) {  // wave-uniform
-      ld_tile<KS>(nx2, db, tile_of(jj + AHEAD), lane);
-    }
-    asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-    const unsigned msk = kmask[items[jj]];
-    k3p_pairs<KS, QT, 0>(cur, ldsh + lane, msk, tile_of(jj), b1, b2, i1);
-    cnt += __popc(msk);
-    ntl++;
-  };
-  if constexpr (NBUF == 3) {
-    for (; j < n; j += 3 * NW) {
-      step(a, an2, j);
-      if (j + NW >= n) break;
-      step(an, a, j + NW);
-      if (j + 2 * NW >= n) break;
-      step(an2, an, j + 2 * NW);
-    }
-  } else {
-    for (; j < n; j += 2 * NW) {
-      step(a, an, j);
-      if (j + NW >= n) break;
-      step(an, a, j + NW);
-    }
-  }
-  }  // !INTER
   K3P_T(ph[4]);
 #pragma unroll
   for (int q = 0; q < QT; q++) {  // tile + packed in-tile index -> DB position (-> DB row)
@@ -1605,7 +1242,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   // fragments for NW = 16, overwrites it)
   const int mq_pre = tid < NQ ? (PRE ? (int)skey[tid] : order[s0 + tid]) : 0;
   __syncthreads();
-  if constexpr (!HF) K3P_T(ph[6]);  // probe: the wait for the workgroup's slowest wave ends here
+  K3P_T(ph[6]);  // probe: the wait for the workgroup's slowest wave ends here
   if (lane == 0) {
     wpairs[wave] = cnt;
     wtiles[wave] = ntl;
@@ -1667,8 +1304,8 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       st += wtiles[w];
       sf += wfull[w];
     }
-    pairs[blockIdx.x] += sp + (HHF || HF ? sf << 32 : 0ull);
-    tiles[blockIdx.x] += st + (HF ? (unsigned long long)nitems_wg << 32 : 0ull);
+    pairs[blockIdx.x] += sp + (HHF ? sf << 32 : 0ull);
+    tiles[blockIdx.x] += st;
   }
   if (xo.stamp) {  // (uniform) option "stamps": the workgroup's first and last tick
     __syncthreads();
@@ -1682,7 +1319,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     atomicAdd(&k3p_prof[2], ph[3] - ph[2]);
     atomicAdd(&k3p_prof[3], ph[4] - ph[3]);
     atomicAdd(&k3p_prof[7], ph[5] - ph[4]);
-    atomicAdd(&k3p_prof[8], HF ? ph[6] - ph[3] : ph[6] - ph[4]);  // HF: phase 1 (heads); else: the tail's barrier wait
+    atomicAdd(&k3p_prof[8], ph[6] - ph[4]);  // the tail's barrier wait
     atomicAdd(&k3p_prof[9], ph[7] - ph[6]);    // per-wave half merge + LDS writes
     atomicAdd(&k3p_prof[10], ph[8] - ph[7]);   // second barrier
     atomicAdd(&k3p_prof[11], ph[9] - ph[8]);   // subset merge + record stores
@@ -1700,7 +1337,7 @@ void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau w
   fprintf(stderr, "K3P_PROBE tail split: half merge %.0f, barrier %.0f, subset merge + records %.0f\n", (double)v[9] / v[4],
           (double)v[10] / v[4], (double)v[11] / v[4]);
   fprintf(stderr, "K3P_PROBE v3 phases if variant>=3: load=setup, sort+scatter=need, need=loop, loop=tail, tail=[7]\n");
-  fprintf(stderr, "K3P_PROBE [7]=%.0f [8]=%.0f (HF: [8] = phase 1, loop - [8] = phase 2; else [8] = the tail barrier wait)\n", (double)v[7] / v[4],
+  fprintf(stderr, "K3P_PROBE [7]=%.0f [8]=%.0f ([8] = the tail barrier wait)\n", (double)v[7] / v[4],
           (double)v[8] / v[4]);
   fprintf(stderr, "K3P_PROBE waves=%llu setup=%.0f need=%.0f loop=%.0f tail=%.0f tiles/wave=%.2f pairs/wave=%.2f (cycles/wave)\n",
           v[4], (double)v[0] / v[4], (double)v[1] / v[4], (double)v[2] / v[4], (double)v[3] / v[4], (double)v[5] / v[4],
@@ -1718,36 +1355,17 @@ void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau w
 // progression are built with DIAG=1 only.
 k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
   if constexpr (IA_K3H_KS == 4) {
-#ifdef IA_K3H_DIAG
-    if (variant == 0) return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 0>;
-    if (variant == 2) return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2>;
-    if (variant == 3) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 3, false>;
-    if (variant == 4) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, false>;
-    if (variant == 5) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true>;
-    if (variant == 8) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, true>;
-    if (variant == 9) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, true>;
-    // 16 waves per workgroup, one tile buffer: slower than 6/11 on cfg3 and cfg4
-    if (variant == 12) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, 16, 1, true, true, false, false, true>;
-    if (variant == 13) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, 16, 1, true, true>;  // 12 with the in-kernel sort
-#endif
-    if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true>;
-    if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true>;
-    if (variant == 14) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true>;
-    if (variant == 15) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true>;
+    constexpr int NW = IA_WGH / IA_WAVE;
+    if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW>;
+    if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true>;
+    if (variant == 14) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true>;
+    if (variant == 15) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true>;
     // 18 / 19: 14 / 15 with the correction products fused onto the hi x hi accumulator (HHX)
-    if (variant == 18)
-      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true, false, 1>;
-    if (variant == 19)
-      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true, false, 1>;
+    if (variant == 18) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true, 1>;
+    if (variant == 19) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true, 1>;
     // 20 / 21: the fused corrections on query-tile pairs (two chains: k3p_hhpairs)
-    if (variant == 20)
-      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, true, false, 2>;
-    if (variant == 21)
-      return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, true, false, 2>;
-#ifdef IA_K3H_DIAG  // rotated DB + head filter: exact, not faster
-    if (variant == 16) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, false, false, true>;
-    if (variant == 17) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 2, true, true, false, false, true, false, true>;
-#endif
+    if (variant == 20) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true, 2>;
+    if (variant == 21) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true, 2>;
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

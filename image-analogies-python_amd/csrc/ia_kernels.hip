@@ -957,8 +957,7 @@ __device__ __forceinline__ double exact_dist_level(const double *__restrict__ db
 
 // MFMA error bound of a row with |a'| <= Rx (ia_internal.h ia_eps_c_h / DESIGN.md §5)
 __device__ __forceinline__ double merge_eps(const MergeArgs &a, double Rx, double qn) {
-  return a.eps_c * (Rx * Rx + 2.0 * Rx * qn) + a.eps_a * (Rx * Rx + 14.0 * Rx + 28.0 * qn + 260.0) +
-         a.eps_r * (Rx + qn) * (Rx + qn);
+  return a.eps_c * (Rx * Rx + 2.0 * Rx * qn) + a.eps_a * (Rx * Rx + 14.0 * Rx + 28.0 * qn + 260.0);
 }
 // Certification threshold of the best exact distance bd: a chunk whose unlisted rows all have
 // MFMA value >= T can hide a row that beats or ties bd only if T <= theta.  Only rows with exact
@@ -1516,171 +1515,6 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_gather_query_p(LevelGeo g, StepDes
   if (xp.W) xo_publish<KS>(xp, m, lane, xh[wv][0], xh[wv][1], i0, i1, i2);
 }
 
-#ifdef IA_K3H_DIAG  // k3p_variant 16 / 17: DIAG=1 builds only
-// ------------------------------------------------------------------------------------------
-// K2r: K2p for the rotated DB and its head-filtered scan (k3p_variant 16 / 17),
-// one wave per query.  Lane c of the wave owns MFMA column c:
-//   * q' (centred, fp64) in LDS; q''_f = sum_g R[f][g] q'_g (lane f < 55, coalesced reads of R^T)
-//   * fragments -2 q'' in the rotated column order (ia_rot_col), 256 in both norm columns
-//   * the pruning record as K2p (projections = q''_0..3, Morton key), with a tighter bound U:
-//     besides the coherence candidates' exact distances, the rows of the query's home tiles
-//     (k_key_lut: the Morton tile where its key falls, +-1; the causal neighbour's home tiles,
-//     whose loads could start with the kernel, gave a looser bound: 43 % instead of 27 % of
-//     the tiles' full rows loaded at 1024^2) are evaluated in f32 from their hi + lo parts;
-//     each gives a rigorous upper bound of the exact distance of a DB row
-//       sqrt(|a - q|^2) <= sqrt(d32) (1 + 2^-17) + 2^-20 (R + |q'| + 1)  (rotated space:
-//       hi + lo within 2^-22 |a''| + 2^-25 per column, f32 q'' within 2^-24, f32 sums within
-//       gamma_64), plus eps_r (R + |q'|)^2 back to unrotated distances
-//   * z0 = U' - |q''_h|^2 + eps + eps_r (R + |q'|)^2: a head value V0 > z0 proves every row of
-//     the value's (row, query) pair farther than U' (K3f's head filter)
-// ------------------------------------------------------------------------------------------
-template <bool IMG, class JS>
-__global__ void __launch_bounds__(IA_WG) k_gather_query_r(LevelGeo g, StepDesc sd, Imgs B, JS jobs,
-                                                          const double *__restrict__ mu_part,
-                                                          double *__restrict__ q64, double *__restrict__ qn2,
-                                                          _Float16 *__restrict__ qf, const double *__restrict__ db64,
-                                                          const double *__restrict__ basis, double ufac, RotArgs ra,
-                                                          float4 *__restrict__ qinfo, Imgs A) {
-  constexpr int D = 55, DS = 56, KS = 4, NWV = IA_WG / IA_WAVE;
-  __shared__ double qsh[NWV][DS], qcs[NWV][DS];
-  __shared__ float qcol[NWV][IA_WAVE];
-  __shared__ double rts[DS * DS];  // R^T of the level (staged once per workgroup, before any exit)
-#if IA_PROBE & 256
-  unsigned long long st2[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#endif
-  IA_STAMP2(0);
-  for (int i = threadIdx.x; i < DS * DS / 2; i += IA_WG)
-    reinterpret_cast<double2 *>(rts)[i] = reinterpret_cast<const double2 *>(ra.rt)[i];
-  __syncthreads();
-  IA_STAMP2(1);
-  const int lane = threadIdx.x & 63, wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int m = blockIdx.x * NWV + wv;
-  if (m >= sd.Mpad) return;
-  if (m >= sd.J * sd.M) {
-    put_qh<KS>(qf, m, lane, 0.);
-    if (lane == 0) {
-      qinfo[3 * m] = make_float4(0.f, 0.f, 0.f, 0.f);
-      qinfo[3 * m + 1] = make_float4(0.f, 0.f, 0.f, 0.f);
-      qinfo[3 * m + 2] = make_float4(-INFINITY, __uint_as_float(IA_PRUNE_KEY_PAD), -INFINITY, 0.f);
-    }
-    return;
-  }
-  const QPix px = ia_qpix(sd, g.bw, m);
-  const JobPtrs jp = jobs.get(px.job);
-  if constexpr (!JS::single) B = job_imgs(B, jp);
-  const int32_t *__restrict__ s = jp.s, *__restrict__ im = jp.im;
-  const int r = px.r, c = px.c, qi = px.qi;
-  int crow = -1;
-  if (qi > 0 && lane < 15) {
-    const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
-    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
-      const int nb = nr * g.bw + nc;
-      const int tr = s[2 * nb] + r - nr, tc = s[2 * nb + 1] + c - nc;
-      if (tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) crow = (im[nb] * g.ah + tr) * g.aw + tc;
-    }
-  }
-  double ss = 0.;
-  if (lane < D) {
-    const double v = feat<1>(B, lane, r, c, 0);
-    q64[(int64_t)m * D + lane] = v;
-    qsh[wv][lane] = v;
-    const double qc = v - mu_part[feat_part<1>(lane)];
-    qcs[wv][lane] = qc;
-    ss = qc * qc;
-  } else if (lane == D) {
-    qcs[wv][lane] = 0.;
-  }
-  ss = wave_sum_d(ss);
-  IA_STAMP2(2);
-  __builtin_amdgcn_wave_barrier();  // qsh / qcs written by this wave's lanes, read below
-  double y = 0.;  // q''_lane (lanes < 55)
-  if (lane < DS) {
-#pragma unroll 8
-    for (int gg = 0; gg < D; gg++) y = fma(rts[gg * DS + lane], qcs[wv][gg], y);
-  }
-  // column c = lane: axis ia_rot_col^-1(c), or a norm / padding column
-  const bool pcol = lane != IA_ROT_HNORM && lane < IA_ROT_TNORM;
-  const double yc = __shfl(y, lane < IA_ROT_HNORM ? lane : lane - 1, 64);
-  put_qh<KS>(qf, m, lane, pcol ? -2.0 * yc : (lane == IA_ROT_HNORM || lane == IA_ROT_TNORM) ? IA_NORM_SCALE : 0.);
-  qcol[wv][lane] = pcol ? (float)yc : 0.f;
-  const double hs = wave_sum_d(lane < IA_ROT_HNORM ? y * y : 0.);  // |q''_h|^2
-  double p[IA_NPC];
-#pragma unroll
-  for (int i = 0; i < IA_NPC; i++) p[i] = __shfl(y, i, 64);
-  const unsigned key = prune_key(p, basis + IA_NPC * D);
-  IA_STAMP2(3);
-  // the key's home tile (one table load) and its two neighbours: rows' f32 distances from hi + lo
-  const int hp = ra.lut[key >> (32 - ra.lb)];
-  const h16x8 *__restrict__ hd = reinterpret_cast<const h16x8 *>(ra.db);
-  const h16x8 *__restrict__ tl = hd + (int64_t)ra.NT * 2 * IA_WAVE;
-  h16x8 pc[3][8];
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    int t = hp - 1 + k;
-    t = t < 0 ? 0 : t >= ra.NT ? ra.NT - 1 : t;
-    pc[k][0] = hd[(t * 2 + 0) * IA_WAVE + lane];
-    pc[k][1] = hd[(t * 2 + 1) * IA_WAVE + lane];
-#pragma unroll
-    for (int q = 0; q < 6; q++) pc[k][2 + q] = tl[((int64_t)t * 6 + q) * IA_WAVE + lane];
-  }
-  double u = DBL_MAX;
-  if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh[wv], IMG ? &A : nullptr);
-  u = wave_min_d_x(u);
-  IA_STAMP2(4);
-  __builtin_amdgcn_wave_barrier();  // qcol
-  const int hh = lane >> 5;
-  float best = INFINITY;
-#pragma unroll
-  for (int k = 0; k < 3; k++) {
-    float part = 0.f;
-#pragma unroll
-    for (int st = 0; st < 4; st++) {
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        const int cc = 16 * st + 8 * hh + e;
-        const float x = (float)pc[k][2 * st][e] + (float)pc[k][2 * st + 1][e];
-        const float d = x - qcol[wv][cc];
-        const bool use = !((st == 0 && hh == 1 && e == 7) || (st == 3 && hh == 1));
-        part = use ? fmaf(d, d, part) : part;
-      }
-    }
-    const bool padh = hh == 1 && (float)pc[k][0][7] >= 50000.f;  // head norm column of a padding row
-    const bool pad = padh || __shfl_xor((int)padh, 32, 64);
-    const float tot = part + __shfl_xor(part, 32, 64);
-    if (!pad) best = fminf(best, tot);
-  }
-  best = wave_min_f_x(best);
-  IA_STAMP2(5);
-  const double R = (double)__uint_as_float(*ra.Rbits);
-  const double qn = sqrt(ss);
-  const double er = ra.eps_r * (R + qn) * (R + qn);
-  if (best < INFINITY) {
-    const double sq = sqrt((double)best) * (1.0 + 0x1p-17) + 0x1p-20 * (R + qn + 1.0);
-    u = fmin(u, sq * sq * (1.0 + 0x1p-40) + er);
-  }
-  if (lane == 0) {
-    qn2[m] = ss;
-    qinfo[3 * m] = make_float4(round_down_f(p[0] - IA_PRUNE_MABS), round_down_f(p[1] - IA_PRUNE_MABS),
-                               round_down_f(p[2] - IA_PRUNE_MABS), round_down_f(p[3] - IA_PRUNE_MABS));
-    qinfo[3 * m + 1] = make_float4(round_up_f(p[0] + IA_PRUNE_MABS), round_up_f(p[1] + IA_PRUNE_MABS),
-                                   round_up_f(p[2] + IA_PRUNE_MABS), round_up_f(p[3] + IA_PRUNE_MABS));
-    const bool fin = u < DBL_MAX;
-    const float up = fin ? round_up_f(u * ufac) : INFINITY;
-    const double eps = ra.eps_c * (R * R + 2.0 * R * qn) + ra.eps_a * (R * R + 14.0 * R + 28.0 * qn + 260.0);
-    const float z0 = fin ? round_up_f(((double)up - hs * (1.0 - 1e-12) + eps + er) * (1.0 + 1e-12)) : INFINITY;
-    qinfo[3 * m + 2] = make_float4(up, __uint_as_float(fin ? key : IA_PRUNE_KEY_INF), z0, 0.f);
-  }
-#if IA_PROBE & 256
-  if (lane == 0 && m == sd.M / 2 && (sd.t % 256) == 128) {
-    __builtin_amdgcn_s_waitcnt(0);
-    const unsigned long long t6 = __builtin_amdgcn_s_memtime();
-    printf("K2R t=%d M=%d stage=%llu feat=%llu rot+key=%llu coh=%llu u2=%llu end=%llu\n", sd.t, sd.M, st2[1] - st2[0],
-           st2[2] - st2[1], st2[3] - st2[2], st2[4] - st2[3], st2[5] - st2[4], t6 - st2[5]);
-  }
-#endif
-}
-
-#endif  // IA_K3H_DIAG
 
 struct MergeOut {  // one pixel's result: B' value (first channel), source pixel and A' image
   double v;
@@ -2682,15 +2516,6 @@ void ia_launch_merge_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &A
 template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
                            const JobSet &jobs, bool fused, hipStream_t st) {
-#ifdef IA_K3H_DIAG  // row_source = 1 (exact rows from the images, 1 channel): measured slower, DIAG=1 builds only
-  if constexpr (CH == 1) {
-    if (ma.img_rows) {
-      if (fused) launch_merge_j<CH, true, true>(g, sd, A, ma, win, jobs, st);
-      else launch_merge_j<CH, false, true>(g, sd, A, ma, win, jobs, st);
-      return;
-    }
-  }
-#endif
   if (fused) launch_merge_j<CH, true, false>(g, sd, A, ma, win, jobs, st);
   else launch_merge_j<CH, false, false>(g, sd, A, ma, win, jobs, st);
 }
@@ -2801,9 +2626,6 @@ int ia_ks_for(int ch) { return ch == 1 ? 4 : ch == 2 ? 7 : 0; }  // 3 channels: 
 int ia_k3h_qtmax(int KS) { return KS == 4 ? 11 : 8; }
 // waves per workgroup of the K3h instance selected by (KS, qt, variant) (ia_k3h.hip getters)
 static int k3h_waves(int KS, int qt, int variant) {
-#ifdef IA_K3H_DIAG
-  if (KS == 4 && qt == 11 && variant == 2) return 4;
-#endif
   return IA_WGH / IA_WAVE;
 }
 static size_t k3h_lds(int KS, int qt, int nw) {
@@ -2891,29 +2713,10 @@ void ia_launch_gather_p(const LevelGeo &g, const StepDesc &sd, const Imgs &B, co
                         double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
                         float4 *qinfo, const Imgs &A, int img_rows, hipStream_t st, const XOPub *xp) {
   const XOPub x = xp ? *xp : XOPub{};
-#ifdef IA_K3H_DIAG
-  if (img_rows) {
-    launch_gather_p_t<true>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, x, st);
-    return;
-  }
-#endif
   (void)img_rows;
   launch_gather_p_t<false>(g, sd, B, jobs, mu, q64, qn2, qf, db64, basis, ufac, qinfo, A, x, st);
 }
 
-#ifdef IA_K3H_DIAG
-void ia_launch_gather_r(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
-                        double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
-                        const RotArgs &ra, float4 *qinfo, const Imgs &A, hipStream_t st) {
-  const dim3 grid(cdiv(sd.Mpad, IA_WG / IA_WAVE));
-  if (jobs.J == 1)
-    hipLaunchKernelGGL((k_gather_query_r<false, JobArg1>), grid, dim3(IA_WG), 0, st, g, sd, job0_imgs(B, jobs),
-                       JobArg1{jobs.j0}, mu, q64, qn2, (_Float16 *)qf, db64, basis, ufac, ra, qinfo, A);
-  else
-    hipLaunchKernelGGL((k_gather_query_r<false, JobArgN>), grid, dim3(IA_WG), 0, st, g, sd, B, JobArgN{jobs.rest}, mu, q64,
-                       qn2, (_Float16 *)qf, db64, basis, ufac, ra, qinfo, A);
-}
-#endif
 
 // split-f16 distance kernels live in ia_k3h.hip, compiled once per (KS, QT) instance
 #define IA_K3H_DECL(ks, qt) k3h_fn ia_k3h_get_##ks##_##qt(int variant);
@@ -2957,27 +2760,22 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
   const int kmax = (NT + nwg - 1) / nwg;  // DB tiles per workgroup
-  const int rev = (variant == 7 || variant == 8 || variant == 10 || variant >= 11) ? (step & 1) : 0;  // alternate steps walk in reverse
-  if (variant == 7) variant = 6;  // 8: + the previous step's query order (no sort)
-  if (variant == 10) variant = 9;  // 9: 6 + pipelined single chains; 10: 9 + reverse walks
-  // the in-kernel sort (3..10, 13, 14) holds <= 512 queries (14 -> 15: the host ran K2s); the
-  // one-tile-per-thread lists of 3, 4 (!INTER) and 16, 17 (HF) <= 512 tiles per workgroup.  The
-  // INTER variants (5..15) walk any number of tiles (the host keeps kmax <= IA_K3P_MAXK_LDS).
-  const bool in_kernel_sort = (variant < 11 || variant == 13 || variant == 14 || variant == 18 || variant == 20) && variant >= 3;
-  const bool tile_lists = variant == 3 || variant == 4 || variant == 16 || variant == 17;
+  const int rev = (variant == 7 || variant >= 11) ? (step & 1) : 0;  // alternate steps walk in reverse
+  if (variant == 7) variant = 6;
+  // the in-kernel sort (7, 14, 18, 20) holds <= 512 queries (wider: the host ran K2s, the
+  // presorted form 15 / 19 / 21 / 11); every variant walks any number of tiles (the host keeps
+  // kmax <= IA_K3P_MAXK_LDS)
+  const bool in_kernel_sort = variant == 6 || variant == 14 || variant == 18 || variant == 20;
   if (in_kernel_sort && Mpad > 512) variant = variant == 14 ? 15 : variant == 18 ? 19 : variant == 20 ? 21 : 1;
-  else if (tile_lists && kmax > 512) variant = 1;
-  if (variant == 16 && Mpad > 512) variant = 17;   // rotated DB (the host keeps kmax <= 512 there)
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t NQ = (size_t)qt * IA_TILE;
-  const bool pre = variant == 11 || variant == 12 || variant == 15 || variant == 17 || variant == 19 || variant == 21;
-  const bool hhf = variant >= 14 && variant <= 21;  // (z, w) per query slot + R_t per tile in LDS (16 / 17: HF too)
-  const int nthr = variant == 12 || variant == 13 ? 16 * IA_WAVE : IA_WGH;  // v12/13: 16 waves (4 per SIMD), one tile buffer
+  const bool pre = variant == 11 || variant == 15 || variant == 19 || variant == 21;
+  const bool hhf = variant >= 14 && variant <= 21;  // (z, w) per query slot + R_t per tile in LDS
+  const int nthr = IA_WGH;
   size_t lds = pre ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 +
                          (size_t)kmax * 40
-                   : ia_k3p_lds(qt, Mpad) + (variant >= 3 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
+                   : ia_k3p_lds(qt, Mpad) + (variant != 1 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
   if (hhf) lds += NQ * 8 + (size_t)kmax * 4;  // (z, w) per sorted query slot, R_t per tile
-  if (variant == 16 || variant == 17) lds += (size_t)kmax * 4;  // HF: pass masks + passing-tile list
   const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
   lds = lds > red ? lds : red;
   // nqb > 1 (presorted variants only): one launch of nqb query blocks x nwg DB chunks

@@ -63,13 +63,6 @@ void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS,
                           float4 *tbox, hipStream_t st);
 // owner-computes sharded step (exchange = 2): the owner's queries sorted into every rank's area
 void ia_launch_query_sort_xo(const float4 *qinfo, const void *qf, const XOSort &xs, hipStream_t st);
-// rotated DB + head-filtered scan (k3p_variant 16 / 17)
-void ia_launch_key_lut(const unsigned *skeys, int64_t NA, int n_tiles, int lb, int *lut, hipStream_t st);
-void ia_launch_db_build_rot(const double *db64, int64_t NA, int n_tiles, const int *pos2row, const double *mu_part,
-                            const double *rt, void *db, unsigned *Rbits, hipStream_t st);
-void ia_launch_gather_r(const LevelGeo &g, const StepDesc &sd, const Imgs &B, const JobSet &jobs, const double *mu,
-                        double *q64, double *qn2, void *qf, const double *db64, const double *basis, double ufac,
-                        const RotArgs &ra, float4 *qinfo, const Imgs &A, hipStream_t st);
 size_t ia_k3p_lds(int qt, int Mpad);
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,

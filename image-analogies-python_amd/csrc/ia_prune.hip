@@ -328,106 +328,6 @@ __global__ void __launch_bounds__(QS_WG) k_query_sort(const float4 *__restrict__
   }
 }
 
-#ifdef IA_K3H_DIAG  // k3p_variant 16 / 17: DIAG=1 builds only
-// K5e: home-tile table of the rotated scan's query bound (k3p_variant 16 / 17, K2r).  Entry b
-// = the Morton tile where keys with top LB bits b start (lower bound in the sorted keys), so a
-// query's key locates the DB rows nearest to it in projection order with one load.
-__global__ void __launch_bounds__(PR_WG) k_key_lut(const unsigned *__restrict__ skeys, int64_t NA, int n_tiles, int lb,
-                                                   int *__restrict__ lut) {
-  const int64_t b = (int64_t)blockIdx.x * PR_WG + threadIdx.x;
-  if (b >= ((int64_t)1 << lb)) return;
-  const unsigned target = (unsigned)(b << (32 - lb));
-  int64_t lo = 0, hi = NA;  // first position with key >= target
-  while (lo < hi) {
-    const int64_t mid = (lo + hi) >> 1;
-    if (skeys[mid] < target) lo = mid + 1;
-    else hi = mid;
-  }
-  const int64_t t = lo / IA_TILE;
-  lut[b] = (int)(t < n_tiles ? t : n_tiles - 1);
-}
-
-// K1r: the rotated split-f16 DB (ia_internal.h) of a pruned 1-channel level,
-// one thread per DB position (Morton order, pos2row).  a' = the fp64 row minus the part means,
-// a'' = R a' in fp64 (R: rows = the level's principal axes by decreasing variance, read
-// transposed, rt[g * 56 + f] = R[f][g]; wave-uniform addresses, i.e. scalar loads), split
-// into f16 hi + lo as k_db_build_h.  Padding positions: zero axes, head norm 60000 (never a
-// candidate, never passes the head filter).  R = max |a''| over the rows (atomicMax) for the
-// certification bound.
-__device__ __forceinline__ void rot_split(double x, _Float16 &hi, _Float16 &lo) {
-  const float xf = (float)x;
-  const _Float16 h = (_Float16)xf;
-  hi = h;
-  lo = (_Float16)(xf - (float)h);
-}
-__global__ void __launch_bounds__(PR_WG) k_db_build_rot(const double *__restrict__ db64, int64_t NA, int n_tiles,
-                                                        const int *__restrict__ pos2row, const double *__restrict__ mu_part,
-                                                        const double *__restrict__ rt, h16x8 *__restrict__ db,
-                                                        unsigned *__restrict__ Rbits) {
-  constexpr int D = 55, DS = 56;
-  const int64_t pos = (int64_t)blockIdx.x * PR_WG + threadIdx.x;
-  const bool inr = pos < (int64_t)n_tiles * IA_TILE;
-  const int64_t row = inr ? (int64_t)pos2row[pos] : NA;
-  const bool real = row < NA;
-  double x[D];
-  const double2 *a2 = reinterpret_cast<const double2 *>(db64 + (real ? row : 0) * DS);
-#pragma unroll
-  for (int k = 0; k < DS / 2; k++) {
-    const double2 v = a2[k];
-    x[2 * k] = real ? v.x - mu_part[prune_part1(2 * k)] : 0.;
-    if (2 * k + 1 < D) x[2 * k + 1] = real ? v.y - mu_part[prune_part1(2 * k + 1)] : 0.;
-  }
-  const int64_t t = pos / IA_TILE;
-  const int j = (int)(pos % IA_TILE);
-  h16x8 *head = db, *tail = db + (int64_t)n_tiles * 2 * IA_WAVE;
-  double hn = 0., tn = 0., y[8];
-#pragma unroll
-  for (int s = 0; s < 4; s++) {
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      // the 8 columns c = 16 s + 8 h + e of this (k-step, lane half)
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        const int c = 16 * s + 8 * h + e;
-        double v = 0.;
-        if (c != IA_ROT_HNORM && c < IA_ROT_TNORM) {
-          const int f = c < IA_ROT_HNORM ? c : c - 1;
-#pragma unroll
-          for (int g = 0; g < D; g++) v = fma(rt[g * DS + f], x[g], v);
-          if (c < IA_ROT_HNORM) hn += v * v;
-          else tn += v * v;
-        }
-        y[e] = v;
-      }
-      if (s == 0 && h == 1) y[7] = real ? hn * (1.0 / IA_NORM_SCALE) : 60000.0;
-      if (s == 3 && h == 1) y[0] = real ? tn * (1.0 / IA_NORM_SCALE) : 0.;
-      h16x8 vh, vl;
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        _Float16 hi, lo;
-        rot_split(y[e], hi, lo);
-        vh[e] = hi;
-        vl[e] = lo;
-      }
-      if (inr) {
-        const int L = h * IA_TILE + j;
-        if (s == 0) {
-          head[(t * 2 + 0) * IA_WAVE + L] = vh;
-          head[(t * 2 + 1) * IA_WAVE + L] = vl;
-        } else {
-          tail[(t * 6 + 2 * (s - 1)) * IA_WAVE + L] = vh;
-          tail[(t * 6 + 2 * (s - 1) + 1) * IA_WAVE + L] = vl;
-        }
-      }
-    }
-  }
-  float R = real ? (float)(sqrt(hn + tn) * (1.0 + 1e-6)) : 0.f;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) R = fmaxf(R, __shfl_xor(R, o, 64));
-  if ((threadIdx.x & 63) == 0 && R > 0.f) atomicMax(Rbits, __float_as_uint(R));
-}
-
-#endif  // IA_K3H_DIAG
 
 // ---- host launchers ---------------------------------------------------------------------------
 void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS, int *order, float4 *sq, void *qfs,
@@ -477,14 +377,3 @@ void ia_launch_table_boxes(const int *sorted_rows, const double *proj, int64_t N
                      rnorm, tnorm);
 }
 
-#ifdef IA_K3H_DIAG
-void ia_launch_key_lut(const unsigned *skeys, int64_t NA, int n_tiles, int lb, int *lut, hipStream_t st) {
-  hipLaunchKernelGGL(k_key_lut, dim3(pr_cdiv((int64_t)1 << lb, PR_WG)), dim3(PR_WG), 0, st, skeys, NA, n_tiles, lb, lut);
-}
-
-void ia_launch_db_build_rot(const double *db64, int64_t NA, int n_tiles, const int *pos2row, const double *mu_part,
-                            const double *rt, void *db, unsigned *Rbits, hipStream_t st) {
-  hipLaunchKernelGGL(k_db_build_rot, dim3(pr_cdiv((int64_t)n_tiles * IA_TILE, PR_WG)), dim3(PR_WG), 0, st, db64, NA, n_tiles,
-                     pos2row, mu_part, rt, (h16x8 *)db, Rbits);
-}
-#endif

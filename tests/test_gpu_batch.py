@@ -76,20 +76,12 @@ def test_batched_levels_match_separate_and_reference(ctx, name, mode):
         assert stb.pruned_levels == len(jb) * (z['L'] - 1)
 
 
-@pytest.mark.parametrize('variant', [7, 14, 16])
+@pytest.mark.parametrize('variant', [7, 14, 20])
 def test_batched_512_pruned_wide_step(ctx, variant):
     """3 jobs on a 512^2 level with the pruned scan forced: 513 queries per step in one scan (the
-    separate runs sort 171 per step) - a different kernel path, the same decisions.  variant 14
-    (hi x hi block filter) and 16 (rotated DB, head filter) run their presorted forms 15 / 17 on
-    the wide steps."""
-    from ia_amd import _native, synth
-    if variant == 16:  # rotated DB + head filter (DESIGN.md §4f): DIAG=1 builds only
-        try:
-            ctx.set_option('k3p_variant', 16)
-        except _native.IAError:
-            pytest.skip('k3p_variant 16 is built with DIAG=1 only')
-        finally:
-            ctx.set_option('k3p_variant', 20)
+    separate runs sort 171 per step) - a different kernel path, the same decisions.  variants 14
+    and 20 (hi x hi block filter) run their presorted forms 15 / 21 on the wide steps."""
+    from ia_amd import synth
     job = synth.make_job(512, n_levels=3)
     ctx.set_option('prune_min_rows', 1)
     ctx.set_option('k3p_variant', variant)

@@ -23,7 +23,7 @@ def _run_debug(ctx, z, prune_all=False, variant=20):
     """prune_all: option prune_min_rows = 1, so every 1-channel level goes through the certified
     pruned scan (K2p -> K3p) instead of only DB levels of >= 2^19 rows; variant:
     the pruned-scan kernel (20: hi x hi block filter with fused corrections, the default; 14: the
-    filter followed by full chains; 16: rotated DB + head filter)."""
+    filter followed by full chains)."""
     from ia_amd import _native
     L, k = z['L'], float(z['k'])
     Bp = [x.copy() for x in z['Bp_init']]
@@ -48,9 +48,9 @@ def _run_debug(ctx, z, prune_all=False, variant=20):
 
 
 @pytest.mark.parametrize('prune_all,variant', [(False, 20), (True, 7), (True, 14), (True, 15), (True, 11), (True, 18),
-                                                (True, 19), (True, 20), (True, 21), (True, 16)],
+                                                (True, 19), (True, 20), (True, 21)],
                          ids=['default', 'pruned_v7', 'pruned', 'pruned_presorted_v15', 'pruned_presorted_v11',
-                              'pruned_v18', 'pruned_presorted_v19', 'pruned_v20', 'pruned_presorted_v21', 'pruned_v16'])
+                              'pruned_v18', 'pruned_presorted_v19', 'pruned_v20', 'pruned_presorted_v21'])
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
 def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     """Every NN pick, coherence pick and compute_distance value of the reference run.  With
@@ -60,14 +60,6 @@ def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     (k_query_sort) + the presorted scan with (15) and without (11) the hi x hi block filter -
     the kernels cfg4's 2048^2 level and every batched step wider than 512 queries run.  18 / 19:
     14 / 15 with the correction products fused onto the hi x hi accumulator."""
-    if variant == 16:  # rotated DB + head filter (DESIGN.md §4f): DIAG=1 builds only
-        from ia_amd import _native
-        try:
-            ctx.set_option('k3p_variant', 16)
-        except _native.IAError:
-            pytest.skip('k3p_variant 16 is built with DIAG=1 only')
-        finally:
-            ctx.set_option('k3p_variant', 20)
     z = load_e2e(name)
     out, Bp, st = _run_debug(ctx, z, prune_all, variant)
     ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]

@@ -40,17 +40,12 @@ def _run_levels(ctx, z, Bp, A_pyr=None, Ap_pyr=None, B_pyr=None):
     return out, st
 
 
-@pytest.fixture(params=[0, 1], ids=['rowdb', 'rowimg'])
+@pytest.fixture(params=[0], ids=['rowdb'])
 def row_source(request, ctx):
-    """exact rows of the rerank / coherence / bound from the fp64 row DB or the A-side images
-    (the latter measured slower: DIAG=1 builds only)"""
-    from ia_amd import _native
-    try:
-        ctx.set_option('row_source', request.param)
-    except _native.IAError:
-        pytest.skip('row_source %d is built with DIAG=1 only' % request.param)
+    """exact rows of the rerank / coherence / bound from the fp64 row DB (the A-image gather of
+    round 2, measured slower, is in git history)"""
+    ctx.set_option('row_source', request.param)
     yield request.param
-    ctx.set_option('row_source', 0)
 
 
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)

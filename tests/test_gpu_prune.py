@@ -10,17 +10,6 @@ import ia_amd  # noqa: F401
 pytestmark = pytest.mark.gpu
 
 
-def _diag_build(ctx):
-    """True when libia was built with DIAG=1 (every kernel version selectable)."""
-    from ia_amd import _native
-    try:
-        ctx.set_option('k3p_variant', 6)
-    except _native.IAError:
-        return False
-    ctx.set_option('k3p_variant', 20)
-    return True
-
-
 def _run(ctx, job, prune, variant=7, group=1):
     from ia_amd import _native
     ctx.set_option('prune', prune)
@@ -44,22 +33,15 @@ def _run(ctx, job, prune, variant=7, group=1):
     return Bp, S, IM, st
 
 
-@pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 16), (1024, 2, 16), (512, 1, 17), (1024, 2, 17),
-                                                      (512, 1, 7), (1024, 2, 7), (512, 1, 11), (1024, 2, 11), (512, 1, 14), (1024, 2, 14),
-                                                      (512, 1, 15), (1024, 2, 15), (512, 1, 18), (1024, 2, 18), (512, 1, 19), (1024, 2, 19),
-                                                      (512, 1, 20), (1024, 2, 20), (512, 1, 21), (1024, 2, 21),
-                                                      (512, 1, 12), (1024, 2, 12), (512, 1, 13), (1024, 2, 13),
-                                                      (512, 1, 10), (1024, 2, 9), (512, 1, 8),
-                                                      (1024, 2, 6), (1024, 2, 5), (1024, 2, 4), (1024, 2, 3),
-                                                      (1024, 2, 1), (512, 1, 0), (512, 1, 2)])
+@pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 7), (1024, 2, 7), (512, 1, 11), (1024, 2, 11), (512, 1, 14),
+                                                      (1024, 2, 14), (512, 1, 15), (1024, 2, 15), (512, 1, 18), (1024, 2, 18),
+                                                      (512, 1, 19), (1024, 2, 19), (512, 1, 20), (1024, 2, 20), (512, 1, 21),
+                                                      (1024, 2, 21)])
 def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
-    """variant = the pruned-scan kernel version (option k3p_variant; the product build holds the
-    default 7, 11 (queries presorted once per step by k_query_sort) and the fallback 1 only; DIAG=1
-    builds the rest, e.g. 12 (presorted, 16 waves with one tile buffer each: 4 waves per SIMD) and
-    13 (12 with the in-kernel sort), both measured slower): every one is exact"""
+    """variant = the pruned-scan kernel version (option k3p_variant: 7 / 11 without, 14 / 15,
+    18 / 19 and 20 (default) / 21 with the hi x hi block filter; 11 / 15 / 19 / 21 with the
+    queries presorted once per step): every one is exact"""
     from ia_amd import synth
-    if variant not in (7, 11, 14, 15, 18, 19, 20, 21) and not _diag_build(ctx):
-        pytest.skip('kernel version %d is built with DIAG=1 only' % variant)
     job = synth.make_job(size)
     Bp0, S0, IM0, st0 = _run(ctx, job, 0)
     Bp1, S1, IM1, st1 = _run(ctx, job, 1, variant)
@@ -72,16 +54,12 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     assert st1.dist_pairs < st1.dist_pairs_full
     assert st1.dist_pairs_full == st0.dist_pairs_full
     assert st1.dist_tiles <= st1.dist_tiles_full and st1.dist_tiles_full == st0.dist_tiles_full
-    if variant in (14, 15, 16, 17, 18, 19, 20, 21):  # block filters: most box-needed pairs stop after a cheap product
+    if variant in (14, 15, 18, 19, 20, 21):  # block filters: most box-needed pairs stop after a cheap product
         assert 0 < st1.dist_pairs_corrected < st1.dist_pairs
         print('filter-passing pairs %.3f of the box-needed ones' % (st1.dist_pairs_corrected / st1.dist_pairs))
     else:
         assert st1.dist_pairs_corrected == 0
-    if variant in (16, 17):  # the head filter leaves most DB tiles' full rows unread
-        assert 0 < st1.dist_tiles_rows < st1.dist_tiles
-        print('full-row tiles %.3f of the heads loaded' % (st1.dist_tiles_rows / st1.dist_tiles))
-    else:
-        assert st1.dist_tiles_rows == 0
+    assert st1.dist_tiles_rows == 0
     print('size %d: pairs left %.3f, DB tiles loaded %.3f, fallbacks %d -> %d'
           % (size, st1.dist_pairs / st1.dist_pairs_full, st1.dist_tiles / st1.dist_tiles_full, st0.fallbacks,
              st1.fallbacks))
@@ -139,10 +117,9 @@ def test_prune_option_rejects_bad_values(ctx):
         ctx.set_option('prune_group', 3)
     with pytest.raises(_native.IAError):
         ctx.set_option('k3p_variant', 22)
-    if not _diag_build(ctx):
-        for v in (6, 12, 13, 16, 17):
-            with pytest.raises(_native.IAError):
-                ctx.set_option('k3p_variant', v)
+    for v in (1, 6, 12, 13, 16, 17):   # earlier versions: in git history only
+        with pytest.raises(_native.IAError):
+            ctx.set_option('k3p_variant', v)
     with pytest.raises(_native.IAError):
         ctx.set_option('prune_min_rows', 0)
 

@@ -1,6 +1,8 @@
-"""Run the cfg3 synthetic job on the GPU and save the synthesised state of the finest levels
-(B' levels, s, im) for offline analysis (tools/prune_study.py).  Usage:
-  python3 tools/dump_state.py <out.npz> [size] [levels...]"""
+"""Run a synthetic job on the GPU (default options: the product kernels) and save the
+synthesised state of the given levels (B' levels, s, im) for offline teacher forcing
+(tools/teacher_force.py) and analysis (tools/prune_study.py).  Usage:
+  python3 tools/dump_state.py <out.npz> [config|size] [levels...]
+config: a name of ia_amd.synth.CONFIGS (cfg3, cfg4, ...) or an integer size (square A = B)."""
 import os
 import sys
 
@@ -11,22 +13,26 @@ import ia_amd  # noqa: F401,E402
 from ia_amd import _native, synth  # noqa: E402
 
 out = sys.argv[1]
-size = int(sys.argv[2]) if len(sys.argv) > 2 else 1024
-job = synth.make_job(size)
+cfg = sys.argv[2] if len(sys.argv) > 2 else '1024'
+kw = dict(size=int(cfg)) if cfg.isdigit() else synth.CONFIGS[cfg][0]
+job = synth.make_job(**kw)
 levels = [int(x) for x in sys.argv[3:]] or [job.L - 2, job.L - 1]
 ctx = _native.Context(0)
 Bp = [x.copy() for x in job.Bp_init]
 S, IM = {}, {}
+st = _native.Stats()
 for level in range(1, job.L):
     S[level], IM[level] = ctx.synthesize_level(
         job.A_pyr[level], job.A_pyr[level - 1], [p[level] for p in job.Ap_pyr_list],
         [p[level - 1] for p in job.Ap_pyr_list], job.B_pyr[level], job.B_pyr[level - 1], Bp[level - 1], Bp[level],
-        job.weights, job.kappa_factor(level))
+        job.weights, job.kappa_factor(level), st)
 d = {}
 for l in levels:
     d['Bp_%d' % l] = Bp[l]
     d['Bp_%d' % (l - 1)] = Bp[l - 1]
     d['s_%d' % l] = S[l]
     d['im_%d' % l] = IM[l]
-np.savez_compressed(out, size=size, levels=np.array(levels), **d)
-print('saved', out, os.path.getsize(out))
+np.savez_compressed(out, size=int(kw['size']) if np.isscalar(kw['size']) else 0, config=cfg, levels=np.array(levels), **d)
+print('saved', out, os.path.getsize(out), 'stats', {k: v for k, v in st.as_dict().items()
+                                                      if k in ('pixels', 'fallbacks', 'reranked', 'bound_violations',
+                                                               'kappa_ambiguous', 'pruned_levels')})

@@ -8,7 +8,10 @@ re-decides sampled pixels on the GPU's own state: B' final for raster-earlier pi
 for the rest, s / im final.  Every decision must match except documented near-ties (NN relative
 gap < 1e-5, kappa relative margin < 1e-12).  Test infrastructure: uses the oracle.
 
-  python tools/teacher_force.py <state.npz> <out.json> [total_pixels] [workers]
+  python tools/teacher_force.py <state.npz> <out.json> [total_pixels] [workers] [finest_min]
+
+finest_min: at least this many pixels on the finest dumped level.  States written by
+tools/dump_state.py with a config name (cfg3, cfg4) rebuild that config's job.
 """
 import json
 import os
@@ -24,10 +27,14 @@ sys.path.insert(0, ROOT)
 _G = {}
 
 
-def _init(path, size):
+def _job(cfg):
     import ia_amd  # noqa: F401
     from ia_amd import synth
-    _G['job'] = synth.make_job(size)
+    return synth.make_job(**(dict(size=int(cfg)) if cfg.isdigit() else synth.CONFIGS[cfg][0]))
+
+
+def _init(path, cfg):
+    _G['job'] = _job(cfg)
     _G['z'] = np.load(path)
     _G['db'] = {}
 
@@ -58,26 +65,25 @@ def main():
     path, out_json = sys.argv[1], sys.argv[2]
     total = int(sys.argv[3]) if len(sys.argv) > 3 else 5000
     workers = int(sys.argv[4]) if len(sys.argv) > 4 else 7
+    finest_min = int(sys.argv[5]) if len(sys.argv) > 5 else 0
     z = np.load(path)
-    size = int(z['size'])
+    cfg = str(z['config']) if 'config' in z.files else str(int(z['size']))
     levels = [int(l) for l in z['levels']]
-    import ia_amd  # noqa: F401
-    from ia_amd import synth
-    job = synth.make_job(size)
+    job = _job(cfg)
     # pixels per level: proportional to sqrt(N) (every level gets a share; the 1024^2 level most)
     npx = {l: int(np.prod(job.B_pyr[l].shape[:2])) for l in levels}
     wts = {l: np.sqrt(npx[l]) for l in levels}
     tot_w = sum(wts.values())
     tasks = []
     for l in levels:
-        n = min(npx[l], max(20, int(round(total * wts[l] / tot_w))))
+        n = min(npx[l], max(20, int(round(total * wts[l] / tot_w)), finest_min if l == max(levels) else 0))
         h, w = job.B_pyr[l].shape[:2]
         rs = np.random.RandomState(1000 + l)
         pix = np.unique(np.concatenate([rs.choice(npx[l], n, replace=False), [0, 1, w - 1, w, npx[l] - 1]]))
         for chunk in np.array_split(pix, max(1, len(pix) // 25)):
             tasks.append((l, chunk))
     t0 = time.time()
-    with Pool(workers, initializer=_init, initargs=(path, size)) as pool:
+    with Pool(workers, initializer=_init, initargs=(path, cfg)) as pool:
         res = [r for part in pool.imap_unordered(_decide, tasks) for r in part]
     per_level = {}
     mism = []
@@ -90,7 +96,7 @@ def main():
             d['mismatches'] += 1
             mism.append({'level': level, 'pixel': qi, 'nn_rel_gap': gap, 'kappa_rel_margin': kgap,
                          'documented_near_tie': gap < 1e-5 or kgap < 1e-12})
-    summary = {'state': os.path.basename(path), 'job': 'synth.make_job(%d) (cfg3)' % size,
+    summary = {'state': os.path.basename(path), 'job': 'synth.make_job(%s)' % cfg,
                'pixels_checked': len(res), 'mismatches': len(mism),
                'undocumented_mismatches': sum(1 for m in mism if not m['documented_near_tie']),
                'per_level': {str(k): per_level[k] for k in sorted(per_level)}, 'mismatch_list': mism,
