@@ -272,8 +272,8 @@ def make_context(args, local):
         cx.set_option('fuse_gather', args.fuse_gather)
     if args.fuse_unpruned:
         cx.set_option('fuse_unpruned', 1)
-    if args.fuse_sort != 1:
-        cx.set_option('fuse_sort', args.fuse_sort)
+    if args.fuse_sort:
+        cx.set_option('fuse_sort', 1)
     if args.shard_unpruned:
         cx.set_option('shard_unpruned', 1)
     if args.shard_emulate > 1:
@@ -379,9 +379,10 @@ def main():
     ap.add_argument('--fuse-gather', type=int, default=1, choices=[0, 1],
                     help='1 (default): on pruned one-job levels the merge of step t and the gather of step t + 1 run '
                          'as one launch (ia_kernels.hip k_merge_gather); 0: separate launches')
-    ap.add_argument('--fuse-sort', type=int, default=1, choices=[0, 1],
-                    help='1 (default): the fused gathers of step t + 1 also sort its queries for the presorted scan '
-                         '(include/ia.h option fuse_sort); 0: the scan sorts them in every workgroup (or K2s)')
+    ap.add_argument('--fuse-sort', type=int, default=0, choices=[0, 1],
+                    help='1: the fused gathers of step t + 1 also sort its queries for the presorted scan (include/ia.h '
+                         'option fuse_sort; measured slower: DESIGN.md §6d); 0 (default): the scan sorts them in every '
+                         'workgroup (or K2s on wide steps)')
     ap.add_argument('--owner-pipeline', type=int, default=0, choices=[0, 1],
                     help='1: pipelined levels in the owner-computes shard mode too (N > 1)')
     ap.add_argument('--fuse-unpruned', type=int, default=0, choices=[0, 1],
@@ -797,6 +798,9 @@ def main():
         if st_all['merge_stamp_launches'] > 0:
             roofline['merge_us_per_launch_timed'] = st_all['merge_stamp_ms'] * 1e3 / st_all['merge_stamp_launches']
             roofline['merge_launches_timed'] = st_all['merge_stamp_launches']
+        if st_all['stamp_gaps'] > 0:
+            roofline['chain_gap_us_timed'] = st_all['stamp_gap_ms'] * 1e3 / st_all['stamp_gaps']
+            roofline['chain_window_ms_timed'] = st_all['stamp_window_ms'] / args.steps
         roofline['timing_timed'] = ('frac_timed / *_timed: every pruned-scan (and fused merge) launch of the %d timed '
                                     'steps, device time = max(workgroup end) - min(workgroup start) from s_memrealtime '
                                     'stamps the kernels write (include/ia.h option "stamps")' % args.steps)

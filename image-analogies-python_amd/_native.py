@@ -52,7 +52,8 @@ class Stats(ctypes.Structure):
                 ('merge_launches_timed', ctypes.c_int64), ('build_rows', ctypes.c_int64),
                 ('k3p_stamp_ms', ctypes.c_double), ('k3p_stamp_launches', ctypes.c_int64),
                 ('k3p_bytes_all', ctypes.c_double), ('merge_stamp_ms', ctypes.c_double),
-                ('merge_stamp_launches', ctypes.c_int64)]
+                ('merge_stamp_launches', ctypes.c_int64), ('stamp_gap_ms', ctypes.c_double),
+                ('stamp_gaps', ctypes.c_int64), ('stamp_window_ms', ctypes.c_double)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -2177,10 +2177,10 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd
 // per-level statistics: sum the per-pixel stats words.  Grid-stride loop over up to 256
 // workgroups; each workgroup reduces in LDS and adds its five integer sums with one u64
 // atomicAdd per counter (integer sums are order-free; counters are zeroed per level)
-// option "stamps": launch i's device time = max(end) - min(start) over the `stride` workgroup
-// slots (unwritten slots are zero), in s_memrealtime ticks; one wave per launch
+// option "stamps": launch i's first workgroup start and last workgroup end over its `stride`
+// workgroup slots (unwritten slots are zero), in s_memrealtime ticks; one wave per launch
 __global__ void __launch_bounds__(IA_WAVE) k_stamp_durations(const unsigned long long *__restrict__ stamps, int stride,
-                                                            unsigned *__restrict__ dur) {
+                                                            unsigned long long *__restrict__ span) {
   const int i = blockIdx.x, lane = threadIdx.x;
   unsigned long long lo = ~0ull, hi = 0ull;
   for (int j = lane; j < stride; j += IA_WAVE) {
@@ -2196,10 +2196,13 @@ __global__ void __launch_bounds__(IA_WAVE) k_stamp_durations(const unsigned long
     lo = l2 < lo ? l2 : lo;
     hi = h2 > hi ? h2 : hi;
   }
-  if (lane == 0) dur[i] = hi >= lo && hi ? (unsigned)(hi - lo) : 0u;
+  if (lane == 0) {
+    span[2 * i] = hi >= lo && hi ? lo : 0ull;
+    span[2 * i + 1] = hi >= lo && hi ? hi : 0ull;
+  }
 }
-void ia_launch_stamp_durations(const unsigned long long *stamps, int n, int stride, unsigned *dur, hipStream_t st) {
-  if (n > 0) hipLaunchKernelGGL(k_stamp_durations, dim3(n), dim3(IA_WAVE), 0, st, stamps, stride, dur);
+void ia_launch_stamp_durations(const unsigned long long *stamps, int n, int stride, unsigned long long *span, hipStream_t st) {
+  if (n > 0) hipLaunchKernelGGL(k_stamp_durations, dim3(n), dim3(IA_WAVE), 0, st, stamps, stride, span);
 }
 
 __global__ void __launch_bounds__(IA_WG) k_reduce_stats(const unsigned *__restrict__ pstat, int64_t n,

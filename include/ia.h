@@ -100,6 +100,10 @@ typedef struct {
   double k3p_bytes_all;     /* algorithmic bytes of those launches (tiles loaded, boxes, queries, records) */
   double merge_stamp_ms;    /* the merges (k_merge_gather / fused k_merge_level) of the same levels */
   int64_t merge_stamp_launches;
+  double stamp_gap_ms;      /* one-job levels: idle time between the chain's kernels (scan end -> merge
+                             * start, merge end -> next scan start), summed */
+  int64_t stamp_gaps;
+  double stamp_window_ms;   /* those levels' first scan start -> last kernel end */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
@@ -176,6 +180,9 @@ int ia_version(void);
  * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge)
  * / 2 (owner computes: each rank brings its own job, every rank scans its shard for all of them,
  * queries and scan records exchanged by peer writes; emulated: one job per shard).
+ * "fuse_sort" = 0 (default) / 1: the fused gathers of step t + 1 also rank its queries' sort keys
+ * across the launch and write the presorted scan inputs (the scan then skips its per-workgroup
+ * sort); exact either way, measured slower.
  * "stamps" = 1: every pruned-scan and fused-merge launch of a pruned level stamps its
  * workgroups' first / last s_memrealtime tick; ia_stats.k3p_stamp_ms / merge_stamp_ms sum the
  * per-launch device times (bench.py roofline.frac_timed: the timed, pipelined steps' own kernels).

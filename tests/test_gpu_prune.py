@@ -70,18 +70,23 @@ def test_fused_gather_equals_separate_launches(ctx, variant):
     """option fuse_gather (ia_kernels.hip k_merge_gather): the merge of step t and the gather of
     step t + 1 in one launch, the step's results handed row to row; with K3 timing every third
     step (time_dist 3: sampled steps run the separate launches) the fused and separate forms
-    alternate within a level.  All three runs bit-identical (21: presorted wide-step scan)."""
+    alternate within a level; option fuse_sort moves the query sort into the fused gathers.  All
+    runs bit-identical (21: presorted wide-step scan)."""
     from ia_amd import synth
     job = synth.make_job(1024)
     runs = []
-    for fuse, stride in ((0, 0), (1, 0), (1, 3)):
+    # (fuse_gather, time_dist, fuse_sort): fuse_sort = the fused gathers also sort the next step
+    # for the presorted scan (k_merge_gather sorted_publish), alone and mixed with sampled steps
+    for fuse, stride, fsort in ((0, 0, 0), (1, 0, 0), (1, 3, 0), (1, 0, 1), (1, 3, 1)):
         ctx.set_option('fuse_gather', fuse)
         ctx.set_option('time_dist', stride)
+        ctx.set_option('fuse_sort', fsort)
         try:
             runs.append(_run(ctx, job, 1, variant))
         finally:
             ctx.set_option('fuse_gather', 1)
             ctx.set_option('time_dist', 0)
+            ctx.set_option('fuse_sort', 0)
     for Bp, S, IM, st in runs[1:]:
         for level in range(1, job.L):
             assert np.array_equal(S[level], runs[0][1][level]), level
@@ -162,3 +167,31 @@ def test_pruned_scan_over_512_tiles_per_workgroup(ctx, variant):
     assert st1.bound_violations == 0 and st0.bound_violations == 0
     assert np.array_equal(s0, s1) and np.array_equal(im0, im1) and np.array_equal(Bp0, Bp1)
     assert st1.dist_tiles < st1.dist_tiles_full
+
+
+@pytest.mark.parametrize('name', ['g64', 'ties128', 'k25', 'g256'])
+def test_fused_sort_matches_reference(ctx, name):
+    """option fuse_sort with every level pruned: each fused merge + gather ranks the next step's
+    keys across its waves and writes the presorted scan inputs (ia_kernels.hip sorted_publish);
+    s, im and B' of every level equal the reference run's."""
+    from ia_amd import _native
+    from golden_util import BIG_CASES, E2E_CASES, load_e2e
+    if name not in E2E_CASES + BIG_CASES:
+        pytest.skip('fixture absent')
+    z = load_e2e(name)
+    L, k = z['L'], float(z['k'])
+    Bp = [x.copy() for x in z['Bp_init']]
+    st = _native.Stats()
+    ctx.set_option('prune_min_rows', 1)
+    ctx.set_option('fuse_sort', 1)
+    try:
+        for level in range(1, L):
+            s, im = ctx.synthesize_level(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
+                                         [p[level - 1] for p in z['Ap_pyr']], z['B_pyr'][level], z['B_pyr'][level - 1],
+                                         Bp[level - 1], Bp[level], z['weights'], 1 + 2.0 ** (level - L) * k, st)
+            assert np.array_equal(s, z['s'][level]) and np.array_equal(im, z['im'][level]), level
+            assert np.array_equal(Bp[level], z['Bp_final'][level]), level
+    finally:
+        ctx.set_option('prune_min_rows', 524288)
+        ctx.set_option('fuse_sort', 0)
+    assert st.bound_violations == 0 and st.kappa_ambiguous == 0 and st.pruned_levels == L - 1
