@@ -274,6 +274,8 @@ def make_context(args, local):
         cx.set_option('fuse_unpruned', 1)
     if args.fuse_sort:
         cx.set_option('fuse_sort', 1)
+    if not args.prefetch_next:
+        cx.set_option('prefetch_next', 0)
     if args.shard_unpruned:
         cx.set_option('shard_unpruned', 1)
     if args.shard_emulate > 1:
@@ -383,6 +385,9 @@ def main():
                     help='1: the fused gathers of step t + 1 also sort its queries for the presorted scan (include/ia.h '
                          'option fuse_sort; measured slower: DESIGN.md §6d); 0 (default): the scan sorts them in every '
                          'workgroup (or K2s on wide steps)')
+    ap.add_argument('--prefetch-next', type=int, default=1, choices=[0, 1],
+                    help='1 (default): fused merge + gather waves load the next query\'s step-independent inputs during '
+                         'the merge (include/ia.h option prefetch_next)')
     ap.add_argument('--owner-pipeline', type=int, default=0, choices=[0, 1],
                     help='1: pipelined levels in the owner-computes shard mode too (N > 1)')
     ap.add_argument('--fuse-unpruned', type=int, default=0, choices=[0, 1],

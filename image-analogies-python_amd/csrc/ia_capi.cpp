@@ -115,6 +115,7 @@ struct ia_ctx {
   int fuse_unpruned = 0;         // option "fuse_unpruned": 1 = also on unpruned levels (K4 + K2h)
   HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
   int hand_rows = 0;
+  int prefetch_next = 1;         // option "prefetch_next" (NextStep::prefetch)
   int fuse_sort = 0;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
                                  // off by default: the scan gets 0.9 us faster, the merge 2.8 us slower
   unsigned long long *kslot = nullptr;  // their per-query key slots (uncached)
@@ -413,6 +414,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "fuse_gather")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_gather must be 0 or 1");
     c->fuse_gather = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "prefetch_next")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: prefetch_next must be 0 or 1");
+    c->prefetch_next = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "fuse_sort")) {
@@ -1347,6 +1353,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         nx.seq = ++c->hseq;
         nx.err = c->xerr.as<unsigned>();
         nx.timeout_ticks = 2000000000LL;
+        nx.prefetch = c->prefetch_next;
         if (ink_n) {  // the next step's queries go straight to every rank's area (else its K2s sorts them)
           nx.xp.W = sharded ? Wsh : 1;
           for (int p = 0; p < nx.xp.W; p++) nx.xp.area[p] = area_s(p, seq + 1);
@@ -1494,6 +1501,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       nx.seq = ++c->hseq;
       nx.err = c->xerr.as<unsigned>();
       nx.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
+      nx.prefetch = c->prefetch_next;
       // the gathers also sort step t + 1 into k_query_sort's outputs when every wave of the launch
       // can be resident at once (each gather waits for all of the step's keys): k_merge_gather
       // holds one wave per SIMD (264 VGPRs), 1,024 on the chip; 768 leaves room for the kernels of

@@ -349,6 +349,7 @@ struct NextStep {
   // at slot x (sinfo / sfrag / sorder: k_query_sort's outputs); the scan then skips its
   // per-workgroup sort (kslot = nullptr: off)
   unsigned long long *kslot;
+  int prefetch;              // option "prefetch_next": the gathers' step-independent inputs load during the merge
   int *sorder;
   float4 *sinfo;
   void *sfrag;

@@ -1395,6 +1395,34 @@ __device__ __forceinline__ void gather_p_pad(int m, int lane, _Float16 *qf, floa
   }
 }
 
+// A fused gather's inputs that do not depend on the launch's own merges, loaded during the merge
+// (k_merge_gather): lane f < 55 the query's feature f as K2p reads it (the B' part stale exactly
+// at the two step-t pixels of QHand, which the gather substitutes), lane k < 15 the causal
+// neighbour k's source pixel and A' image (stale at the same two pixels)
+struct QPre {
+  bool on = false;
+  double v = 0.;
+  int sr = 0, sc = 0, si = 0;
+};
+__device__ __forceinline__ QPre qpre_load(const LevelGeo &g, const StepDesc &sn, const Imgs &B, const JobPtrs &jp, int m, int lane) {
+  constexpr int D = 55;
+  QPre p;
+  p.on = true;
+  const QPix px = ia_qpix(sn, g.bw, m);
+  const int r = px.r, c = px.c;
+  if (lane < D) p.v = feat<1>(B, lane, r, c, 0);
+  if (px.qi > 0 && lane < 15) {
+    const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
+    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < px.qi) {
+      const int nb = nr * g.bw + nc;
+      p.sr = jp.s[2 * nb];
+      p.sc = jp.s[2 * nb + 1];
+      p.si = jp.im[nb];
+    }
+  }
+  return p;
+}
+
 // K2p's work for one query m of step sd (one wave): q64, qn2, fragments, pruning record (also
 // returned, uniform, for the owner-computes publish); xh0 / xh1 (optional) receive the query's
 // hi / lo columns
@@ -1404,7 +1432,8 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
                                                double *__restrict__ qn2, _Float16 *__restrict__ qf,
                                                const double *__restrict__ db64, const double *__restrict__ basis, double ufac,
                                                float4 *__restrict__ qinfo, const Imgs &A, double *qsh, _Float16 *xh0,
-                                               _Float16 *xh1, const QHand &h, float4 &o0, float4 &o1, float4 &o2) {
+                                               _Float16 *xh1, const QHand &h, float4 &o0, float4 &o1, float4 &o2,
+                                               const QPre &pf = QPre{}) {
   constexpr int D = 55, KD = 16 * KS;
   static_assert(KD <= IA_WAVE, "one feature per lane");
   const QPix px = ia_qpix(sd, g.bw, m);
@@ -1421,6 +1450,8 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
         sr = h.s0r; sc = h.s0c; si = h.i0;
       } else if (FUSE && nr == h.r1 && nc == h.c1) {
         sr = h.s1r; sc = h.s1c; si = h.i1;
+      } else if (pf.on) {
+        sr = pf.sr; sc = pf.sc; si = pf.si;
       } else {
         sr = s[2 * nb]; sc = s[2 * nb + 1]; si = im[nb];
       }
@@ -1434,7 +1465,16 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
   if (lane < KD) {
     const int f = lane;
     if (f < D) {
-      const double v = feat_q1<FUSE>(B, f, r, c, h);
+      double v;
+      if (pf.on) {  // prefetched; the B' part substituted at the two step-t pixels
+        v = pf.v;
+        if (FUSE && f >= 43) {
+          const int k = f - 43, y = ia_reflect(r + k / 5 - 2, B.h), x = ia_reflect(c + k % 5 - 2, B.w);
+          v = (y == h.r0 && x == h.c0) ? h.v0 : (y == h.r1 && x == h.c1) ? h.v1 : v;
+        }
+      } else {
+        v = feat_q1<FUSE>(B, f, r, c, h);
+      }
       q64[(int64_t)m * D + f] = v;
       qsh[f] = v;
       const double qc = v - mu_part[feat_part<1>(f)];
@@ -1529,11 +1569,14 @@ struct MergeOut {  // one pixel's result: B' value (first channel), source pixel
 // the weighted one (kappa rule) and its row's A' value (the B' write) from the same round.
 // Candidates beyond the 49 rerank lanes (rare) are evaluated by the lanes that listed them.
 // Wave reductions use DPP / permlane exchanges (no LDS round trips).
-template <int CH, bool IMG, int RPL>
+struct NoPre {
+  __device__ __forceinline__ void operator()() const {}
+};
+template <int CH, bool IMG, int RPL, class Pre = NoPre>
 __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &a,
                                             int m, const JobPtrs &jp, const QPix &px,
                                             double *qs, double *ws, int *cand_row, float *cand_v,
-                                            MergeOut *out = nullptr) {
+                                            MergeOut *out = nullptr, Pre pre = Pre{}) {
 #if IA_PROBE & 8
   unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1651,6 +1694,9 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   int my_row = lane < NCOH ? crow : (lane - NCOH < n_cand ? cand_row[lane - NCOH] : -1);
   const float my_v = lane >= NCOH && my_row >= 0 ? cand_v[lane - NCOH] : FLT_MAX;
   IA_STAMP(2);
+  // (k_merge_gather: the next query's step-independent inputs are loaded here, in flight together
+  // with round 2's rows instead of after them)
+  pre();
 
   // ---- round 2: one fp64-DB row + its A' value per lane
   double unw = DBL_MAX, wsq = 0.;
@@ -1995,12 +2041,18 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
   QHand h;
   int mn = -1;   // this wave's query of step t + 1
   int job = 0;
+  QPre pf;       // its step-independent inputs, prefetched during the merge (pruned levels)
   if (w < JM) {
     const QPix px = ia_qpix(sd, g.bw, w);
     job = px.job;
     const JobPtrs jp = jobs.get(job);
     MergeOut o;
-    merge_fused<1, false, RPL>(g, sd, A, ma, w, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv], &o);
+    if (px.c + 1 < g.bw) mn = job * nx.sn.M + (px.r - nx.sn.r0);
+    const Imgs Bj = JS::single ? B : job_imgs(B, jp);
+    auto pre = [&]() {
+      if (PR && nx.prefetch && mn >= 0) pf = qpre_load(g, nx.sn, Bj, jp, mn, lane);
+    };
+    merge_fused<1, false, RPL>(g, sd, A, ma, w, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv], &o, pre);
     if (px.r + 1 < g.bh && px.c >= 2) {  // row r + 1 gathers (r + 1, c - 2) at step t + 1
       HandSlot *hs = nx.hand + (int64_t)job * g.bh + px.r;
       if (lane == 0) {
@@ -2018,7 +2070,6 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
     h.s0r = o.pr;
     h.s0c = o.pc;
     h.i0 = o.img;
-    if (px.c + 1 < g.bw) mn = job * nx.sn.M + (px.r - nx.sn.r0);
   } else if (w < JM + J) {
     job = w - JM;
     if (nx.sn.t - 3 * (nx.sn.r0 + nx.sn.M - 1) == 0) mn = job * nx.sn.M + nx.sn.M - 1;  // a row enters at column 0
@@ -2067,7 +2118,7 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
   if constexpr (PR) {
     const bool pub = (XO && nx.xp.W) || (!XO && nx.kslot);
     gather_p_query<KS, false, true>(g, nx.sn, B, jp, mn, lane, nx.mu, nx.q64, nx.qn2, qf, ma.db64, nx.basis, nx.ufac,
-                                    nx.qinfo, A, qsh[wv], pub ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2);
+                                    nx.qinfo, A, qsh[wv], pub ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2, pf);
     if (XO && nx.xp.W) xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
     if (!XO && nx.kslot) sorted_publish<KS>(nx, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
   } else {

@@ -180,6 +180,9 @@ int ia_version(void);
  * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge)
  * / 2 (owner computes: each rank brings its own job, every rank scans its shard for all of them,
  * queries and scan records exchanged by peer writes; emulated: one job per shard).
+ * "prefetch_next" = 1 (default) / 0: a fused merge + gather wave loads its next query's inputs
+ * that do not depend on the launch's own merges (features, causal neighbours' sources) while
+ * its merge's DB rows load.
  * "fuse_sort" = 0 (default) / 1: the fused gathers of step t + 1 also rank its queries' sort keys
  * across the launch and write the presorted scan inputs (the scan then skips its per-workgroup
  * sort); exact either way, measured slower.

@@ -26,12 +26,16 @@ for level in range(1, job.L):
         job.A_pyr[level], job.A_pyr[level - 1], [p[level] for p in job.Ap_pyr_list],
         [p[level - 1] for p in job.Ap_pyr_list], job.B_pyr[level], job.B_pyr[level - 1], Bp[level - 1], Bp[level],
         job.weights, job.kappa_factor(level), st)
+# B' of a synthesised level is A' at its sources (B'[p] = A'_im[p][s[p]], the merge's writeback),
+# so only s (int16) and im (uint8) travel; tools/teacher_force.py rebuilds B' from the job's A'
+# pyramid and checks it against the sha1 of the GPU's B' bytes stored here
+import hashlib  # noqa: E402
 d = {}
-for l in levels:
-    d['Bp_%d' % l] = Bp[l]
-    d['Bp_%d' % (l - 1)] = Bp[l - 1]
-    d['s_%d' % l] = S[l]
-    d['im_%d' % l] = IM[l]
+for l in sorted(set(levels) | {l - 1 for l in levels if l > 1}):
+    assert S[l].max() < 32768 and IM[l].max() < 256
+    d['s_%d' % l] = S[l].astype(np.int16)
+    d['im_%d' % l] = IM[l].astype(np.uint8)
+    d['bpsha_%d' % l] = np.frombuffer(hashlib.sha1(np.ascontiguousarray(Bp[l]).tobytes()).digest(), dtype=np.uint8)
 np.savez_compressed(out, size=int(kw['size']) if np.isscalar(kw['size']) else 0, config=cfg, levels=np.array(levels), **d)
 print('saved', out, os.path.getsize(out), 'stats', {k: v for k, v in st.as_dict().items()
                                                       if k in ('pixels', 'fallbacks', 'reranked', 'bound_violations',

@@ -33,9 +33,26 @@ def _job(cfg):
     return synth.make_job(**(dict(size=int(cfg)) if cfg.isdigit() else synth.CONFIGS[cfg][0]))
 
 
+def rebuild_bp(job, z, level):
+    """B' of a synthesised level from its source maps: B'[p] = A'_im[p][s[p]] (the merge's
+    writeback), checked against the sha1 of the GPU's own B' bytes (tools/dump_state.py)"""
+    import hashlib
+    s = z['s_%d' % level].astype(np.int64)
+    im = z['im_%d' % level].astype(np.int64)
+    Ap = np.stack([p[level] for p in job.Ap_pyr_list])
+    bp = Ap[im, s[:, 0], s[:, 1]].reshape(job.B_pyr[level].shape[:2])
+    if hashlib.sha1(np.ascontiguousarray(bp).tobytes()).digest() != z['bpsha_%d' % level].tobytes():
+        raise SystemExit("level %d: B' rebuilt from s / im differs from the GPU's B'" % level)
+    return bp
+
+
 def _init(path, cfg):
     _G['job'] = _job(cfg)
-    _G['z'] = np.load(path)
+    z = np.load(path)
+    _G['z'] = {k: z[k] for k in z.files}
+    for l in sorted({int(k.split('_')[1]) for k in z.files if k.startswith('s_')}):
+        if 'Bp_%d' % l not in _G['z']:
+            _G['z']['Bp_%d' % l] = rebuild_bp(_G['job'], z, l)
     _G['db'] = {}
 
 
