@@ -368,12 +368,13 @@ def main():
                     help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
-    ap.add_argument('--k3p-variant', type=int, default=20, choices=[7, 11, 14, 15, 18, 19, 20, 21],
+    ap.add_argument('--k3p-variant', type=int, default=20, choices=[7, 11, 14, 15, 18, 19, 20, 21, 22, 23],
                     help='pruned-scan kernel version (ia_k3h.hip k3h_prune3, DESIGN.md §4b): 7 = need tests interleaved '
                          'with the contraction, bitonic in-kernel query sort, reverse walks on alternate steps; 11 = 7 on '
                          'queries presorted once per step; 14 / 15 = 7 / 11 with the hi x hi block filter; 18 / 19 = 14 / '
                          '15 with the correction products fused onto the hi x hi accumulator (single chains); 20 '
-                         '(default) / 21 = the same on query-tile pairs (two chains)')
+                         '(default) / 21 = the same on query-tile pairs (two chains); 22 / 23 = 14 / 15 streaming only the '
+                         'hi halves of the DB tiles, the whole tile loaded for the filter-passing ones (chains one tile later)')
     ap.add_argument('--pipeline', type=int, default=1, choices=[0, 1],
                     help='1 (default; one-job configs and replicas): consecutive levels overlap (two libia '
                          'contexts, each level\'s steps waiting only for the steps of the previous level they read; '
@@ -817,6 +818,7 @@ def main():
         # the hi x hi block filter: every box-needed pair runs the hi x hi product; only this share
         # also runs the two correction products and the top-2 epilogue (mfma_* above count 3)
         roofline['pairs_corrected_frac'] = st['dist_pairs_corrected'] / max(st['dist_pairs'], 1.)
+        roofline['tiles_passing_frac'] = st['dist_tiles_rows'] / max(st['dist_tiles'], 1.)
     out = {'metric': METRIC, 'value': value, 'unit': "B' px/s", 'n_gpus': world, 'steps': args.steps,
            'warmup': args.warmup, 'ms_per_step': elapsed * 1e3 / args.steps, 'higher_is_better': True,
            'scaling': 'strong' if (sw is not None or (args.mode == 'shard' and jobs < max(world, args.shard_emulate)))

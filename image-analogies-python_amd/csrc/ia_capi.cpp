@@ -366,8 +366,8 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
                                             // queries, presorted 21 above); 14 / 15: the filter, then full
                                             // chains; 18 / 19: fused, single chains; 7 / 11: v7 (DESIGN.md
                                             // §4b); the other versions of §4b / §4f are in git history
-    if (value != 7 && value != 11 && value != 14 && value != 15 && value != 18 && value != 19 && value != 20 && value != 21)
-      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14, 15 or 18..21");
+    if (value != 7 && value != 11 && value != 14 && value != 15 && (value < 18 || value > 23))
+      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14, 15 or 18..23");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -1273,8 +1273,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         const char *dbp = (const char *)c->db.p + (size_t)(x.t0 - g.tile0) * tile_bytes;
         const int kv = c->k3p_variant;
         // the in-kernel-sort variant (ink: 20 / 14 / 18 / 7) or its presorted form
-        const int k3x = ink ? ((kv == 14 || kv == 15) ? 14 : (kv == 18 || kv == 19) ? 18 : (kv == 7 || kv == 11) ? 7 : 20)
-                            : ((kv == 14 || kv == 15) ? 15 : (kv == 18 || kv == 19) ? 19 : (kv == 7 || kv == 11) ? 11 : 21);
+        const int k3x = ink ? ((kv == 14 || kv == 15) ? 14 : (kv == 18 || kv == 19) ? 18 : (kv == 7 || kv == 11) ? 7
+                               : (kv == 22 || kv == 23) ? 22 : 20)
+                            : ((kv == 14 || kv == 15) ? 15 : (kv == 18 || kv == 19) ? 19 : (kv == 7 || kv == 11) ? 11
+                               : (kv == 22 || kv == 23) ? 23 : 21);
         ia_launch_k3p(ink ? QTs : xo_QTx, dbp, loc + XOLayout::FRAG, reinterpret_cast<const float4 *>(loc + XOLayout::INFO),
                       mas[i].boxes, mas[i].pos2row, n, 0, sd.M, ink ? Mpj : Mrec, nch, nullptr, nullptr,
                       c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
@@ -1398,11 +1400,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     const bool wide = sd.Mpad > 512 || (c->k3p_blocks && sd.Mpad > qtmax * IA_TILE);
     // sorted by the previous launch's gathers: the presorted form of the variant, no K2s
     const bool gsorted = fsort && gathered == t && gsort;
-    const int k3v = (kv == 11 || kv == 15 || kv == 19 || kv == 21) ? kv
+    const int k3v = (kv == 11 || kv == 15 || kv == 19 || kv == 21 || kv == 23) ? kv
                     : (prune && (wide || gsorted)
-                           ? (kv == 14 ? 15 : kv == 18 ? 19 : kv == 20 ? 21 : 11)
+                           ? (kv == 14 ? 15 : kv == 18 ? 19 : kv == 20 ? 21 : kv == 22 ? 23 : 11)
                            : kv);
-    const bool presorted = k3v == 11 || k3v == 15 || k3v == 19 || k3v == 21;
+    const bool presorted = k3v == 11 || k3v == 15 || k3v == 19 || k3v == 21 || k3v == 23;
     const float4 *tboxp = gsorted ? nullptr : c->qs_tbox.as<float4>();  // nullptr: boxes from the slice
     if (prune && presorted && !gsorted)
       ia_launch_query_sort(qinfot, c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
@@ -1587,7 +1589,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                                 " did not arrive within 20 s (peer-write exchange)");
   }
   if (stats) {
-    unsigned long long ctr[5], prs[4], pfull = 0;
+    unsigned long long ctr[5], prs[4], pfull = 0, ptp = 0, ptps[4] = {0, 0, 0, 0};
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
     {  // per-workgroup counter slots (no same-address atomics in the distance kernel)
       std::vector<unsigned long long> slots(4 * IA_NWG_H);
@@ -1599,13 +1601,22 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           if (j < 2) {  // pair slots: (pairs with corrections << 32) + pairs (k3p_variant 14/15)
             prs[j] += v & 0xffffffffull;
             pfull += v >> 32;
-          } else {
-            prs[j] += v;
+          } else {  // tile slots: (tiles with a filter-passing block << 32) + tiles loaded
+            prs[j] += v & 0xffffffffull;
+            ptp += v >> 32;
+            ptps[j] += v >> 32;
           }
         }
       }
     }
     const double pair_flops = 2.0 * g.D * IA_TILE * IA_TILE;  // one (DB tile, query tile) pair
+    // algorithmic DB bytes of the pruned scan: whole tiles, or (k3p_variant 22 / 23) the hi half
+    // of every loaded tile + the lo half of the tiles with a filter-passing block
+    const bool split_stream = c->k3p_variant == 22 || c->k3p_variant == 23;
+    auto tile_stream_bytes = [&](double tiles, double passing) {
+      const double tb = ia_k3h_tile_bytes(g.KS);
+      return split_stream ? 0.5 * tb * (tiles + passing) : tb * tiles;
+    };
     if (prune) {
       dist_flops = pair_flops * (double)(prs[0] + prs[1]);
       flops_timed = pair_flops * (double)prs[1];
@@ -1616,6 +1627,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     stats->dist_tiles += prune ? (double)(prs[2] + prs[3]) : tiles_full;
     stats->dist_tiles_full += tiles_full;
     stats->dist_pairs_corrected += (double)pfull;
+    stats->dist_tiles_rows += (double)ptp;
     float ms_db = 0.f, ms_syn = 0.f, ms_k1b = 0.f, ms_k1 = 0.f;
     hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
     hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);
@@ -1689,7 +1701,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         stats->stamp_gaps += ng;
         stats->stamp_window_ms += (double)(std::max(sp[2 * k3_n - 1], m[2 * mg_n - 1]) - sp[0]) * 1e-5;
       }
-      stats->k3p_bytes_all += (double)(prs[2] + prs[3]) * ia_k3h_tile_bytes(g.KS) + bytes_all_fixed;
+      stats->k3p_bytes_all += tile_stream_bytes((double)(prs[2] + prs[3]), (double)ptp) + bytes_all_fixed;
     }
     if (stride && ns > 0) {
       double tot = 0.;
@@ -1705,7 +1717,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         stats->prune_ms_timed += tot;
         stats->prune_launches_timed += launches_timed;
         stats->prune_flops_timed += flops_timed;
-        stats->prune_bytes_timed += (double)prs[3] * ia_k3h_tile_bytes(g.KS) + bytes_timed_fixed;
+        stats->prune_bytes_timed += tile_stream_bytes((double)prs[3], (double)ptps[3]) + bytes_timed_fixed;
       }
     }
   }

@@ -20,6 +20,13 @@ __device__ __forceinline__ void ld_tile(h16x8 (&a)[2 * KS], const h16x8 *__restr
 #pragma unroll
   for (int p = 0; p < 2 * KS; p++) a[p] = src[TileFmt<KS>::off(p, lane)];
 }
+// the hi pieces (2s) of a tile only: half its bytes (k3p_variant 22 / 23)
+template <int KS>
+__device__ __forceinline__ void ld_hi(h16x8 (&h)[KS], const h16x8 *__restrict__ db, int64_t tile, int lane) {
+  const h16x8 *src = db + tile * TileFmt<KS>::STRIDE;
+#pragma unroll
+  for (int s = 0; s < KS; s++) h[s] = src[TileFmt<KS>::off(2 * s, lane)];
+}
 
 #ifndef IA_PROBE
 #define IA_PROBE 0
@@ -366,6 +373,32 @@ __device__ __forceinline__ void k3p_hhpipe(const h16x8 (&a)[2 * KS], const h16x8
       }
     }
     k3p_hhpipe<KS, QT, Q + 1>(a, lq, msk, rt, qzt, qzw, acc, pass);
+  }
+}
+
+// HHX = 3 (k3p_variant 22 / 23): the same filter on a hi-only tile buffer (ld_hi); the blocks
+// that pass run their full chains one tile later, from the whole tile loaded only then
+template <int KS, int QT, int Q>
+__device__ __forceinline__ void k3p_hhpipe_h(const h16x8 (&h)[KS], const h16x8 *lq, unsigned msk, float rt,
+                                             const float *qzt, const float *qzw, f32x16 (&acc)[2], unsigned &pass) {
+  if constexpr (Q <= QT) {
+    constexpr int NP = 2 * KS;
+    if constexpr (Q < QT) {
+      if ((msk >> Q) & 1u) {
+        const h16x8 *qb = lq + Q * NP * IA_WAVE;
+        f32x16 c = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < KS; s++) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(h[s], qb[(2 * s) * IA_WAVE], c, 0, 0, 0);
+        acc[Q & 1] = c;
+      }
+    }
+    if constexpr (Q >= 1) {
+      if ((msk >> (Q - 1)) & 1u) {
+        const float lim = fmaf(rt, qzw[(Q - 1) * IA_TILE] + fmaf(rt, 0x1p-9f, 0x1p-20f), qzt[(Q - 1) * IA_TILE]);
+        pass |= __ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull ? 1u << (Q - 1) : 0u;
+      }
+    }
+    k3p_hhpipe_h<KS, QT, Q + 1>(h, lq, msk, rt, qzt, qzw, acc, pass);
   }
 }
 
@@ -906,7 +939,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   float *qzt = reinterpret_cast<float *>(items + K);                    // HHF: [NQ] z per sorted slot
   float *qzw = qzt + NQ;                                                // HHF: [NQ] w per sorted slot
   float *wR = qzw + NQ;                                                 // HHF: [K] R_t of the WG's tiles
-  __shared__ unsigned wpairs[NW], wtiles[NW], wfull[NW];
+  __shared__ unsigned wpairs[NW], wtiles[NW], wfull[NW], wtp[NW];
   __shared__ int wcnt[NW];
   const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1137,7 +1170,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     b2[q] = FLT_MAX;
     i1[q] = 0x7fffffff;
   }
-  unsigned cnt = 0, ntl = 0, nfull = 0;
+  unsigned cnt = 0, ntl = 0, nfull = 0, ntp = 0;  // ntp: DB tiles with a filter-passing block
   {
     K3P_T(ph[3]);
     // ---- 3'/4'. need tests interleaved with the contraction: wave v walks tiles k = v mod NW;
@@ -1181,6 +1214,45 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     };
     unsigned m;
     int k = next_k(wave, m);
+    if constexpr (HHX == 3) {
+    // ---- k3p_variant 22 / 23: the DB stream carries only the hi halves (3.5 of 7 KiB per tile
+    // at KS = 4).  Per tile: the hi x hi filter of its box-needed blocks on a hi buffer (two in
+    // rotation, the next tile's in flight); the whole tile is then loaded only when a block
+    // passed (else an L2-hot dummy: equal outstanding loads on every path) and its full chains
+    // (k3p_pairs: v14's products and records) run one tile later, while the next tile is
+    // filtered.  MALL / HBM bytes: hi of every needed tile + lo of the passing ones (39 % of the
+    // loaded tiles at cfg3); the full reload's hi half is an L2 hit (loaded one tile earlier).
+    h16x8 ha[KS], hb[KS];
+    const int k_spec = min(wave, K - 1);  // the global round's speculative tile, now L2-hot
+    ld_hi<KS>(ha, db, tk(k < K ? k : k_spec), lane);
+    unsigned pprev = 0u;
+    int kprev = 0;
+    auto step3 = [&](const h16x8(&cur)[KS], h16x8(&nxt)[KS]) {
+      unsigned mn;
+      const int kn = next_k(grab(), mn);
+      ld_hi<KS>(nxt, db, tk(kn < K ? kn : k), lane);  // unconditional (see below)
+      asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
+      f32x16 acc[2];
+      unsigned pass = 0;
+      k3p_hhpipe_h<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
+      if (pprev) k3p_pairs<KS, QT, 0>(a, ldsh + lane, pprev, tk(kprev), b1, b2, i1);
+      ld_tile<KS>(a, db, tk(pass ? k : k_spec), lane);
+      nfull += __popc(pass);
+      ntp += pass != 0u;
+      pprev = pass;
+      kprev = k;
+      cnt += __popc(m);
+      ntl++;
+      k = kn;
+      m = mn;
+    };
+    while (k < K) {
+      step3(ha, hb);
+      if (k >= K) break;
+      step3(hb, ha);
+    }
+    if (pprev) k3p_pairs<KS, QT, 0>(a, ldsh + lane, pprev, tk(kprev), b1, b2, i1);
+    } else {
     // (re)load the first needed tile unconditionally (usually the speculative one again: a
     // cache hit), so the loop is entered with the same outstanding loads on every path
     ld_tile<KS>(a, db, tk(k < K ? k : min(wave, K - 1)), lane);
@@ -1196,18 +1268,21 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         unsigned pass = 0;
         k3p_hhpairs<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), tk(k), b1, b2, i1, pass);
         nfull += __popc(pass);
+        ntp += pass != 0u;
       } else if constexpr (HHF && HHX == 1) {
         f32x16 acc[2];
         unsigned pass = 0;
         k3p_hhfuse<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), tk(k), b1, b2, i1, acc,
                               pass);
         nfull += __popc(pass);
+        ntp += pass != 0u;
       } else if constexpr (HHF) {
         f32x16 acc[2];
         unsigned pass = 0;
         k3p_hhpipe<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
         if (pass) k3p_pairs<KS, QT, 0>(cur, ldsh + lane, pass, tk(k), b1, b2, i1);
         nfull += __popc(pass);
+        ntp += pass != 0u;
       } else {
         k3p_pairs<KS, QT, 0>(cur, ldsh + lane, m, tk(k), b1, b2, i1);
       }
@@ -1221,6 +1296,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       if (k >= K) break;
       step(an, a);
     }
+    }  // HHX != 3
   }
   K3P_T(ph[4]);
 #pragma unroll
@@ -1247,6 +1323,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     wpairs[wave] = cnt;
     wtiles[wave] = ntl;
     wfull[wave] = nfull;
+    wtp[wave] = ntp;
   }
   Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32], inside the query-fragment area
 #pragma unroll
@@ -1297,15 +1374,16 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   }
   K3P_T(ph[9]);
   if (tid == 0) {  // the workgroup's own counter slots (stream-ordered launches: no atomics)
-    unsigned long long sp = 0, st = 0, sf = 0;
+    unsigned long long sp = 0, st = 0, sf = 0, stp = 0;
 #pragma unroll
     for (int w = 0; w < NW; w++) {
       sp += wpairs[w];
       st += wtiles[w];
       sf += wfull[w];
+      stp += wtp[w];
     }
     pairs[blockIdx.x] += sp + (HHF ? sf << 32 : 0ull);
-    tiles[blockIdx.x] += st;
+    tiles[blockIdx.x] += st + (stp << 32);  // (tiles with a filter-passing block << 32) + tiles loaded
   }
   if (xo.stamp) {  // (uniform) option "stamps": the workgroup's first and last tick
     __syncthreads();
@@ -1366,6 +1444,9 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     // 20 / 21: the fused corrections on query-tile pairs (two chains: k3p_hhpairs)
     if (variant == 20) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true, 2>;
     if (variant == 21) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true, 2>;
+    // 22 / 23: the filter on hi-only tile loads, full chains of the passing tiles deferred
+    if (variant == 22) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true, 3>;
+    if (variant == 23) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true, 3>;
     return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
   } else {
     return nullptr;

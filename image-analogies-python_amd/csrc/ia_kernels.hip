@@ -2819,12 +2819,13 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   // the in-kernel sort (7, 14, 18, 20) holds <= 512 queries (wider: the host ran K2s, the
   // presorted form 15 / 19 / 21 / 11); every variant walks any number of tiles (the host keeps
   // kmax <= IA_K3P_MAXK_LDS)
-  const bool in_kernel_sort = variant == 6 || variant == 14 || variant == 18 || variant == 20;
-  if (in_kernel_sort && Mpad > 512) variant = variant == 14 ? 15 : variant == 18 ? 19 : variant == 20 ? 21 : 1;
+  const bool in_kernel_sort = variant == 6 || variant == 14 || variant == 18 || variant == 20 || variant == 22;
+  if (in_kernel_sort && Mpad > 512)
+    variant = variant == 14 ? 15 : variant == 18 ? 19 : variant == 20 ? 21 : variant == 22 ? 23 : 1;
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t NQ = (size_t)qt * IA_TILE;
-  const bool pre = variant == 11 || variant == 15 || variant == 19 || variant == 21;
-  const bool hhf = variant >= 14 && variant <= 21;  // (z, w) per query slot + R_t per tile in LDS
+  const bool pre = variant == 11 || variant == 15 || variant == 19 || variant == 21 || variant == 23;
+  const bool hhf = variant >= 14 && variant <= 23;  // (z, w) per query slot + R_t per tile in LDS
   const int nthr = IA_WGH;
   size_t lds = pre ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 +
                          (size_t)kmax * 40

@@ -71,10 +71,11 @@ def make_job(size=1024, b_size=None, n_levels=None, k=0.5, seed_a=1, seed_b=2, s
     A_pyr = compute_gaussian_pyramid(A, _config.n_sm, n_levels)
     Ap_pyr = compute_gaussian_pyramid(Ap, _config.n_sm, n_levels)
     B_pyr = compute_gaussian_pyramid(B, _config.n_sm, n_levels)
-    if level_align == 'fine' and len(B_pyr) > len(A_pyr):
-        B_pyr = B_pyr[len(B_pyr) - len(A_pyr):]
     L = min(len(A_pyr), len(B_pyr))
-    A_pyr, Ap_pyr, B_pyr = A_pyr[:L], Ap_pyr[:L], B_pyr[:L]
+    # the deeper pyramid drops its extra coarse levels ('fine': finest levels paired, as
+    # sweep.Sweep / config.level_align) or its extra fine levels ('coarse', the reference)
+    sl = slice(-L, None) if level_align == 'fine' else slice(None, L)
+    A_pyr, Ap_pyr, B_pyr = A_pyr[sl], Ap_pyr[sl], B_pyr[sl]
     Bp = initialize_Bp(B_pyr, init_rand=True, seed=seed_bp)
     weights = _config.compute_weights(_config.n_sm, _config.n_lg, _config.n_half, 1)
     return Job(A_pyr, [Ap_pyr], B_pyr, Bp, k, weights)

@@ -76,8 +76,9 @@ typedef struct {
   double dist_pairs_corrected; /* k3p_variant 14/15: pairs whose hi x hi value passed the bound
                                 * (correction products + top-2 epilogue run); 16/17: pairs whose
                                 * head (15-axis partial distance) passed; else 0 */
-  double dist_tiles_rows;   /* k3p_variant 16/17: DB tiles whose full rows were loaded after the
-                             * head filter (dist_tiles counts the heads); else 0 */
+  double dist_tiles_rows;   /* hi x hi block filter (k3p_variant 14, 15, 18..21): loaded DB tiles with
+                             * at least one block passing the filter (the only ones whose lo halves
+                             * the correction products read) */
   /* feature-gather kernels (bench.py roofline.gathers; DESIGN.md §4 algorithmic bytes) */
   double k1b_ms;            /* K1b k_db64_build (fp64 row DB), device ms summed over the levels */
   double k1b_bytes;         /* its algorithmic bytes: A-side images read once + N_A rows written */

@@ -48,9 +48,10 @@ def _run_debug(ctx, z, prune_all=False, variant=20):
 
 
 @pytest.mark.parametrize('prune_all,variant', [(False, 20), (True, 7), (True, 14), (True, 15), (True, 11), (True, 18),
-                                                (True, 19), (True, 20), (True, 21)],
+                                                (True, 19), (True, 20), (True, 21), (True, 22), (True, 23)],
                          ids=['default', 'pruned_v7', 'pruned', 'pruned_presorted_v15', 'pruned_presorted_v11',
-                              'pruned_v18', 'pruned_presorted_v19', 'pruned_v20', 'pruned_presorted_v21'])
+                              'pruned_v18', 'pruned_presorted_v19', 'pruned_v20', 'pruned_presorted_v21', 'pruned_v22',
+                              'pruned_presorted_v23'])
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
 def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     """Every NN pick, coherence pick and compute_distance value of the reference run.  With
@@ -65,9 +66,8 @@ def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]
     if prune_all:
         assert st.pruned_levels == (z['L'] - 1 if ch == 1 else 0)
-    if variant in (14, 15, 16, 18, 19, 20, 21) and st.pruned_levels > 0:  # the block filters run on pruned levels only
+    if variant in (14, 15, 18, 19, 20, 21, 22, 23) and st.pruned_levels > 0:  # the block filters run on pruned levels only
         assert 0 < st.dist_pairs_corrected <= st.dist_pairs
-    if variant == 16 and st.pruned_levels > 0:
         assert 0 < st.dist_tiles_rows <= st.dist_tiles
     assert st.bound_violations == 0 and st.kappa_ambiguous == 0
     app, coh, dist = [], [], []

@@ -36,11 +36,12 @@ def _run(ctx, job, prune, variant=7, group=1):
 @pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 7), (1024, 2, 7), (512, 1, 11), (1024, 2, 11), (512, 1, 14),
                                                       (1024, 2, 14), (512, 1, 15), (1024, 2, 15), (512, 1, 18), (1024, 2, 18),
                                                       (512, 1, 19), (1024, 2, 19), (512, 1, 20), (1024, 2, 20), (512, 1, 21),
-                                                      (1024, 2, 21)])
+                                                      (1024, 2, 21), (512, 1, 22), (1024, 2, 22), (512, 1, 23),
+                                                      (1024, 2, 23)])
 def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     """variant = the pruned-scan kernel version (option k3p_variant: 7 / 11 without, 14 / 15,
-    18 / 19 and 20 (default) / 21 with the hi x hi block filter; 11 / 15 / 19 / 21 with the
-    queries presorted once per step): every one is exact"""
+    18 / 19, 20 (default) / 21 and 22 / 23 (hi-only tile stream) with the hi x hi block filter;
+    the odd ones with the queries presorted once per step): every one is exact"""
     from ia_amd import synth
     job = synth.make_job(size)
     Bp0, S0, IM0, st0 = _run(ctx, job, 0)
@@ -54,12 +55,13 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     assert st1.dist_pairs < st1.dist_pairs_full
     assert st1.dist_pairs_full == st0.dist_pairs_full
     assert st1.dist_tiles <= st1.dist_tiles_full and st1.dist_tiles_full == st0.dist_tiles_full
-    if variant in (14, 15, 18, 19, 20, 21):  # block filters: most box-needed pairs stop after a cheap product
+    if variant in (14, 15, 18, 19, 20, 21, 22, 23):  # block filters: most box-needed pairs stop after a cheap product
         assert 0 < st1.dist_pairs_corrected < st1.dist_pairs
-        print('filter-passing pairs %.3f of the box-needed ones' % (st1.dist_pairs_corrected / st1.dist_pairs))
+        assert 0 < st1.dist_tiles_rows <= st1.dist_tiles   # loaded tiles with a filter-passing block
+        print('filter-passing pairs %.3f of the box-needed ones, tiles %.3f of the loaded ones'
+              % (st1.dist_pairs_corrected / st1.dist_pairs, st1.dist_tiles_rows / st1.dist_tiles))
     else:
-        assert st1.dist_pairs_corrected == 0
-    assert st1.dist_tiles_rows == 0
+        assert st1.dist_pairs_corrected == 0 and st1.dist_tiles_rows == 0
     print('size %d: pairs left %.3f, DB tiles loaded %.3f, fallbacks %d -> %d'
           % (size, st1.dist_pairs / st1.dist_pairs_full, st1.dist_tiles / st1.dist_tiles_full, st0.fallbacks,
              st1.fallbacks))
@@ -121,15 +123,15 @@ def test_prune_option_rejects_bad_values(ctx):
     with pytest.raises(_native.IAError):
         ctx.set_option('prune_group', 3)
     with pytest.raises(_native.IAError):
-        ctx.set_option('k3p_variant', 22)
-    for v in (1, 6, 12, 13, 16, 17):   # earlier versions: in git history only
+        ctx.set_option('k3p_variant', 24)
+    for v in (1, 6, 12, 13, 16, 17, 24):   # earlier versions: in git history only
         with pytest.raises(_native.IAError):
             ctx.set_option('k3p_variant', v)
     with pytest.raises(_native.IAError):
         ctx.set_option('prune_min_rows', 0)
 
 
-@pytest.mark.parametrize('variant', [14, 15, 7, 11, 18, 19, 20, 21])
+@pytest.mark.parametrize('variant', [14, 15, 7, 11, 18, 19, 20, 21, 22, 23])
 def test_pruned_scan_over_512_tiles_per_workgroup(ctx, variant):
     """a DB of more than 256 x 512 tiles (> 4.19 M rows: here A 2048 x 2080,
     133,120 tiles, 520 per workgroup) against a small B.  The pruned scan keeps every workgroup's
