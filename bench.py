@@ -404,8 +404,11 @@ def main():
                          'chunk) workgroups, 0 = one launch per query block')
     ap.add_argument('--prune-group', type=int, default=1, choices=[1, 2, 4, 8],
                     help='pruned levels: Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)')
-    ap.add_argument('--prune-min-rows', type=int, default=524288,
-                    help='smallest DB (rows) the pruned scan is used on (default: the 1024^2 level)')
+    ap.add_argument('--prune-min-rows', type=int, default=None,
+                    help='smallest DB (rows) the pruned scan is used on (default: 262,144 = the 512^2 level too for '
+                         'the pipelined cfg3 job, where its lighter scan interferes less with the finest level: '
+                         '+0.9-1.9 %% on three boxes, profiles/r04/prune512; 524,288 = the 1024^2 level otherwise, '
+                         'libia\'s own default: cfg4 lost 4 %% with 262,144, profiles/r04/k3p_hi)')
     ap.add_argument('--shard-unpruned', action='store_true',
                     help='shard (or emulate shards of) levels that scan unpruned too (default: only pruned levels, '
                          'DESIGN.md §7)')
@@ -432,6 +435,8 @@ def main():
         ap.error('cfg5 is a sweep of independent jobs (replicas only): --mode shard does not apply')
     if args.config == 'cfg5' and args.shard_emulate > 1 and not args.sequential:
         ap.error('--shard-emulate takes one job per level call: add --sequential for cfg5')
+    if args.prune_min_rows is None:
+        args.prune_min_rows = 262144 if (args.config == 'cfg3' and args.pipeline) else 524288
     if args.traffic_json is None:
         args.traffic_json = os.path.join(ROOT, 'profiles', 'k3p_traffic_%s.json' % args.config)
     import torch

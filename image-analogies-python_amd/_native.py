@@ -53,21 +53,28 @@ class Stats(ctypes.Structure):
                 ('k3p_stamp_ms', ctypes.c_double), ('k3p_stamp_launches', ctypes.c_int64),
                 ('k3p_bytes_all', ctypes.c_double), ('merge_stamp_ms', ctypes.c_double),
                 ('merge_stamp_launches', ctypes.c_int64), ('stamp_gap_ms', ctypes.c_double),
-                ('stamp_gaps', ctypes.c_int64), ('stamp_window_ms', ctypes.c_double)]
+                ('stamp_gaps', ctypes.c_int64), ('stamp_window_ms', ctypes.c_double), ('prune_rows', ctypes.c_int64)]
+
+    # fields that describe only the levels with the largest DB seen (build_rows / prune_rows)
+    _BUILD = ('k1b_ms', 'k1b_bytes', 'k1_ms', 'k1_bytes', 'build_levels')
+    _PRUNE = ('prune_ms_timed', 'prune_launches_timed', 'prune_flops_timed', 'prune_bytes_timed', 'k3p_stamp_ms',
+              'k3p_stamp_launches', 'k3p_bytes_all', 'merge_stamp_ms', 'merge_stamp_launches', 'stamp_gap_ms',
+              'stamp_gaps', 'stamp_window_ms')
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
     def add(self, other):
         """accumulate another Stats (e.g. of a concurrent context) field by field (the DB-build
-        timings keep the largest level's, as libia does)"""
-        if other.build_rows > self.build_rows:
-            for k in ('k1b_ms', 'k1b_bytes', 'k1_ms', 'k1_bytes', 'build_levels'):
-                setattr(self, k, 0)
-            self.build_rows = other.build_rows
+        and pruned-scan timings keep the largest level's, as libia does)"""
+        for rows, group in (('build_rows', self._BUILD), ('prune_rows', self._PRUNE)):
+            if getattr(other, rows) > getattr(self, rows):
+                for k in group:
+                    setattr(self, k, 0)
+                setattr(self, rows, getattr(other, rows))
         for k, _ in self._fields_:
-            if k == 'build_rows' or (k in ('k1b_ms', 'k1b_bytes', 'k1_ms', 'k1_bytes', 'build_levels')
-                                     and other.build_rows < self.build_rows):
+            if k in ('build_rows', 'prune_rows') or (k in self._BUILD and other.build_rows < self.build_rows) or \
+                    (k in self._PRUNE and other.prune_rows < self.prune_rows):
                 continue
             setattr(self, k, getattr(self, k) + getattr(other, k))
 

@@ -1671,7 +1671,20 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     stats->synth_ms += ms_syn;
     stats->dist_launches += dist_launches;
     stats->dist_flops += dist_flops;
-    if (stamped && k3_n + mg_n > 0) {
+    // the pruned scan's timing fields (prune_*, k3p_*, merge_stamp_*, stamp_*) describe the
+    // pruned levels with the largest DB seen (prune_rows: the bench's finest level), like k1*_ms
+    bool prune_acc = false;
+    if (prune && g.NA >= stats->prune_rows) {
+      if (g.NA > stats->prune_rows) {
+        stats->prune_ms_timed = stats->prune_flops_timed = stats->prune_bytes_timed = 0.;
+        stats->prune_launches_timed = 0;
+        stats->k3p_stamp_ms = stats->k3p_bytes_all = stats->merge_stamp_ms = stats->stamp_gap_ms = stats->stamp_window_ms = 0.;
+        stats->k3p_stamp_launches = stats->merge_stamp_launches = stats->stamp_gaps = 0;
+        stats->prune_rows = g.NA;
+      }
+      prune_acc = true;
+    }
+    if (stamped && prune_acc && k3_n + mg_n > 0) {
       std::vector<unsigned long long> sp((size_t)2 * (k3_n + mg_n));  // (start, end) per launch: K3p, then merges
       HIP_TRY(hipMemcpy(sp.data(), c->stamp_dur.p, sp.size() * 8, hipMemcpyDeviceToHost));
       double tk = 0., tm = 0.;
@@ -1713,7 +1726,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       stats->dist_ms += tot;
       stats->dist_launches_timed += launches_timed;
       stats->dist_flops_timed += flops_timed;
-      if (prune) {  // the pruned scan alone (bench roofline): time, MFMA flops, algorithmic bytes
+      if (prune_acc) {  // the pruned scan alone (bench roofline): time, MFMA flops, algorithmic bytes
         stats->prune_ms_timed += tot;
         stats->prune_launches_timed += launches_timed;
         stats->prune_flops_timed += flops_timed;

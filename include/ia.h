@@ -105,6 +105,8 @@ typedef struct {
                              * start, merge end -> next scan start), summed */
   int64_t stamp_gaps;
   double stamp_window_ms;   /* those levels' first scan start -> last kernel end */
+  int64_t prune_rows;       /* DB rows of the pruned levels in prune_*, k3p_*, merge_stamp_* and
+                             * stamp_* (the largest pruned level seen: the bench's finest) */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
