@@ -116,8 +116,9 @@ struct ia_ctx {
   HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
   int hand_rows = 0;
   int prefetch_next = 1;         // option "prefetch_next" (NextStep::prefetch)
-  int fuse_sort = 0;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
-                                 // off by default: the scan gets 0.9 us faster, the merge 2.8 us slower
+  int fuse_sort = 2;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
+                                 // 2 (auto) = on levels whose widest step has >= IA_FUSE_SORT_MINQ queries: a
+                                 // 342-query step loses 1.7 us, a 683-query step gains 3
   unsigned long long *kslot = nullptr;  // their per-query key slots (uncached)
   int kslot_n = 0;
   unsigned hseq = 0;
@@ -422,7 +423,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
   if (!std::strcmp(name, "fuse_sort")) {
-    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_sort must be 0 or 1");
+    if (value < 0 || value > 2) return fail(IA_EINVAL, "ia_set_option: fuse_sort must be 0, 1 or 2");
     c->fuse_sort = value;
     return IA_OK;
   }
@@ -631,6 +632,7 @@ int ia_wavefront_step(int h, int w, int64_t t, int *r0, int *M) {
 }
 
 #define IA_FUSE_SORT_MAXW 768  // waves of a k_merge_gather launch whose gathers sort the next step
+#define IA_FUSE_SORT_MINQ 512  // fuse_sort 2: the widest step's queries (all jobs) from which the gathers sort
 
 static bool shard_level(int64_t n_tiles, int world) { return world > 1 && n_tiles >= 64 * (int64_t)world; }
 
@@ -1092,7 +1094,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   };
   int64_t gathered = -1;  // the step whose gather the previous fused launch ran
   bool gsort = false;     // ... and that launch also sorted it (option "fuse_sort": no K2s, no in-scan sort)
-  const bool fsort = chain && prune && c->fuse_sort && !xo;
+  const bool fsort = chain && prune && !xo && (c->fuse_sort == 1 || (c->fuse_sort == 2 && Mtmax >= IA_FUSE_SORT_MINQ));
   const int64_t n_timed = stride ? (T + stride - 1) / stride : 0;
   for (auto *v : {&c->evs, &c->evg, &c->evm})
     if ((int64_t)v->size() < 2 * n_timed) {

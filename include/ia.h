@@ -186,9 +186,10 @@ int ia_version(void);
  * "prefetch_next" = 1 (default) / 0: a fused merge + gather wave loads its next query's inputs
  * that do not depend on the launch's own merges (features, causal neighbours' sources) while
  * its merge's DB rows load.
- * "fuse_sort" = 0 (default) / 1: the fused gathers of step t + 1 also rank its queries' sort keys
- * across the launch and write the presorted scan inputs (the scan then skips its per-workgroup
- * sort); exact either way, measured slower.
+ * "fuse_sort" = 2 (default, auto) / 1 / 0: the fused gathers of step t + 1 also rank its queries'
+ * sort keys across the launch and write the presorted scan inputs (no K2s launch, no per-workgroup
+ * sort in the scan).  2: on levels whose widest step has >= 512 queries (all jobs), where it
+ * replaces a K2s launch and is measured faster; exact either way.
  * "stamps" = 1: every pruned-scan and fused-merge launch of a pruned level stamps its
  * workgroups' first / last s_memrealtime tick; ia_stats.k3p_stamp_ms / merge_stamp_ms sum the
  * per-launch device times (bench.py roofline.frac_timed: the timed, pipelined steps' own kernels).
