@@ -71,9 +71,9 @@ struct DevBuf {
 };
 
 struct JobBufs {
-  DevBuf B, Bc, Bpc, Bp, S, IM, W, DSRC, DDIST, pstat;
+  DevBuf B, Bc, Bpc, Bp, S, IM, W, DSRC, DDIST, pstat, NN;
   void release() {
-    for (DevBuf *b : {&B, &Bc, &Bpc, &Bp, &S, &IM, &W, &DSRC, &DDIST, &pstat}) b->release();
+    for (DevBuf *b : {&B, &Bc, &Bpc, &Bp, &S, &IM, &W, &DSRC, &DDIST, &pstat, &NN}) b->release();
   }
 };
 
@@ -116,6 +116,8 @@ struct ia_ctx {
   HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
   int hand_rows = 0;
   int prefetch_next = 1;         // option "prefetch_next" (NextStep::prefetch)
+  int nn_bound = 1;              // option "nn_bound" (JobPtrs::nn): the pruned one-rank levels' gathers also
+                                 // bound U' by the causal neighbours' exact NN rows, shifted
   int fuse_sort = 2;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
                                  // 2 (auto) = on levels whose widest step has >= IA_FUSE_SORT_MINQ queries: a
                                  // 342-query step loses 1.7 us, a 683-query step gains 3
@@ -415,6 +417,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "fuse_gather")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_gather must be 0 or 1");
     c->fuse_gather = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "nn_bound")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: nn_bound must be 0 or 1");
+    c->nn_bound = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "prefetch_next")) {
@@ -849,9 +856,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     }
     HIP_TRY(hipMemsetAsync(p.pstat, 0, (size_t)NB * 4, c->st));
   }
-  if ((rc = c->jobs.ensure(sizeof(JobPtrs) * J))) return rc;
-  HIP_TRY(hipMemcpyAsync(c->jobs.p, jp.data(), sizeof(JobPtrs) * J, hipMemcpyHostToDevice, c->st));
-  const JobSet djobs{jp[0], c->jobs.as<JobPtrs>(), J};
 
   // matcher: split-f16 when the channel count has a K3h instance and every image value fits
   // (IA_F16_MAXABS, one 4-byte read-back per level); otherwise the fp32 MFMA scan
@@ -885,6 +889,19 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                                     xo ? J * ((Mmax + IA_TILE - 1) / IA_TILE * IA_TILE) : 0);
   const bool prune = c->prune && use_h && g.ch == 1 && g.NA >= c->prune_min_rows && Mpad_max <= 4096 &&
                      (g.n_tiles + IA_NWG_H - 1) / IA_NWG_H <= IA_K3P_MAXK_LDS;
+  // option "nn_bound": per-pixel exact NN rows of a pruned one-rank level (-1 until merged)
+  for (int j = 0; j < J; j++) {
+    jp[j].nn = nullptr;
+    if (prune && !multi && c->nn_bound) {
+      JobBufs &b = c->jb[j];
+      if ((rc = b.NN.ensure((size_t)NB * 4))) return rc;
+      jp[j].nn = b.NN.as<int32_t>();
+      HIP_TRY(hipMemsetAsync(jp[j].nn, 0xFF, (size_t)NB * 4, c->st));
+    }
+  }
+  if ((rc = c->jobs.ensure(sizeof(JobPtrs) * J))) return rc;
+  HIP_TRY(hipMemcpyAsync(c->jobs.p, jp.data(), sizeof(JobPtrs) * J, hipMemcpyHostToDevice, c->st));
+  const JobSet djobs{jp[0], c->jobs.as<JobPtrs>(), J};
   if (xo && !prune)
     return fail(IA_EINVAL, "ia_synthesize_level: exchange = 2 shards pruned levels only (1 channel, split-f16, <= 4096 "
                            "queries per step)");

@@ -188,6 +188,9 @@ struct JobPtrs {
   double *dbg_dist;
   const double *weights;       // compute_distance weights
   double kf;                   // kappa factor 1 + 2^(level - L) k
+  int32_t *nn;                 // option "nn_bound" (pruned one-rank levels): per pixel the row of its
+                               // certified exact NN (-1: none yet), written by the merge; the gathers
+                               // shift the causal neighbours' rows into extra U' candidates (nullptr: off)
 };
 // the jobs of a launch.  A single job (the common case) travels in the kernel arguments
 // (JobArg1: its pointers are plain kernel-argument loads, as before batching); a batch reads
@@ -325,7 +328,8 @@ struct HandSlot {          // uncached: row r's step-t result for row r + 1's st
   double v;                // B' value
   int sr, sc, im;          // source pixel, A' image
   unsigned seq;            // the step's seq, stored after the fields above completed
-  unsigned pad[2];
+  int nn;                  // its exact NN row (option "nn_bound"; -1: none)
+  unsigned pad;
 };
 struct NextStep {
   StepDesc sn;             // step t + 1

@@ -1303,6 +1303,7 @@ struct QHand {
   int r0 = -1, c0 = -1, r1 = -1, c1 = -1;
   double v0 = 0., v1 = 0.;
   int s0r = 0, s0c = 0, i0 = 0, s1r = 0, s1c = 0, i1 = 0;
+  int n0 = -1, n1 = -1;  // their exact NN rows (option "nn_bound")
 };
 template <bool FUSE>
 __device__ __forceinline__ double feat_q1(const Imgs &B, int f, int r, int c, const QHand &h) {
@@ -1403,6 +1404,7 @@ struct QPre {
   bool on = false;
   double v = 0.;
   int sr = 0, sc = 0, si = 0;
+  int nn = -1;  // lane 15 + k: causal neighbour k's exact NN row (option "nn_bound")
 };
 __device__ __forceinline__ QPre qpre_load(const LevelGeo &g, const StepDesc &sn, const Imgs &B, const JobPtrs &jp, int m, int lane) {
   constexpr int D = 55;
@@ -1419,6 +1421,10 @@ __device__ __forceinline__ QPre qpre_load(const LevelGeo &g, const StepDesc &sn,
       p.sc = jp.s[2 * nb + 1];
       p.si = jp.im[nb];
     }
+  }
+  if (px.qi > 0 && jp.nn && lane >= 15 && lane < 30) {
+    const int k = lane - 15, nr = r - 2 + k / 5, nc = c - 2 + k % 5;
+    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < px.qi) p.nn = jp.nn[nr * g.bw + nc];
   }
   return p;
 }
@@ -1439,24 +1445,43 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
   const QPix px = ia_qpix(sd, g.bw, m);
   const int32_t *__restrict__ s = jp.s, *__restrict__ im = jp.im;
   const int r = px.r, c = px.c, qi = px.qi;
-  // coherence candidate of this lane (lanes 0..14, product(rows, cols) order as merge_fused)
+  // U' candidate of this lane: lanes 0..14 the coherence candidates (product(rows, cols) order as
+  // merge_fused); with option "nn_bound" lanes 15..29 the same causal neighbours' exact NN rows,
+  // shifted by the neighbour's offset like a coherence candidate.  Any DB row's exact distance
+  // bounds the NN distance from above, so U' stays a valid bound whatever row a slot holds (an
+  // out-of-range or missing one is skipped); only its tightness depends on them.
   int crow = -1;
-  if (qi > 0 && lane < 15) {
-    const int nr = r - 2 + lane / 5, nc = c - 2 + lane % 5;
+  const bool nnl = jp.nn && lane >= 15 && lane < 30;
+  if (qi > 0 && (lane < 15 || nnl)) {
+    const int k = lane < 15 ? lane : lane - 15;
+    const int nr = r - 2 + k / 5, nc = c - 2 + k % 5;
     if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
       const int nb = nr * g.bw + nc;
-      int sr, sc, si;
-      if (FUSE && nr == h.r0 && nc == h.c0) {
-        sr = h.s0r; sc = h.s0c; si = h.i0;
-      } else if (FUSE && nr == h.r1 && nc == h.c1) {
-        sr = h.s1r; sc = h.s1c; si = h.i1;
-      } else if (pf.on) {
-        sr = pf.sr; sc = pf.sc; si = pf.si;
+      int sr = -1, sc = 0, si = 0;
+      if (!nnl) {
+        if (FUSE && nr == h.r0 && nc == h.c0) {
+          sr = h.s0r; sc = h.s0c; si = h.i0;
+        } else if (FUSE && nr == h.r1 && nc == h.c1) {
+          sr = h.s1r; sc = h.s1c; si = h.i1;
+        } else if (pf.on) {
+          sr = pf.sr; sc = pf.sc; si = pf.si;
+        } else {
+          sr = s[2 * nb]; sc = s[2 * nb + 1]; si = im[nb];
+        }
       } else {
-        sr = s[2 * nb]; sc = s[2 * nb + 1]; si = im[nb];
+        const int row = (FUSE && nr == h.r0 && nc == h.c0) ? h.n0
+                        : (FUSE && nr == h.r1 && nc == h.c1) ? h.n1
+                        : pf.on ? pf.nn : jp.nn[nb];
+        const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
+        if (row >= 0 && row < g.NA) {
+          si = (int)((unsigned)row / hw);
+          const unsigned rem = (unsigned)row - (unsigned)si * hw;
+          sr = (int)(rem / (unsigned)g.aw);
+          sc = (int)(rem - (unsigned)sr * (unsigned)g.aw);
+        }
       }
       const int tr = sr + r - nr, tc = sc + c - nc;
-      if (tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) crow = (si * g.ah + tr) * g.aw + tc;
+      if (sr >= 0 && tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) crow = (si * g.ah + tr) * g.aw + tc;
     }
   }
   double ss = 0., p[IA_NPC];
@@ -1559,6 +1584,7 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_gather_query_p(LevelGeo g, StepDes
 struct MergeOut {  // one pixel's result: B' value (first channel), source pixel and A' image
   double v;
   int pr, pc, img;
+  int nn;  // its certified exact NN row (-1: none)
 };
 
 // Fused single-rank merge of query m: certified exact NN + coherence + kappa + writeback.
@@ -1872,6 +1898,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     s[2 * qi] = pr;
     s[2 * qi + 1] = pc;
     im[qi] = img;
+    if (jp.nn) jp.nn[qi] = bi >= 0 && bi < a.NA ? bi : -1;  // option "nn_bound"
     // per-pixel stats word (no shared-counter atomics: hundreds of waves adding to one
     // address serialise at L2 and dominated this kernel); reduced once per level
     const int slot = placed + 0;
@@ -1896,6 +1923,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     out->pr = pr;
     out->pc = pc;
     out->img = img;
+    out->nn = bi >= 0 && bi < a.NA ? bi : -1;
   }
 #if IA_PROBE & 8
   if (lane == 0 && m == sd.M / 2 && (sd.t % 256) == 128) {
@@ -2060,6 +2088,7 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
         hs->sr = o.pr;
         hs->sc = o.pc;
         hs->im = o.img;
+        hs->nn = o.nn;
       }
       ia_stores_done();
       if (lane == 0) __hip_atomic_store(&hs->seq, nx.seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
@@ -2070,6 +2099,7 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
     h.s0r = o.pr;
     h.s0c = o.pc;
     h.i0 = o.img;
+    h.n0 = o.nn;
   } else if (w < JM + J) {
     job = w - JM;
     if (nx.sn.t - 3 * (nx.sn.r0 + nx.sn.M - 1) == 0) mn = job * nx.sn.M + nx.sn.M - 1;  // a row enters at column 0
@@ -2113,6 +2143,7 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
     h.s1r = hs->sr;
     h.s1c = hs->sc;
     h.i1 = hs->im;
+    h.n1 = hs->nn;
   }
   __builtin_amdgcn_wave_barrier();  // the merge's LDS rows are done with
   if constexpr (PR) {

@@ -183,6 +183,10 @@ int ia_version(void);
  * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge)
  * / 2 (owner computes: each rank brings its own job, every rank scans its shard for all of them,
  * queries and scan records exchanged by peer writes; emulated: one job per shard).
+ * "nn_bound" = 1 (default) / 0: on pruned one-rank levels the merge also keeps each pixel's certified
+ * exact NN row, and the gathers bound U' (the pruned scan's radius) by the causal neighbours' NN
+ * rows shifted by the neighbour's offset as well as by the coherence candidates (exact either way:
+ * any DB row's exact distance bounds the NN distance).
  * "prefetch_next" = 1 (default) / 0: a fused merge + gather wave loads its next query's inputs
  * that do not depend on the launch's own merges (features, causal neighbours' sources) while
  * its merge's DB rows load.

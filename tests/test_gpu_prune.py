@@ -88,7 +88,7 @@ def test_fused_gather_equals_separate_launches(ctx, variant):
         finally:
             ctx.set_option('fuse_gather', 1)
             ctx.set_option('time_dist', 0)
-            ctx.set_option('fuse_sort', 0)
+            ctx.set_option('fuse_sort', 2)
     for Bp, S, IM, st in runs[1:]:
         for level in range(1, job.L):
             assert np.array_equal(S[level], runs[0][1][level]), level
@@ -195,5 +195,29 @@ def test_fused_sort_matches_reference(ctx, name):
             assert np.array_equal(Bp[level], z['Bp_final'][level]), level
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('fuse_sort', 0)
+        ctx.set_option('fuse_sort', 2)
     assert st.bound_violations == 0 and st.kappa_ambiguous == 0 and st.pruned_levels == L - 1
+
+
+def test_nn_bound_is_exact_and_tighter(ctx):
+    """option nn_bound (default on): the gathers also bound U' by the causal neighbours' exact NN
+    rows, shifted.  Exact with and without it (the 1024^2 job's two pruned levels: s, im and B'
+    identical), and the scan contracts fewer pairs with it (a smaller radius per query)."""
+    from ia_amd import synth
+    job = synth.make_job(1024)
+    ctx.set_option('nn_bound', 0)
+    try:
+        Bp0, S0, IM0, st0 = _run(ctx, job, 1, 20)
+    finally:
+        ctx.set_option('nn_bound', 1)
+    Bp1, S1, IM1, st1 = _run(ctx, job, 1, 20)
+    for level in range(1, job.L):
+        assert np.array_equal(S0[level], S1[level]), level
+        assert np.array_equal(IM0[level], IM1[level]), level
+        assert np.array_equal(Bp0[level], Bp1[level]), level
+    assert st0.bound_violations == 0 and st1.bound_violations == 0
+    assert st1.dist_pairs < st0.dist_pairs
+    print('pairs %.4f -> %.4f of the full scan, corrected %.4f -> %.4f, fallbacks %d -> %d'
+          % (st0.dist_pairs / st0.dist_pairs_full, st1.dist_pairs / st1.dist_pairs_full,
+             st0.dist_pairs_corrected / st0.dist_pairs_full, st1.dist_pairs_corrected / st1.dist_pairs_full,
+             st0.fallbacks, st1.fallbacks))

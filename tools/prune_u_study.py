@@ -4,6 +4,9 @@ finest level, the fraction of DB tiles the step's sorted query tiles need (the u
 streams) and of (DB tile, query tile) pairs, with U = the best coherence candidate's exact
 distance (K2p's bound today) and with U = f x the exact NN distance (f = 1, 1.07, 1.2): what
 any tighter bound could reach.  Test infrastructure (uses the oracle's feature code).
+Also two candidate sources K2p could add to U: every causal neighbour's exact NN row, shifted by the
+neighbour's offset (the coherence rule applied to NN picks the kappa rule overruled), and the
+coarser level's pick upsampled (2 s + (r mod 2, c mod 2)).
   python3 tools/prune_u_study.py <state.npz> [step]"""
 import os
 import sys
@@ -61,13 +64,66 @@ for r in range(r_lo, r_hi + 1):
 Q, Uc = np.array(qs), np.array(us)
 an2 = (X ** 2).sum(axis=1)
 Qc = Q - mu
-dnn = np.array([max(0.0, (an2 - 2 * X @ qc).min() + qc @ qc) for qc in Qc])   # exact-enough NN distance
+
+
+def nn_rows(Qs):
+    """exact-enough NN row and distance of each query (centred dot products, chunked)"""
+    rows, ds = [], []
+    for i in range(0, len(Qs), 64):
+        qc = Qs[i:i + 64] - mu
+        d = an2[None] - 2 * qc @ X.T
+        j = d.argmin(axis=1)
+        rows.append(j)
+        ds.append(np.maximum(0.0, d[np.arange(len(j)), j] + (qc ** 2).sum(axis=1)))
+    return np.concatenate(rows), np.concatenate(ds)
+
+
+_, dnn = nn_rows(Q)
+# candidate sources: the causal neighbours' NN rows shifted, and the coarse level's pick upsampled
+nbq, nbkey = [], {}
+for r in range(r_lo, r_hi + 1):
+    c = step - 3 * r
+    qi = r * w + c
+    for rr in range(max(0, r - 2), r + 1):
+        for rc in range(max(0, c - 2), min(w, c + 3)):
+            ri = rr * w + rc
+            if ri < qi and ri not in nbkey:
+                nbkey[ri] = len(nbq)
+                nbq.append(O.query_feature(Bf, Bp_sm, O.state_at(Bp_f, job.Bp_init[level], ri), rr, rc, w))
+nb_rows, _ = nn_rows(np.array(nbq))
+hc, wc = job.B_pyr[level - 1].shape[:2]
+Ahc, Awc = job.A_pyr[level - 1].shape[:2]
+sc, imc = z['s_%d' % (level - 1)].astype(np.int64), z['im_%d' % (level - 1)].astype(np.int64)
+Uns, Uup = [], []
+for k, r in enumerate(range(r_lo, r_hi + 1)):
+    c = step - 3 * r
+    qi = r * w + c
+    best = Uc[k]
+    for rr in range(max(0, r - 2), r + 1):
+        for rc in range(max(0, c - 2), min(w, c + 3)):
+            ri = rr * w + rc
+            if ri < qi:
+                row = int(nb_rows[nbkey[ri]])
+                img, rem = divmod(row, A_h * A_w)
+                pr, pc = divmod(rem, A_w)
+                pr, pc = pr + r - rr, pc + c - rc
+                if 0 <= pr < A_h and 0 <= pc < A_w:
+                    best = min(best, ((As[(img * A_h + pr) * A_w + pc] - Q[k]) ** 2).sum())
+    Uns.append(best)
+    ci = min(r // 2, hc - 1) * wc + min(c // 2, wc - 1)
+    pr, pc = 2 * sc[ci, 0] + r % 2, 2 * sc[ci, 1] + c % 2
+    up = ((As[(imc[ci] * A_h + pr) * A_w + pc] - Q[k]) ** 2).sum() if pr < A_h and pc < A_w else np.inf
+    Uup.append(min(best, up))
+Uns, Uup = np.array(Uns), np.array(Uup)
 Qp = Qc @ U_.T
 M = len(Q)
 qorder = np.argsort(morton([quant(Qp[:, i], lo[i], hi[i], bits) for i in range(npc)], bits), kind='stable')
 print('%s level %d step %d: %d queries; U / NN median %.3f (p10 %.3f, p90 %.3f)' % (
     cfg, level, step, M, np.median(Uc / dnn), np.percentile(Uc / dnn, 10), np.percentile(Uc / dnn, 90)))
-for label, Ub in (('U = coherence (today)', Uc), ('U = 1.2 NN', 1.2 * dnn), ('U = 1.07 NN', 1.07 * dnn),
+for label, Ub in (('+ neighbours NN shifted', Uns), ('+ coarse pick upsampled', Uup)):
+    print('  %-24s U / NN median %.3f (p10 %.3f, p90 %.3f)' % (label, np.median(Ub / dnn), np.percentile(Ub / dnn, 10),
+                                                              np.percentile(Ub / dnn, 90)))
+for label, Ub in (('U = coherence (today)', Uc), ('U = + nbr NN shifted', Uns), ('U = + coarse upsampled', Uup), ('U = 1.2 NN', 1.2 * dnn), ('U = 1.07 NN', 1.07 * dnn),
                   ('U = NN', dnn)):
     need = np.zeros(nt, dtype=bool)
     pairs = 0
