@@ -278,6 +278,8 @@ def make_context(args, local):
         cx.set_option('prefetch_next', 0)
     if not args.nn_bound:
         cx.set_option('nn_bound', 0)
+    if args.k3p_lockstep:
+        cx.set_option('k3p_lockstep', 1)
     if args.shard_unpruned:
         cx.set_option('shard_unpruned', 1)
     if args.shard_emulate > 1:
@@ -389,6 +391,9 @@ def main():
                          'option fuse_sort); 0: the scan sorts them in every workgroup (or K2s on wide steps); 2 '
                          '(default): 1 on levels whose widest step has >= 512 queries (cfg4: +0.9%%), else 0 (cfg3: '
                          '+2.3%%; DESIGN.md §6d)')
+    ap.add_argument('--k3p-lockstep', type=int, default=0, choices=[0, 1],
+                    help='1: the query blocks of a multi-block scan launch walk each DB chunk in lockstep (L2 reuse; '
+                         'include/ia.h option k3p_lockstep)')
     ap.add_argument('--nn-bound', type=int, default=1, choices=[0, 1],
                     help='1 (default): the pruned levels\' gathers also bound U\' by the causal neighbours\' exact NN rows '
                          '(include/ia.h option nn_bound)')

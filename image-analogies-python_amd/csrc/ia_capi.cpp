@@ -116,6 +116,9 @@ struct ia_ctx {
   HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
   int hand_rows = 0;
   int prefetch_next = 1;         // option "prefetch_next" (NextStep::prefetch)
+  int k3p_lockstep = 0;           // option "k3p_lockstep" (XOScan::prog): blocks of a chunk in lockstep
+  unsigned long long *kprog = nullptr;  // their progress slots (uncached, IA_KPROG_N)
+  unsigned kpseq = 0;
   int nn_bound = 1;              // option "nn_bound" (JobPtrs::nn): the pruned one-rank levels' gathers also
                                  // bound U' by the causal neighbours' exact NN rows, shifted
   int fuse_sort = 2;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
@@ -347,6 +350,7 @@ void ia_destroy(ia_ctx *c) {
   if (c->xbuf) hipFree(c->xbuf);
   if (c->hand) hipFree(c->hand);
   if (c->kslot) hipFree(c->kslot);
+  if (c->kprog) hipFree(c->kprog);
   c->xerr.release();
   c->xo_inv.release();
   hipStreamDestroy(c->st);
@@ -417,6 +421,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "fuse_gather")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_gather must be 0 or 1");
     c->fuse_gather = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "k3p_lockstep")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: k3p_lockstep must be 0 or 1");
+    c->k3p_lockstep = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "nn_bound")) {
@@ -638,6 +647,7 @@ int ia_wavefront_step(int h, int w, int64_t t, int *r0, int *M) {
   return IA_OK;
 }
 
+#define IA_KPROG_N 1024       // option "k3p_lockstep": progress slots (workgroups of one multi-block launch)
 #define IA_FUSE_SORT_MAXW 768  // waves of a k_merge_gather launch whose gathers sort the next step
 #define IA_FUSE_SORT_MINQ 512  // fuse_sort 2: the widest step's queries (all jobs) from which the gathers sort
 
@@ -1447,10 +1457,21 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           if ((n + nch - 1) / nch <= IA_K3P_MAXK_LDS) {
             const int qtb = (qtt + nqb - 1) / nqb;
             const float *tn = c->tnorm.as<float>() + x.t0;
+            unsigned long long *prog = nullptr;  // option "k3p_lockstep"
+            if (c->k3p_lockstep && (nch & 7) == 0 && nqb * nch <= IA_KPROG_N) {
+              if (!c->kprog) {
+                HIP_TRY(hipStreamSynchronize(c->st));
+                HIP_TRY(hipExtMallocWithFlags((void **)&c->kprog, IA_KPROG_N * 8, hipDeviceMallocUncached));
+                HIP_TRY(hipMemset(c->kprog, 0, IA_KPROG_N * 8));
+                HIP_TRY(hipDeviceSynchronize());
+              }
+              prog = c->kprog;
+              if (++c->kpseq == 0) c->kpseq = 1;
+            }
             ia_launch_k3p(qtb, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, 0, Mt, sd.Mpad, nch,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t, c->qs_order.as<int>(),
-                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp());
+                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp(), prog, c->kpseq);
             m.nwg = nch;
             pairs_full += (double)n * qtt;
             tiles_full += (double)n * nqb;

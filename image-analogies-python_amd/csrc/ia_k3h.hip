@@ -882,6 +882,50 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // counter slot then holds (pairs with corrections << 32) + box-needed pairs.  HHX: how the
 // correction products follow the filter (0: full chains, 1: fused single chains, 2: fused on
 // query-tile pairs, k3p_hhpairs).
+// option "k3p_lockstep": a multi-block launch's workgroups of one DB chunk (block b = 0..nqb-1,
+// workgroup ids equal mod 8: one XCD) publish their tile-grab progress every 8 tiles (uncached
+// slot prog[b nwg + wg], tagged with the launch's pseq; "done" when the chunk is exhausted); a
+// wave whose grab passes plim (LDS) waits until every other block of the chunk is within
+// IA_K3P_LEAD tiles, so the trailing block's loads hit the L2 lines the leading one brought in.
+// Bounded: a block not yet started (stale tag) or a wait beyond IA_K3P_LOCK_TICKS unlocks the
+// workgroup for the rest of the launch.  Only the order in time changes; every tile is scanned
+// exactly as without it.
+__device__ __forceinline__ void k3p_lockstep(const XOScan &xo, int g, int K, int qblk, int wg, int nwg, int nqb, int lane,
+                                             int &plim) {
+  if (lane != 0) return;
+  if ((g & 7) == 0 || g >= K)
+    __hip_atomic_store(xo.prog + (int64_t)qblk * nwg + wg,
+                       ((unsigned long long)xo.pseq << 32) | (unsigned)(g >= K ? 0x7fffffff : g), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  if (g >= K || g <= __hip_atomic_load(&plim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
+  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+  for (;;) {
+    int pmin = 0x7fffffff;
+    bool known = true;
+    for (int b = 0; b < nqb; b++) {
+      if (b == qblk) continue;
+      // relaxed: the slots are uncached, and only the timing depends on what is read
+      const unsigned long long v =
+          __hip_atomic_load(xo.prog + (int64_t)b * nwg + wg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if ((unsigned)(v >> 32) != xo.pseq) {
+        known = false;
+        break;
+      }
+      pmin = min(pmin, (int)(unsigned)v);
+    }
+    if (!known || (long long)__builtin_amdgcn_s_memrealtime() - t0 > IA_K3P_LOCK_TICKS) {
+      __hip_atomic_store(&plim, 0x7fffffff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // unlocked
+      return;
+    }
+    if (g <= pmin + IA_K3P_LEAD) {
+      __hip_atomic_fetch_max(&plim, min(pmin, 0x7fffffff - IA_K3P_LEAD) + IA_K3P_LEAD, __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_WORKGROUP);
+      return;
+    }
+    __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 template <int KS, int QT, int NW, bool PRE = false, bool HHF = false, int HHX = 0>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
@@ -1003,7 +1047,11 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
   }
   __shared__ int kctr;  // next tile index to hand out
-  if (tid == 0) kctr = NW;
+  __shared__ int plim;  // option "k3p_lockstep": tiles grabbed before the other blocks are checked again
+  if (tid == 0) {
+    kctr = NW;
+    plim = IA_K3P_LEAD;
+  }
   if constexpr (PRE) __syncthreads();
   // the query-tile boxes (min lo, max hi, max U' over the tile's real queries) by 32-lane
   // butterflies over the sorted slots in LDS: the in-kernel-sort path, and the presorted path
@@ -1199,10 +1247,13 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     };
     // tiles handed out through an LDS counter (balances the waves' pair counts; the records stay
     // exact, only which subset holds which row varies)
+    const bool lock = xo.prog != nullptr && nqb > 1;
     auto grab = [&]() -> int {
       int g = 0;
       if (lane == 0) g = atomicAdd(&kctr, 1);
-      return __builtin_amdgcn_readfirstlane(g);
+      g = __builtin_amdgcn_readfirstlane(g);
+      if (lock) k3p_lockstep(xo, g, K, qblk, wg, nwg, nqb, lane, plim);
+      return g;
     };
     auto next_k = [&](int k, unsigned &m) -> int {
       for (; k < K; k = grab()) {
@@ -1217,11 +1268,12 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     if constexpr (HHX == 3) {
     // ---- k3p_variant 22 / 23: the DB stream carries only the hi halves (3.5 of 7 KiB per tile
     // at KS = 4).  Per tile: the hi x hi filter of its box-needed blocks on a hi buffer (two in
-    // rotation, the next tile's in flight); the whole tile is then loaded only when a block
-    // passed (else an L2-hot dummy: equal outstanding loads on every path) and its full chains
+    // rotation, the next tile's in flight); the tile's lo halves are then loaded only when a
+    // block passed (its hi halves copied from the hi buffer; else the same load instructions at
+    // one lane-uniform address: equal outstanding loads on every path) and its full chains
     // (k3p_pairs: v14's products and records) run one tile later, while the next tile is
-    // filtered.  MALL / HBM bytes: hi of every needed tile + lo of the passing ones (39 % of the
-    // loaded tiles at cfg3); the full reload's hi half is an L2 hit (loaded one tile earlier).
+    // filtered.  MALL / HBM bytes: hi of every needed tile + lo of the passing ones (15 % of the
+    // loaded tiles at cfg3 with option nn_bound, 46 % without).
     h16x8 ha[KS], hb[KS];
     const int k_spec = min(wave, K - 1);  // the global round's speculative tile, now L2-hot
     ld_hi<KS>(ha, db, tk(k < K ? k : k_spec), lane);
@@ -1236,7 +1288,18 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       unsigned pass = 0;
       k3p_hhpipe_h<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
       if (pprev) k3p_pairs<KS, QT, 0>(a, ldsh + lane, pprev, tk(kprev), b1, b2, i1);
-      ld_tile<KS>(a, db, tk(pass ? k : k_spec), lane);
+      {
+        // a passing tile: its lo pieces (the hi ones are copied from cur); otherwise the same
+        // instructions at one lane-uniform address (one request each, no bytes streamed), so
+        // every path keeps the same outstanding loads
+        const h16x8 *src = db + (pass ? tk(k) : tk(k_spec)) * TileFmt<KS>::STRIDE;
+#pragma unroll
+        for (int s2 = 0; s2 < KS; s2++) a[2 * s2 + 1] = src[pass ? TileFmt<KS>::off(2 * s2 + 1, lane) : 0];
+        if (pass) {
+#pragma unroll
+          for (int s2 = 0; s2 < KS; s2++) a[2 * s2] = cur[s2];
+        }
+      }
       nfull += __popc(pass);
       ntp += pass != 0u;
       pprev = pass;

@@ -2840,7 +2840,7 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
                    const float4 *tbox, const float *tnorm, hipStream_t st, int nqb, int qt_end, const XOScan *xo,
-                   unsigned long long *stamp) {
+                   unsigned long long *stamp, unsigned long long *prog, unsigned pseq) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
@@ -2870,6 +2870,10 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   XOScan x{};  // off unless an owner-computes step passes its exchange
   if (xo) x = *xo;
   x.stamp = stamp;
+  if (prog && nqb > 1) {  // option "k3p_lockstep"
+    x.prog = prog;
+    x.pseq = pseq;
+  }
   allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nqb * nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row,
                      NT, qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm, nqb, qt_end, x);

@@ -183,6 +183,9 @@ int ia_version(void);
  * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge)
  * / 2 (owner computes: each rank brings its own job, every rank scans its shard for all of them,
  * queries and scan records exchanged by peer writes; emulated: one job per shard).
+ * "k3p_lockstep" = 0 (default) / 1: in a pruned-scan launch over several query blocks (steps
+ * wider than 352 queries, cfg4) the blocks of each DB chunk grab its tiles within 32 of each
+ * other (bounded waits), so the trailing block reads them from the XCD's L2.
  * "nn_bound" = 1 (default) / 0: on pruned one-rank levels the merge also keeps each pixel's certified
  * exact NN row, and the gathers bound U' (the pruned scan's radius) by the causal neighbours' NN
  * rows shifted by the neighbour's offset as well as by the coherence candidates (exact either way:
