@@ -261,8 +261,8 @@ def make_context(args, local):
     ALL_CTX.append(cx)
     cx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
     cx.set_option('prune', args.prune)
-    if args.k3p_variant != 20:
-        cx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15, 18..21
+    if args.k3p_variant != 22:
+        cx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15, 18..23
     cx.set_option('prune_min_rows', args.prune_min_rows)
     if args.k3p_blocks != 1:
         cx.set_option('k3p_blocks', args.k3p_blocks)
@@ -278,8 +278,6 @@ def make_context(args, local):
         cx.set_option('prefetch_next', 0)
     if not args.nn_bound:
         cx.set_option('nn_bound', 0)
-    if args.k3p_lockstep:
-        cx.set_option('k3p_lockstep', 1)
     if args.shard_unpruned:
         cx.set_option('shard_unpruned', 1)
     if args.shard_emulate > 1:
@@ -372,13 +370,14 @@ def main():
                     help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
-    ap.add_argument('--k3p-variant', type=int, default=20, choices=[7, 11, 14, 15, 18, 19, 20, 21, 22, 23],
+    ap.add_argument('--k3p-variant', type=int, default=22, choices=[7, 11, 14, 15, 18, 19, 20, 21, 22, 23],
                     help='pruned-scan kernel version (ia_k3h.hip k3h_prune3, DESIGN.md §4b): 7 = need tests interleaved '
                          'with the contraction, bitonic in-kernel query sort, reverse walks on alternate steps; 11 = 7 on '
                          'queries presorted once per step; 14 / 15 = 7 / 11 with the hi x hi block filter; 18 / 19 = 14 / '
-                         '15 with the correction products fused onto the hi x hi accumulator (single chains); 20 '
-                         '(default) / 21 = the same on query-tile pairs (two chains); 22 / 23 = 14 / 15 streaming only the '
-                         'hi halves of the DB tiles, the whole tile loaded for the filter-passing ones (chains one tile later)')
+                         '15 with the correction products fused onto the hi x hi accumulator (single chains); 20 / 21 = '
+                         'the same on query-tile pairs (two chains); 22 (default) / 23 = 14 / 15 streaming only the hi '
+                         'halves of the DB tiles, the lo halves loaded for the filter-passing ones (chains one tile '
+                         'later); steps wider than 512 queries run 21 under 20 and 22')
     ap.add_argument('--pipeline', type=int, default=1, choices=[0, 1],
                     help='1 (default; one-job configs and replicas): consecutive levels overlap (two libia '
                          'contexts, each level\'s steps waiting only for the steps of the previous level they read; '
@@ -391,9 +390,6 @@ def main():
                          'option fuse_sort); 0: the scan sorts them in every workgroup (or K2s on wide steps); 2 '
                          '(default): 1 on levels whose widest step has >= 512 queries (cfg4: +0.9%%), else 0 (cfg3: '
                          '+2.3%%; DESIGN.md §6d)')
-    ap.add_argument('--k3p-lockstep', type=int, default=0, choices=[0, 1],
-                    help='1: the query blocks of a multi-block scan launch walk each DB chunk in lockstep (L2 reuse; '
-                         'include/ia.h option k3p_lockstep)')
     ap.add_argument('--nn-bound', type=int, default=1, choices=[0, 1],
                     help='1 (default): the pruned levels\' gathers also bound U\' by the causal neighbours\' exact NN rows '
                          '(include/ia.h option nn_bound)')
@@ -416,10 +412,10 @@ def main():
     ap.add_argument('--prune-group', type=int, default=1, choices=[1, 2, 4, 8],
                     help='pruned levels: Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)')
     ap.add_argument('--prune-min-rows', type=int, default=None,
-                    help='smallest DB (rows) the pruned scan is used on (default: 262,144 = the 512^2 level too for '
-                         'the pipelined cfg3 job, where its lighter scan interferes less with the finest level: '
-                         '+0.9-1.9 %% on three boxes, profiles/r04/prune512; 524,288 = the 1024^2 level otherwise, '
-                         'libia\'s own default: cfg4 lost 4 %% with 262,144, profiles/r04/k3p_hi)')
+                    help='smallest DB (rows) the pruned scan is used on (default: 262,144 = the 512^2 A level too for '
+                         'the pipelined cfg3 and cfg4 jobs, where its lighter scan interferes less with the finest level: '
+                         'cfg3 +0.9-1.9 %% on three boxes (profiles/r04/prune512), cfg4 +2.3 %% with option nn_bound '
+                         '(profiles/r04/nn_bound); 524,288 = the 1024^2 level otherwise, libia\'s own default)')
     ap.add_argument('--shard-unpruned', action='store_true',
                     help='shard (or emulate shards of) levels that scan unpruned too (default: only pruned levels, '
                          'DESIGN.md §7)')
@@ -447,7 +443,7 @@ def main():
     if args.config == 'cfg5' and args.shard_emulate > 1 and not args.sequential:
         ap.error('--shard-emulate takes one job per level call: add --sequential for cfg5')
     if args.prune_min_rows is None:
-        args.prune_min_rows = 262144 if (args.config == 'cfg3' and args.pipeline) else 524288
+        args.prune_min_rows = 262144 if (args.config in ('cfg3', 'cfg4') and args.pipeline) else 524288
     if args.traffic_json is None:
         args.traffic_json = os.path.join(ROOT, 'profiles', 'k3p_traffic_%s.json' % args.config)
     import torch

@@ -107,7 +107,7 @@ struct ia_ctx {
   int shard_unpruned = 0;        // option "shard_unpruned": 1 = shard levels that scan unpruned too
   int prune_group = 1;           // option "prune_group": Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)
   int matcher = IA_MATCH_F16X3;  // option "matcher"
-  int k3p_variant = 20;          // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
+  int k3p_variant = 22;          // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   int k3p_blocks = 1;            // option "k3p_blocks": 1 = a wide step's presorted pruned scan is one launch over
                                  // all its query blocks (2-D grid); 0 = one launch per block
@@ -116,9 +116,6 @@ struct ia_ctx {
   HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
   int hand_rows = 0;
   int prefetch_next = 1;         // option "prefetch_next" (NextStep::prefetch)
-  int k3p_lockstep = 0;           // option "k3p_lockstep" (XOScan::prog): blocks of a chunk in lockstep
-  unsigned long long *kprog = nullptr;  // their progress slots (uncached, IA_KPROG_N)
-  unsigned kpseq = 0;
   int nn_bound = 1;              // option "nn_bound" (JobPtrs::nn): the pruned one-rank levels' gathers also
                                  // bound U' by the causal neighbours' exact NN rows, shifted
   int fuse_sort = 2;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
@@ -350,7 +347,6 @@ void ia_destroy(ia_ctx *c) {
   if (c->xbuf) hipFree(c->xbuf);
   if (c->hand) hipFree(c->hand);
   if (c->kslot) hipFree(c->kslot);
-  if (c->kprog) hipFree(c->kprog);
   c->xerr.release();
   c->xo_inv.release();
   hipStreamDestroy(c->st);
@@ -368,7 +364,8 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     c->stamps = value;
     return IA_OK;
   }
-  if (!std::strcmp(name, "k3p_variant")) {  // 20 (default) / 21: hi x hi block filter with the correction
+  if (!std::strcmp(name, "k3p_variant")) {  // 22 (default; hi-only DB stream, presorted steps run 21) / 20 /
+                                            // 21: hi x hi block filter with the correction
                                             // products fused on query-tile pairs (in-kernel sort up to 512
                                             // queries, presorted 21 above); 14 / 15: the filter, then full
                                             // chains; 18 / 19: fused, single chains; 7 / 11: v7 (DESIGN.md
@@ -421,11 +418,6 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "fuse_gather")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_gather must be 0 or 1");
     c->fuse_gather = value;
-    return IA_OK;
-  }
-  if (!std::strcmp(name, "k3p_lockstep")) {
-    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: k3p_lockstep must be 0 or 1");
-    c->k3p_lockstep = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "nn_bound")) {
@@ -647,7 +639,6 @@ int ia_wavefront_step(int h, int w, int64_t t, int *r0, int *M) {
   return IA_OK;
 }
 
-#define IA_KPROG_N 1024       // option "k3p_lockstep": progress slots (workgroups of one multi-block launch)
 #define IA_FUSE_SORT_MAXW 768  // waves of a k_merge_gather launch whose gathers sort the next step
 #define IA_FUSE_SORT_MINQ 512  // fuse_sort 2: the widest step's queries (all jobs) from which the gathers sort
 
@@ -1431,7 +1422,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     const bool gsorted = fsort && gathered == t && gsort;
     const int k3v = (kv == 11 || kv == 15 || kv == 19 || kv == 21 || kv == 23) ? kv
                     : (prune && (wide || gsorted)
-                           ? (kv == 14 ? 15 : kv == 18 ? 19 : kv == 20 ? 21 : kv == 22 ? 23 : 11)
+                           ? (kv == 14 ? 15 : kv == 18 ? 19 : kv == 20 || kv == 22 ? 21 : 11)
                            : kv);
     const bool presorted = k3v == 11 || k3v == 15 || k3v == 19 || k3v == 21 || k3v == 23;
     const float4 *tboxp = gsorted ? nullptr : c->qs_tbox.as<float4>();  // nullptr: boxes from the slice
@@ -1457,21 +1448,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           if ((n + nch - 1) / nch <= IA_K3P_MAXK_LDS) {
             const int qtb = (qtt + nqb - 1) / nqb;
             const float *tn = c->tnorm.as<float>() + x.t0;
-            unsigned long long *prog = nullptr;  // option "k3p_lockstep"
-            if (c->k3p_lockstep && (nch & 7) == 0 && nqb * nch <= IA_KPROG_N) {
-              if (!c->kprog) {
-                HIP_TRY(hipStreamSynchronize(c->st));
-                HIP_TRY(hipExtMallocWithFlags((void **)&c->kprog, IA_KPROG_N * 8, hipDeviceMallocUncached));
-                HIP_TRY(hipMemset(c->kprog, 0, IA_KPROG_N * 8));
-                HIP_TRY(hipDeviceSynchronize());
-              }
-              prog = c->kprog;
-              if (++c->kpseq == 0) c->kpseq = 1;
-            }
             ia_launch_k3p(qtb, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, 0, Mt, sd.Mpad, nch,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t, c->qs_order.as<int>(),
-                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp(), prog, c->kpseq);
+                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp());
             m.nwg = nch;
             pairs_full += (double)n * qtt;
             tiles_full += (double)n * nqb;

@@ -320,14 +320,7 @@ struct XOScan {
   unsigned *err;                  // bit 2: a tile flag did not arrive in time
   long long timeout_ticks;
   unsigned long long *stamp;      // option "stamps" (any K3p launch, owner-computes or not): per-WG ticks
-  // option "k3p_lockstep" (one launch of nqb > 1 query blocks): the blocks of a DB chunk (same
-  // XCD) grab its tiles within IA_K3P_LEAD of each other, so the trailing block reads them from
-  // the XCD's L2; per-WG progress slots (pseq << 32 | tiles grabbed), uncached (nullptr: off)
-  unsigned long long *prog;
-  unsigned pseq;
 };
-#define IA_K3P_LEAD 32          // tiles a block of a chunk may run ahead of the chunk's slowest other block
-#define IA_K3P_LOCK_TICKS 1000  // longest wait for the other blocks (10 us of s_memrealtime), then unlocked
 
 // fused K4(t) + K2p(t + 1) (k_merge_gather, option "fuse_gather"): the next step's gather
 // outputs (the other parity half of the query buffers) and the per-row handoff slots

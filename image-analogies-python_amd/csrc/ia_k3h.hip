@@ -882,50 +882,6 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // counter slot then holds (pairs with corrections << 32) + box-needed pairs.  HHX: how the
 // correction products follow the filter (0: full chains, 1: fused single chains, 2: fused on
 // query-tile pairs, k3p_hhpairs).
-// option "k3p_lockstep": a multi-block launch's workgroups of one DB chunk (block b = 0..nqb-1,
-// workgroup ids equal mod 8: one XCD) publish their tile-grab progress every 8 tiles (uncached
-// slot prog[b nwg + wg], tagged with the launch's pseq; "done" when the chunk is exhausted); a
-// wave whose grab passes plim (LDS) waits until every other block of the chunk is within
-// IA_K3P_LEAD tiles, so the trailing block's loads hit the L2 lines the leading one brought in.
-// Bounded: a block not yet started (stale tag) or a wait beyond IA_K3P_LOCK_TICKS unlocks the
-// workgroup for the rest of the launch.  Only the order in time changes; every tile is scanned
-// exactly as without it.
-__device__ __forceinline__ void k3p_lockstep(const XOScan &xo, int g, int K, int qblk, int wg, int nwg, int nqb, int lane,
-                                             int &plim) {
-  if (lane != 0) return;
-  if ((g & 7) == 0 || g >= K)
-    __hip_atomic_store(xo.prog + (int64_t)qblk * nwg + wg,
-                       ((unsigned long long)xo.pseq << 32) | (unsigned)(g >= K ? 0x7fffffff : g), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-  if (g >= K || g <= __hip_atomic_load(&plim, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP)) return;
-  const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-  for (;;) {
-    int pmin = 0x7fffffff;
-    bool known = true;
-    for (int b = 0; b < nqb; b++) {
-      if (b == qblk) continue;
-      // relaxed: the slots are uncached, and only the timing depends on what is read
-      const unsigned long long v =
-          __hip_atomic_load(xo.prog + (int64_t)b * nwg + wg, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      if ((unsigned)(v >> 32) != xo.pseq) {
-        known = false;
-        break;
-      }
-      pmin = min(pmin, (int)(unsigned)v);
-    }
-    if (!known || (long long)__builtin_amdgcn_s_memrealtime() - t0 > IA_K3P_LOCK_TICKS) {
-      __hip_atomic_store(&plim, 0x7fffffff, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);  // unlocked
-      return;
-    }
-    if (g <= pmin + IA_K3P_LEAD) {
-      __hip_atomic_fetch_max(&plim, min(pmin, 0x7fffffff - IA_K3P_LEAD) + IA_K3P_LEAD, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_WORKGROUP);
-      return;
-    }
-    __builtin_amdgcn_s_sleep(2);
-  }
-}
-
 template <int KS, int QT, int NW, bool PRE = false, bool HHF = false, int HHX = 0>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
@@ -1047,11 +1003,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
   }
   __shared__ int kctr;  // next tile index to hand out
-  __shared__ int plim;  // option "k3p_lockstep": tiles grabbed before the other blocks are checked again
-  if (tid == 0) {
-    kctr = NW;
-    plim = IA_K3P_LEAD;
-  }
+  if (tid == 0) kctr = NW;
   if constexpr (PRE) __syncthreads();
   // the query-tile boxes (min lo, max hi, max U' over the tile's real queries) by 32-lane
   // butterflies over the sorted slots in LDS: the in-kernel-sort path, and the presorted path
@@ -1247,13 +1199,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     };
     // tiles handed out through an LDS counter (balances the waves' pair counts; the records stay
     // exact, only which subset holds which row varies)
-    const bool lock = xo.prog != nullptr && nqb > 1;
     auto grab = [&]() -> int {
       int g = 0;
       if (lane == 0) g = atomicAdd(&kctr, 1);
-      g = __builtin_amdgcn_readfirstlane(g);
-      if (lock) k3p_lockstep(xo, g, K, qblk, wg, nwg, nqb, lane, plim);
-      return g;
+      return __builtin_amdgcn_readfirstlane(g);
     };
     auto next_k = [&](int k, unsigned &m) -> int {
       for (; k < K; k = grab()) {

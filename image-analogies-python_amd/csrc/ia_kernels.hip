@@ -2840,7 +2840,7 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
                    const float4 *tbox, const float *tnorm, hipStream_t st, int nqb, int qt_end, const XOScan *xo,
-                   unsigned long long *stamp, unsigned long long *prog, unsigned pseq) {
+                   unsigned long long *stamp) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
@@ -2852,7 +2852,7 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   // kmax <= IA_K3P_MAXK_LDS)
   const bool in_kernel_sort = variant == 6 || variant == 14 || variant == 18 || variant == 20 || variant == 22;
   if (in_kernel_sort && Mpad > 512)
-    variant = variant == 14 ? 15 : variant == 18 ? 19 : variant == 20 ? 21 : variant == 22 ? 23 : 1;
+    variant = variant == 14 ? 15 : variant == 18 ? 19 : variant == 20 || variant == 22 ? 21 : 1;
   const k3p_fn fn = g4[qt - 1](variant);
   const size_t NQ = (size_t)qt * IA_TILE;
   const bool pre = variant == 11 || variant == 15 || variant == 19 || variant == 21 || variant == 23;
@@ -2870,10 +2870,6 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   XOScan x{};  // off unless an owner-computes step passes its exchange
   if (xo) x = *xo;
   x.stamp = stamp;
-  if (prog && nqb > 1) {  // option "k3p_lockstep"
-    x.prog = prog;
-    x.pseq = pseq;
-  }
   allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nqb * nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row,
                      NT, qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm, nqb, qt_end, x);

@@ -155,13 +155,14 @@ int ia_version(void);
  * "prune_min_rows" DB rows (default 2^19): (DB tile, query tile) pairs a
  * projection bound proves farther than the query's best coherence candidate are skipped.
  * "k3p_variant" / "k3_variant": kernel versions of DESIGN.md §4b; the product build accepts
- * k3p_variant 20 (default: the pruned scan sorts a step's queries itself up to 512 of them, a
- * step wider than that is sorted once by k_query_sort and runs 21; every box-needed block runs
- * the hi x hi product first and adds the correction products + top-2 only when a value can lie
- * within the query's bound), 21 (always presorted), 14 / 15 (filter, then full chains), 18 / 19
- * (fused corrections, single chains), 7 / 11 (no block filter) and k3_variant 1; DIAG=1 builds
- * every version, including 16 / 17 (rotated DB: rows on the level's 55 principal axes, a 15-axis
- * head filter before the full rows; unsharded levels, else 14 / 15).
+ * k3p_variant 22 (default: the pruned scan sorts a step's queries itself up to 512 of them and
+ * streams only the hi halves of the DB tiles; every box-needed block runs the hi x hi product
+ * first, and a tile with a block whose value can lie within its query's bound loads its lo
+ * halves for the full products + top-2 one tile later; a step wider than 512 queries is sorted
+ * once by k_query_sort and runs 21), 20 (the same on whole tiles; 21 presorted), 23 (22
+ * presorted), 14 / 15 (filter, then full chains), 18 / 19 (fused corrections, single chains),
+ * 7 / 11 (no block filter) and k3_variant 1.  The other versions of DESIGN.md §4b / §4f are in
+ * git history.
  * "k3p_blocks" = 1 (default) / 0: a presorted pruned scan wider than one launch's 11 query tiles
  * runs as ONE launch of (query block x DB chunk) workgroups instead of one launch per block.
  * "fuse_gather" = 1 (default) / 0: on one-job unsharded pruned levels the merge of step t and the
@@ -183,9 +184,6 @@ int ia_version(void);
  * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge)
  * / 2 (owner computes: each rank brings its own job, every rank scans its shard for all of them,
  * queries and scan records exchanged by peer writes; emulated: one job per shard).
- * "k3p_lockstep" = 0 (default) / 1: in a pruned-scan launch over several query blocks (steps
- * wider than 352 queries, cfg4) the blocks of each DB chunk grab its tiles within 32 of each
- * other (bounded waits), so the trailing block reads them from the XCD's L2.
  * "nn_bound" = 1 (default) / 0: on pruned one-rank levels the merge also keeps each pixel's certified
  * exact NN row, and the gathers bound U' (the pruned scan's radius) by the causal neighbours' NN
  * rows shifted by the neighbour's offset as well as by the coherence candidates (exact either way:

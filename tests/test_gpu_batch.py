@@ -94,7 +94,7 @@ def test_batched_512_pruned_wide_step(ctx, variant):
         Ss, IMs, sts = _run(ctx, z, js, False)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 20)
+        ctx.set_option('k3p_variant', 22)
     for j in range(len(jb)):
         for level in range(1, job.L):
             assert np.array_equal(Sb[j][level], Ss[j][level]) and np.array_equal(IMb[j][level], IMs[j][level])
@@ -157,7 +157,7 @@ def test_device_sweep_two_streams_equals_one(ctx):
 
 
 @pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_seq', 'pruned_v11', 'pruned_v18', 'pruned_v20',
-                                  'pruned_lockstep', 'pruned_lockstep_v22'])
+                                  'pruned_v23'])
 def test_batched_g256_wide_steps_match_reference(ctx, mode):
     """8 jobs on the golden g256 run's A side: job 0 is the reference's own
     run, jobs 1..7 other kappas and B' seeds.  On the 256^2 level a step holds 8 x 86 = 688
@@ -167,17 +167,14 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
         2 query blocks x 128 DB chunks (k3p_blocks = 1, the default);
       pruned_seq: the same as one launch per query block (k3p_blocks = 0);
       pruned_v11: without the hi x hi block filter;
-      pruned_lockstep(_v22): the two blocks of each DB chunk in lockstep (option k3p_lockstep;
-        with the hi-only DB stream).
+      pruned_v23: the hi-only DB stream's presorted form.
     Job 0 must reproduce the reference's s, im and B' on every level; every job must equal its
     own separate run (86-query steps: a single launch, the in-kernel sort)."""
     z = load_e2e('g256')
     if mode != 'unpruned':
         ctx.set_option('prune_min_rows', 1)
-    if mode in ('pruned_v11', 'pruned_v18', 'pruned_v20', 'pruned_lockstep_v22'):
+    if mode in ('pruned_v11', 'pruned_v18', 'pruned_v20', 'pruned_v23'):
         ctx.set_option('k3p_variant', int(mode[-2:]))
-    if mode.startswith('pruned_lockstep'):
-        ctx.set_option('k3p_lockstep', 1)
     if mode == 'pruned_seq':
         ctx.set_option('k3p_blocks', 0)
     try:
@@ -187,9 +184,8 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
         Ss, IMs, sts = _run(ctx, z, js, False)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 20)
+        ctx.set_option('k3p_variant', 22)
         ctx.set_option('k3p_blocks', 1)
-        ctx.set_option('k3p_lockstep', 0)
     h, w = z['B_pyr'][-1].shape
     assert 8 * min(h, (w + 2) // 3) > 512
     for level in range(1, z['L']):   # job 0 is the reference's own run

@@ -43,7 +43,7 @@ def _run_debug(ctx, z, prune_all=False, variant=20):
             out[level] = (s, im, dbg)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 20)
+        ctx.set_option('k3p_variant', 22)
     return out, Bp, st
 
 
