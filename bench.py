@@ -272,7 +272,7 @@ def make_context(args, local):
         cx.set_option('fuse_gather', args.fuse_gather)
     if args.fuse_unpruned:
         cx.set_option('fuse_unpruned', 1)
-    if args.fuse_sort != 2:
+    if args.fuse_sort:
         cx.set_option('fuse_sort', args.fuse_sort)
     if not args.prefetch_next:
         cx.set_option('prefetch_next', 0)
@@ -385,11 +385,10 @@ def main():
     ap.add_argument('--fuse-gather', type=int, default=1, choices=[0, 1],
                     help='1 (default): on pruned one-job levels the merge of step t and the gather of step t + 1 run '
                          'as one launch (ia_kernels.hip k_merge_gather); 0: separate launches')
-    ap.add_argument('--fuse-sort', type=int, default=2, choices=[0, 1, 2],
+    ap.add_argument('--fuse-sort', type=int, default=0, choices=[0, 1, 2],
                     help='1: the fused gathers of step t + 1 also sort its queries for the presorted scan (include/ia.h '
-                         'option fuse_sort); 0: the scan sorts them in every workgroup (or K2s on wide steps); 2 '
-                         '(default): 1 on levels whose widest step has >= 512 queries (cfg4: +0.9%%), else 0 (cfg3: '
-                         '+2.3%%; DESIGN.md §6d)')
+                         'option fuse_sort); 0 (default): the scan sorts them in every workgroup (or K2s on wide steps); '
+                         '2: 1 on levels whose widest step has >= 512 queries (DESIGN.md §6d)')
     ap.add_argument('--nn-bound', type=int, default=1, choices=[0, 1],
                     help='1 (default): the pruned levels\' gathers also bound U\' by the causal neighbours\' exact NN rows '
                          '(include/ia.h option nn_bound)')

@@ -28,6 +28,31 @@ namespace {
 
 thread_local std::string g_last_error;
 
+// Waves of the handoff-chained launches (k_merge_gather: a gather waits for the merge of the row
+// above) of every level in flight in this process.  A wave waits only for its row predecessor
+// and no two waves share one, so a stall needs every resident slot held by a waiter whose
+// predecessor is not yet dispatched: >= 2 x the resident slots (4 per CU at k_merge_gather's
+// 264 VGPRs) chained waves in flight at once.  A level chains only if its widest launch fits in
+// the budget left (ia_synthesize_levels is synchronous: its launches are done when it returns);
+// otherwise it runs the separate gather / merge launches.  (cfg5's 16-job batches of 512^2
+// steps, 2,736 waves per launch on three streams, hit the 20 s handoff timeout without this.)
+static std::atomic<int> g_chain_waves{0};
+struct ChainReservation {
+  int n = 0;
+  ~ChainReservation() {
+    if (n) g_chain_waves.fetch_sub(n);
+  }
+  bool take(int w, int budget) {
+    int cur = g_chain_waves.load();
+    while (cur + w <= budget)
+      if (g_chain_waves.compare_exchange_weak(cur, cur + w)) {
+        n = w;
+        return true;
+      }
+    return false;
+  }
+};
+
 int fail(int code, const std::string &msg) {
   g_last_error = msg;
   return code;
@@ -118,9 +143,11 @@ struct ia_ctx {
   int prefetch_next = 1;         // option "prefetch_next" (NextStep::prefetch)
   int nn_bound = 1;              // option "nn_bound" (JobPtrs::nn): the pruned one-rank levels' gathers also
                                  // bound U' by the causal neighbours' exact NN rows, shifted
-  int fuse_sort = 2;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
-                                 // 2 (auto) = on levels whose widest step has >= IA_FUSE_SORT_MINQ queries: a
-                                 // 342-query step loses 1.7 us, a 683-query step gains 3
+  int fuse_sort = 0;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
+                                 // 2 = on levels whose widest step has >= IA_FUSE_SORT_MINQ queries; off by
+                                 // default: no gain left with nn_bound
+  int chain_budget = 0;          // waves of handoff-chained launches this context's CUs hold deadlock-free
+                                 // (ia_init: 2 x the resident merge-gather waves - a margin; see g_chain_waves)
   unsigned long long *kslot = nullptr;  // their per-query key slots (uncached)
   int kslot_n = 0;
   unsigned hseq = 0;
@@ -314,6 +341,10 @@ int ia_init(int device, ia_ctx **out) {
   if (se != hipSuccess) {
     delete c;
     return fail(IA_EHIP, "ia_init: hipStreamCreate failed");
+  }
+  {  // g_chain_waves: 4 resident k_merge_gather waves per CU of this context's slice, twice, less 1/16
+    const int ncu = split_n > 1 ? prop.multiProcessorCount / split_n : prop.multiProcessorCount;
+    c->chain_budget = 2 * 4 * ncu - (2 * 4 * ncu) / 16;
   }
   hipEventCreate(&c->lv0);
   hipEventCreate(&c->lv1);
@@ -1076,8 +1107,12 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   // (batched jobs: one handoff row set per job.  Unpruned levels - K2h fused, option
   // "fuse_unpruned" - measured slower: their longer fused launches delay the pipelined finest
   // level's scans, and cfg5's batched 512^2 steps lose 1-2 %)
-  const bool chain = c->fuse_gather && use_h && g.ch == 1 && ma.img_rows == 0 && g.bw >= 3 &&
-                     (prune || c->fuse_unpruned) && ((!multi && !xo && mas[0].nwg <= 4 * IA_WAVE) || (xo && prune));
+  bool chain = c->fuse_gather && use_h && g.ch == 1 && ma.img_rows == 0 && g.bw >= 3 &&
+               (prune || c->fuse_unpruned) && ((!multi && !xo && mas[0].nwg <= 4 * IA_WAVE) || (xo && prune));
+  // (one-rank levels: the process-wide chained-wave budget, g_chain_waves; a launch holds at most
+  // Mpad + J waves: merges, entering rows, pads)
+  ChainReservation chain_res;
+  if (chain && !xo && !chain_res.take((int)(Mpad_max + J), c->chain_budget)) chain = false;
   if (chain) {
     const int hrows = g.bh * J;  // per job (local owner)
     if (c->hand_rows < hrows) {
@@ -1112,7 +1147,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   };
   int64_t gathered = -1;  // the step whose gather the previous fused launch ran
   bool gsort = false;     // ... and that launch also sorted it (option "fuse_sort": no K2s, no in-scan sort)
-  const bool fsort = chain && prune && !xo && (c->fuse_sort == 1 || (c->fuse_sort == 2 && Mtmax >= IA_FUSE_SORT_MINQ));
+  // (the gathers' sort waits for every wave of its launch: only while all chained waves in flight
+  // fit the resident slots, half the budget)
+  const bool fsort = chain && prune && !xo && (c->fuse_sort == 1 || (c->fuse_sort == 2 && Mtmax >= IA_FUSE_SORT_MINQ)) &&
+                     g_chain_waves.load() <= c->chain_budget / 2;
   const int64_t n_timed = stride ? (T + stride - 1) / stride : 0;
   for (auto *v : {&c->evs, &c->evg, &c->evm})
     if ((int64_t)v->size() < 2 * n_timed) {

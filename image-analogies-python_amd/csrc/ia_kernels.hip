@@ -2070,6 +2070,10 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
   int mn = -1;   // this wave's query of step t + 1
   int job = 0;
   QPre pf;       // its step-independent inputs, prefetched during the merge (pruned levels)
+#if IA_PROBE & 8  // diagnostic build only: fused merge + gather phase stamps of one sampled wave
+  unsigned long long gs[5] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0};
+  const bool gprobe = w == sd.M / 2 && (sd.t % 256) == 128 && JM == sd.M;
+#endif
   if (w < JM) {
     const QPix px = ia_qpix(sd, g.bw, w);
     job = px.job;
@@ -2100,6 +2104,10 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
     h.s0c = o.pc;
     h.i0 = o.img;
     h.n0 = o.nn;
+#if IA_PROBE & 8
+    __builtin_amdgcn_s_waitcnt(0);
+    gs[1] = __builtin_amdgcn_s_memtime();
+#endif
   } else if (w < JM + J) {
     job = w - JM;
     if (nx.sn.t - 3 * (nx.sn.r0 + nx.sn.M - 1) == 0) mn = job * nx.sn.M + nx.sn.M - 1;  // a row enters at column 0
@@ -2145,6 +2153,10 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
     h.i1 = hs->im;
     h.n1 = hs->nn;
   }
+#if IA_PROBE & 8
+  __builtin_amdgcn_s_waitcnt(0);
+  gs[2] = __builtin_amdgcn_s_memtime();
+#endif
   __builtin_amdgcn_wave_barrier();  // the merge's LDS rows are done with
   if constexpr (PR) {
     const bool pub = (XO && nx.xp.W) || (!XO && nx.kslot);
@@ -2155,6 +2167,13 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
   } else {
     gather_h_query_fused<KS>(g, nx.sn, B, mn, lane, nx.mu, nx.q64, nx.qn2, qf, h);
   }
+#if IA_PROBE & 8
+  __builtin_amdgcn_s_waitcnt(0);
+  gs[3] = __builtin_amdgcn_s_memtime();
+  if (gprobe && lane == 0)
+    printf("GSTAMP bw=%d t=%d M=%d merge=%llu handoff_wait=%llu gather=%llu\n", g.bw, sd.t, sd.M, gs[1] - gs[0],
+           gs[2] - gs[1], gs[3] - gs[2]);
+#endif
 }
 template <int RPL, bool PR, bool XO, class JS>
 __global__ void __launch_bounds__(IA_PQ_WG) k_merge_gather(LevelGeo g, StepDesc sd, Imgs A, MergeArgs ma, JS jobs,

@@ -191,10 +191,13 @@ int ia_version(void);
  * "prefetch_next" = 1 (default) / 0: a fused merge + gather wave loads its next query's inputs
  * that do not depend on the launch's own merges (features, causal neighbours' sources) while
  * its merge's DB rows load.
- * "fuse_sort" = 2 (default, auto) / 1 / 0: the fused gathers of step t + 1 also rank its queries'
- * sort keys across the launch and write the presorted scan inputs (no K2s launch, no per-workgroup
- * sort in the scan).  2: on levels whose widest step has >= 512 queries (all jobs), where it
- * replaces a K2s launch and is measured faster; exact either way.
+ * "fuse_sort" = 0 (default) / 1 / 2: the fused gathers of step t + 1 also rank its queries' sort
+ * keys across the launch and write the presorted scan inputs (no K2s launch, no per-workgroup
+ * sort in the scan).  2: only on levels whose widest step has >= 512 queries (all jobs).  Exact
+ * either way; no faster since option nn_bound.
+ * Fused merge + gather launches (option "fuse_gather") wait row to row; a level uses them only
+ * while the chained waves of all levels in flight in the process stay under twice the GPU's
+ * resident k_merge_gather waves (else it runs separate launches; ia_capi.cpp g_chain_waves).
  * "stamps" = 1: every pruned-scan and fused-merge launch of a pruned level stamps its
  * workgroups' first / last s_memrealtime tick; ia_stats.k3p_stamp_ms / merge_stamp_ms sum the
  * per-launch device times (bench.py roofline.frac_timed: the timed, pipelined steps' own kernels).

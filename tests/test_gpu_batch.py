@@ -249,3 +249,37 @@ def test_cfg5_sweep_full_size(ctx):
         assert len(mism) <= max(1, npx // 100), (level, mism)
     for c in ctxs[1:]:
         c.close()
+
+
+def test_cfg5_pruned_batches_fit_the_chain_budget(ctx):
+    """cfg5 with its 512^2 finest levels pruned (prune_min_rows 262,144): 16-job batches put
+    16 x 171 = 2,736 queries in a step, and three contexts run such levels at once.  Fused
+    merge + gather launches that many waves wide could stall on each other's row handoffs (every
+    resident slot held by a wave whose predecessor row is not dispatched); the process-wide
+    chained-wave budget (ia_capi.cpp g_chain_waves) makes those levels run separate launches.
+    The run must finish and equal the unpruned batched run bit for bit."""
+    from ia_amd import _native, sweep, synth
+    n = synth.CONFIGS['cfg5'][0]['size']
+    A = synth.smooth(n, n, 2, 1)
+    sw = sweep.Sweep(A, [synth.filt(A)], synth.smooth(n, n, 2, 2), sweep.cfg5_jobs())
+    dev = torch.device('cuda', 0)
+    ctxs = [ctx, _native.Context(0), _native.Context(0)]
+    try:
+        ref = sweep.DeviceSweep(sw, range(len(sw.jobs)), torch, dev)
+        ref.run(ctxs, _native.Stats(), batched=True, max_batch=16)
+        for c in ctxs:
+            c.set_option('prune_min_rows', 262144)
+        ds = sweep.DeviceSweep(sw, range(len(sw.jobs)), torch, dev)
+        st = _native.Stats()
+        ds.run(ctxs, st, batched=True, max_batch=16)
+        torch.cuda.synchronize()
+    finally:
+        ctx.set_option('prune_min_rows', 524288)
+        for c in ctxs[1:]:
+            c.close()
+    assert st.pruned_levels > 0 and st.bound_violations == 0
+    for j in range(len(sw.jobs)):
+        for level in range(1, sw.L[j]):
+            assert np.array_equal(ds.S[j][level].cpu().numpy(), ref.S[j][level].cpu().numpy()), (j, level)
+            assert np.array_equal(ds.IM[j][level].cpu().numpy(), ref.IM[j][level].cpu().numpy()), (j, level)
+            assert np.array_equal(ds.Bp[j][level].cpu().numpy(), ref.Bp[j][level].cpu().numpy()), (j, level)

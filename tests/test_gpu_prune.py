@@ -88,7 +88,7 @@ def test_fused_gather_equals_separate_launches(ctx, variant):
         finally:
             ctx.set_option('fuse_gather', 1)
             ctx.set_option('time_dist', 0)
-            ctx.set_option('fuse_sort', 2)
+            ctx.set_option('fuse_sort', 0)
     for Bp, S, IM, st in runs[1:]:
         for level in range(1, job.L):
             assert np.array_equal(S[level], runs[0][1][level]), level
@@ -195,7 +195,7 @@ def test_fused_sort_matches_reference(ctx, name):
             assert np.array_equal(Bp[level], z['Bp_final'][level]), level
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('fuse_sort', 2)
+        ctx.set_option('fuse_sort', 0)
     assert st.bound_violations == 0 and st.kappa_ambiguous == 0 and st.pruned_levels == L - 1
 
 

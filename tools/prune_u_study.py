@@ -94,11 +94,28 @@ nb_rows, _ = nn_rows(np.array(nbq))
 hc, wc = job.B_pyr[level - 1].shape[:2]
 Ahc, Awc = job.A_pyr[level - 1].shape[:2]
 sc, imc = z['s_%d' % (level - 1)].astype(np.int64), z['im_%d' % (level - 1)].astype(np.int64)
-Uns, Uup = [], []
+Uns, Uup, Uold = [], [], []
 for k, r in enumerate(range(r_lo, r_hi + 1)):
     c = step - 3 * r
     qi = r * w + c
     best = Uc[k]
+    # the candidates of every neighbour but the two merged one step earlier ((r, c-1), (r-1, c+2)):
+    # what a gather could evaluate before that step's merges end
+    old_best = np.inf
+    for rr in range(max(0, r - 2), r + 1):
+        for rc in range(max(0, c - 2), min(w, c + 3)):
+            ri = rr * w + rc
+            if ri < qi and (rr, rc) not in ((r, c - 1), (r - 1, c + 2)):
+                pr, pc = s[ri, 0] + r - rr, s[ri, 1] + c - rc
+                if 0 <= pr < A_h and 0 <= pc < A_w:
+                    old_best = min(old_best, ((As[(A_h * im[ri] + pr) * A_w + pc] - Q[k]) ** 2).sum())
+                row = int(nb_rows[nbkey[ri]])
+                img, rem = divmod(row, A_h * A_w)
+                pr, pc = divmod(rem, A_w)
+                pr, pc = pr + r - rr, pc + c - rc
+                if 0 <= pr < A_h and 0 <= pc < A_w:
+                    old_best = min(old_best, ((As[(img * A_h + pr) * A_w + pc] - Q[k]) ** 2).sum())
+    Uold.append(old_best)
     for rr in range(max(0, r - 2), r + 1):
         for rc in range(max(0, c - 2), min(w, c + 3)):
             ri = rr * w + rc
@@ -114,16 +131,17 @@ for k, r in enumerate(range(r_lo, r_hi + 1)):
     pr, pc = 2 * sc[ci, 0] + r % 2, 2 * sc[ci, 1] + c % 2
     up = ((As[(imc[ci] * A_h + pr) * A_w + pc] - Q[k]) ** 2).sum() if pr < A_h and pc < A_w else np.inf
     Uup.append(min(best, up))
-Uns, Uup = np.array(Uns), np.array(Uup)
+Uns, Uup, Uold = np.array(Uns), np.array(Uup), np.array(Uold)
 Qp = Qc @ U_.T
 M = len(Q)
 qorder = np.argsort(morton([quant(Qp[:, i], lo[i], hi[i], bits) for i in range(npc)], bits), kind='stable')
 print('%s level %d step %d: %d queries; U / NN median %.3f (p10 %.3f, p90 %.3f)' % (
     cfg, level, step, M, np.median(Uc / dnn), np.percentile(Uc / dnn, 10), np.percentile(Uc / dnn, 90)))
-for label, Ub in (('+ neighbours NN shifted', Uns), ('+ coarse pick upsampled', Uup)):
+for label, Ub in (('+ neighbours NN shifted', Uns), ('+ coarse pick upsampled', Uup),
+                  ('nbr sets w/o step-t px', Uold)):
     print('  %-24s U / NN median %.3f (p10 %.3f, p90 %.3f)' % (label, np.median(Ub / dnn), np.percentile(Ub / dnn, 10),
                                                               np.percentile(Ub / dnn, 90)))
-for label, Ub in (('U = coherence (today)', Uc), ('U = + nbr NN shifted', Uns), ('U = + coarse upsampled', Uup), ('U = 1.2 NN', 1.2 * dnn), ('U = 1.07 NN', 1.07 * dnn),
+for label, Ub in (('U = coherence (today)', Uc), ('U = + nbr NN shifted', Uns), ('U = + coarse upsampled', Uup), ('U = w/o step-t pixels', Uold), ('U = 1.2 NN', 1.2 * dnn), ('U = 1.07 NN', 1.07 * dnn),
                   ('U = NN', dnn)):
     need = np.zeros(nt, dtype=bool)
     pairs = 0
