@@ -278,6 +278,8 @@ def make_context(args, local):
         cx.set_option('prefetch_next', 0)
     if not args.nn_bound:
         cx.set_option('nn_bound', 0)
+    if args.prefetch_rows:
+        cx.set_option('prefetch_rows', 1)
     if args.shard_unpruned:
         cx.set_option('shard_unpruned', 1)
     if args.shard_emulate > 1:
@@ -389,6 +391,9 @@ def main():
                     help='1: the fused gathers of step t + 1 also sort its queries for the presorted scan (include/ia.h '
                          'option fuse_sort); 0 (default): the scan sorts them in every workgroup (or K2s on wide steps); '
                          '2: 1 on levels whose widest step has >= 512 queries (DESIGN.md §6d)')
+    ap.add_argument('--prefetch-rows', type=int, default=0, choices=[0, 1],
+                    help='1: fused merge + gather waves also start the next query\'s older U\' candidate rows into LDS '
+                         '(LDS-DMA) after the merge\'s row round (include/ia.h option prefetch_rows)')
     ap.add_argument('--nn-bound', type=int, default=1, choices=[0, 1],
                     help='1 (default): the pruned levels\' gathers also bound U\' by the causal neighbours\' exact NN rows '
                          '(include/ia.h option nn_bound)')
@@ -414,7 +419,9 @@ def main():
                     help='smallest DB (rows) the pruned scan is used on (default: 262,144 = the 512^2 A level too for '
                          'the pipelined cfg3 and cfg4 jobs, where its lighter scan interferes less with the finest level: '
                          'cfg3 +0.9-1.9 %% on three boxes (profiles/r04/prune512), cfg4 +2.3 %% with option nn_bound '
-                         '(profiles/r04/nn_bound); 524,288 = the 1024^2 level otherwise, libia\'s own default)')
+                         '(profiles/r04/nn_bound); cfg5\'s 512^2 finest levels: 9.27 -> 14.59 M px/s (profiles/r04/nn_bound4); '
+                         '524,288 = the 1024^2 level otherwise, libia\'s own default: the sequential cfg3 job loses 1.9 %% '
+                         'with 262,144)')
     ap.add_argument('--shard-unpruned', action='store_true',
                     help='shard (or emulate shards of) levels that scan unpruned too (default: only pruned levels, '
                          'DESIGN.md §7)')
@@ -442,7 +449,8 @@ def main():
     if args.config == 'cfg5' and args.shard_emulate > 1 and not args.sequential:
         ap.error('--shard-emulate takes one job per level call: add --sequential for cfg5')
     if args.prune_min_rows is None:
-        args.prune_min_rows = 262144 if (args.config in ('cfg3', 'cfg4') and args.pipeline) else 524288
+        args.prune_min_rows = 262144 if ((args.config in ('cfg3', 'cfg4') and args.pipeline) or args.config == 'cfg5') \
+            else 524288
     if args.traffic_json is None:
         args.traffic_json = os.path.join(ROOT, 'profiles', 'k3p_traffic_%s.json' % args.config)
     import torch
