@@ -141,7 +141,6 @@ struct ia_ctx {
   HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
   int hand_rows = 0;
   int prefetch_next = 1;         // option "prefetch_next" (NextStep::prefetch)
-  int prefetch_rows = 0;         // option "prefetch_rows" (NextStep::prefetch_rows, ia_kernels.hip qpre_rows)
   int nn_bound = 1;              // option "nn_bound" (JobPtrs::nn): the pruned one-rank levels' gathers also
                                  // bound U' by the causal neighbours' exact NN rows, shifted
   int fuse_sort = 0;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
@@ -455,11 +454,6 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "nn_bound")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: nn_bound must be 0 or 1");
     c->nn_bound = value;
-    return IA_OK;
-  }
-  if (!std::strcmp(name, "prefetch_rows")) {
-    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: prefetch_rows must be 0 or 1");
-    c->prefetch_rows = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "prefetch_next")) {
@@ -1568,7 +1562,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       nx.err = c->xerr.as<unsigned>();
       nx.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
       nx.prefetch = c->prefetch_next;
-      nx.prefetch_rows = c->prefetch_rows;
       // the gathers also sort step t + 1 into k_query_sort's outputs when every wave of the launch
       // can be resident at once (each gather waits for all of the step's keys): k_merge_gather
       // holds one wave per SIMD (264 VGPRs), 1,024 on the chip; 768 leaves room for the kernels of

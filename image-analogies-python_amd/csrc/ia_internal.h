@@ -354,7 +354,6 @@ struct NextStep {
   // per-workgroup sort (kslot = nullptr: off)
   unsigned long long *kslot;
   int prefetch;              // option "prefetch_next": the gathers' step-independent inputs load during the merge
-  int prefetch_rows;         // option "prefetch_rows": ... and their older U' candidate rows, by LDS-DMA
   int *sorder;
   float4 *sinfo;
   void *sfrag;

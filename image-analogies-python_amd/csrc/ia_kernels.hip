@@ -1405,10 +1405,6 @@ struct QPre {
   double v = 0.;
   int sr = 0, sc = 0, si = 0;
   int nn = -1;  // lane 15 + k: causal neighbour k's exact NN row (option "nn_bound")
-  // option "prefetch_rows": this lane's U' candidate row (-1: none), its fp64 row already on its
-  // way into the wave's LDS slice (qpre_rows)
-  bool rows = false;
-  int crow = -1;
 };
 __device__ __forceinline__ QPre qpre_load(const LevelGeo &g, const StepDesc &sn, const Imgs &B, const JobPtrs &jp, int m, int lane) {
   constexpr int D = 55;
@@ -1452,37 +1448,6 @@ __device__ __forceinline__ int ucand_row(const LevelGeo &g, int r, int c, int nr
   return (sr >= 0 && tr >= 0 && tr < g.ah && tc >= 0 && tc < g.aw) ? (si * g.ah + tr) * g.aw + tc : -1;
 }
 
-// option "prefetch_rows" (k_merge_gather, pruned levels): after the merge's own row round, each
-// lane whose U' candidate of the next query comes from a neighbour older than step t starts its
-// fp64 DB row (56 doubles, 28 16-byte pieces) into the wave's LDS slice rl by LDS-DMA (piece j of
-// lane L at rl[64 j + 2 L]); the rows land while the merge finishes and the row above hands its
-// pixel over, so the gather computes those distances from LDS.  The two step-t neighbours
-// ((r, c - 1), (r - 1, c + 2): lanes 9 / 11 and 24 / 26) are left out of U' (their sources exist
-// only after this launch's merges; any subset of DB rows still bounds the NN distance from above).
-// Nothing in the compiler orders a ds_read behind these loads: merge_gather_body waits vmcnt(0)
-// before the gather.
-__device__ __forceinline__ void qpre_rows(const LevelGeo &g, const StepDesc &sn, int m, int lane, QPre &p,
-                                          const double *__restrict__ db64, double *rl) {
-  const QPix px = ia_qpix(sn, g.bw, m);
-  const int r = px.r, c = px.c;
-  p.rows = true;
-  p.crow = -1;
-  if (px.qi > 0 && lane < 30) {
-    const bool nnl = lane >= 15;
-    const int k = nnl ? lane - 15 : lane;
-    const int nr = r - 2 + k / 5, nc = c - 2 + k % 5;
-    if (k != 9 && k != 11 && nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < px.qi)
-      p.crow = ucand_row(g, r, c, nr, nc, nnl, p.sr, p.sc, p.si, p.nn);
-  }
-  if (p.crow >= 0) {
-    const double *src = db64 + (int64_t)p.crow * Geo<1>::DS;
-#pragma unroll
-    for (int j = 0; j < Geo<1>::DS / 2; j++)
-      __builtin_amdgcn_global_load_lds((const void *)(src + 2 * j), (__attribute__((address_space(3))) void *)(rl + 64 * j), 16,
-                                       0, 0);
-  }
-}
-
 // K2p's work for one query m of step sd (one wave): q64, qn2, fragments, pruning record (also
 // returned, uniform, for the owner-computes publish); xh0 / xh1 (optional) receive the query's
 // hi / lo columns
@@ -1493,7 +1458,7 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
                                                const double *__restrict__ db64, const double *__restrict__ basis, double ufac,
                                                float4 *__restrict__ qinfo, const Imgs &A, double *qsh, _Float16 *xh0,
                                                _Float16 *xh1, const QHand &h, float4 &o0, float4 &o1, float4 &o2,
-                                               const QPre &pf = QPre{}, const double *pf_rows_lds = nullptr) {
+                                               const QPre &pf = QPre{}) {
   constexpr int D = 55, KD = 16 * KS;
   static_assert(KD <= IA_WAVE, "one feature per lane");
   const QPix px = ia_qpix(sd, g.bw, m);
@@ -1506,9 +1471,7 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
   // out-of-range or missing one is skipped); only its tightness depends on them.
   int crow = -1;
   const bool nnl = jp.nn && lane >= 15 && lane < 30;
-  if (pf.rows) {
-    crow = pf.crow;  // its row is in the wave's LDS slice (qpre_rows)
-  } else if (qi > 0 && (lane < 15 || nnl)) {
+  if (qi > 0 && (lane < 15 || nnl)) {
     const int k = lane < 15 ? lane : lane - 15;
     const int nr = r - 2 + k / 5, nc = c - 2 + k % 5;
     if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
@@ -1566,17 +1529,7 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
   for (int i = 0; i < IA_NPC; i++) p[i] = wave_sum_d_x(p[i]);
   __builtin_amdgcn_wave_barrier();  // qsh written by this wave's lanes, read below
   double u = DBL_MAX;
-  if (pf.rows) {  // (the caller waited for the LDS-DMA rows before this gather's own stores)
-    if (crow >= 0) {
-      const double *rl = pf_rows_lds + 2 * lane;
-      u = pw_sum<55>([&](int f) {
-        const double d = rl[64 * (f >> 1) + (f & 1)] - qsh[f];
-        return d * d;
-      });
-    }
-  } else if (crow >= 0) {
-    u = exact_dist_level<1>(db64, crow, qsh, IMG ? &A : nullptr);
-  }
+  if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh, IMG ? &A : nullptr);
   u = wave_min_d_x(u);
   // the pruning record (uniform values): projection interval, U' and the Morton key, and K3p's
   // hi x hi block filter bound (k3p_variant 14/15, ia_k3h.hip k3p_filtered): value bound
@@ -1656,11 +1609,11 @@ struct MergeOut {  // one pixel's result: B' value (first channel), source pixel
 struct NoPre {
   __device__ __forceinline__ void operator()() const {}
 };
-template <int CH, bool IMG, int RPL, class Pre = NoPre, class Pre2 = NoPre>
+template <int CH, bool IMG, int RPL, class Pre = NoPre>
 __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &a,
                                             int m, const JobPtrs &jp, const QPix &px,
                                             double *qs, double *ws, int *cand_row, float *cand_v,
-                                            MergeOut *out = nullptr, Pre pre = Pre{}, Pre2 pre2 = Pre2{}) {
+                                            MergeOut *out = nullptr, Pre pre = Pre{}) {
 #if IA_PROBE & 8
   unsigned long long stamp[8] = {0, 0, 0, 0, 0, 0, 0, 0};
 #endif
@@ -1802,9 +1755,6 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   if (unw == 12345.) stamp[7] = 2;
 #endif
   IA_STAMP(3);
-  // (k_merge_gather: the next query's older U' candidate rows start into LDS here, after this
-  // round's own rows were waited for)
-  pre2();
 
   // exact NN candidates of this lane: its rerank row, then any overflow it listed (rare)
   double nd = (lane >= NCOH && my_row >= 0) ? unw : DBL_MAX;
@@ -2113,8 +2063,6 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
   __shared__ int crsh[IA_PQ_WPB][IA_WAVE];
   __shared__ float cvsh[IA_PQ_WPB][IA_WAVE];
   __shared__ __attribute__((aligned(16))) _Float16 xh[IA_PQ_WPB][2][16 * KS];  // owner publish: hi / lo columns
-  // option "prefetch_rows": the next query's U' candidate rows (qpre_rows; lanes 0..31, 28 pieces)
-  __shared__ __attribute__((aligned(16))) double rsh[PR ? IA_PQ_WPB : 1][PR ? 64 * Geo<1>::DS / 2 : 1];
   if (XO && w >= JM + J + (nx.sn.Mpad - J * nx.sn.M)) {  // the waiter (nx.wait_n > 0 only)
     // after an earlier timeout of this context: no waiting (one lost peer costs one timeout)
     if (__hip_atomic_load(nx.err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return;
@@ -2147,11 +2095,7 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
     auto pre = [&]() {
       if (PR && nx.prefetch && mn >= 0) pf = qpre_load(g, nx.sn, Bj, jp, mn, lane);
     };
-    auto pre2 = [&]() {
-      if constexpr (PR)
-        if (nx.prefetch_rows && pf.on) qpre_rows(g, nx.sn, mn, lane, pf, ma.db64, rsh[wv]);
-    };
-    merge_fused<1, false, RPL>(g, sd, A, ma, w, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv], &o, pre, pre2);
+    merge_fused<1, false, RPL>(g, sd, A, ma, w, jp, px, qsh[wv], wsh[wv], crsh[wv], cvsh[wv], &o, pre);
     if (px.r + 1 < g.bh && px.c >= 2) {  // row r + 1 gathers (r + 1, c - 2) at step t + 1
       HandSlot *hs = nx.hand + (int64_t)job * g.bh + px.r;
       if (lane == 0) {
@@ -2227,11 +2171,8 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
   __builtin_amdgcn_wave_barrier();  // the merge's LDS rows are done with
   if constexpr (PR) {
     const bool pub = (XO && nx.xp.W) || (!XO && nx.kslot);
-    // the LDS-DMA rows of qpre_rows have landed (nothing else orders the gather's ds_reads behind
-    // them; waited here, before the gather issues stores of its own)
-    if (pf.rows) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     gather_p_query<KS, false, true>(g, nx.sn, B, jp, mn, lane, nx.mu, nx.q64, nx.qn2, qf, ma.db64, nx.basis, nx.ufac,
-                                    nx.qinfo, A, qsh[wv], pub ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2, pf, rsh[wv]);
+                                    nx.qinfo, A, qsh[wv], pub ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2, pf);
     if (XO && nx.xp.W) xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
     if (!XO && nx.kslot) sorted_publish<KS>(nx, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
   } else {

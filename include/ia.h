@@ -184,10 +184,6 @@ int ia_version(void);
  * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge)
  * / 2 (owner computes: each rank brings its own job, every rank scans its shard for all of them,
  * queries and scan records exchanged by peer writes; emulated: one job per shard).
- * "prefetch_rows" = 0 (default) / 1: with prefetch_next, a fused merge + gather wave also starts
- * the fp64 rows of its next query's U' candidates that come from neighbours older than the step
- * into LDS (LDS-DMA) after the merge's own row round; the gather then takes their distances from
- * LDS and leaves the two step-t neighbours' candidates out of U' (exact either way).
  * "nn_bound" = 1 (default) / 0: on pruned one-rank levels the merge also keeps each pixel's certified
  * exact NN row, and the gathers bound U' (the pruned scan's radius) by the causal neighbours' NN
  * rows shifted by the neighbour's offset as well as by the coherence candidates (exact either way:

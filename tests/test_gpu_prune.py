@@ -171,13 +171,12 @@ def test_pruned_scan_over_512_tiles_per_workgroup(ctx, variant):
     assert st1.dist_tiles < st1.dist_tiles_full
 
 
-@pytest.mark.parametrize('opt', ['fuse_sort', 'prefetch_rows'])
+@pytest.mark.parametrize('opt', ['fuse_sort'])
 @pytest.mark.parametrize('name', ['g64', 'ties128', 'k25', 'g256'])
 def test_fused_sort_matches_reference(ctx, name, opt):
-    """options fuse_sort / prefetch_rows with every level pruned: each fused merge + gather ranks
-    the next step's keys across its waves and writes the presorted scan inputs (ia_kernels.hip
-    sorted_publish), or starts the next query's older U' candidate rows into LDS by LDS-DMA
-    (qpre_rows); s, im and B' of every level equal the reference run's."""
+    """option fuse_sort with every level pruned: each fused merge + gather ranks the next step's
+    keys across its waves and writes the presorted scan inputs (ia_kernels.hip sorted_publish);
+    s, im and B' of every level equal the reference run's."""
     from ia_amd import _native
     from golden_util import BIG_CASES, E2E_CASES, load_e2e
     if name not in E2E_CASES + BIG_CASES:
@@ -224,22 +223,3 @@ def test_nn_bound_is_exact_and_tighter(ctx):
              st0.dist_pairs_corrected / st0.dist_pairs_full, st1.dist_pairs_corrected / st1.dist_pairs_full,
              st0.fallbacks, st1.fallbacks))
 
-
-def test_prefetch_rows_is_exact(ctx):
-    """option prefetch_rows at 1024^2 (both pruned levels): the gathers take the older U'
-    candidates' rows from LDS (LDS-DMA during the merge) and leave the two step-t neighbours'
-    candidates out of U'; s, im and B' equal the default run's bit for bit."""
-    from ia_amd import synth
-    job = synth.make_job(1024)
-    Bp0, S0, IM0, st0 = _run(ctx, job, 1, 22)
-    ctx.set_option('prefetch_rows', 1)
-    try:
-        Bp1, S1, IM1, st1 = _run(ctx, job, 1, 22)
-    finally:
-        ctx.set_option('prefetch_rows', 0)
-    for level in range(1, job.L):
-        assert np.array_equal(S0[level], S1[level]), level
-        assert np.array_equal(IM0[level], IM1[level]), level
-        assert np.array_equal(Bp0[level], Bp1[level]), level
-    assert st1.bound_violations == 0
-    print('pairs %.4f -> %.4f of the full scan' % (st0.dist_pairs / st0.dist_pairs_full, st1.dist_pairs / st1.dist_pairs_full))
