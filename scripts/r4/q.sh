@@ -11,6 +11,6 @@ IA_TEST_SHARE_GPU=1 timeout -k 10 600 python -u -m pytest tests/test_gpu_multira
 tail -3 $O/pytest_multirank.log
 IA_BENCH_SHARE_GPU=1 IA_BENCH_BACKEND=gloo timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --steps 2 --warmup 1 --no-cpu-baseline > $O/bench_n2.json 2> $O/bench_n2.err || { echo "bench n2 failed"; tail -30 $O/bench_n2.err; exit 1; }
 python3 -c "
-import json; d=json.load(open('$O/bench_n2.json'))
+import json; d=[json.loads(l) for l in open('$O/bench_n2.json') if l.startswith('{')][0]
 print({k: d.get(k) for k in ('value','value_replicas','value_strong','shard_parity','strong_parity','ms_per_step')})"
 echo ALL-OK
