@@ -815,6 +815,10 @@ def main():
         roofline['k3_us_per_launch_timed'] = st_all['k3p_stamp_ms'] * 1e3 / st_all['k3p_stamp_launches']
         roofline['k3_launches_timed'] = st_all['k3p_stamp_launches']
         roofline['algorithmic_bytes_per_launch_timed'] = st_all['k3p_bytes_all'] / st_all['k3p_stamp_launches']
+        # the launch = its workgroups' start spread (dispatch, CUs held by concurrent kernels)
+        # + their mean duration + the imbalance tail
+        roofline['k3_wg_us_timed'] = st_all['k3p_stamp_wg_ms'] * 1e3 / st_all['k3p_stamp_launches']
+        roofline['k3_start_spread_us_timed'] = st_all['k3p_stamp_start_ms'] * 1e3 / st_all['k3p_stamp_launches']
         if st_all['merge_stamp_launches'] > 0:
             roofline['merge_us_per_launch_timed'] = st_all['merge_stamp_ms'] * 1e3 / st_all['merge_stamp_launches']
             roofline['merge_launches_timed'] = st_all['merge_stamp_launches']

@@ -1016,7 +1016,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   int64_t k3_n = 0, mg_n = 0;
   if (stamped) {
     if ((rc = c->stamp_k3.ensure((size_t)k3_cap * IA_NWG_H * 16)) || (rc = c->stamp_mg.ensure((size_t)mg_cap * mg_stride * 16)) ||
-        (rc = c->stamp_dur.ensure((size_t)(k3_cap + mg_cap) * 16)))
+        (rc = c->stamp_dur.ensure((size_t)(2 * k3_cap + mg_cap) * 16)))
       return rc;
     HIP_TRY(hipMemsetAsync(c->stamp_k3.p, 0, (size_t)k3_cap * IA_NWG_H * 16, c->st));
     HIP_TRY(hipMemsetAsync(c->stamp_mg.p, 0, (size_t)mg_cap * mg_stride * 16, c->st));
@@ -1612,7 +1612,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   HIP_TRY(hipEventRecord(c->lv2, c->st));
   if (stamped) {  // per-launch device ticks: K3p launches first, then the merges
     ia_launch_stamp_durations(c->stamp_k3.as<unsigned long long>(), (int)k3_n, IA_NWG_H, c->stamp_dur.as<unsigned long long>(),
-                              c->st);
+                              c->st, c->stamp_dur.as<unsigned long long>() + 2 * (k3_n + mg_n));
     ia_launch_stamp_durations(c->stamp_mg.as<unsigned long long>(), (int)mg_n, mg_stride,
                               c->stamp_dur.as<unsigned long long>() + 2 * k3_n, c->st);
   }
@@ -1737,6 +1737,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         stats->prune_ms_timed = stats->prune_flops_timed = stats->prune_bytes_timed = 0.;
         stats->prune_launches_timed = 0;
         stats->k3p_stamp_ms = stats->k3p_bytes_all = stats->merge_stamp_ms = stats->stamp_gap_ms = stats->stamp_window_ms = 0.;
+        stats->k3p_stamp_start_ms = stats->k3p_stamp_wg_ms = 0.;
         stats->k3p_stamp_launches = stats->merge_stamp_launches = stats->stamp_gaps = 0;
         stats->prune_rows = g.NA;
       }
@@ -1749,6 +1750,18 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       for (int64_t i = 0; i < k3_n; i++) tk += (double)(sp[2 * i + 1] - sp[2 * i]);
       for (int64_t i = k3_n; i < k3_n + mg_n; i++) tm += (double)(sp[2 * i + 1] - sp[2 * i]);
       stats->k3p_stamp_ms += tk * 1e-5;  // 100 MHz ticks
+      {  // the launches' start spread and mean workgroup duration (k_stamp_durations span2)
+        std::vector<unsigned long long> s2((size_t)2 * k3_n);
+        HIP_TRY(hipMemcpy(s2.data(), c->stamp_dur.as<unsigned long long>() + 2 * (k3_n + mg_n), s2.size() * 8,
+                          hipMemcpyDeviceToHost));
+        double ss = 0., sw = 0.;
+        for (int64_t i = 0; i < k3_n; i++) {
+          ss += (double)s2[2 * i];
+          sw += (double)s2[2 * i + 1];
+        }
+        stats->k3p_stamp_start_ms += ss * 1e-5;
+        stats->k3p_stamp_wg_ms += sw * 1e-5;
+      }
       stats->k3p_stamp_launches += k3_n;
       stats->merge_stamp_ms += tm * 1e-5;
       stats->merge_stamp_launches += mg_n;

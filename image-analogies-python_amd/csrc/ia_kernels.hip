@@ -2291,30 +2291,45 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd
 // atomicAdd per counter (integer sums are order-free; counters are zeroed per level)
 // option "stamps": launch i's first workgroup start and last workgroup end over its `stride`
 // workgroup slots (unwritten slots are zero), in s_memrealtime ticks; one wave per launch
+// span2 (optional): per launch the last workgroup start - the first, and the mean workgroup
+// duration (ticks)
 __global__ void __launch_bounds__(IA_WAVE) k_stamp_durations(const unsigned long long *__restrict__ stamps, int stride,
-                                                            unsigned long long *__restrict__ span) {
+                                                            unsigned long long *__restrict__ span,
+                                                            unsigned long long *__restrict__ span2) {
   const int i = blockIdx.x, lane = threadIdx.x;
-  unsigned long long lo = ~0ull, hi = 0ull;
+  unsigned long long lo = ~0ull, hi = 0ull, smax = 0ull, dsum = 0ull, n = 0ull;
   for (int j = lane; j < stride; j += IA_WAVE) {
     const unsigned long long a = stamps[2 * ((int64_t)i * stride + j)], b = stamps[2 * ((int64_t)i * stride + j) + 1];
     if (a) {
       lo = a < lo ? a : lo;
       hi = b > hi ? b : hi;
+      smax = a > smax ? a : smax;
+      dsum += b > a ? b - a : 0ull;
+      n++;
     }
   }
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {
-    const unsigned long long l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64);
+    const unsigned long long l2 = __shfl_xor(lo, o, 64), h2 = __shfl_xor(hi, o, 64), m2 = __shfl_xor(smax, o, 64);
     lo = l2 < lo ? l2 : lo;
     hi = h2 > hi ? h2 : hi;
+    smax = m2 > smax ? m2 : smax;
+    dsum += __shfl_xor(dsum, o, 64);
+    n += __shfl_xor(n, o, 64);
   }
   if (lane == 0) {
-    span[2 * i] = hi >= lo && hi ? lo : 0ull;
-    span[2 * i + 1] = hi >= lo && hi ? hi : 0ull;
+    const bool ok = hi >= lo && hi;
+    span[2 * i] = ok ? lo : 0ull;
+    span[2 * i + 1] = ok ? hi : 0ull;
+    if (span2) {
+      span2[2 * i] = ok ? smax - lo : 0ull;
+      span2[2 * i + 1] = ok && n ? dsum / n : 0ull;
+    }
   }
 }
-void ia_launch_stamp_durations(const unsigned long long *stamps, int n, int stride, unsigned long long *span, hipStream_t st) {
-  if (n > 0) hipLaunchKernelGGL(k_stamp_durations, dim3(n), dim3(IA_WAVE), 0, st, stamps, stride, span);
+void ia_launch_stamp_durations(const unsigned long long *stamps, int n, int stride, unsigned long long *span, hipStream_t st,
+                               unsigned long long *span2) {
+  if (n > 0) hipLaunchKernelGGL(k_stamp_durations, dim3(n), dim3(IA_WAVE), 0, st, stamps, stride, span, span2);
 }
 
 __global__ void __launch_bounds__(IA_WG) k_reduce_stats(const unsigned *__restrict__ pstat, int64_t n,

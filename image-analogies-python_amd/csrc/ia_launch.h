@@ -23,7 +23,8 @@ void ia_launch_db64_build(const LevelGeo &g, const Imgs &A, double *db64, hipStr
 int ia_db64_stride(int ch);
 void ia_launch_reduce_stats(const unsigned *pstat, int64_t n, unsigned long long *counters, hipStream_t st);
 // option "stamps": per launch (min start, max end) ticks over its stride workgroup slots
-void ia_launch_stamp_durations(const unsigned long long *stamps, int n, int stride, unsigned long long *span, hipStream_t st);
+void ia_launch_stamp_durations(const unsigned long long *stamps, int n, int stride, unsigned long long *span, hipStream_t st,
+                               unsigned long long *span2 = nullptr);
 void ia_launch_dense_db(int KH, const double *pts, int64_t n, int d, int n_tiles, const double *mu, float4 *db,
                         unsigned *Rbits, hipStream_t st);
 void ia_launch_dense_query(int KH, const double *q, int64_t nq, int d, int Mpad, const double *mu, double *qn2, float *qf,

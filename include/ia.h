@@ -107,6 +107,8 @@ typedef struct {
   double stamp_window_ms;   /* those levels' first scan start -> last kernel end */
   int64_t prune_rows;       /* DB rows of the pruned levels in prune_*, k3p_*, merge_stamp_* and
                              * stamp_* (the largest pruned level seen: the bench's finest) */
+  double k3p_stamp_start_ms; /* the same K3p launches: last workgroup start - first start, summed */
+  double k3p_stamp_wg_ms;    /* ... their mean workgroup duration (end - start), summed */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
