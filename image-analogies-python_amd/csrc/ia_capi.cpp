@@ -924,7 +924,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   // option "nn_bound": per-pixel exact NN rows of a pruned one-rank level (-1 until merged)
   for (int j = 0; j < J; j++) {
     jp[j].nn = nullptr;
-    if (prune && (!multi || xo) && c->nn_bound) {  // (owner-computes: the owner merges its own job)
+    if (prune && c->nn_bound) {  // (every merge form writes it: fused, owner-computes, exchange finishes)
       JobBufs &b = c->jb[j];
       if ((rc = b.NN.ensure((size_t)NB * 4))) return rc;
       jp[j].nn = b.NN.as<int32_t>();

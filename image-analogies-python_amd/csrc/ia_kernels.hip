@@ -1139,7 +1139,7 @@ template <int CH>
 __device__ void finish_pick(const LevelGeo &g, const Imgs &A, const double *__restrict__ db64, int r, int c,
                             int64_t app_ix, const CohPick &ck, const double *q, int32_t *__restrict__ s,
                             int32_t *__restrict__ im, double *__restrict__ Bp, const double *__restrict__ weights, double kf,
-                            unsigned *pstat, unsigned stat) {
+                            unsigned *pstat, unsigned stat, int32_t *__restrict__ nn = nullptr) {
   constexpr int D = Geo<CH>::D;
   const int lane = threadIdx.x & 63;
   const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
@@ -1173,6 +1173,7 @@ __device__ void finish_pick(const LevelGeo &g, const Imgs &A, const double *__re
     s[2 * qi + 1] = pc;
     im[qi] = img;
     if (pstat) pstat[qi] = stat | (kamb ? 1u << 29 : 0u) | (coh_won ? 1u << 30 : 0u);
+    if (nn) nn[qi] = app_ix >= 0 && app_ix < (int64_t)g.NA ? (int)app_ix : -1;  // option "nn_bound"
   }
 }
 // coherence + kappa + writeback for query pixel (r, c) whose NN row is app_ix
@@ -1180,9 +1181,10 @@ template <int CH>
 __device__ void finish_pixel(const LevelGeo &g, const Imgs &A, const double *__restrict__ db64, int r, int c, int64_t app_ix,
                              const double *q,
                              int32_t *__restrict__ s, int32_t *__restrict__ im, double *__restrict__ Bp,
-                             const double *__restrict__ weights, double kf, unsigned *pstat, unsigned stat) {
+                             const double *__restrict__ weights, double kf, unsigned *pstat, unsigned stat,
+                             int32_t *__restrict__ nn = nullptr) {
   const CohPick ck = coherence_pick<CH>(g, db64, r, c, q, s, im);
-  finish_pick<CH>(g, A, db64, r, c, app_ix, ck, q, s, im, Bp, weights, kf, pstat, stat);
+  finish_pick<CH>(g, A, db64, r, c, app_ix, ck, q, s, im, Bp, weights, kf, pstat, stat, nn);
 }
 
 // Both distances of DB row `row` against query q from ONE set of feature loads (the row of the
@@ -1984,7 +1986,7 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_level(LevelGeo g, StepDesc s
   return;
 #endif
   if constexpr (FUSED) {
-    finish_pixel<CH>(g, A, ma.db64, px.r, px.c, wn.idx, q, jp.s, jp.im, jp.Bp, jp.weights, jp.kf, jp.pstat, stat);
+    finish_pixel<CH>(g, A, ma.db64, px.r, px.c, wn.idx, q, jp.s, jp.im, jp.Bp, jp.weights, jp.kf, jp.pstat, stat, jp.nn);
   } else {
     if ((threadIdx.x & 63) == 0) {
       win[m] = wn;
@@ -2212,7 +2214,7 @@ __global__ void __launch_bounds__(IA_WG) k_finish_level(LevelGeo g, StepDesc sd,
   const JobPtrs jp = jobs.get(px.job);
   const unsigned prev = jp.pstat ? jp.pstat[px.qi] : 0u;
   finish_pixel<CH>(g, A, db64, px.r, px.c, bi, q64 + (int64_t)m * Geo<CH>::D, jp.s, jp.im, jp.Bp, jp.weights, jp.kf,
-                   jp.pstat, prev);
+                   jp.pstat, prev, jp.nn);
 }
 
 // Sharded level, peer-write exchange (option "exchange" = 1): the certified winner of this
@@ -2282,7 +2284,7 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_xchg(LevelGeo g, StepDesc sd
       bi = 0;
       if (lane == 0) atomicOr(xa.err, 2u);
     }
-    finish_pick<CH>(g, A, ma.db64, px.r, px.c, bi, ck, q, jp.s, jp.im, jp.Bp, jp.weights, jp.kf, jp.pstat, stat);
+    finish_pick<CH>(g, A, ma.db64, px.r, px.c, bi, ck, q, jp.s, jp.im, jp.Bp, jp.weights, jp.kf, jp.pstat, stat, jp.nn);
   }
 }
 
