@@ -278,8 +278,6 @@ def make_context(args, local):
         cx.set_option('prefetch_next', 0)
     if not args.nn_bound:
         cx.set_option('nn_bound', 0)
-    if args.k3p_pool:
-        cx.set_option('k3p_pool', args.k3p_pool)
     if args.shard_unpruned:
         cx.set_option('shard_unpruned', 1)
     if args.shard_emulate > 1:
@@ -391,9 +389,6 @@ def main():
                     help='1: the fused gathers of step t + 1 also sort its queries for the presorted scan (include/ia.h '
                          'option fuse_sort); 0 (default): the scan sorts them in every workgroup (or K2s on wide steps); '
                          '2: 1 on levels whose widest step has >= 512 queries (DESIGN.md §6d)')
-    ap.add_argument('--k3p-pool', type=int, default=0,
-                    help='percentage of a one-rank scan\'s DB tiles handed out from a shared pool to whichever '
-                         'workgroups finish their own first (include/ia.h option k3p_pool; 0: off)')
     ap.add_argument('--nn-bound', type=int, default=1, choices=[0, 1],
                     help='1 (default): the pruned levels\' gathers also bound U\' by the causal neighbours\' exact NN rows '
                          '(include/ia.h option nn_bound)')

@@ -141,8 +141,6 @@ struct ia_ctx {
   HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
   int hand_rows = 0;
   int prefetch_next = 1;         // option "prefetch_next" (NextStep::prefetch)
-  int k3p_pool = 0;              // option "k3p_pool": % of a one-rank v22 scan's tiles in the shared pool (XOScan)
-  DevBuf pool;                   // its counters and per-workgroup lists, two step parities
   int nn_bound = 1;              // option "nn_bound" (JobPtrs::nn): the pruned one-rank levels' gathers also
                                  // bound U' by the causal neighbours' exact NN rows, shifted
   int fuse_sort = 0;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
@@ -365,7 +363,7 @@ void ia_destroy(ia_ctx *c) {
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
                     &c->boxes, &c->qinfo, &c->pairs, &c->ord, &c->qs_order, &c->qs_info, &c->qs_frag, &c->qs_tbox, &c->tnorm,
-                    &c->stamp_k3, &c->stamp_mg, &c->stamp_dur, &c->pool,
+                    &c->stamp_k3, &c->stamp_mg, &c->stamp_dur,
                     &c->py_in, &c->py_tmp, &c->py_sm, &c->py_mm, &c->py_out})
     b->release();
   for (auto *v : {&c->evs, &c->evg, &c->evm, &c->p_ev[0], &c->p_ev[1], &c->p_ev[2]})
@@ -451,11 +449,6 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "fuse_gather")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: fuse_gather must be 0 or 1");
     c->fuse_gather = value;
-    return IA_OK;
-  }
-  if (!std::strcmp(name, "k3p_pool")) {
-    if (value < 0 || value > 50) return fail(IA_EINVAL, "ia_set_option: k3p_pool is a percentage, 0..50");
-    c->k3p_pool = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "nn_bound")) {
@@ -1153,7 +1146,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     qinfo = prune ? c->qinfo.as<float4>() + h * 3 * Mpad_max : nullptr;
   };
   int64_t gathered = -1;  // the step whose gather the previous fused launch ran
-  bool pool_fresh = true;  // option "k3p_pool": zero both parities' counters at the level's first pooled scan
   bool gsort = false;     // ... and that launch also sorted it (option "fuse_sort": no K2s, no in-scan sort)
   // (the gathers' sort waits for every wave of its launch: only while all chained waves in flight
   // fit the resident slots, half the budget)
@@ -1482,8 +1474,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       for (size_t i = 0; i < shards.size(); i++) {
         const Shard &x = shards[i];
         MergeArgs &m = mas[i];
-        m.pool_list = nullptr;  // option "k3p_pool": set below by a pooled scan only
-        m.pool_cnt = nullptr;
         const int n = x.t1 - x.t0;
         const char *dbp = (const char *)c->db.p + (size_t)(x.t0 - g.tile0) * tile_bytes;
         m.nwg = x.nwg;
@@ -1521,47 +1511,12 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t,
                           c->qs_order.as<int>(), 0, sd.r0, nullptr, tboxp, tn, c->st, 1, 0, nullptr, k3_stamp());
-          else if (prune) {
-            // option "k3p_pool" (one-rank, one query block, v22 in-kernel sort; every merge of such
-            // a level is merge_fused, which reads the lists): the last k3p_pool % of each chunk's
-            // tiles go to a shared pool, stream-ordered counters alternating by step parity
-            XOScan pxs{};
-            const XOScan *pxp = nullptr;
-            m.pool_list = nullptr;
-            m.pool_cnt = nullptr;
-            if (c->k3p_pool > 0 && k3v == 22 && nqb == 1 && !multi && !xo && shards.size() == 1) {
-              const int kfull = (n + x.nwg - 1) / x.nwg;
-              const int ks = std::max(1, kfull - std::max(1, kfull * c->k3p_pool / 100));
-              const int p0 = std::min(n, x.nwg * ks), np = n - p0;
-              const int pl = 4 * ((np + x.nwg - 1) / x.nwg) + 8;
-              const size_t per = 2 + (size_t)x.nwg * pl + (size_t)x.nwg;  // ints per parity
-              if (np > 0) {
-                if (c->pool.cap < 2 * per * 4 || pool_fresh) {
-                  if ((rc = c->pool.ensure(2 * per * 4))) return rc;
-                  HIP_TRY(hipMemsetAsync(c->pool.p, 0, 2 * per * 4, c->st));
-                  pool_fresh = false;
-                }
-                int *base = c->pool.as<int>() + (sd.t & 1) * per, *other = c->pool.as<int>() + ((sd.t + 1) & 1) * per;
-                pxs.pool_ctr = base;
-                pxs.pool_ctr_next = other;
-                pxs.pool_list = base + 2;
-                pxs.pool_cnt = base + 2 + (size_t)x.nwg * pl;
-                pxs.pool_ks = ks;
-                pxs.pool_p0 = p0;
-                pxs.pool_pl = pl;
-                pxp = &pxs;
-                m.pool_list = pxs.pool_list;
-                m.pool_cnt = pxs.pool_cnt;
-                m.pool_pl = pl;
-                m.pool_tend = p0;
-              }
-            }
+          else if (prune)
             ia_launch_k3p(qt, dbp, c->qf.p, qinfot, m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
                           k3v, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
-                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, pxp, k3_stamp());
-          }
+                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, nullptr, k3_stamp());
           else if (use_h)
             ia_launch_k3h(g.KS, qt, dbp, c->qf.p, n, x.tpw, qt0, Mt, x.nwg, m.pos0, g.n_tiles, (float4 *)m.rec,
                           (float *)m.recT, c->k3_variant, c->st);

@@ -106,10 +106,6 @@ struct MergeArgs {
   unsigned *xo_err = nullptr;         // bit 3: a record did not arrive in time
   long long xo_timeout = 0;
   unsigned long long *stamp = nullptr;  // option "stamps": this launch's per-workgroup (start, end)
-  // option "k3p_pool": chunk w = tiles w + nwg k below pool_tend + its listed pool tiles
-  const int *pool_list = nullptr;
-  const int *pool_cnt = nullptr;
-  int pool_pl = 0, pool_tend = 0;
 };
 
 // Per-launch device timing without HIP events (option "stamps"): every workgroup of a stamped
@@ -324,16 +320,6 @@ struct XOScan {
   unsigned *err;                  // bit 2: a tile flag did not arrive in time
   long long timeout_ticks;
   unsigned long long *stamp;      // option "stamps" (any K3p launch, owner-computes or not): per-WG ticks
-  // option "k3p_pool" (one-rank in-kernel-sort launches, k3p_variant 22): workgroup wg's own tiles
-  // are wg + nwg k for k < pool_ks; the rest, tiles [pool_p0, NT), form a pool that workgroups
-  // take one tile at a time (pool_ctr) once their own are done, listing each in pool_list[wg
-  // pool_pl + i], i < pool_cnt[wg] (the merge's certification rescans read it; -1: none);
-  // pool_ctr_next = the next launch's counter, zeroed here (pool_ctr = nullptr: off)
-  int *pool_ctr;
-  int *pool_ctr_next;
-  int *pool_list;
-  int *pool_cnt;
-  int pool_ks, pool_p0, pool_pl;
 };
 
 // fused K4(t) + K2p(t + 1) (k_merge_gather, option "fuse_gather"): the next step's gather

@@ -929,10 +929,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     qinfo += 3 * (int64_t)qblk * Mpad;
   }
   const int qtb = PRE ? min(QT, qt_end - qt0) : QT;  // query tiles of this block (PRE: the last may hold fewer)
-  // option "k3p_pool" (XOScan::pool_ctr; one-rank in-kernel-sort v22 launches): own tiles k < pool_ks only
-  const bool pool = HHX == 3 && !PRE && xo.pool_ctr != nullptr && !xo.on && nqb == 1;
-  const int K = pool ? min((NT - wg + nwg - 1) / nwg, xo.pool_ks)
-                     : (NT - wg + nwg - 1) / nwg;  // tiles wg + nwg*k, k < K (host: nwg <= NT, K <= IA_K3P_MAXK_LDS)
+  const int K = (NT - wg + nwg - 1) / nwg;  // tiles wg + nwg*k, k < K (host: nwg <= NT, K <= IA_K3P_MAXK_LDS)
   // rev: this step walks the workgroup's tiles in reverse (alternate steps: the tiles read last
   // by one step are read first by the next, while they are still in the memory-side cache)
   auto tk = [&](int k) { return wg + nwg * (rev ? K - 1 - k : k); };
@@ -1006,12 +1003,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
   }
   __shared__ int kctr;  // next tile index to hand out
-  __shared__ int pcnt;  // option "k3p_pool": pool list slots taken by this workgroup
-  if (tid == 0) {
-    kctr = NW;
-    pcnt = 0;
-    if (pool && blockIdx.x == 0) *xo.pool_ctr_next = 0;  // the next launch's pool (stream-ordered)
-  }
+  if (tid == 0) kctr = NW;
   if constexpr (PRE) __syncthreads();
   // the query-tile boxes (min lo, max hi, max U' over the tile's real queries) by 32-lane
   // butterflies over the sorted slots in LDS: the in-kernel-sort path, and the presorted path
@@ -1188,7 +1180,8 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     const float4 ctl = cl ? tlo[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
     const float4 cth = cl ? thi[lane] : ctl;
     const float ctu = cl ? tU[lane] : -INFINITY;
-    auto need_box = [&](const float4 blo, const float4 bhi) -> unsigned {
+    auto need_k = [&](int k) -> unsigned {
+      const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
       const bool cpass = cl && prune_lb(blo, bhi, ctl, cth) <= ctu;
       const unsigned coarse = (unsigned)__ballot(cpass);
       unsigned msk = 0;
@@ -1204,7 +1197,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       }
       return msk & coarse;
     };
-    auto need_k = [&](int k) -> unsigned { return need_box(wbox[2 * k], wbox[2 * k + 1]); };
     // tiles handed out through an LDS counter (balances the waves' pair counts; the records stay
     // exact, only which subset holds which row varies)
     auto grab = [&]() -> int {
@@ -1272,41 +1264,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       step3(hb, ha);
     }
     if (pprev) k3p_pairs<KS, QT, 0>(a, ldsh + lane, pprev, tk(kprev), b1, b2, i1);
-    if (pool) {
-      // option "k3p_pool": own tiles done - take pool tiles one at a time (a list slot first, so
-      // every tile taken is listed for the merge), each tested, filtered and contracted at once
-      const int NP = NT - xo.pool_p0;
-      for (;;) {
-        int slot = 0, pi = 0;
-        if (lane == 0) {
-          slot = atomicAdd(&pcnt, 1);
-          pi = slot < xo.pool_pl ? atomicAdd(xo.pool_ctr, 1) : NP;
-        }
-        slot = __builtin_amdgcn_readfirstlane(slot);
-        pi = __builtin_amdgcn_readfirstlane(pi);
-        if (slot >= xo.pool_pl) break;
-        const int t = xo.pool_p0 + pi;
-        if (lane == 0) xo.pool_list[(int64_t)wg * xo.pool_pl + slot] = pi < NP ? t : -1;
-        if (pi >= NP) break;
-        const unsigned mk = need_box(boxes[2 * t], boxes[2 * t + 1]);
-        if (mk) {
-          h16x8 hh[KS];
-          ld_hi<KS>(hh, db, t, lane);
-          const float rt = tnorm[t];
-          f32x16 acc[2];
-          unsigned pass = 0;
-          k3p_hhpipe_h<KS, QT, 0>(hh, ldsh + lane, mk, rt, qzt + (lane & 31), qzw + (lane & 31), acc, pass);
-          if (pass) {
-            ld_tile<KS>(a, db, t, lane);
-            k3p_pairs<KS, QT, 0>(a, ldsh + lane, pass, t, b1, b2, i1);
-          }
-          nfull += __popc(pass);
-          ntp += pass != 0u;
-          cnt += __popc(mk);
-          ntl++;
-        }
-      }
-    }
     } else {
     // (re)load the first needed tile unconditionally (usually the speculative one again: a
     // cache hit), so the loop is entered with the same outstanding loads on every path
@@ -1438,7 +1395,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       stp += wtp[w];
     }
     pairs[blockIdx.x] += sp + (HHF ? sf << 32 : 0ull);
-    if (pool) xo.pool_cnt[wg] = min(pcnt, xo.pool_pl);
     tiles[blockIdx.x] += st + (stp << 32);  // (tiles with a filter-passing block << 32) + tiles loaded
   }
   if (xo.stamp) {  // (uniform) option "stamps": the workgroup's first and last tick

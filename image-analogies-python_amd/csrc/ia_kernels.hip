@@ -1821,15 +1821,10 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
           tst = a.xo_nch;
           tend = ia_shard_off(a.NT, a.xo_W, sh + 1);
         }
-        // (option "k3p_pool": the chunk's own tiles end at pool_tend; its listed pool tiles follow)
-        if (a.pool_cnt) tend = min(tend, (int64_t)a.pool_tend);
-        const int npl = a.pool_cnt ? a.pool_cnt[wgid] : 0;
-        const int64_t nown = t0 < tend ? (tend - t0 + tst - 1) / tst : 0;
-        for (int64_t tb = 0; tb < nown + npl; tb += IA_WAVE) {
-          const int64_t x = tb + lane;  // the chunk's x-th tile: own ones, then the listed pool ones
-          const int64_t t = x < nown ? t0 + tst * x : x < nown + npl ? a.pool_list[(int64_t)wgid * a.pool_pl + (x - nown)] : -1;
+        for (int64_t tb = 0; t0 + tst * tb < tend; tb += IA_WAVE) {
+          const int64_t t = t0 + tst * (tb + lane);
           bool nd = false;
-          if (t >= 0) nd = prune_lb(a.boxes[2 * t], a.boxes[2 * t + 1], ql, qh) <= ub;
+          if (t < tend) nd = prune_lb(a.boxes[2 * t], a.boxes[2 * t + 1], ql, qh) <= ub;
           unsigned long long nm = __ballot(nd);
           while (nm) {
             const int j0 = __ffsll((long long)nm) - 1;
@@ -1840,10 +1835,8 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
               nm &= nm - 1;
             }
             const int j = lane < 32 ? j0 : j1;
-            const int64_t tj0 = __shfl(t, j0 < 0 ? 0 : j0, 64), tj1 = __shfl(t, j1 < 0 ? 0 : j1, 64);
-            const int64_t tj = lane < 32 ? tj0 : tj1;
             if (j >= 0) {
-              const int64_t i = a.pos2row[tj * IA_TILE + (lane & 31)];
+              const int64_t i = a.pos2row[(t0 + tst * (tb + j)) * IA_TILE + (lane & 31)];
               if (i < a.NA) {
                 const double d = exact_dist_level<CH>(a.db64, i, qs, IMG ? &A : nullptr);
                 if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }

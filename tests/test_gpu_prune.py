@@ -223,51 +223,3 @@ def test_nn_bound_is_exact_and_tighter(ctx):
              st0.dist_pairs_corrected / st0.dist_pairs_full, st1.dist_pairs_corrected / st1.dist_pairs_full,
              st0.fallbacks, st1.fallbacks))
 
-
-
-@pytest.mark.parametrize('pct', [5, 20, 50])
-def test_k3p_pool_is_exact(ctx, pct):
-    """option k3p_pool (1024^2 job, both pruned levels, k3p_variant 22): the last pct % of every
-    workgroup's DB tiles go to a shared pool taken tile by tile by whichever workgroups finish
-    first, listed for the merge's certification rescans; s, im and B' equal the default run's."""
-    from ia_amd import synth
-    job = synth.make_job(1024)
-    Bp0, S0, IM0, st0 = _run(ctx, job, 1, 22)
-    ctx.set_option('k3p_pool', pct)
-    try:
-        Bp1, S1, IM1, st1 = _run(ctx, job, 1, 22)
-    finally:
-        ctx.set_option('k3p_pool', 0)
-    for level in range(1, job.L):
-        assert np.array_equal(S0[level], S1[level]), level
-        assert np.array_equal(IM0[level], IM1[level]), level
-        assert np.array_equal(Bp0[level], Bp1[level]), level
-    assert st1.bound_violations == 0
-    assert st1.dist_tiles_full == st0.dist_tiles_full
-    print('pct %d: tiles %d vs %d, fallbacks %d vs %d' % (pct, st1.dist_tiles, st0.dist_tiles, st1.fallbacks, st0.fallbacks))
-
-
-@pytest.mark.parametrize('name', ['g64', 'ties128', 'k25', 'g256'])
-def test_k3p_pool_matches_reference(ctx, name):
-    """option k3p_pool with every level pruned on the golden runs: bit-identical to the reference"""
-    from ia_amd import _native
-    from golden_util import BIG_CASES, E2E_CASES, load_e2e
-    if name not in E2E_CASES + BIG_CASES:
-        pytest.skip('fixture absent')
-    z = load_e2e(name)
-    L, k = z['L'], float(z['k'])
-    Bp = [x.copy() for x in z['Bp_init']]
-    st = _native.Stats()
-    ctx.set_option('prune_min_rows', 1)
-    ctx.set_option('k3p_pool', 25)
-    try:
-        for level in range(1, L):
-            s, im = ctx.synthesize_level(z['A_pyr'][level], z['A_pyr'][level - 1], [p[level] for p in z['Ap_pyr']],
-                                         [p[level - 1] for p in z['Ap_pyr']], z['B_pyr'][level], z['B_pyr'][level - 1],
-                                         Bp[level - 1], Bp[level], z['weights'], 1 + 2.0 ** (level - L) * k, st)
-            assert np.array_equal(s, z['s'][level]) and np.array_equal(im, z['im'][level]), level
-            assert np.array_equal(Bp[level], z['Bp_final'][level]), level
-    finally:
-        ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_pool', 0)
-    assert st.bound_violations == 0 and st.kappa_ambiguous == 0 and st.pruned_levels == L - 1
