@@ -295,6 +295,9 @@ def pipe_contexts(args, local, ctx):
         ctx.set_option('stream_priority', hi)
         for cx in extra:
             cx.set_option('stream_priority', lo)
+    if not args.coarse_fuse_gather:   # the coarser levels' merge and gather as separate launches
+        for cx in extra:
+            cx.set_option('fuse_gather', 0)
     return extra
 
 
@@ -370,6 +373,9 @@ def main():
                     help='distance-scan MFMA: split-f16 (3 f16 MFMAs per 16 k) or fp32; both certified exact')
     ap.add_argument('--prune', type=int, default=1, choices=[0, 1],
                     help='certified pruned distance scan on large 1-channel levels (DESIGN.md §4b); identical results')
+    ap.add_argument('--coarse-fuse-gather', type=int, default=1, choices=[0, 1],
+                    help='0: the pipelined coarser levels run their merge and next gather as separate launches '
+                         '(shorter-resident waves beside the finest level\'s scans); 1 (default): fused like the finest')
     ap.add_argument('--k3p-variant', type=int, default=22, choices=[7, 11, 14, 15, 18, 19, 20, 21, 22, 23],
                     help='pruned-scan kernel version (ia_k3h.hip k3h_prune3, DESIGN.md §4b): 7 = need tests interleaved '
                          'with the contraction, bitonic in-kernel query sort, reverse walks on alternate steps; 11 = 7 on '
