@@ -262,7 +262,7 @@ def make_context(args, local):
     cx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
     cx.set_option('prune', args.prune)
     if args.k3p_variant != 22:
-        cx.set_option('k3p_variant', args.k3p_variant)     # 7, 11, 14, 15, 18..23
+        cx.set_option('k3p_variant', args.k3p_variant)     # 20, 21, 22, 24, 25
     cx.set_option('prune_min_rows', args.prune_min_rows)
     if args.k3p_blocks != 1:
         cx.set_option('k3p_blocks', args.k3p_blocks)
@@ -376,14 +376,13 @@ def main():
     ap.add_argument('--coarse-fuse-gather', type=int, default=1, choices=[0, 1],
                     help='0: the pipelined coarser levels run their merge and next gather as separate launches '
                          '(shorter-resident waves beside the finest level\'s scans); 1 (default): fused like the finest')
-    ap.add_argument('--k3p-variant', type=int, default=22, choices=[7, 11, 14, 15, 18, 19, 20, 21, 22, 23],
-                    help='pruned-scan kernel version (ia_k3h.hip k3h_prune3, DESIGN.md §4b): 7 = need tests interleaved '
-                         'with the contraction, bitonic in-kernel query sort, reverse walks on alternate steps; 11 = 7 on '
-                         'queries presorted once per step; 14 / 15 = 7 / 11 with the hi x hi block filter; 18 / 19 = 14 / '
-                         '15 with the correction products fused onto the hi x hi accumulator (single chains); 20 / 21 = '
-                         'the same on query-tile pairs (two chains); 22 (default) / 23 = 14 / 15 streaming only the hi '
-                         'halves of the DB tiles, the lo halves loaded for the filter-passing ones (chains one tile '
-                         'later); steps wider than 512 queries run 21 under 20 and 22')
+    ap.add_argument('--k3p-variant', type=int, default=22, choices=[20, 21, 22, 24, 25],
+                    help='pruned-scan kernel version (ia_k3h.hip k3h_prune3, DESIGN.md §4b/§4h/§4i): 20 / 21 = whole '
+                         'DB tiles in two register buffers, hi x hi block filter with the corrections fused on '
+                         'query-tile pairs (in-kernel query sort / presorted); 22 = the hi-only tile stream, the lo '
+                         'halves of filter-passing tiles one tile later; 24 / 25 = two passes: the hi stream by '
+                         'LDS-DMA two tiles deep, then the passing tiles\' full chains.  Steps wider than 512 queries '
+                         'run the presorted form (20 and 22: 21; 24: 25)')
     ap.add_argument('--pipeline', type=int, default=1, choices=[0, 1],
                     help='1 (default; one-job configs and replicas): consecutive levels overlap (two libia '
                          'contexts, each level\'s steps waiting only for the steps of the previous level they read; '

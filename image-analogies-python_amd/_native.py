@@ -112,6 +112,7 @@ EXPORTS = {
                                         ctypes.POINTER(ctypes.c_double)]),
     'ia_merge_winners': (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
                                         ctypes.c_void_p, ctypes.c_void_p]),
+    'ia_chain_budget': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     'ia_wavefront_shape': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_int64),
                                           ctypes.POINTER(ctypes.c_int64)]),
     'ia_wavefront_step': (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.c_int64, ctypes.POINTER(ctypes.c_int),
@@ -457,6 +458,11 @@ def shard_rows(n_rows, world, rank):
     perm = np.arange(t0, t1, dtype=np.int64) * (TILE_MUL % nt) % nt  # ia_tile_perm (ia_internal.h)
     rows = (np.arange(32)[:, None] * nt + perm[None, :]).ravel()
     return np.sort(rows[rows < n_rows])
+
+
+def chain_budget(n_cu, vgprs, api_blocks_per_cu, wg_threads=64):
+    """include/ia.h ia_chain_budget: deadlock-free handoff-chained waves in flight (0: never chain)"""
+    return lib().ia_chain_budget(n_cu, vgprs, api_blocks_per_cu, wg_threads)
 
 
 def wavefront_shape(h, w):

@@ -31,11 +31,13 @@ thread_local std::string g_last_error;
 // Waves of the handoff-chained launches (k_merge_gather: a gather waits for the merge of the row
 // above) of every level in flight in this process.  A wave waits only for its row predecessor
 // and no two waves share one, so a stall needs every resident slot held by a waiter whose
-// predecessor is not yet dispatched: >= 2 x the resident slots (4 per CU at k_merge_gather's
-// 264 VGPRs) chained waves in flight at once.  A level chains only if its widest launch fits in
-// the budget left (ia_synthesize_levels is synchronous: its launches are done when it returns);
-// otherwise it runs the separate gather / merge launches.  (cfg5's 16-job batches of 512^2
-// steps, 2,736 waves per launch on three streams, hit the 20 s handoff timeout without this.)
+// predecessor is not yet dispatched: >= 2 x the resident slots chained waves in flight at once.
+// The resident slots come from the compiled k_merge_gather instances (ia_chain_budget, at
+// ia_init: VGPRs and the occupancy API; 4 waves per CU at round 4's 264 VGPRs).  A level
+// chains only if its widest launch fits in the budget left (ia_synthesize_levels is
+// synchronous: its launches are done when it returns); otherwise it runs the separate gather /
+// merge launches.  (cfg5's 16-job batches of 512^2 steps, 2,736 waves per launch on three
+// streams, hit the 20 s handoff timeout without this.)
 static std::atomic<int> g_chain_waves{0};
 struct ChainReservation {
   int n = 0;
@@ -342,9 +344,11 @@ int ia_init(int device, ia_ctx **out) {
     delete c;
     return fail(IA_EHIP, "ia_init: hipStreamCreate failed");
   }
-  {  // g_chain_waves: 4 resident k_merge_gather waves per CU of this context's slice, twice, less 1/16
+  {  // g_chain_waves: the resident k_merge_gather waves of this context's CU slice, twice, less 1/16
     const int ncu = split_n > 1 ? prop.multiProcessorCount / split_n : prop.multiProcessorCount;
-    c->chain_budget = 2 * 4 * ncu - (2 * 4 * ncu) / 16;
+    int vg = 0, nb = 0, wt = 0;
+    ia_merge_gather_occupancy(&vg, &nb, &wt);
+    c->chain_budget = ia_chain_budget(ncu, vg, nb, wt);  // 0: never chain (separate launches)
   }
   hipEventCreate(&c->lv0);
   hipEventCreate(&c->lv1);
@@ -395,14 +399,14 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     c->stamps = value;
     return IA_OK;
   }
-  if (!std::strcmp(name, "k3p_variant")) {  // 22 (default; hi-only DB stream, presorted steps run 21) / 20 /
-                                            // 21: hi x hi block filter with the correction
-                                            // products fused on query-tile pairs (in-kernel sort up to 512
-                                            // queries, presorted 21 above); 14 / 15: the filter, then full
-                                            // chains; 18 / 19: fused, single chains; 7 / 11: v7 (DESIGN.md
-                                            // §4b); the other versions of §4b / §4f are in git history
-    if (value != 7 && value != 11 && value != 14 && value != 15 && (value < 18 || value > 23))
-      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 7, 11, 14, 15 or 18..23");
+  if (!std::strcmp(name, "k3p_variant")) {  // 24 / 25 two passes (a hi stream three
+                                            // tiles deep, then the passing tiles' chains); 22 hi-only
+                                            // stream with the chains one tile later; 20 / 21 whole tiles,
+                                            // corrections fused on query-tile pairs.  In-kernel sort up to
+                                            // 512 queries (20, 22, 24), presorted above (21, 25); the other
+                                            // versions are in git history
+    if (value != 20 && value != 21 && value != 22 && value != 24 && value != 25)
+      return fail(IA_EINVAL, "ia_set_option: k3p_variant is 20, 21, 22, 24 or 25");
     c->k3p_variant = value;
     return IA_OK;
   }
@@ -654,6 +658,21 @@ int ia_pipeline_depend(ia_ctx *c, ia_ctx *prev, int prev_gen) {
 
 int ia_pipeline_generation(ia_ctx *c) { return c ? c->p_gen.load() : -1; }
 
+int ia_chain_budget(int n_cu, int vgprs, int api_blocks_per_cu, int wg_threads) {
+  // resident waves per CU: the VGPR bound (512 registers per lane and SIMD, allocated in
+  // granules of 8, at most 8 waves per SIMD, 4 SIMDs) and the occupancy API's workgroups; above
+  // 3 waves per SIMD the SGPR file can bind too, where the API is known to answer one workgroup
+  // too many (MI355X_MICROARCH.md, residency): then one workgroup per CU less
+  if (n_cu <= 0 || vgprs <= 0 || api_blocks_per_cu <= 0 || wg_threads <= 0) return 0;
+  const int alloc = (vgprs + 7) / 8 * 8;
+  const int per_simd = alloc > 512 ? 0 : std::min(8, 512 / alloc);
+  const int wpb = (wg_threads + IA_WAVE - 1) / IA_WAVE;
+  int per_cu = std::min(4 * per_simd, api_blocks_per_cu * wpb);
+  if (per_simd > 3) per_cu = std::min(per_cu, (api_blocks_per_cu - 1) * wpb);
+  if (per_cu <= 0) return 0;
+  const int slots = per_cu * n_cu;
+  return 2 * slots - (2 * slots) / 16;
+}
 int ia_wavefront_shape(int h, int w, int64_t *steps, int64_t *max_queries) {
   if (h < 1 || w < 1) return fail(IA_EINVAL, "ia_wavefront_shape: empty level");
   if (steps) *steps = (int64_t)w + 3 * (int64_t)(h - 1);
@@ -1000,7 +1019,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       (rc = c->rec.ensure(rec_stride * shards.size() * 16)) || (rc = c->recT.ensure(rec_stride * shards.size() * 4)) ||
       (rc = c->win.ensure((size_t)Mtmax * 16)) || (rc = c->allwin.ensure((size_t)Mtmax * 16 * Wsh)) ||
       (rc = c->counters.ensure(5 * 8)) ||
-      (rc = c->pairs.ensure(4 * IA_NWG_H * 8)) || (rc = c->ord.ensure(2 * 4096 * 4)) ||
+      (rc = c->pairs.ensure(6 * IA_NWG_H * 8)) || (rc = c->ord.ensure(2 * 4096 * 4)) ||
       (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 * 2 : 16)))
     return rc;
   if (prune && ((rc = c->qs_order.ensure((size_t)Mpad_max * 4)) || (rc = c->qs_info.ensure((size_t)Mpad_max * 3 * 16)) ||
@@ -1012,14 +1031,17 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   const bool stamped = c->stamps && prune;
   const int64_t k3_cap = T * (int64_t)shards.size() * (c->k3p_blocks ? 1 : 8);
   const int mg_stride = (int)Mpad_max + J + 64;
-  const int64_t mg_cap = T * J;
+  const int64_t mg_cap = T * (xo ? J : 1);  // merge launches per step: one, or one per owned job (exchange 2)
   int64_t k3_n = 0, mg_n = 0;
   if (stamped) {
-    if ((rc = c->stamp_k3.ensure((size_t)k3_cap * IA_NWG_H * 16)) || (rc = c->stamp_mg.ensure((size_t)mg_cap * mg_stride * 16)) ||
+    // the slots start zeroed (fresh buffers here; the slots a level used are cleared after it)
+    const size_t k3b = (size_t)k3_cap * IA_NWG_H * 16, mgb = (size_t)mg_cap * mg_stride * 16;
+    const bool fresh_k3 = c->stamp_k3.cap < k3b, fresh_mg = c->stamp_mg.cap < mgb;
+    if ((rc = c->stamp_k3.ensure(k3b)) || (rc = c->stamp_mg.ensure(mgb)) ||
         (rc = c->stamp_dur.ensure((size_t)(2 * k3_cap + mg_cap) * 16)))
       return rc;
-    HIP_TRY(hipMemsetAsync(c->stamp_k3.p, 0, (size_t)k3_cap * IA_NWG_H * 16, c->st));
-    HIP_TRY(hipMemsetAsync(c->stamp_mg.p, 0, (size_t)mg_cap * mg_stride * 16, c->st));
+    if (fresh_k3) HIP_TRY(hipMemsetAsync(c->stamp_k3.p, 0, c->stamp_k3.cap, c->st));
+    if (fresh_mg) HIP_TRY(hipMemsetAsync(c->stamp_mg.p, 0, c->stamp_mg.cap, c->st));
   }
   auto k3_stamp = [&]() -> unsigned long long * {
     return stamped && k3_n < k3_cap ? c->stamp_k3.as<unsigned long long>() + (size_t)2 * IA_NWG_H * k3_n++ : nullptr;
@@ -1028,8 +1050,9 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     return stamped && mg_n < mg_cap ? c->stamp_mg.as<unsigned long long>() + (size_t)2 * mg_stride * mg_n++ : nullptr;
   };
   double bytes_all_fixed = 0.;  // algorithmic bytes of every pruned launch besides its DB tiles
-  // per-workgroup counters of the pruned scan: [pairs | pairs (timed steps) | tiles | tiles (timed)][wg]
-  HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 4 * IA_NWG_H * 8, c->st));
+  // per-workgroup counters of the pruned scan: [pairs | pairs (timed steps) | tiles | tiles (timed) |
+  // extra half-tiles | extra half-tiles (timed)][wg]
+  HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 6 * IA_NWG_H * 8, c->st));
   HIP_TRY(hipMemsetAsync(c->Rbits.p, 0, 4, c->st));
   HIP_TRY(hipMemsetAsync(c->counters.p, 0, 5 * 8, c->st));
 
@@ -1111,8 +1134,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                (prune || c->fuse_unpruned) && ((!multi && !xo && mas[0].nwg <= 4 * IA_WAVE) || (xo && prune));
   // (one-rank levels: the process-wide chained-wave budget, g_chain_waves; a launch holds at most
   // Mpad + J waves: merges, entering rows, pads)
+  // Owner-computes levels (exchange 2) take the same reservation: their fused launches chain
+  // rows like any other (and wait for peers' records besides, which never depend on a chained
+  // wave of this process), so the same budget keeps them deadlock-free
   ChainReservation chain_res;
-  if (chain && !xo && !chain_res.take((int)(Mpad_max + J), c->chain_budget)) chain = false;
+  if (chain && !chain_res.take((int)(Mpad_max + J) + (xo ? 1 : 0), c->chain_budget)) chain = false;
   if (chain) {
     const int hrows = g.bh * J;  // per job (local owner)
     if (c->hand_rows < hrows) {
@@ -1330,11 +1356,8 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         xs.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
         const char *dbp = (const char *)c->db.p + (size_t)(x.t0 - g.tile0) * tile_bytes;
         const int kv = c->k3p_variant;
-        // the in-kernel-sort variant (ink: 20 / 14 / 18 / 7) or its presorted form
-        const int k3x = ink ? ((kv == 14 || kv == 15) ? 14 : (kv == 18 || kv == 19) ? 18 : (kv == 7 || kv == 11) ? 7
-                               : (kv == 22 || kv == 23) ? 22 : 20)
-                            : ((kv == 14 || kv == 15) ? 15 : (kv == 18 || kv == 19) ? 19 : (kv == 7 || kv == 11) ? 11
-                               : (kv == 22 || kv == 23) ? 23 : 21);
+        // the in-kernel-sort variant (ink: 20 / 22 / 24) or its presorted form (21 / 25)
+        const int k3x = ink ? (kv == 21 ? 20 : kv == 25 ? 24 : kv) : (kv == 24 || kv == 25 ? 25 : 21);
         ia_launch_k3p(ink ? QTs : xo_QTx, dbp, loc + XOLayout::FRAG, reinterpret_cast<const float4 *>(loc + XOLayout::INFO),
                       mas[i].boxes, mas[i].pos2row, n, 0, sd.M, ink ? Mpj : Mrec, nch, nullptr, nullptr,
                       c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
@@ -1458,11 +1481,8 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     const bool wide = sd.Mpad > 512 || (c->k3p_blocks && sd.Mpad > qtmax * IA_TILE);
     // sorted by the previous launch's gathers: the presorted form of the variant, no K2s
     const bool gsorted = fsort && gathered == t && gsort;
-    const int k3v = (kv == 11 || kv == 15 || kv == 19 || kv == 21 || kv == 23) ? kv
-                    : (prune && (wide || gsorted)
-                           ? (kv == 14 ? 15 : kv == 18 ? 19 : kv == 20 || kv == 22 ? 21 : 11)
-                           : kv);
-    const bool presorted = k3v == 11 || k3v == 15 || k3v == 19 || k3v == 21 || k3v == 23;
+    const int k3v = (kv == 21 || kv == 25) ? kv : (prune && (wide || gsorted) ? (kv == 24 ? 25 : 21) : kv);
+    const bool presorted = k3v == 21 || k3v == 25;
     const float4 *tboxp = gsorted ? nullptr : c->qs_tbox.as<float4>();  // nullptr: boxes from the slice
     if (prune && presorted && !gsorted)
       ia_launch_query_sort(qinfot, c->qf.p, sd.Mpad, g.KS, c->qs_order.as<int>(), c->qs_info.as<float4>(),
@@ -1615,6 +1635,9 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                               c->st, c->stamp_dur.as<unsigned long long>() + 2 * (k3_n + mg_n));
     ia_launch_stamp_durations(c->stamp_mg.as<unsigned long long>(), (int)mg_n, mg_stride,
                               c->stamp_dur.as<unsigned long long>() + 2 * k3_n, c->st);
+    // clear only the slots this level wrote (the whole buffer was cleared per level)
+    if (k3_n) HIP_TRY(hipMemsetAsync(c->stamp_k3.p, 0, (size_t)k3_n * IA_NWG_H * 16, c->st));
+    if (mg_n) HIP_TRY(hipMemsetAsync(c->stamp_mg.p, 0, (size_t)mg_n * mg_stride * 16, c->st));
   }
   if (stats)
     for (int j = 0; j < J; j++) ia_launch_reduce_stats(jp[j].pstat, NB, c->counters.as<unsigned long long>(), c->st);
@@ -1647,10 +1670,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                                 " did not arrive within 20 s (peer-write exchange)");
   }
   if (stats) {
-    unsigned long long ctr[5], prs[4], pfull = 0, ptp = 0, ptps[4] = {0, 0, 0, 0};
+    unsigned long long ctr[5], prs[4], pfull = 0, ptp = 0, ext[2] = {0, 0};
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
     {  // per-workgroup counter slots (no same-address atomics in the distance kernel)
-      std::vector<unsigned long long> slots(4 * IA_NWG_H);
+      std::vector<unsigned long long> slots(6 * IA_NWG_H);
       HIP_TRY(hipMemcpy(slots.data(), c->pairs.p, slots.size() * 8, hipMemcpyDeviceToHost));
       for (int j = 0; j < 4; j++) {
         prs[j] = 0;
@@ -1662,19 +1685,20 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           } else {  // tile slots: (tiles with a filter-passing block << 32) + tiles loaded
             prs[j] += v & 0xffffffffull;
             ptp += v >> 32;
-            ptps[j] += v >> 32;
           }
         }
       }
+      for (int w = 0; w < IA_NWG_H; w++) {  // DB half-tiles loaded besides one per loaded tile
+        ext[0] += slots[4 * IA_NWG_H + w];
+        ext[1] += slots[5 * IA_NWG_H + w];
+      }
     }
     const double pair_flops = 2.0 * g.D * IA_TILE * IA_TILE;  // one (DB tile, query tile) pair
-    // algorithmic DB bytes of the pruned scan: whole tiles, or (k3p_variant 22 / 23) the hi half
-    // of every loaded tile + the lo half of the tiles with a filter-passing block
-    const bool split_stream = c->k3p_variant == 22 || c->k3p_variant == 23;
-    auto tile_stream_bytes = [&](double tiles, double passing) {
-      const double tb = ia_k3h_tile_bytes(g.KS);
-      return split_stream ? 0.5 * tb * (tiles + passing) : tb * tiles;
-    };
+    // algorithmic DB bytes of the pruned scan, as each launch's kernel counted them (ADVICE r4:
+    // steps wider than 512 queries run another variant than the option names): one half tile
+    // (hi or lo) per loaded tile + the extra halves (whole tiles: the lo halves; hi-only stream:
+    // the lo halves of the filter-passing tiles; two passes: the passing tiles again, whole)
+    auto tile_stream_bytes = [&](double tiles, double extra) { return 0.5 * ia_k3h_tile_bytes(g.KS) * (tiles + extra); };
     if (prune) {
       dist_flops = pair_flops * (double)(prs[0] + prs[1]);
       flops_timed = pair_flops * (double)prs[1];
@@ -1785,7 +1809,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         stats->stamp_gaps += ng;
         stats->stamp_window_ms += (double)(std::max(sp[2 * k3_n - 1], m[2 * mg_n - 1]) - sp[0]) * 1e-5;
       }
-      stats->k3p_bytes_all += tile_stream_bytes((double)(prs[2] + prs[3]), (double)ptp) + bytes_all_fixed;
+      stats->k3p_bytes_all += tile_stream_bytes((double)(prs[2] + prs[3]), (double)(ext[0] + ext[1])) + bytes_all_fixed;
     }
     if (stride && ns > 0) {
       double tot = 0.;
@@ -1801,7 +1825,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         stats->prune_ms_timed += tot;
         stats->prune_launches_timed += launches_timed;
         stats->prune_flops_timed += flops_timed;
-        stats->prune_bytes_timed += tile_stream_bytes((double)prs[3], (double)ptps[3]) + bytes_timed_fixed;
+        stats->prune_bytes_timed += tile_stream_bytes((double)prs[3], (double)ext[1]) + bytes_timed_fixed;
       }
     }
   }

@@ -28,6 +28,39 @@ __device__ __forceinline__ void ld_hi(h16x8 (&h)[KS], const h16x8 *__restrict__ 
   for (int s = 0; s < KS; s++) h[s] = src[TileFmt<KS>::off(2 * s, lane)];
 }
 
+// k3p_variant 24 / 25: the hi pieces of a tile by LDS-DMA (global_load_lds_dwordx4) into a
+// 3.5 KiB slot of the wave's ring in LDS: pieces 0, 2, 4 (1 KiB, every lane) at slot + 0, 1, 2
+// KiB, the compact piece 6 (512 B, lanes 0-31) at slot + 3 KiB.  Four vector-memory operations
+// per tile, issued by inline asm: the compiler then neither knows of the pending LDS writes nor
+// inserts its own (vmcnt(0)) waits before LDS accesses it cannot prove disjoint from them; the
+// consumer waits with an explicit s_waitcnt vmcnt before it reads a slot (ring_wait, which
+// clobbers "memory", so no LDS read is scheduled above it).  The DMAs write LDS only, never a
+// register, so nothing the register allocator does can observe them early.
+#define IA_HSLOT 224  // h16x8 per ring slot (3.5 KiB)
+__device__ __forceinline__ void dma16(const void *g, unsigned lds_addr) {
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr), "v"(g) : "memory", "m0");
+}
+template <int KS>
+__device__ __forceinline__ void dma_hi(const h16x8 *__restrict__ db, int64_t tile, h16x8 *slot, int lane) {
+  static_assert(KS == 4, "ring slots hold compact 1-channel tiles");
+  const h16x8 *src = db + tile * TileFmt<KS>::STRIDE;
+  const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) h16x8 *)slot;
+#pragma unroll
+  for (int s = 0; s < 3; s++) dma16(src + TileFmt<KS>::off(2 * s, lane), base + s * 1024u);
+  if (lane < 32) dma16(src + TileFmt<KS>::off(6, lane), base + 3072u);
+}
+template <int N>
+__device__ __forceinline__ void ring_wait() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// the MFMA A operand (hi pieces) of a ring slot: piece 6's upper-half lanes repeat the lower half
+__device__ __forceinline__ void slot_hi(h16x8 (&h)[4], const h16x8 *slot, int lane) {
+  h[0] = slot[lane];
+  h[1] = slot[IA_WAVE + lane];
+  h[2] = slot[2 * IA_WAVE + lane];
+  h[3] = slot[3 * IA_WAVE + (lane & 31)];
+}
+
 #ifndef IA_PROBE
 #define IA_PROBE 0
 #endif
@@ -347,48 +380,20 @@ __device__ __forceinline__ float k3p_min16(const f32x16 &c) {
   const float m4 = fminf(fminf(c[12], c[13]), c[14]);
   return fminf(fminf(fminf(m0, m1), fminf(m2, m3)), fminf(m4, c[15]));
 }
-// HHF, two phases per DB tile: (1) the hi x hi products of every needed block, software-
-// pipelined over two accumulators (the bound test of block q - 1 is issued after the MFMAs of
-// block q, so it overlaps the matrix core) -> the mask of blocks that can hold a value within
-// their query's bound; (2) those blocks only: the full 12-MFMA chains (k3p_pairs, the same
-// product order as v7, so their values and records are v7's) and the top-2 epilogue.
-template <int KS, int QT, int Q>
-__device__ __forceinline__ void k3p_hhpipe(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, float rt,
-                                           const float *qzt, const float *qzw, f32x16 (&acc)[2], unsigned &pass) {
-  if constexpr (Q <= QT) {
-    constexpr int NP = 2 * KS;
-    if constexpr (Q < QT) {
-      if ((msk >> Q) & 1u) acc[Q & 1] = k3p_hh<KS>(a, lq + Q * NP * IA_WAVE);
-    }
-    if constexpr (Q >= 1) {
-      if ((msk >> (Q - 1)) & 1u) {
-        const float lim = fmaf(rt, qzw[(Q - 1) * IA_TILE] + fmaf(rt, 0x1p-9f, 0x1p-20f), qzt[(Q - 1) * IA_TILE]);
-#if IA_PROBE & 64  // timing only (results invalid): no block passes (bit 31 keeps the test alive)
-        pass |= __ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull ? 1u << 31 : 0u;
-#elif IA_PROBE & 128  // timing only: every block passes (the filter's overhead alone)
-        pass |= (1u << (Q - 1)) | (__ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull ? 1u << 31 : 0u);
-#else
-        pass |= __ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull ? 1u << (Q - 1) : 0u;
-#endif
-      }
-    }
-    k3p_hhpipe<KS, QT, Q + 1>(a, lq, msk, rt, qzt, qzw, acc, pass);
-  }
-}
-
 // HHX = 3 (k3p_variant 22 / 23): the same filter on a hi-only tile buffer (ld_hi); the blocks
 // that pass run their full chains one tile later, from the whole tile loaded only then
-template <int KS, int QT, int Q>
+// HO (k3p_variant 24 / 25): the query fragments in LDS are the hi pieces only ([QT][KS][64])
+template <int KS, int QT, int Q, bool HO = false>
 __device__ __forceinline__ void k3p_hhpipe_h(const h16x8 (&h)[KS], const h16x8 *lq, unsigned msk, float rt,
                                              const float *qzt, const float *qzw, f32x16 (&acc)[2], unsigned &pass) {
   if constexpr (Q <= QT) {
-    constexpr int NP = 2 * KS;
+    constexpr int NP = 2 * KS, QS = HO ? KS : NP, PS = HO ? 1 : 2;
     if constexpr (Q < QT) {
       if ((msk >> Q) & 1u) {
-        const h16x8 *qb = lq + Q * NP * IA_WAVE;
+        const h16x8 *qb = lq + Q * QS * IA_WAVE;
         f32x16 c = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int s = 0; s < KS; s++) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(h[s], qb[(2 * s) * IA_WAVE], c, 0, 0, 0);
+        for (int s = 0; s < KS; s++) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(h[s], qb[(PS * s) * IA_WAVE], c, 0, 0, 0);
         acc[Q & 1] = c;
       }
     }
@@ -398,42 +403,76 @@ __device__ __forceinline__ void k3p_hhpipe_h(const h16x8 (&h)[KS], const h16x8 *
         pass |= __ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull ? 1u << (Q - 1) : 0u;
       }
     }
-    k3p_hhpipe_h<KS, QT, Q + 1>(h, lq, msk, rt, qzt, qzw, acc, pass);
+    k3p_hhpipe_h<KS, QT, Q + 1, HO>(h, lq, msk, rt, qzt, qzw, acc, pass);
   }
 }
 
-// HHX (k3p_variant 18 / 19 = 14 / 15 with the corrections fused): the same hi x hi filter, but a
-// passing block keeps its hi x hi accumulator and only adds the 8 correction products (lo x hi,
-// hi x lo) before the top-2 epilogue: 12 MFMAs per passing block instead of 4 + 12.  The
-// products are v14's, summed in another order; ia_eps_c_h bounds the fp32 accumulation for any
-// order, so the records stay certified.  Pipelined like k3p_hhpipe: the hi x hi chain of block q
-// is issued before the test (and corrections, epilogue) of block q - 1.
-template <int KS, int QT, int Q>
-__device__ __forceinline__ void k3p_hhfuse(const h16x8 (&a)[2 * KS], const h16x8 *lq, unsigned msk, float rt,
-                                           const float *qzt, const float *qzw, int t, float (&b1)[QT], float (&b2)[QT],
-                                           int (&i1)[QT], f32x16 (&acc)[2], unsigned &pass) {
-  if constexpr (Q <= QT) {
-    constexpr int NP = 2 * KS;
-    if constexpr (Q < QT) {
-      if ((msk >> Q) & 1u) acc[Q & 1] = k3p_hh<KS>(a, lq + Q * NP * IA_WAVE);
-    }
-    if constexpr (Q >= 1) {
-      if ((msk >> (Q - 1)) & 1u) {
-        const float lim = fmaf(rt, qzw[(Q - 1) * IA_TILE] + fmaf(rt, 0x1p-9f, 0x1p-20f), qzt[(Q - 1) * IA_TILE]);
-        if (__ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull) {  // wave-uniform
-          pass |= 1u << (Q - 1);
-          f32x16 &c = acc[(Q - 1) & 1];
-          const h16x8 *qb = lq + (Q - 1) * NP * IA_WAVE;
+// k3p_variant 24 / 25, second pass: the full 12-MFMA chains of a tile's filter-passing blocks
+// with the query hi pieces at qh ([QT][KS][64], LDS) and the lo pieces at ql (same layout, LDS):
+// the products and their order are k3p_chain's / k3p_chain2's, so values and records are v14's
+template <int KS>
+__device__ __forceinline__ f32x16 k3p_chain_hl(const h16x8 (&a)[2 * KS], const h16x8 *qh, const h16x8 *ql) {
+  f32x16 c = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int s = 0; s < KS; s++) {
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], qb[(2 * s) * IA_WAVE], c, 0, 0, 0);
-            c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], qb[(2 * s + 1) * IA_WAVE], c, 0, 0, 0);
-          }
-          k3p_epi1(c, t, b1[Q - 1], b2[Q - 1], i1[Q - 1]);
-        }
+  for (int s = 0; s < KS; s++) {
+    const h16x8 xh = qh[s * IA_WAVE], xl = ql[s * IA_WAVE];
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], xh, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], xl, c, 0, 0, 0);
+    c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], xh, c, 0, 0, 0);
+  }
+  return c;
+}
+template <int KS>
+__device__ __forceinline__ void k3p_chain2_hl(const h16x8 (&a)[2 * KS], const h16x8 *qh0, const h16x8 *ql0, const h16x8 *qh1,
+                                              const h16x8 *ql1, f32x16 &c0, f32x16 &c1) {
+  constexpr f32x16 zero = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  c0 = zero;
+  c1 = zero;
+#pragma unroll
+  for (int s = 0; s < KS; s++) {
+    const h16x8 x0h = qh0[s * IA_WAVE], x0l = ql0[s * IA_WAVE], x1h = qh1[s * IA_WAVE], x1l = ql1[s * IA_WAVE];
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x0h, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x1h, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0l, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1l, c1, 0, 0, 0);
+    c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0h, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1h, c1, 0, 0, 0);
+  }
+}
+// k3p_pairs with the query hi / lo pieces in separate LDS arrays (qh, ql: [QT][KS][64], lane offset
+// included)
+template <int KS, int QT, int QP>
+__device__ __forceinline__ void k3p_pairs_hl(const h16x8 (&a)[2 * KS], const h16x8 *qh, const h16x8 *ql, unsigned msk, int t,
+                                             float (&b1)[QT], float (&b2)[QT], int (&i1)[QT]) {
+  if constexpr (2 * QP < QT) {
+    constexpr int QS = KS * IA_WAVE, q0 = 2 * QP, q1 = 2 * QP + 1;
+    const unsigned m2 = (msk >> q0) & 3u;
+    if constexpr (q1 < QT) {
+      if (m2 == 3u) {
+        f32x16 c0, c1;
+        k3p_chain2_hl<KS>(a, qh + q0 * QS, ql + q0 * QS, qh + q1 * QS, ql + q1 * QS, c0, c1);
+        k3h_epi2<QT, true>(c0, c1, q0, true, 0, t, b1, b2, i1);
+      } else if (m2 != 0u) {
+        const bool sel = m2 == 2u;
+        const int qq = sel ? q1 : q0;
+        const f32x16 c = k3p_chain_hl<KS>(a, qh + qq * QS, ql + qq * QS);
+        float x1 = sel ? b1[q1] : b1[q0], x2 = sel ? b2[q1] : b2[q0];
+        int xi = sel ? i1[q1] : i1[q0];
+        k3p_epi1(c, t, x1, x2, xi);
+        b1[q0] = sel ? b1[q0] : x1;
+        b2[q0] = sel ? b2[q0] : x2;
+        i1[q0] = sel ? i1[q0] : xi;
+        b1[q1] = sel ? x1 : b1[q1];
+        b2[q1] = sel ? x2 : b2[q1];
+        i1[q1] = sel ? xi : i1[q1];
+      }
+    } else {
+      if (m2 == 1u) {
+        const f32x16 c = k3p_chain_hl<KS>(a, qh + q0 * QS, ql + q0 * QS);
+        k3p_epi1(c, t, b1[q0], b2[q0], i1[q0]);
       }
     }
-    k3p_hhfuse<KS, QT, Q + 1>(a, lq, msk, rt, qzt, qzw, t, b1, b2, i1, acc, pass);
+    k3p_pairs_hl<KS, QT, QP + 1>(a, qh, ql, msk, t, b1, b2, i1);
   }
 }
 
@@ -520,322 +559,6 @@ __device__ __forceinline__ void k3p_hhpairs(const h16x8 (&a)[2 * KS], const h16x
   }
 }
 
-// V (option "k3p_variant"): 0 = per-tile box loads and a full-key rank sort (first version);
-// 1 = the wave's tile boxes held in registers (one coalesced load per 64 tiles, read back with
-// v_readlane: the tile walk has no memory latency left), unique 20-bit-key rank sort;
-// 2 = as 1 with the coarse query-tile test only (diagnostic: no per-query test)
-template <int KS, int QT, int NW, int V>
-__global__ void __launch_bounds__(NW * IA_WAVE, 1)
-k3h_prune(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
-          const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
-          float4 *__restrict__ rec, float *__restrict__ recT, unsigned long long *__restrict__ pairs,
-          unsigned long long *__restrict__ tiles, int rev, const int *__restrict__ ord_in, int n_in,
-           int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox, const float *__restrict__ tnorm,
-           int /*nqb: one query block*/, int /*qt_end*/, XOScan /*xo: PRE launches only*/) {
-  constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
-  static_assert(QT <= 32, "need masks are 32-bit");
-  extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
-  float4 *qlo = reinterpret_cast<float4 *>(ldsh + QT * NP * IA_WAVE);  // [NQ]
-  float4 *qhi = qlo + NQ;                                               // [NQ]
-  float *qU = reinterpret_cast<float *>(qhi + NQ);                     // [NQ]
-  float4 *tlo = reinterpret_cast<float4 *>(qU + NQ);                   // [QT] query-tile boxes
-  float4 *thi = tlo + QT;                                               // [QT]
-  float *tU = reinterpret_cast<float *>(thi + QT);                     // [QT] max U' of the tile
-  unsigned *skey = reinterpret_cast<unsigned *>(tU + ((QT + 3) & ~3));  // [Mpad]
-  int *order = reinterpret_cast<int *>(skey + Mpad);                    // [Mpad] sorted -> query
-  __shared__ unsigned wpairs[NW], wtiles[NW];
-  const int lane = threadIdx.x & 63, half = lane >> 5;
-  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int wg = blockIdx.x, tstep = nwg * NW;
-  int t = wg + nwg * wave;
-  unsigned long long pt0 = 0, pt1 = 0, pt2 = 0, pt3 = 0, pneed = 0, px = 0, py = 0;
-  K3P_T(pt0);
-
-  h16x8 a[NP], an[NP];
-  {  // speculative first tile (usually needed), overlapping the query setup
-    ld_tile<KS>(a, db, min(t, NT - 1), lane);
-  }
-  float4 rlo = make_float4(0.f, 0.f, 0.f, 0.f), rhi = rlo;  // V >= 1: boxes of the wave's tiles
-  int chunk = -1;
-  if constexpr (V >= 1) {  // the first 64 of them, also overlapping the query setup
-    const int tt = t + tstep * lane;
-    if (tt < NT) {
-      rlo = boxes[2 * tt];
-      rhi = boxes[2 * tt + 1];
-    }
-    chunk = 0;
-  }
-  // 1. rank sort of the step's queries by key (index breaks ties)
-  if constexpr (V == 0) {
-    for (int i = threadIdx.x; i < Mpad; i += WGT) skey[i] = __float_as_uint(qinfo[3 * i + 2].y);
-    __syncthreads();
-    for (int i = threadIdx.x; i < Mpad; i += WGT) {
-      const unsigned k = skey[i];
-      int rank = 0;
-      for (int j = 0; j < Mpad; j += 4) {
-        const uint4 kk = *reinterpret_cast<const uint4 *>(skey + j);
-        rank += (kk.x < k || (kk.x == k && j < i)) + (kk.y < k || (kk.y == k && j + 1 < i)) +
-                (kk.z < k || (kk.z == k && j + 2 < i)) + (kk.w < k || (kk.w == k && j + 3 < i));
-      }
-      order[rank] = i;
-    }
-  } else {
-    // unique keys: the key's top 20 bits (5 per axis) above the 12-bit query index (Mpad <= 4096),
-    // so a rank is one unsigned compare per key
-    for (int i = threadIdx.x; i < Mpad; i += WGT) skey[i] = (__float_as_uint(qinfo[3 * i + 2].y) & 0xFFFFF000u) | (unsigned)i;
-    __syncthreads();
-    for (int i = threadIdx.x; i < Mpad; i += WGT) {
-      const unsigned k = skey[i];
-      int rank = 0;
-      for (int j = 0; j < Mpad; j += 4) {
-        const uint4 kk = *reinterpret_cast<const uint4 *>(skey + j);
-        rank += (int)(kk.x < k) + (int)(kk.y < k) + (int)(kk.z < k) + (int)(kk.w < k);
-      }
-      order[rank] = i;
-    }
-  }
-  __syncthreads();
-  const int s0 = qt0 * IA_TILE;
-  for (int x = threadIdx.x; x < NQ; x += WGT) {
-    const int mq = order[s0 + x];
-    qlo[x] = qinfo[3 * mq];
-    qhi[x] = qinfo[3 * mq + 1];
-    qU[x] = qinfo[3 * mq + 2].x;
-  }
-  for (int e = threadIdx.x; e < QT * NP * IA_WAVE; e += WGT) {
-    const int L = e & 63, pq = e >> 6, qt = pq / NP, p = pq - qt * NP;
-    const int mq = order[s0 + qt * IA_TILE + (L & 31)];
-    ldsh[e] = qf[((int64_t)(mq >> 5) * NP + p) * IA_WAVE + (L & 32) + (mq & 31)];
-  }
-  __syncthreads();
-  if (threadIdx.x < QT) {
-    float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-    float u = -INFINITY;
-    for (int q = 0; q < IA_TILE; q++) {
-      const int x = threadIdx.x * IA_TILE + q;
-      if (qU[x] == -INFINITY) continue;  // padding slot
-      const float4 l = qlo[x], h = qhi[x];
-      lo = make_float4(fminf(lo.x, l.x), fminf(lo.y, l.y), fminf(lo.z, l.z), fminf(lo.w, l.w));
-      hi = make_float4(fmaxf(hi.x, h.x), fmaxf(hi.y, h.y), fmaxf(hi.z, h.z), fmaxf(hi.w, h.w));
-      u = fmaxf(u, qU[x]);
-    }
-    tlo[threadIdx.x] = lo;
-    thi[threadIdx.x] = hi;
-    tU[threadIdx.x] = u;
-  }
-  __syncthreads();
-
-  // 2. need mask of DB tile tt over the QT query tiles (wave-uniform)
-  auto need_box = [&](const float4 &blo, const float4 &bhi) -> unsigned {
-    bool c = false;
-    if (lane < QT) c = prune_lb(blo, bhi, tlo[lane], thi[lane]) <= tU[lane];
-    const unsigned coarse = (unsigned)__ballot(c);
-    if constexpr (V == 2) return coarse;
-    unsigned msk = 0;
-#pragma unroll
-    for (int pr = 0; pr < NPAIR; pr++) {
-      if ((coarse >> (2 * pr)) & 3u) {
-        const int j = 2 * pr + half, x = j * IA_TILE + (lane & 31);
-        bool nd = false;
-        if (j < QT) nd = prune_lb(blo, bhi, qlo[x], qhi[x]) <= qU[x];
-        const unsigned long long b = __ballot(nd);
-        msk |= (((unsigned)b != 0u ? 1u : 0u) | ((unsigned)(b >> 32) != 0u ? 2u : 0u)) << (2 * pr);
-      }
-    }
-    return msk & coarse;
-  };
-  auto need = [&](int tt) -> unsigned {
-    const float4 blo = boxes[2 * tt], bhi = boxes[2 * tt + 1];
-    return need_box(blo, bhi);
-  };
-  auto next_needed = [&](int tt, unsigned &msk) -> int {
-    for (; tt < NT; tt += tstep) {
-      msk = need(tt);
-      if (msk) return tt;
-    }
-    msk = 0;
-    return tt;
-  };
-
-  float b1[QT], b2[QT];
-  int i1[QT];  // tile of b1 (packed epilogue)
-#pragma unroll
-  for (int q = 0; q < QT; q++) {
-    b1[q] = FLT_MAX;
-    b2[q] = FLT_MAX;
-    i1[q] = 0x7fffffff;
-  }
-  unsigned cnt = 0, ntl = 0;  // pairs contracted, DB tiles loaded
-  if constexpr (V == 0) {
-    unsigned msk = t < NT ? need(t) : 0u;
-    if (!msk && t < NT) {
-      t = next_needed(t + tstep, msk);
-      ld_tile<KS>(a, db, min(t, NT - 1), lane);
-    }
-    while (t < NT) {
-      unsigned mn;
-      const int tn = next_needed(t + tstep, mn);
-      {
-        ld_tile<KS>(an, db, min(tn, NT - 1), lane);
-      }
-      asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-      // 3. the needed pairs of tile t
-      k3p_pairs<KS, QT, 0>(a, ldsh + lane, msk, t, b1, b2, i1);
-      cnt += __popc(msk);
-      ntl++;
-#pragma unroll
-      for (int p = 0; p < NP; p++) a[p] = an[p];
-      t = tn;
-      msk = mn;
-    }
-  } else {
-    // the wave's k-th tile is t0w + tstep*k; lane j holds the box of tile k = 64*chunk + j
-    const int t0w = t;
-    const int K = t0w < NT ? (NT - t0w + tstep - 1) / tstep : 0;
-    auto rl = [](float v, int j) { return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), j)); };
-    auto box_need = [&](int k) -> unsigned {
-      if ((k >> 6) != chunk) {  // wave-uniform: the next 64 boxes in one coalesced load
-        chunk = k >> 6;
-        const int tt = t0w + tstep * (64 * chunk + lane);
-        if (tt < NT) {
-          rlo = boxes[2 * tt];
-          rhi = boxes[2 * tt + 1];
-        }
-      }
-      const int j = k & 63;
-      const float4 blo = make_float4(rl(rlo.x, j), rl(rlo.y, j), rl(rlo.z, j), rl(rlo.w, j));
-      const float4 bhi = make_float4(rl(rhi.x, j), rl(rhi.y, j), rl(rhi.z, j), rl(rhi.w, j));
-      return need_box(blo, bhi);
-    };
-    auto next_k = [&](int k, unsigned &m) -> int {
-      for (; k < K; k++) {
-        m = box_need(k);
-        if (m) return k;
-      }
-      m = 0;
-      return K;
-    };
-    unsigned msk;
-    K3P_T(pt1);
-    K3P_T(px);
-    int k = next_k(0, msk);
-    K3P_T(py);
-    pneed += py - px;
-    if (k > 0 && k < K) {  // the speculative first tile is not needed: load the first needed one
-      ld_tile<KS>(a, db, (t0w + tstep * k), lane);
-    }
-    while (k < K) {
-      unsigned mn;
-      K3P_T(px);
-      const int kn = next_k(k + 1, mn);
-      K3P_T(py);
-      pneed += py - px;
-      if (kn < K) {  // wave-uniform; never a clamped dummy load: with every wave of the grid
-                     // re-reading one tile at its end, that tile's L2 channel serialised ~16 MiB
-        ld_tile<KS>(an, db, (t0w + tstep * kn), lane);
-      }
-      asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-      // 3. the needed pairs of tile t
-      k3p_pairs<KS, QT, 0>(a, ldsh + lane, msk, t0w + tstep * k, b1, b2, i1);
-      cnt += __popc(msk);
-      ntl++;
-#pragma unroll
-      for (int p = 0; p < NP; p++) a[p] = an[p];
-      k = kn;
-      msk = mn;
-    }
-    K3P_T(pt2);
-  }
-#pragma unroll
-  for (int q = 0; q < QT; q++) {  // tile + packed in-tile index -> DB position
-    const int r = (int)(__float_as_uint(b1[q]) & 15u);
-    i1[q] = b1[q] == FLT_MAX ? 0x7fffffff : i1[q] * IA_TILE + 4 * half + (r & 3) + 8 * (r >> 2);
-  }
-
-  // 4. merge the 2*NW subsets of each query (as K3h); records go to the original query slots
-  __syncthreads();
-  unsigned long long ps1 = 0, ps2 = 0;
-  K3P_T(ps1);
-  if (lane == 0) {
-    wpairs[wave] = cnt;
-    wtiles[wave] = ntl;
-  }
-  Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32], inside the query-fragment area
-#pragma unroll
-  for (int q = 0; q < QT; q++) {
-    Top2 mine = {b1[q], FLT_MAX, b2[q], i1[q], 0x7fffffff};
-    Top2 other;
-    other.v1 = __shfl_xor(b1[q], 32, 64);
-    other.i1 = __shfl_xor(i1[q], 32, 64);
-    other.T = __shfl_xor(b2[q], 32, 64);
-    other.v2 = FLT_MAX;
-    other.i2 = 0x7fffffff;
-    Top2 mrg = half == 0 ? top2_merge(mine, other) : top2_merge(other, mine);
-    if (half == 0) red[(wave * QT + q) * IA_TILE + lane] = mrg;
-  }
-  __syncthreads();
-  K3P_T(ps2);
-  unsigned long long pw1 = 0, pw2 = 0, pw3 = 0;
-  for (int x = threadIdx.x; x < NQ; x += WGT) {
-    Top2 m = red[x];
-#pragma unroll
-    for (int w = 1; w < NW; w++) m = top2_merge(m, red[(w * QT) * IA_TILE + x]);
-    K3P_T(pw1);
-    const int mq = order[s0 + x];
-    if (mq < M) {
-      const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
-      const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
-#if IA_PROBE & 16
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-      K3P_T(pw2);
-      rec[(int64_t)mq * nwg + wg] = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
-      recT[(int64_t)mq * nwg + wg] = m.T;
-    }
-  }
-#if IA_PROBE & 16
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-  K3P_T(pw3);
-  if (threadIdx.x == 0) {
-    unsigned long long s = 0, n = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) {
-      s += wpairs[w];
-      n += wtiles[w];
-    }
-    if constexpr (V == 0) {
-      atomicAdd(pairs, s);
-      atomicAdd(tiles, n);
-    } else {  // the workgroup's own slots: launches are stream-ordered, so no atomics (512
-              // same-address device atomics per launch serialise far from the CU)
-      pairs[wg] += s;
-      tiles[wg] += n;
-    }
-  }
-#if IA_PROBE & 16
-  if constexpr (V >= 1) {
-    K3P_T(pt3);
-    if (lane == 0 && M == Mpad - 10 && wg < 8) {  // 1024^2 plateau (M = 342), 8 sampled WGs
-      atomicAdd(&k3p_prof[0], pt1 - pt0);
-      atomicAdd(&k3p_prof[1], pneed);
-      atomicAdd(&k3p_prof[2], pt2 - pt1);
-      atomicAdd(&k3p_prof[3], pt3 - pt2);
-      atomicAdd(&k3p_prof[4], 1ull);
-      atomicAdd(&k3p_prof[5], (unsigned long long)ntl);
-      atomicAdd(&k3p_prof[6], (unsigned long long)cnt);
-      if (pw2 != 0) {
-        atomicAdd(&k3p_prof[7], pw1 - ps2);
-        atomicAdd(&k3p_prof[8], pw2 - pw1);
-        atomicAdd(&k3p_prof[9], pw3 - pw2);
-        atomicAdd(&k3p_prof[11], pt3 - pw3);
-        atomicAdd(&k3p_prof[10], 1ull);
-      }
-    }
-  }
-#endif
-}
-
 #if defined(IA_K3H_KS) && defined(IA_K3H_QT)
 #define IA_K3H_CAT2(a, b, c) a##b##_##c
 #define IA_K3H_CAT(a, b, c) IA_K3H_CAT2(a, b, c)
@@ -891,13 +614,21 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
            int r0, int *__restrict__ ord_out, const float4 *__restrict__ tbox, const float *__restrict__ tnorm,
            int nqb, int qt_end, XOScan xo) {
   constexpr int NP = 2 * KS, NPAIR = (QT + 1) / 2, WGT = NW * IA_WAVE, NQ = QT * IA_TILE;
-  constexpr int NE = PRE ? 1 : (IA_K3P3_MAXQ / IA_TILE * NP * IA_WAVE + WGT - 1) / WGT;  // unsorted fragments per thread
+  // unsorted fragments per thread (HHX 4: the hi pieces only)
+  constexpr int NE = PRE ? 1 : (IA_K3P3_MAXQ / IA_TILE * (HHX == 4 ? KS : NP) * IA_WAVE + WGT - 1) / WGT;
   static_assert(QT <= 32 && 2 * NW >= QT, "need masks are 32-bit; one query tile per half wave");
   // the in-kernel sort holds one query per thread; the tile walk takes any K (the launcher keeps
   // K <= IA_K3P_MAXK_LDS: the boxes, need masks and R_t of the WG's tiles live in LDS)
   static_assert(WGT >= IA_K3P3_MAXQ, "one query per thread");
+  static_assert(HHF && HHX >= 2 && HHX <= 4, "the product variants: 20 / 21 (HHX 2), 22 (3), 24 / 25 (4)");
   extern __shared__ h16x8 ldsh[];  // sorted query fragments [QT][NP][64], reused for the merge
-  float4 *qlo = reinterpret_cast<float4 *>(ldsh + QT * NP * IA_WAVE);  // [NQ]
+  // HHX 4: ldsh holds the hi pieces only ([QT][KS][64]); the waves' LDS-DMA rings of the hi
+  // stream ([NW][3] slots of 3.5 KiB; the lo pieces in the second pass) are a static array of
+  // their own, so the compiler can tell that no other LDS access aliases a pending DMA (it puts
+  // a vmcnt(0) before any LDS access it cannot prove disjoint from one)
+  constexpr int QFP = HHX == 4 ? KS : NP;
+  __shared__ h16x8 ring[HHX == 4 ? NW * 3 * IA_HSLOT : 1];
+  float4 *qlo = reinterpret_cast<float4 *>(ldsh + QT * QFP * IA_WAVE);  // [NQ]
   float4 *qhi = qlo + NQ;                                               // [NQ]
   float *qU = reinterpret_cast<float *>(qhi + NQ);                     // [NQ]
   float4 *tlo = reinterpret_cast<float4 *>(qU + NQ);                   // [QT] query-tile boxes
@@ -939,7 +670,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   float *qzt = reinterpret_cast<float *>(items + K);                    // HHF: [NQ] z per sorted slot
   float *qzw = qzt + NQ;                                                // HHF: [NQ] w per sorted slot
   float *wR = qzw + NQ;                                                 // HHF: [K] R_t of the WG's tiles
+  int *plk = reinterpret_cast<int *>(wR + K);                           // HHX 4: [K] filter-passing tiles
+  unsigned *plm = reinterpret_cast<unsigned *>(plk + K);                // HHX 4: [K] their passing blocks
   __shared__ unsigned wpairs[NW], wtiles[NW], wfull[NW], wtp[NW];
+  __shared__ int pctr;  // HHX 4: passing tiles handed out
   __shared__ int wcnt[NW];
   const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -949,10 +683,12 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   const unsigned long long stamp0 = xo.stamp ? ia_clock() : 0ull;
 
   // ---- 1. one global round
-  h16x8 a[NP], an[NP], an2[NP];
-  {
-    ld_tile<KS>(a, db, tk(min(wave, K - 1)), lane);
-  }
+  h16x8 a[NP], an[NP];
+  // HHX 4: the wave's first two tiles (static: wave, wave + NW) go to its ring speculatively (93 %
+  // of the tiles are needed at 1024^2) once the global round's loads are in, so they are in
+  // flight during the query sort (spec_hi below)
+  h16x8 *wring = ring + wave * 3 * IA_HSLOT;
+  if constexpr (HHX != 4) ld_tile<KS>(a, db, tk(min(wave, K - 1)), lane);
   if constexpr (PRE) {
     if (xo.on) {
       // owner-computes sharded step: this block's tiles come from their owner's K2s (another
@@ -975,7 +711,14 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
     // this launch's slice of the presorted queries, straight into LDS
     const h16x8 *qs = qf + (int64_t)qt0 * NP * IA_WAVE;
-    for (int e = tid; e < QT * NP * IA_WAVE; e += WGT) ldsh[e] = e < qtb * NP * IA_WAVE ? qs[e] : h16x8{};
+    if constexpr (HHX == 4) {  // hi pieces only
+      for (int e = tid; e < QT * KS * IA_WAVE; e += WGT) {
+        const int pq = e >> 6, qt = pq / KS, s2 = pq - qt * KS;
+        ldsh[e] = qt < qtb ? qs[(qt * NP + 2 * s2) * IA_WAVE + (e & 63)] : h16x8{};
+      }
+    } else {
+      for (int e = tid; e < QT * NP * IA_WAVE; e += WGT) ldsh[e] = e < qtb * NP * IA_WAVE ? qs[e] : h16x8{};
+    }
     for (int x = tid; x < NQ; x += WGT) {
       const int sl = s0 + x;
       const bool ok = sl < Mpad && x < qtb * IA_TILE;  // slots past the block: padding (never contracted)
@@ -1002,9 +745,21 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       if constexpr (HHF) wR[x] = tnorm[t];
     }
   }
+  auto spec_hi = [&]() {
+    if constexpr (HHX == 4) {
+      dma_hi<KS>(db, tk(min(wave, K - 1)), wring, lane);
+      dma_hi<KS>(db, tk(min(wave + NW, K - 1)), wring + IA_HSLOT, lane);
+    }
+  };
   __shared__ int kctr;  // next tile index to hand out
-  if (tid == 0) kctr = NW;
-  if constexpr (PRE) __syncthreads();
+  if (tid == 0) {
+    kctr = HHX == 4 ? 2 * NW : NW;  // HHX 4: each wave's first two tiles are static (the speculative loads)
+    pctr = NW;
+  }
+  if constexpr (PRE) {
+    __syncthreads();
+    spec_hi();
+  }
   // the query-tile boxes (min lo, max hi, max U' over the tile's real queries) by 32-lane
   // butterflies over the sorted slots in LDS: the in-kernel-sort path, and the presorted path
   // when the step was sorted by its gathers (option "fuse_sort": no k_query_sort, tbox = nullptr)
@@ -1066,12 +821,15 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     mzw = u.w;
     mkey = (__float_as_uint(u.y) & 0xFFFFF000u) | (unsigned)tid;  // unique (Mpad <= 4096)
   }
-  const int ne = Mpad / IA_TILE * NP * IA_WAVE;
+  constexpr int NPL = HHX == 4 ? KS : NP;  // pieces per query tile loaded here (HHX 4: hi, 2s)
+  const int ne = Mpad / IA_TILE * NPL * IA_WAVE;
   h16x8 qe[NE];
 #pragma unroll
   for (int i = 0; i < NE; i++) {
-    const int e = tid + WGT * i;
-    qe[i] = qf[e < ne ? e : 0];  // unconditional: equal vmcnt on every path
+    int e = tid + WGT * i;
+    e = e < ne ? e : 0;
+    if constexpr (HHX == 4) e = ((e >> 6) / KS * NP + 2 * ((e >> 6) % KS)) * IA_WAVE + (e & 63);
+    qe[i] = qf[e];  // unconditional: equal vmcnt on every path
   }
   for (int x = tid; x < K; x += WGT) {
     const int t = tk(x);
@@ -1085,6 +843,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   }
   __syncthreads();
   K3P_T(ph[1]);
+  spec_hi();
 
   // ---- 2. sort, scatter to sorted slots, query-tile boxes
   if (Mpad > IA_K3P_RANK_MAX) {  // (uniform) up to IA_K3P_RANK_MAX queries the rank count
@@ -1152,9 +911,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   for (int i = 0; i < NE; i++) {
     const int e = tid + WGT * i;
     if (e < ne) {
-      const int L = e & 63, pq = e >> 6, tq = pq / NP, p = pq - tq * NP;
+      const int L = e & 63, pq = e >> 6, tq = pq / NPL, p = pq - tq * NPL;  // (HHX 4: p = hi piece s)
       const int x = rankof[tq * IA_TILE + (L & 31)] - s0;
-      if (x >= 0 && x < NQ) ldsh[((x >> 5) * NP + p) * IA_WAVE + (L & 32) + (x & 31)] = qe[i];
+      if (x >= 0 && x < NQ) ldsh[((x >> 5) * NPL + p) * IA_WAVE + (L & 32) + (x & 31)] = qe[i];
     }
   }
   tile_boxes();
@@ -1212,6 +971,120 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       m = 0;
       return K;
     };
+    if constexpr (HHX == 4) {
+    // ---- k3p_variant 24 / 25: two passes over the workgroup's tiles.
+    // (a) the hi stream: the hi halves (3.5 of 7 KiB per tile at KS = 4) by LDS-DMA into the
+    //     wave's ring of three LDS slots, two tiles in flight while the third is filtered: per tile
+    //     the hi x hi filter of its box-needed blocks (k3p_hhpipe_h on the slot); a tile with a
+    //     passing block goes to a list in LDS.  The loop issues no other vector-memory instruction
+    //     (need tests, the tile counter and the list are LDS / VALU work) and exactly four DMAs per
+    //     tile (past the last needed tile the same four from the wave's last tile, into the slot
+    //     that is never read), so "vmcnt(8)" before a slot is read waits for that slot alone.
+    // (b) after a barrier the query lo pieces are staged into the ring area and the listed tiles
+    //     are handed out through an LDS counter: whole tiles (two register buffers) and the full
+    //     12-MFMA chains of their passing blocks (k3p_pairs_hl: v14's products and records).
+    // Tiles: wave w walks k = w + NW j (the first two are the speculative DMAs issued before the
+    // query sort).  No LDS atomic in this loop: the compiler puts a vmcnt(0) before any LDS
+    // atomic while an LDS-DMA is pending, so the passing tiles go to per-wave lists (plk / plm
+    // at w + NW n) instead of one counted list.
+    int kw = wave + 2 * NW;  // the next tile of this wave's walk
+    int np = 0;              // this wave's passing tiles
+    int kc = wave < K ? wave : -1, kq = wave + NW < K ? wave + NW : -1;
+    unsigned mc = kc >= 0 ? need_k(kc) : 0u, mq = kq >= 0 ? need_k(kq) : 0u;
+    int klast = kq >= 0 ? kq : min(wave, K - 1);  // the wave's last tile (its dummy DMA: L2-hot)
+    int sl = 0;                                   // ring slot of tile kc (kq: sl + 1, next: sl + 2, mod 3)
+    while (kc >= 0) {
+      // the next needed tile of the walk (need tests inline) into slot sl + 2
+      unsigned mn = 0u;
+      for (; kw < K; kw += NW) {
+        mn = need_k(kw);
+        if (mn) break;
+      }
+      const bool ok = kw < K;
+      const int kn = ok ? kw : -1;
+      dma_hi<KS>(db, tk(ok ? kw : klast), wring + (sl == 0 ? 2 : sl - 1) * IA_HSLOT, lane);
+      if (ok) {
+        klast = kw;
+        kw += NW;
+      }
+      ring_wait<8>();  // slot sl landed; the two younger tiles stay in flight
+      h16x8 hc[KS];
+      slot_hi(hc, wring + sl * IA_HSLOT, lane);
+      f32x16 acc[2];
+      unsigned pass = 0;
+      k3p_hhpipe_h<KS, QT, 0, true>(hc, ldsh + lane, mc, wR[kc], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
+      cnt += __popc(mc);
+      ntl++;
+      if (pass) {  // wave-uniform
+        nfull += __popc(pass);
+        ntp++;
+        if (lane == 0) {
+          plk[wave + NW * np] = kc;
+          plm[wave + NW * np] = pass;
+        }
+        np++;
+      }
+      kc = kq;
+      mc = mq;
+      kq = kn;
+      mq = mn;
+      sl = sl == 2 ? 0 : sl + 1;
+    }
+    ring_wait<0>();   // the DMAs past the last tile land before the ring area is reused
+    if (lane == 0) wcnt[wave] = np;
+    __syncthreads();  // every wave's passing tiles are listed, every ring is idle
+    // the passing tiles in list order: entry j = wave w's n-th, w the first with j < sum wcnt[..w]
+    int npass = 0;
+#pragma unroll
+    for (int w = 0; w < NW; w++) npass += wcnt[w];
+    auto pent = [&](int jj) -> int {  // list entry -> index into plk / plm
+      int w = 0;
+      for (; w < NW - 1 && jj >= wcnt[w]; w++) jj -= wcnt[w];
+      return w + NW * jj;
+    };
+    int j = wave;  // passing tiles: wave w takes list entry w first, then entries from pctr
+    if (j < npass) ld_tile<KS>(a, db, tk(plk[pent(j)]), lane);
+    // the query lo pieces into the ring area ([QT][KS][64], the hi layout): this launch's sorted
+    // slots, gathered from the unsorted fragments through the sort (PRE: the presorted slice)
+    h16x8 *qlo_f = ring;
+    for (int e = tid; e < QT * KS * IA_WAVE; e += WGT) {
+      const int L = e & 63, pq = e >> 6, qt = pq / KS, s2 = pq - qt * KS;
+      h16x8 v = {};
+      if constexpr (PRE) {
+        if (qt < qtb) v = qf[((int64_t)(qt0 + qt) * NP + 2 * s2 + 1) * IA_WAVE + L];
+      } else {
+        const int sx = s0 + qt * IA_TILE + (L & 31);
+        if (sx < Mpad) {
+          const int mq2 = order[sx];
+          v = qf[((int64_t)(mq2 >> 5) * NP + 2 * s2 + 1) * IA_WAVE + (L & 32) + (mq2 & 31)];
+        }
+      }
+      qlo_f[e] = v;
+    }
+    __syncthreads();
+    if (j < npass) {
+      auto grab2 = [&]() -> int {
+        int g = 0;
+        if (lane == 0) g = atomicAdd(&pctr, 1);
+        return __builtin_amdgcn_readfirstlane(g);
+      };
+      auto step4 = [&](const h16x8(&cur)[NP], h16x8(&nxt)[NP]) {
+        const int jn = grab2();
+        const int xj = pent(j);
+        const int kj = plk[xj];
+        const unsigned pj = plm[xj];
+        ld_tile<KS>(nxt, db, tk(jn < npass ? plk[pent(jn)] : kj), lane);  // unconditional (equal vmcnt)
+        asm volatile("" ::: "memory");
+        k3p_pairs_hl<KS, QT, 0>(cur, ldsh + lane, qlo_f + lane, pj, tk(kj), b1, b2, i1);
+        j = jn;
+      };
+      while (j < npass) {
+        step4(a, an);
+        if (j >= npass) break;
+        step4(an, a);
+      }
+    }
+    } else {
     unsigned m;
     int k = next_k(wave, m);
     if constexpr (HHX == 3) {
@@ -1276,27 +1149,11 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       // makes the MFMAs below wait for the prefetch itself
       ld_tile<KS>(nxt, db, tk(kn < K ? kn : k), lane);
       asm volatile("" ::: "memory");  // LDS query fragments are re-read per tile, not hoisted
-      if constexpr (HHF && HHX == 2) {
+      {  // HHX 2: the fused corrections on query-tile pairs
         unsigned pass = 0;
         k3p_hhpairs<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), tk(k), b1, b2, i1, pass);
         nfull += __popc(pass);
         ntp += pass != 0u;
-      } else if constexpr (HHF && HHX == 1) {
-        f32x16 acc[2];
-        unsigned pass = 0;
-        k3p_hhfuse<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), tk(k), b1, b2, i1, acc,
-                              pass);
-        nfull += __popc(pass);
-        ntp += pass != 0u;
-      } else if constexpr (HHF) {
-        f32x16 acc[2];
-        unsigned pass = 0;
-        k3p_hhpipe<KS, QT, 0>(cur, ldsh + lane, m, wR[k], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
-        if (pass) k3p_pairs<KS, QT, 0>(cur, ldsh + lane, pass, tk(k), b1, b2, i1);
-        nfull += __popc(pass);
-        ntp += pass != 0u;
-      } else {
-        k3p_pairs<KS, QT, 0>(cur, ldsh + lane, m, tk(k), b1, b2, i1);
       }
       cnt += __popc(m);
       ntl++;
@@ -1309,6 +1166,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       step(an, a);
     }
     }  // HHX != 3
+    }  // HHX != 4
   }
   K3P_T(ph[4]);
 #pragma unroll
@@ -1396,6 +1254,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
     pairs[blockIdx.x] += sp + (HHF ? sf << 32 : 0ull);
     tiles[blockIdx.x] += st + (stp << 32);  // (tiles with a filter-passing block << 32) + tiles loaded
+    // DB half-tiles loaded besides one per loaded tile (the algorithmic bytes):
+    // whole tiles (HHX <= 2): the lo half of each; hi-only stream (3): the lo halves of the
+    // passing tiles; two passes (4): the passing tiles again, whole
+    tiles[blockIdx.x + 2 * IA_NWG_H] += HHX == 4 ? 2 * stp : HHX == 3 ? stp : st;
   }
   if (xo.stamp) {  // (uniform) option "stamps": the workgroup's first and last tick
     __syncthreads();
@@ -1439,27 +1301,21 @@ void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau w
 
 #if defined(IA_K3H_KS) && defined(IA_K3H_QT)
 // pruned scan instance (1 channel only: KS = 4)
-// The product library holds the default pruned scan (variant 6 kernel; the launcher adds the
-// reverse walks of variant 7) and variant 1, the fallback for steps beyond v3+'s limits (more
-// than 512 queries or 512 tiles per workgroup).  The other versions of DESIGN.md §4b's
-// progression are built with DIAG=1 only.
+// The product library holds the pruned scans of DESIGN.md §4b that are still selectable (the
+// earlier versions - no filter, single chains, v0-v19 and v23 - are in the history of this
+// file up to round 4): in-kernel query sort (steps of <= 512 queries) / presorted form.
 k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
   if constexpr (IA_K3H_KS == 4) {
     constexpr int NW = IA_WGH / IA_WAVE;
-    if (variant == 6) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW>;
-    if (variant == 11) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true>;
-    if (variant == 14) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true>;
-    if (variant == 15) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true>;
-    // 18 / 19: 14 / 15 with the correction products fused onto the hi x hi accumulator (HHX)
-    if (variant == 18) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true, 1>;
-    if (variant == 19) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true, 1>;
-    // 20 / 21: the fused corrections on query-tile pairs (two chains: k3p_hhpairs)
+    // 20 / 21: whole tiles in two register buffers, the fused corrections on query-tile pairs
     if (variant == 20) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true, 2>;
     if (variant == 21) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true, 2>;
-    // 22 / 23: the filter on hi-only tile loads, full chains of the passing tiles deferred
+    // 22: the filter on hi-only tile loads, full chains of the passing tiles one tile later
     if (variant == 22) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true, 3>;
-    if (variant == 23) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true, 3>;
-    return k3h_prune<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, 1>;
+    // 24 / 25: a hi stream three tiles deep, then the passing tiles' full chains (two passes)
+    if (variant == 24) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true, 4>;
+    if (variant == 25) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true, 4>;
+    return nullptr;
   } else {
     return nullptr;
   }

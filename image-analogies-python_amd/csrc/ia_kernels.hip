@@ -2645,6 +2645,28 @@ void ia_launch_merge_gather(const LevelGeo &g, const StepDesc &sd, const Imgs &A
     hipLaunchKernelGGL((k_merge_gather<4, false, false, JobArgN>), grid, dim3(IA_PQ_WG), 0, st, g, sd, A, ma, JobArgN{jobs.rest},
                        B, nx);
 }
+// the chained-wave budget's inputs (ia_capi.cpp, ia_chain_budget): over every k_merge_gather
+// instance the library launches, the most VGPRs per lane and the fewest workgroups per CU the
+// occupancy API admits, from the compiled kernels themselves
+void ia_merge_gather_occupancy(int *vgprs, int *blocks_per_cu, int *wg_threads) {
+  const void *fns[] = {(const void *)k_merge_gather<4, true, true, JobArg1>, (const void *)k_merge_gather<4, true, false, JobArg1>,
+                       (const void *)k_merge_gather<4, false, false, JobArg1>, (const void *)k_merge_gather<4, true, false, JobArgN>,
+                       (const void *)k_merge_gather<4, false, false, JobArgN>};
+  int vmax = 0, bmin = 1 << 30;
+  for (const void *fn : fns) {
+    hipFuncAttributes fa;
+    int nb = 0;
+    if (hipFuncGetAttributes(&fa, fn) != hipSuccess || hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, IA_PQ_WG, 0) != hipSuccess) {
+      bmin = 0;
+      continue;
+    }
+    vmax = std::max(vmax, (int)fa.numRegs);
+    bmin = std::min(bmin, nb);
+  }
+  *vgprs = vmax;
+  *blocks_per_cu = bmin;
+  *wg_threads = IA_PQ_WG;
+}
 template <int CH>
 static void launch_merge_t(const LevelGeo &g, const StepDesc &sd, const Imgs &A, const MergeArgs &ma, Winner *win,
                            const JobSet &jobs, bool fused, hipStream_t st) {
@@ -2892,25 +2914,36 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
   const int kmax = (NT + nwg - 1) / nwg;  // DB tiles per workgroup
-  const int rev = (variant == 7 || variant >= 11) ? (step & 1) : 0;  // alternate steps walk in reverse
-  if (variant == 7) variant = 6;
-  // the in-kernel sort (7, 14, 18, 20) holds <= 512 queries (wider: the host ran K2s, the
-  // presorted form 15 / 19 / 21 / 11); every variant walks any number of tiles (the host keeps
-  // kmax <= IA_K3P_MAXK_LDS)
-  const bool in_kernel_sort = variant == 6 || variant == 14 || variant == 18 || variant == 20 || variant == 22;
-  if (in_kernel_sort && Mpad > 512)
-    variant = variant == 14 ? 15 : variant == 18 ? 19 : variant == 20 || variant == 22 ? 21 : 1;
-  const k3p_fn fn = g4[qt - 1](variant);
+  const int rev = step & 1;  // alternate steps walk in reverse
+  // the in-kernel sort (20, 22, 24) holds <= 512 queries (wider: the host ran K2s, the presorted
+  // form 21 / 25); every variant walks any number of tiles (the host keeps kmax <= IA_K3P_MAXK_LDS)
+  const bool in_kernel_sort = variant == 20 || variant == 22 || variant == 24;
+  if (in_kernel_sort && Mpad > 512) variant = variant == 24 ? 25 : 21;
   const size_t NQ = (size_t)qt * IA_TILE;
-  const bool pre = variant == 11 || variant == 15 || variant == 19 || variant == 21 || variant == 23;
-  const bool hhf = variant >= 14 && variant <= 23;  // (z, w) per query slot + R_t per tile in LDS
   const int nthr = IA_WGH;
-  size_t lds = pre ? (size_t)qt * 8 * IA_WAVE * 16 + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 +
-                         (size_t)kmax * 40
-                   : ia_k3p_lds(qt, Mpad) + (variant != 1 ? (size_t)Mpad * 4 + (size_t)kmax * 40 : 0);
-  if (hhf) lds += NQ * 8 + (size_t)kmax * 4;  // (z, w) per sorted query slot, R_t per tile
-  const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
-  lds = lds > red ? lds : red;
+  auto dyn_lds = [&](int v) {
+    const bool pre = v == 21 || v == 25;
+    const size_t qfrag = (size_t)qt * (v >= 24 ? 4 : 8) * IA_WAVE * 16;  // v24 / 25: hi pieces only
+    size_t l = pre ? qfrag + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 + (size_t)kmax * 40
+                   : ia_k3p_lds(qt, Mpad) - (size_t)qt * 8 * IA_WAVE * 16 + qfrag + (size_t)Mpad * 4 + (size_t)kmax * 40;
+    l += NQ * 8 + (size_t)kmax * 4;            // (z, w) per sorted query slot, R_t per tile
+    if (v >= 24) l += (size_t)kmax * 8;        // the filter-passing tiles and their blocks
+    const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
+    return l > red ? l : red;
+  };
+  size_t lds = dyn_lds(variant);
+  if (variant >= 24) {  // the static LDS-DMA rings (86 KiB) + this launch's dynamic part must fit 160 KiB
+    hipFuncAttributes fa;
+    const k3p_fn f24 = g4[qt - 1](variant);
+    const size_t stat = f24 && hipFuncGetAttributes(&fa, (const void *)f24) == hipSuccess ? fa.sharedSizeBytes : 0;
+    if (!f24 || stat + lds > 160 * 1024) {  // (many tiles per workgroup or wide steps): the one-pass forms
+      variant = variant == 25 ? 21 : 22;
+      lds = dyn_lds(variant);
+    }
+  }
+  const k3p_fn fn = g4[qt - 1](variant);
+  if (!fn) return;  // (the host accepts only the built variants: ia_set_option)
+  const bool pre = variant == 21 || variant == 25;
   // nqb > 1 (presorted variants only): one launch of nqb query blocks x nwg DB chunks
   if (!pre && !(xo && xo->on)) nqb = 1;
   if (nqb == 1) qt_end = qt0 + qt;

@@ -65,6 +65,7 @@ void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS,
 // owner-computes sharded step (exchange = 2): the owner's queries sorted into every rank's area
 void ia_launch_query_sort_xo(const float4 *qinfo, const void *qf, const XOSort &xs, hipStream_t st);
 size_t ia_k3p_lds(int qt, int Mpad);
+void ia_merge_gather_occupancy(int *vgprs, int *blocks_per_cu, int *wg_threads);
 void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,

@@ -310,6 +310,11 @@ int ia_k3_microbench(ia_ctx *ctx, int64_t n_rows, int M, int reps, double *us_pe
  * smallest distance, then smallest row.  cand is world x nq (dist, row) pairs, rank-major. */
 int ia_merge_winners(const double *dist, const int64_t *row, int world, int64_t nq,
                      double *dist_out, int64_t *row_out);
+/* Budget of handoff-chained waves (fused merge + gather launches whose waves wait for the row
+ * above) a context may have in flight deadlock-free: 2 x the resident waves of its n_cu CUs, less
+ * 1/16, from the compiled kernel's VGPRs per lane, the occupancy API's workgroups per CU and its
+ * workgroup size; 0 = never chain.  ia_init computes it from k_merge_gather itself. */
+int ia_chain_budget(int n_cu, int vgprs, int api_blocks_per_cu, int wg_threads);
 /* Wavefront schedule of a level (t = col + 3*row): number of steps and max queries per step. */
 int ia_wavefront_shape(int h, int w, int64_t *steps, int64_t *max_queries);
 /* Pixels of step t: rows r0 .. r0+M-1, pixel (r, t - 3r).  Used by the level driver. */

@@ -164,3 +164,20 @@ def test_window_sizes_other_than_the_reference_are_refused():
     for bad in (dict(n_sm=3, n_lg=3, n_half=4), dict(n_sm=5, n_lg=5, n_half=12)):
         with pytest.raises(ValueError):
             check_windows(types.SimpleNamespace(**bad))
+
+
+def test_chain_budget_from_kernel_attributes():
+    """the chained-wave budget (fused merge + gather launches whose waves wait
+    for the row above) is derived from the compiled kernel's attributes, not a literal.  Stand-in
+    attributes: round 4's k_merge_gather (264 VGPRs: one wave per SIMD, the occupancy API's 4
+    one-wave workgroups per CU) gives 2 x 4 x 256 less 1/16 = 1,920 on 256 CUs; fewer resident
+    waves shrink it, a kernel that cannot be resident disables chaining."""
+    assert _native.chain_budget(256, 264, 4, 64) == 1920
+    assert _native.chain_budget(128, 264, 4, 64) == 960              # a CU slice (rehearsal streams)
+    assert _native.chain_budget(256, 264, 2, 64) == 960              # the API admits fewer: it wins
+    assert _native.chain_budget(256, 200, 8, 64) == 2 * 8 * 256 - (2 * 8 * 256) // 16   # 2 waves per SIMD
+    # above 3 waves per SIMD the SGPRs can bind and the API may answer one workgroup too many
+    assert _native.chain_budget(256, 96, 20, 64) == 2 * 19 * 256 - (2 * 19 * 256) // 16
+    assert _native.chain_budget(256, 600, 4, 64) == 0               # no resident wave: never chain
+    assert _native.chain_budget(256, 264, 0, 64) == 0
+    assert _native.chain_budget(0, 264, 4, 64) == 0

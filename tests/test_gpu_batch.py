@@ -76,11 +76,11 @@ def test_batched_levels_match_separate_and_reference(ctx, name, mode):
         assert stb.pruned_levels == len(jb) * (z['L'] - 1)
 
 
-@pytest.mark.parametrize('variant', [7, 14, 20])
+@pytest.mark.parametrize('variant', [20, 22, 24])
 def test_batched_512_pruned_wide_step(ctx, variant):
     """3 jobs on a 512^2 level with the pruned scan forced: 513 queries per step in one scan (the
-    separate runs sort 171 per step) - a different kernel path, the same decisions.  variants 14
-    and 20 (hi x hi block filter) run their presorted forms 15 / 21 on the wide steps."""
+    separate runs sort 171 per step) - a different kernel path, the same decisions.  The wide
+    steps run the presorted forms (20 and 22: 21; 24: 25)."""
     from ia_amd import synth
     job = synth.make_job(512, n_levels=3)
     ctx.set_option('prune_min_rows', 1)
@@ -156,8 +156,7 @@ def test_device_sweep_two_streams_equals_one(ctx):
     assert st2.pixels == st1.pixels and st2.coherence_wins == st1.coherence_wins and st2.bound_violations == 0
 
 
-@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_seq', 'pruned_v11', 'pruned_v18', 'pruned_v20',
-                                  'pruned_v23'])
+@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_seq', 'pruned_v20', 'pruned_v24'])
 def test_batched_g256_wide_steps_match_reference(ctx, mode):
     """8 jobs on the golden g256 run's A side: job 0 is the reference's own
     run, jobs 1..7 other kappas and B' seeds.  On the 256^2 level a step holds 8 x 86 = 688
@@ -166,14 +165,14 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
       pruned: prune_min_rows = 1, the presorted wide-step path K2s + v21 as ONE launch of
         2 query blocks x 128 DB chunks (k3p_blocks = 1, the default);
       pruned_seq: the same as one launch per query block (k3p_blocks = 0);
-      pruned_v11: without the hi x hi block filter;
-      pruned_v23: the hi-only DB stream's presorted form.
+      pruned_v20: the same kernels under option k3p_variant 20;
+      pruned_v24: the two-pass scan's presorted form v25.
     Job 0 must reproduce the reference's s, im and B' on every level; every job must equal its
     own separate run (86-query steps: a single launch, the in-kernel sort)."""
     z = load_e2e('g256')
     if mode != 'unpruned':
         ctx.set_option('prune_min_rows', 1)
-    if mode in ('pruned_v11', 'pruned_v18', 'pruned_v20', 'pruned_v23'):
+    if mode in ('pruned_v20', 'pruned_v24'):
         ctx.set_option('k3p_variant', int(mode[-2:]))
     if mode == 'pruned_seq':
         ctx.set_option('k3p_blocks', 0)

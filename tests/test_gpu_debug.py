@@ -19,11 +19,10 @@ from golden_util import BIG_CASES, E2E_CASES, load_e2e
 pytestmark = pytest.mark.gpu
 
 
-def _run_debug(ctx, z, prune_all=False, variant=20):
+def _run_debug(ctx, z, prune_all=False, variant=22):
     """prune_all: option prune_min_rows = 1, so every 1-channel level goes through the certified
     pruned scan (K2p -> K3p) instead of only DB levels of >= 2^19 rows; variant:
-    the pruned-scan kernel (20: hi x hi block filter with fused corrections, the default; 14: the
-    filter followed by full chains)."""
+    the pruned-scan kernel (option k3p_variant; 22 = the library default)."""
     from ia_amd import _native
     L, k = z['L'], float(z['k'])
     Bp = [x.copy() for x in z['Bp_init']]
@@ -47,26 +46,24 @@ def _run_debug(ctx, z, prune_all=False, variant=20):
     return out, Bp, st
 
 
-@pytest.mark.parametrize('prune_all,variant', [(False, 20), (True, 7), (True, 14), (True, 15), (True, 11), (True, 18),
-                                                (True, 19), (True, 20), (True, 21), (True, 22), (True, 23)],
-                         ids=['default', 'pruned_v7', 'pruned', 'pruned_presorted_v15', 'pruned_presorted_v11',
-                              'pruned_v18', 'pruned_presorted_v19', 'pruned_v20', 'pruned_presorted_v21', 'pruned_v22',
-                              'pruned_presorted_v23'])
+@pytest.mark.parametrize('prune_all,variant', [(False, 22), (True, 20), (True, 21), (True, 22), (True, 24), (True, 25)],
+                         ids=['default', 'pruned_v20', 'pruned_presorted_v21', 'pruned_v22', 'pruned_v24',
+                              'pruned_presorted_v25'])
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)
 def test_debug_records_match_reference_calls(ctx, name, prune_all, variant):
     """Every NN pick, coherence pick and compute_distance value of the reference run.  With
     prune_all, the pruned scan K3p decides every 1-channel level (the bench's
-    dominant kernel checked directly against the reference's own per-pixel picks).  Variants 15
-    and 11 force the presorted wide-step path on every step: the per-step query sort K2s
-    (k_query_sort) + the presorted scan with (15) and without (11) the hi x hi block filter -
-    the kernels cfg4's 2048^2 level and every batched step wider than 512 queries run.  18 / 19:
-    14 / 15 with the correction products fused onto the hi x hi accumulator."""
+    dominant kernel checked directly against the reference's own per-pixel picks).  Variants 21
+    and 25 force the presorted wide-step path on every step: the per-step query sort K2s
+    (k_query_sort) + the presorted scan - the kernels cfg4's 2048^2 level and every batched step
+    wider than 512 queries run.  20 / 21: whole tiles; 22: the hi-only stream; 24 / 25: the
+    two-pass scan (LDS-DMA hi stream, then the passing tiles' full chains)."""
     z = load_e2e(name)
     out, Bp, st = _run_debug(ctx, z, prune_all, variant)
     ch = 1 if z['A_pyr'][0].ndim == 2 else z['A_pyr'][0].shape[2]
     if prune_all:
         assert st.pruned_levels == (z['L'] - 1 if ch == 1 else 0)
-    if variant in (14, 15, 18, 19, 20, 21, 22, 23) and st.pruned_levels > 0:  # the block filters run on pruned levels only
+    if st.pruned_levels > 0:  # the hi x hi block filter runs on pruned levels only
         assert 0 < st.dist_pairs_corrected <= st.dist_pairs
         assert 0 < st.dist_tiles_rows <= st.dist_tiles
     assert st.bound_violations == 0 and st.kappa_ambiguous == 0

@@ -10,7 +10,7 @@ import ia_amd  # noqa: F401
 pytestmark = pytest.mark.gpu
 
 
-def _run(ctx, job, prune, variant=7, group=1):
+def _run(ctx, job, prune, variant=22, group=1):
     from ia_amd import _native
     ctx.set_option('prune', prune)
     ctx.set_option('prune_group', group)
@@ -33,15 +33,11 @@ def _run(ctx, job, prune, variant=7, group=1):
     return Bp, S, IM, st
 
 
-@pytest.mark.parametrize('size,n_pruned,variant', [(512, 1, 7), (1024, 2, 7), (512, 1, 11), (1024, 2, 11), (512, 1, 14),
-                                                      (1024, 2, 14), (512, 1, 15), (1024, 2, 15), (512, 1, 18), (1024, 2, 18),
-                                                      (512, 1, 19), (1024, 2, 19), (512, 1, 20), (1024, 2, 20), (512, 1, 21),
-                                                      (1024, 2, 21), (512, 1, 22), (1024, 2, 22), (512, 1, 23),
-                                                      (1024, 2, 23)])
+@pytest.mark.parametrize('size,n_pruned,variant', [(sz, n, v) for v in (20, 21, 22, 24, 25) for sz, n in ((512, 1), (1024, 2))])
 def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
-    """variant = the pruned-scan kernel version (option k3p_variant: 7 / 11 without, 14 / 15,
-    18 / 19, 20 (default) / 21 and 22 / 23 (hi-only tile stream) with the hi x hi block filter;
-    the odd ones with the queries presorted once per step): every one is exact"""
+    """variant = the pruned-scan kernel version (option k3p_variant): 20 / 21 whole tiles, 22 the
+    hi-only tile stream, 24 / 25 the two-pass scan (LDS-DMA hi stream, then the passing tiles'
+    chains); the odd ones with the queries presorted once per step.  Every one is exact."""
     from ia_amd import synth
     job = synth.make_job(size)
     Bp0, S0, IM0, st0 = _run(ctx, job, 0)
@@ -55,25 +51,23 @@ def test_pruned_equals_unpruned(ctx, size, n_pruned, variant):
     assert st1.dist_pairs < st1.dist_pairs_full
     assert st1.dist_pairs_full == st0.dist_pairs_full
     assert st1.dist_tiles <= st1.dist_tiles_full and st1.dist_tiles_full == st0.dist_tiles_full
-    if variant in (14, 15, 18, 19, 20, 21, 22, 23):  # block filters: most box-needed pairs stop after a cheap product
-        assert 0 < st1.dist_pairs_corrected < st1.dist_pairs
-        assert 0 < st1.dist_tiles_rows <= st1.dist_tiles   # loaded tiles with a filter-passing block
-        print('filter-passing pairs %.3f of the box-needed ones, tiles %.3f of the loaded ones'
-              % (st1.dist_pairs_corrected / st1.dist_pairs, st1.dist_tiles_rows / st1.dist_tiles))
-    else:
-        assert st1.dist_pairs_corrected == 0 and st1.dist_tiles_rows == 0
+    # every variant has the hi x hi block filter: most box-needed pairs stop after a cheap product
+    assert 0 < st1.dist_pairs_corrected < st1.dist_pairs
+    assert 0 < st1.dist_tiles_rows <= st1.dist_tiles   # loaded tiles with a filter-passing block
+    print('filter-passing pairs %.3f of the box-needed ones, tiles %.3f of the loaded ones'
+          % (st1.dist_pairs_corrected / st1.dist_pairs, st1.dist_tiles_rows / st1.dist_tiles))
     print('size %d: pairs left %.3f, DB tiles loaded %.3f, fallbacks %d -> %d'
           % (size, st1.dist_pairs / st1.dist_pairs_full, st1.dist_tiles / st1.dist_tiles_full, st0.fallbacks,
              st1.fallbacks))
 
 
-@pytest.mark.parametrize('variant', [20, 21])
+@pytest.mark.parametrize('variant', [21, 22, 24, 25])
 def test_fused_gather_equals_separate_launches(ctx, variant):
     """option fuse_gather (ia_kernels.hip k_merge_gather): the merge of step t and the gather of
     step t + 1 in one launch, the step's results handed row to row; with K3 timing every third
     step (time_dist 3: sampled steps run the separate launches) the fused and separate forms
     alternate within a level; option fuse_sort moves the query sort into the fused gathers.  All
-    runs bit-identical (21: presorted wide-step scan)."""
+    runs bit-identical (21 / 25: presorted wide-step scans)."""
     from ia_amd import synth
     job = synth.make_job(1024)
     runs = []
@@ -106,7 +100,7 @@ def test_pruned_groups_equal_unpruned(ctx, size, group):
     from ia_amd import synth
     job = synth.make_job(size)
     Bp0, S0, IM0, st0 = _run(ctx, job, 0)
-    Bp1, S1, IM1, st1 = _run(ctx, job, 1, 14, group)
+    Bp1, S1, IM1, st1 = _run(ctx, job, 1, 24, group)
     for level in range(1, job.L):
         assert np.array_equal(S0[level], S1[level]), level
         assert np.array_equal(IM0[level], IM1[level]), level
@@ -122,22 +116,21 @@ def test_prune_option_rejects_bad_values(ctx):
         ctx.set_option('prune', 2)
     with pytest.raises(_native.IAError):
         ctx.set_option('prune_group', 3)
-    with pytest.raises(_native.IAError):
-        ctx.set_option('k3p_variant', 24)
-    for v in (1, 6, 12, 13, 16, 17, 24):   # earlier versions: in git history only
+    for v in (1, 6, 7, 11, 12, 13, 14, 15, 16, 17, 18, 19, 23, 26):   # earlier versions: in git history only
         with pytest.raises(_native.IAError):
             ctx.set_option('k3p_variant', v)
     with pytest.raises(_native.IAError):
         ctx.set_option('prune_min_rows', 0)
 
 
-@pytest.mark.parametrize('variant', [14, 15, 7, 11, 18, 19, 20, 21, 22, 23])
+@pytest.mark.parametrize('variant', [20, 21, 22, 24, 25])
 def test_pruned_scan_over_512_tiles_per_workgroup(ctx, variant):
     """a DB of more than 256 x 512 tiles (> 4.19 M rows: here A 2048 x 2080,
     133,120 tiles, 520 per workgroup) against a small B.  The pruned scan keeps every workgroup's
     tile boxes in LDS (up to IA_K3P_MAXK_LDS tiles); every tile must be scanned, in the
-    in-kernel-sort (14, 7) and the presorted (15, 11) forms: the level must equal the unpruned
-    scan bit for bit."""
+    in-kernel-sort (20, 22, 24) and the presorted (21, 25) forms (24 / 25: beyond the LDS budget of
+    their static DMA rings the launcher takes 22 / 21): the level must equal the unpruned scan bit
+    for bit."""
     from ia_amd import _native, synth
     from ia_amd import config as _c
     ah, aw, bh, bw = 2048, 2080, 48, 48
@@ -208,10 +201,10 @@ def test_nn_bound_is_exact_and_tighter(ctx):
     job = synth.make_job(1024)
     ctx.set_option('nn_bound', 0)
     try:
-        Bp0, S0, IM0, st0 = _run(ctx, job, 1, 20)
+        Bp0, S0, IM0, st0 = _run(ctx, job, 1, 24)
     finally:
         ctx.set_option('nn_bound', 1)
-    Bp1, S1, IM1, st1 = _run(ctx, job, 1, 20)
+    Bp1, S1, IM1, st1 = _run(ctx, job, 1, 24)
     for level in range(1, job.L):
         assert np.array_equal(S0[level], S1[level]), level
         assert np.array_equal(IM0[level], IM1[level]), level
