@@ -659,6 +659,11 @@ def main():
     # also time the other stream's kernels, so the roofline comes from one extra sequential pass
     concurrent = len(ctxs) > 1 or (args.pipeline and sw is None and (not owner or pipe_owner) and args.shard_jobs <= 1)
     elapsed, stats = timed(args.steps, run, not concurrent, hc)
+    # N = 1 self-check: the last timed step's fetched B', s, im (every level)
+    # must equal, bit for bit, a one-stream sequential run of the same job - the roofline pass
+    # below when the timed steps ran concurrently (pipelined levels, several cfg5 streams), else
+    # one extra run
+    h_timed = hc.digest() if world == 1 else None
     dj1 = h_shard = None
     if world > 1 and args.mode == 'shard':
         # this rank's own job (owner mode: job `rank`; every rank holds every job otherwise: job
@@ -671,6 +676,14 @@ def main():
         _, stats_rl = timed(1, lambda st: run(st, [ctx]), True)
     else:
         stats_rl = stats
+        if world == 1:
+            run(_native.Stats(), [ctx])
+    parity = None
+    if world == 1:
+        hc.fetch()
+        parity = hc.digest() == h_timed
+        log('[bench] timed run %s the one-stream sequential run (sha1 of B\', s, im of every level)'
+            % ('equals' if parity else 'DIFFERS FROM'))
     value_replicas = value_strong = shard_parity = strong_parity = None
     strong_info = None
     if world > 1 and args.mode == 'shard':
@@ -896,10 +909,31 @@ def main():
         out['value_strong'] = value_strong
         out['strong_parity'] = strong_parity
         out['config']['strong'] = strong_info
+        # BASELINE config 3 is ONE 1024^2 analogy with its A database sharded
+        # over the GPUs, so the headline at N > 1 is that one-job run (strong scaling); the N-job
+        # weak reading (each rank owns a job, every rank scans its 1/N of the DB for all of them)
+        # moves to value_weak beside value_replicas
+        out['value_weak'] = value
+        out['ms_per_step_weak'] = out['ms_per_step']
+        out['config']['weak'] = {'jobs': jobs, 'exchange': args.exchange, 'parallelism': out['config']['parallelism'],
+                                 'scaling': 'weak', 'note': 'value_weak = %d %s jobs sharing A, one owned per rank, '
+                                                            'every pruned level\'s DB sharded %d ways' % (jobs, args.config, world)}
+        if value_strong is not None:
+            out['value'] = value_strong
+            out['ms_per_step'] = strong_info['ms_per_step']
+            out['scaling'] = 'strong'
+            out['config']['parallelism'] = strong_info['parallelism']
+            out['config']['jobs_per_step'] = 1
+        else:   # the one-job run failed on some rank: the weak reading stays the value, said so
+            out['config']['headline'] = 'value = the weak reading (the one-job sharded run failed: config.strong)'
     if value_replicas is not None:
         out['value_replicas'] = value_replicas
         out['config']['replicas'] = ('value_replicas = %d independent cfg jobs, one per GPU, no collective '
                                      '(B\' px/s aggregate)' % world)
+    if parity is not None:
+        out['parity'] = parity
+        out['config']['parity'] = ("sha1 of the last timed step's fetched B', s, im (every level) == a one-stream "
+                                   'sequential run of the same job on this GPU')
     if cpu is not None:
         out['cpu_baseline'] = cpu
     if rank == 0:
@@ -908,9 +942,9 @@ def main():
         cx.close()
     if dist:
         dist.destroy_process_group()
-    if shard_parity is False or strong_parity is False:
-        log('[bench] PARITY FAILURE: a sharded run differs from the single-GPU run (shard_parity %s, strong_parity %s)'
-            % (shard_parity, strong_parity))
+    if shard_parity is False or strong_parity is False or parity is False:
+        log('[bench] PARITY FAILURE: a run differs from its reference run (parity %s, shard_parity %s, strong_parity %s)'
+            % (parity, shard_parity, strong_parity))
         sys.exit(3)
 
 

@@ -138,6 +138,8 @@ def lib():
                               'or __graft_entry__.build(); there is no CPU fallback' % LIB_PATH)
             L = ctypes.CDLL(LIB_PATH)
             for name, (res, args) in EXPORTS.items():
+                if os.environ.get('IA_LIBIA') and not hasattr(L, name):
+                    continue   # a diagnostic / earlier-round library (same-box A/B): its own symbol set
                 fn = getattr(L, name)
                 fn.restype = res
                 fn.argtypes = args

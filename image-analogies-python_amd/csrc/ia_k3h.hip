@@ -65,7 +65,7 @@ __device__ __forceinline__ void slot_hi(h16x8 (&h)[4], const h16x8 *slot, int la
 #define IA_PROBE 0
 #endif
 #if IA_PROBE & 16  // diagnostic build only: per-wave phase cycle sums of the pruned scan (K3p, V >= 1)
-__device__ unsigned long long k3p_prof[12];
+__device__ unsigned long long k3p_prof[16];
 #define K3P_T(x) do { __builtin_amdgcn_sched_barrier(0); x = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define K3P_T(x) do { } while (0)
@@ -987,52 +987,112 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     // query sort).  No LDS atomic in this loop: the compiler puts a vmcnt(0) before any LDS
     // atomic while an LDS-DMA is pending, so the passing tiles go to per-wave lists (plk / plm
     // at w + NW n) instead of one counted list.
-    int kw = wave + 2 * NW;  // the next tile of this wave's walk
-    int np = 0;              // this wave's passing tiles
-    int kc = wave < K ? wave : -1, kq = wave + NW < K ? wave + NW : -1;
-    unsigned mc = kc >= 0 ? need_k(kc) : 0u, mq = kq >= 0 ? need_k(kq) : 0u;
-    int klast = kq >= 0 ? kq : min(wave, K - 1);  // the wave's last tile (its dummy DMA: L2-hot)
-    int sl = 0;                                   // ring slot of tile kc (kq: sl + 1, next: sl + 2, mod 3)
-    while (kc >= 0) {
-      // the next needed tile of the walk (need tests inline) into slot sl + 2
-      unsigned mn = 0u;
-      for (; kw < K; kw += NW) {
-        mn = need_k(kw);
-        if (mn) break;
-      }
-      const bool ok = kw < K;
-      const int kn = ok ? kw : -1;
-      dma_hi<KS>(db, tk(ok ? kw : klast), wring + (sl == 0 ? 2 : sl - 1) * IA_HSLOT, lane);
-      if (ok) {
-        klast = kw;
-        kw += NW;
-      }
-      ring_wait<8>();  // slot sl landed; the two younger tiles stay in flight
-      h16x8 hc[KS];
-      slot_hi(hc, wring + sl * IA_HSLOT, lane);
-      f32x16 acc[2];
-      unsigned pass = 0;
-      k3p_hhpipe_h<KS, QT, 0, true>(hc, ldsh + lane, mc, wR[kc], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
-      cnt += __popc(mc);
-      ntl++;
-      if (pass) {  // wave-uniform
-        nfull += __popc(pass);
-        ntp++;
-        if (lane == 0) {
-          plk[wave + NW * np] = kc;
-          plm[wave + NW * np] = pass;
+    // the box need test of a tile with the wave's per-query bounds held in registers (lane L of
+    // pair pr: sorted slot (2 pr + L / 32) 32 + L % 32): no LDS round trip per query-tile pair
+    float4 pql[NPAIR], pqh[NPAIR];
+    float pqu[NPAIR];
+#pragma unroll
+    for (int pr = 0; pr < NPAIR; pr++) {
+      const int jq = 2 * pr + half, x = jq * IA_TILE + (lane & 31);
+      const bool ok = jq < QT;
+      pql[pr] = ok ? qlo[x] : make_float4(0.f, 0.f, 0.f, 0.f);
+      pqh[pr] = ok ? qhi[x] : make_float4(0.f, 0.f, 0.f, 0.f);
+      pqu[pr] = ok ? qU[x] : -INFINITY;
+    }
+    auto need_r = [&](int k) -> unsigned {
+      const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
+      const bool cpass = cl && prune_lb(blo, bhi, ctl, cth) <= ctu;
+      const unsigned coarse = (unsigned)__ballot(cpass);
+      unsigned msk = 0;
+#pragma unroll
+      for (int pr = 0; pr < NPAIR; pr++) {
+        if ((coarse >> (2 * pr)) & 3u) {
+          const unsigned long long b = __ballot(prune_lb(blo, bhi, pql[pr], pqh[pr]) <= pqu[pr]);
+          msk |= (((unsigned)b != 0u ? 1u : 0u) | ((unsigned)(b >> 32) != 0u ? 2u : 0u)) << (2 * pr);
         }
-        np++;
       }
+      return msk & coarse;
+    };
+    // the query lo pieces of this launch's sorted slots ([QT][KS][64], the hi layout), gathered
+    // from the unsorted fragments through the sort (PRE: the presorted slice) into registers now:
+    // the loads are in flight during the stream, and its ring area receives them afterwards
+    constexpr int NLO = (QT * KS * IA_WAVE + WGT - 1) / WGT;
+    h16x8 lo_r[NLO];
+#pragma unroll
+    for (int i = 0; i < NLO; i++) {
+      const int e = tid + WGT * i;
+      const int L = e & 63, pq = e >> 6, qt = pq / KS, s2 = pq - qt * KS;
+      int64_t src = -1;
+      if (e < QT * KS * IA_WAVE) {
+        if constexpr (PRE) {
+          if (qt < qtb) src = ((int64_t)(qt0 + qt) * NP + 2 * s2 + 1) * IA_WAVE + L;
+        } else {
+          const int sx = s0 + qt * IA_TILE + (L & 31);
+          if (sx < Mpad) {
+            const int mq2 = order[sx];
+            src = ((int64_t)(mq2 >> 5) * NP + 2 * s2 + 1) * IA_WAVE + (L & 32) + (mq2 & 31);
+          }
+        }
+      }
+      lo_r[i] = qf[src >= 0 ? src : 0];
+      if (src < 0) lo_r[i] = h16x8{};
+    }
+    // the wave walks k = wave + NW j.  Its first two tiles were requested speculatively (before
+    // the sort); later tiles are requested only when needed, the search for the next needed one
+    // (need tests) running one tile ahead, while the older two are in flight
+    int np = 0;  // this wave's passing tiles
+    int kc = wave, kq = wave + NW;                     // tiles in slots sl, sl + 1 (>= K: none)
+    const int klast = min(wave, K - 1);                 // the dummy DMA's source (L2-hot)
+    unsigned mc = kc < K ? need_r(kc) : 0u, mq = kq < K ? need_r(kq) : 0u;
+    auto next_needed = [&](int k, unsigned &m) -> int {  // first needed tile >= k of the walk
+      m = 0u;
+      for (; k < K; k += NW) {
+        m = need_r(k);
+        if (m) break;
+      }
+      return k;
+    };
+    unsigned mn;
+    int kn = next_needed(wave + 2 * NW, mn);
+    int sl = 0;  // ring slot of tile kc
+    while (kc < K) {
+      const bool ok = kn < K;
+      dma_hi<KS>(db, tk(ok ? kn : klast), wring + (sl == 0 ? 2 : sl - 1) * IA_HSLOT, lane);
+      unsigned m2;
+      const int k2 = next_needed(ok ? kn + NW : K, m2);
+      ring_wait<8>();  // slot sl landed; the two younger tiles stay in flight
+      if (mc) {  // wave-uniform (0: a speculative tile that is not needed)
+        h16x8 hc[KS];
+        slot_hi(hc, wring + sl * IA_HSLOT, lane);
+        f32x16 acc[2];
+        unsigned pass = 0;
+        k3p_hhpipe_h<KS, QT, 0, true>(hc, ldsh + lane, mc, wR[kc], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
+        cnt += __popc(mc);
+        if (pass) {  // wave-uniform
+          nfull += __popc(pass);
+          ntp++;
+          if (lane == 0) {
+            plk[wave + NW * np] = kc;
+            plm[wave + NW * np] = pass;
+          }
+          np++;
+        }
+      }
+      ntl++;
       kc = kq;
       mc = mq;
       kq = kn;
       mq = mn;
+      kn = k2;
+      mn = m2;
       sl = sl == 2 ? 0 : sl + 1;
     }
     ring_wait<0>();   // the DMAs past the last tile land before the ring area is reused
+    unsigned long long pq0 = 0, pq1 = 0, pq2 = 0, pq3 = 0;
+    K3P_T(pq0);
     if (lane == 0) wcnt[wave] = np;
     __syncthreads();  // every wave's passing tiles are listed, every ring is idle
+    K3P_T(pq1);
     // the passing tiles in list order: entry j = wave w's n-th, w the first with j < sum wcnt[..w]
     int npass = 0;
 #pragma unroll
@@ -1043,25 +1103,21 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       return w + NW * jj;
     };
     int j = wave;  // passing tiles: wave w takes list entry w first, then entries from pctr
-    if (j < npass) ld_tile<KS>(a, db, tk(plk[pent(j)]), lane);
     // the query lo pieces into the ring area ([QT][KS][64], the hi layout): this launch's sorted
     // slots, gathered from the unsorted fragments through the sort (PRE: the presorted slice)
     h16x8 *qlo_f = ring;
-    for (int e = tid; e < QT * KS * IA_WAVE; e += WGT) {
-      const int L = e & 63, pq = e >> 6, qt = pq / KS, s2 = pq - qt * KS;
-      h16x8 v = {};
-      if constexpr (PRE) {
-        if (qt < qtb) v = qf[((int64_t)(qt0 + qt) * NP + 2 * s2 + 1) * IA_WAVE + L];
-      } else {
-        const int sx = s0 + qt * IA_TILE + (L & 31);
-        if (sx < Mpad) {
-          const int mq2 = order[sx];
-          v = qf[((int64_t)(mq2 >> 5) * NP + 2 * s2 + 1) * IA_WAVE + (L & 32) + (mq2 & 31)];
-        }
-      }
-      qlo_f[e] = v;
+#pragma unroll
+    for (int i = 0; i < NLO; i++) {
+      const int e = tid + WGT * i;
+      if (e < QT * KS * IA_WAVE) qlo_f[e] = lo_r[i];
     }
+    // (C) the DB rows of the passing tiles' positions, staged by the second pass behind the lo
+    // pieces (rowmap[32 k + j] = pos2row of the WG's tile k, position j): the records' row
+    // lookups below are then LDS reads instead of dependent global loads
+    int *rowmap = reinterpret_cast<int *>(ring + QT * KS * IA_WAVE);
+    if (j < npass) ld_tile<KS>(a, db, tk(plk[pent(j)]), lane);  // in flight during the barrier
     __syncthreads();
+    K3P_T(pq2);
     if (j < npass) {
       auto grab2 = [&]() -> int {
         int g = 0;
@@ -1074,8 +1130,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         const int kj = plk[xj];
         const unsigned pj = plm[xj];
         ld_tile<KS>(nxt, db, tk(jn < npass ? plk[pent(jn)] : kj), lane);  // unconditional (equal vmcnt)
+        const int prow = pos2row[(int64_t)tk(kj) * IA_TILE + (lane & 31)];
         asm volatile("" ::: "memory");
-        k3p_pairs_hl<KS, QT, 0>(cur, ldsh + lane, qlo_f + lane, pj, tk(kj), b1, b2, i1);
+        k3p_pairs_hl<KS, QT, 0>(cur, ldsh + lane, qlo_f + lane, pj, kj, b1, b2, i1);  // i1: the WG-local tile
+        if (lane < 32) rowmap[kj * IA_TILE + lane] = prow;
         j = jn;
       };
       while (j < npass) {
@@ -1084,6 +1142,15 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         step4(an, a);
       }
     }
+    K3P_T(pq3);
+#if IA_PROBE & 16
+    if (lane == 0 && M == Mpad - 10 && wg < 8) {  // two-pass phases: stream, barrier, lo staging, chains
+      atomicAdd(&k3p_prof[12], pq0 - ph[3]);
+      atomicAdd(&k3p_prof[13], pq1 - pq0);
+      atomicAdd(&k3p_prof[14], pq2 - pq1);
+      atomicAdd(&k3p_prof[15], pq3 - pq2);
+    }
+#endif
     } else {
     unsigned m;
     int k = next_k(wave, m);
@@ -1169,6 +1236,16 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }  // HHX != 4
   }
   K3P_T(ph[4]);
+  if constexpr (HHX == 4) {
+    // i1 holds WG-local tiles whose rows the second pass staged in LDS (every wave's)
+    const int *rowmap = reinterpret_cast<const int *>(ring + QT * KS * IA_WAVE);
+    __syncthreads();
+#pragma unroll
+    for (int q = 0; q < QT; q++) {
+      const int r = (int)(__float_as_uint(b1[q]) & 15u);
+      i1[q] = b1[q] == FLT_MAX ? 0x7fffffff : rowmap[i1[q] * IA_TILE + 4 * half + (r & 3) + 8 * (r >> 2)];
+    }
+  } else {
 #pragma unroll
   for (int q = 0; q < QT; q++) {  // tile + packed in-tile index -> DB position (-> DB row)
     const int r = (int)(__float_as_uint(b1[q]) & 15u);
@@ -1182,6 +1259,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     i1[q] = b1[q] == FLT_MAX ? 0x7fffffff : pos;
 #endif
   }
+  }  // HHX != 4
 
   // ---- 5. merge the 2*NW subsets of each query; records go to the original query slots
   // (the slice's query order is read before the reduction area, which extends past the
@@ -1284,8 +1362,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
 
 #if (IA_PROBE & 16) && defined(IA_K3H_KS) && defined(IA_K3H_QT) && IA_K3H_KS == 4 && IA_K3H_QT == 11
 void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau wave, to stderr
-  unsigned long long v[12];
+  unsigned long long v[16];
   if (hipMemcpyFromSymbol(v, HIP_SYMBOL(k3p_prof), sizeof(v)) != hipSuccess || v[4] == 0) return;
+  fprintf(stderr, "K3P_PROBE two-pass (v24/25): stream %.0f, barrier %.0f, lo staging %.0f, chains %.0f\n", (double)v[12] / v[4],
+          (double)v[13] / v[4], (double)v[14] / v[4], (double)v[15] / v[4]);
   fprintf(stderr, "K3P_PROBE tail split: half merge %.0f, barrier %.0f, subset merge + records %.0f\n", (double)v[9] / v[4],
           (double)v[10] / v[4], (double)v[11] / v[4]);
   fprintf(stderr, "K3P_PROBE v3 phases if variant>=3: load=setup, sort+scatter=need, need=loop, loop=tail, tail=[7]\n");
@@ -1294,7 +1374,7 @@ void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau w
   fprintf(stderr, "K3P_PROBE waves=%llu setup=%.0f need=%.0f loop=%.0f tail=%.0f tiles/wave=%.2f pairs/wave=%.2f (cycles/wave)\n",
           v[4], (double)v[0] / v[4], (double)v[1] / v[4], (double)v[2] / v[4], (double)v[3] / v[4], (double)v[5] / v[4],
           (double)v[6] / v[4]);
-  unsigned long long z[12] = {};
+  unsigned long long z[16] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(k3p_prof), z, sizeof(z));
 }
 #endif

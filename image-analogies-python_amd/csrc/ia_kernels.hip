@@ -2936,7 +2936,9 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
     hipFuncAttributes fa;
     const k3p_fn f24 = g4[qt - 1](variant);
     const size_t stat = f24 && hipFuncGetAttributes(&fa, (const void *)f24) == hipSuccess ? fa.sharedSizeBytes : 0;
-    if (!f24 || stat + lds > 160 * 1024) {  // (many tiles per workgroup or wide steps): the one-pass forms
+    // (and the second pass stages the lo pieces + a row map of the WG's tiles in the rings' 84 KiB)
+    const bool ring_fits = (size_t)qt * 4 * IA_WAVE * 16 + (size_t)kmax * IA_TILE * 4 <= (size_t)8 * 3 * 3584;
+    if (!f24 || !ring_fits || stat + lds > 160 * 1024) {  // (many tiles per workgroup or wide steps): the one-pass forms
       variant = variant == 25 ? 21 : 22;
       lds = dyn_lds(variant);
     }

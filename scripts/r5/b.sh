@@ -23,6 +23,10 @@ run base_v22_seq libia_base.so --pipeline 0 || exit 1
 run new_v24_seq libia.so --pipeline 0 --k3p-variant 24 || exit 1
 run new_v24_b libia.so --k3p-variant 24 || exit 1
 run base_v22_b libia_base.so || exit 1
-IA_LIBIA=$PWD/image-analogies-python_amd/libia_probe16.so timeout -k 10 300 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --pipeline 0 > $O/probe.json 2> $O/probe.err || { echo "probe failed"; tail -20 $O/probe.err; exit 1; }
-grep K3P_PROBE $O/probe.err | tail -4
+for v in 22 24; do
+IA_LIBIA=$PWD/image-analogies-python_amd/libia_probe16.so timeout -k 10 300 python -u bench.py --steps 1 --warmup 0 --no-cpu-baseline --pipeline 0 --k3p-variant $v > $O/probe_v$v.json 2> $O/probe_v$v.err || { echo "probe failed"; tail -20 $O/probe_v$v.err; exit 1; }
+echo "== probe v$v"; grep K3P_PROBE $O/probe_v$v.err | tail -5
+done
+timeout -k 10 120 ./tools/gap_micro 2000 > $O/gap_micro.txt 2>&1 || { echo "gap_micro failed"; cat $O/gap_micro.txt; exit 1; }
+cat $O/gap_micro.txt
 echo ALL-OK

@@ -51,4 +51,9 @@ def test_two_ranks_bit_exact_to_single_gpu(config, exchange, tmp_path):
     assert 'shard_error' not in line['config'], line['config'].get('shard_error')
     assert line['shard_parity'] is True
     assert line['strong_parity'] is True and line['value_strong'] > 0
+    # the headline is BASELINE config 3 as named: ONE job, its DB sharded over the ranks (strong
+    # scaling); the N-job weak reading rides along as value_weak
+    assert line['value'] == line['value_strong'] and line['scaling'] == 'strong'
+    assert line['config']['jobs_per_step'] == 1 and line['config']['parallelism'].endswith('_jobs1')
+    assert line['value_weak'] > 0 and line['config']['weak']['scaling'] == 'weak'
     assert line['stats']['bound_violations'] == 0 and line['stats']['kappa_ambiguous'] == 0
