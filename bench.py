@@ -376,13 +376,13 @@ def main():
     ap.add_argument('--coarse-fuse-gather', type=int, default=1, choices=[0, 1],
                     help='0: the pipelined coarser levels run their merge and next gather as separate launches '
                          '(shorter-resident waves beside the finest level\'s scans); 1 (default): fused like the finest')
-    ap.add_argument('--k3p-variant', type=int, default=22, choices=[20, 21, 22, 24, 25],
+    ap.add_argument('--k3p-variant', type=int, default=24, choices=[20, 21, 22, 24, 25],
                     help='pruned-scan kernel version (ia_k3h.hip k3h_prune3, DESIGN.md §4b/§4h/§4i): 20 / 21 = whole '
                          'DB tiles in two register buffers, hi x hi block filter with the corrections fused on '
                          'query-tile pairs (in-kernel query sort / presorted); 22 = the hi-only tile stream, the lo '
                          'halves of filter-passing tiles one tile later; 24 / 25 = two passes: the hi stream by '
-                         'LDS-DMA two tiles deep, then the passing tiles\' full chains.  Steps wider than 512 queries '
-                         'run the presorted form (20 and 22: 21; 24: 25)')
+                         'LDS-DMA two tiles deep, then the passing tiles\' full chains (default).  Steps wider than 512 '
+                         'queries run 21 (the measured fastest presorted form)')
     ap.add_argument('--pipeline', type=int, default=1, choices=[0, 1],
                     help='1 (default; one-job configs and replicas): consecutive levels overlap (two libia '
                          'contexts, each level\'s steps waiting only for the steps of the previous level they read; '

@@ -134,7 +134,7 @@ struct ia_ctx {
   int shard_unpruned = 0;        // option "shard_unpruned": 1 = shard levels that scan unpruned too
   int prune_group = 1;           // option "prune_group": Morton tiles interleaved in groups of G (ia_prune.hip k_make_table)
   int matcher = IA_MATCH_F16X3;  // option "matcher"
-  int k3p_variant = 22;          // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
+  int k3p_variant = 24;          // option "k3p_variant": pruned-scan kernel version (ia_k3h.hip k3h_prune*)
   int k3_variant = 1;            // option "k3_variant": K3h epilogue (0 compare/select, 1 packed index)
   int k3p_blocks = 1;            // option "k3p_blocks": 1 = a wide step's presorted pruned scan is one launch over
                                  // all its query blocks (2-D grid); 0 = one launch per block
@@ -426,7 +426,7 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     return IA_OK;
   }
   if (!std::strcmp(name, "row_source")) {
-    if (value != 0) return fail(IA_EINVAL, "ia_set_option: row_source 1 is built with DIAG=1 only (measured slower)");
+    if (value != 0) return fail(IA_EINVAL, "ia_set_option: row_source is 0 (the image-gathered rows, measured slower, are in git history only)");
     c->row_source = value;
     return IA_OK;
   }
@@ -1357,7 +1357,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         const char *dbp = (const char *)c->db.p + (size_t)(x.t0 - g.tile0) * tile_bytes;
         const int kv = c->k3p_variant;
         // the in-kernel-sort variant (ink: 20 / 22 / 24) or its presorted form (21 / 25)
-        const int k3x = ink ? (kv == 21 ? 20 : kv == 25 ? 24 : kv) : (kv == 24 || kv == 25 ? 25 : 21);
+        const int k3x = ink ? (kv == 21 ? 20 : kv == 25 ? 24 : kv) : (kv == 25 ? 25 : 21);
         ia_launch_k3p(ink ? QTs : xo_QTx, dbp, loc + XOLayout::FRAG, reinterpret_cast<const float4 *>(loc + XOLayout::INFO),
                       mas[i].boxes, mas[i].pos2row, n, 0, sd.M, ink ? Mpj : Mrec, nch, nullptr, nullptr,
                       c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
@@ -1481,7 +1481,9 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     const bool wide = sd.Mpad > 512 || (c->k3p_blocks && sd.Mpad > qtmax * IA_TILE);
     // sorted by the previous launch's gathers: the presorted form of the variant, no K2s
     const bool gsorted = fsort && gathered == t && gsort;
-    const int k3v = (kv == 21 || kv == 25) ? kv : (prune && (wide || gsorted) ? (kv == 24 ? 25 : 21) : kv);
+    // wide steps: the presorted form; under 24 that is 21 (cfg4's two-block steps measured faster
+    // with whole tiles than with the two-pass form 25: 6.20 vs 6.03 M px/s)
+    const int k3v = (kv == 21 || kv == 25) ? kv : (prune && (wide || gsorted) ? 21 : kv);
     const bool presorted = k3v == 21 || k3v == 25;
     const float4 *tboxp = gsorted ? nullptr : c->qs_tbox.as<float4>();  // nullptr: boxes from the slice
     if (prune && presorted && !gsorted)

@@ -564,7 +564,7 @@ __device__ __forceinline__ void k3p_hhpairs(const h16x8 (&a)[2 * KS], const h16x
 #define IA_K3H_CAT(a, b, c) IA_K3H_CAT2(a, b, c)
 // variant (option "k3_variant"): 0 = compare/select epilogue, 1 = packed-index epilogue
 // The product library holds only the packed-index epilogue (variant 1); the compare/select
-// epilogue (0) and the probes (2, 3) are experiments, built with DIAG=1 only.
+// epilogue (0) and the probes (2, 3) are in git history.
 k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
   (void)variant;
   return k3h_scan<IA_K3H_KS, IA_K3H_QT, IA_WGH / IA_WAVE, true>;
@@ -673,7 +673,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   int *plk = reinterpret_cast<int *>(wR + K);                           // HHX 4: [K] filter-passing tiles
   unsigned *plm = reinterpret_cast<unsigned *>(plk + K);                // HHX 4: [K] their passing blocks
   __shared__ unsigned wpairs[NW], wtiles[NW], wfull[NW], wtp[NW];
-  __shared__ int pctr;  // HHX 4: passing tiles handed out
+  __shared__ int pcount, pctr;  // HHX 4: passing tiles listed / handed out
   __shared__ int wcnt[NW];
   const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -753,8 +753,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   };
   __shared__ int kctr;  // next tile index to hand out
   if (tid == 0) {
-    kctr = HHX == 4 ? 2 * NW : NW;  // HHX 4: each wave's first two tiles are static (the speculative loads)
-    pctr = NW;
+    kctr = HHX == 4 ? 2 * NW : NW;  // HHX 4: each wave's first two tiles are static (the speculative DMAs)
+    pcount = 0;
+    pctr = 0;
   }
   if constexpr (PRE) {
     __syncthreads();
@@ -1037,29 +1038,34 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       lo_r[i] = qf[src >= 0 ? src : 0];
       if (src < 0) lo_r[i] = h16x8{};
     }
-    // the wave walks k = wave + NW j.  Its first two tiles were requested speculatively (before
-    // the sort); later tiles are requested only when needed, the search for the next needed one
-    // (need tests) running one tile ahead, while the older two are in flight
+    // the wave's first two tiles (wave, wave + NW) were requested speculatively (before the
+    // sort); later ones come from the LDS counter (from 2 NW on: the waves' shares balance) and
+    // are requested only when needed, the search for the next needed one (need tests, counter)
+    // running one tile ahead, while the older two are in flight.  (The DMAs are inline asm, so
+    // the compiler puts no vmcnt(0) before the counter's LDS atomic.)
     int np = 0;  // this wave's passing tiles
+    int kown = -1;       // its first one (tile, passing blocks)
+    unsigned mown = 0u;
     int kc = wave, kq = wave + NW;                     // tiles in slots sl, sl + 1 (>= K: none)
     const int klast = min(wave, K - 1);                 // the dummy DMA's source (L2-hot)
     unsigned mc = kc < K ? need_r(kc) : 0u, mq = kq < K ? need_r(kq) : 0u;
-    auto next_needed = [&](int k, unsigned &m) -> int {  // first needed tile >= k of the walk
+    auto next_needed = [&](unsigned &m) -> int {  // the next needed tile from the counter (>= K: none)
       m = 0u;
-      for (; k < K; k += NW) {
+      int k = grab();
+      for (; k < K; k = grab()) {
         m = need_r(k);
         if (m) break;
       }
       return k;
     };
     unsigned mn;
-    int kn = next_needed(wave + 2 * NW, mn);
+    int kn = next_needed(mn);
     int sl = 0;  // ring slot of tile kc
     while (kc < K) {
       const bool ok = kn < K;
       dma_hi<KS>(db, tk(ok ? kn : klast), wring + (sl == 0 ? 2 : sl - 1) * IA_HSLOT, lane);
-      unsigned m2;
-      const int k2 = next_needed(ok ? kn + NW : K, m2);
+      unsigned m2 = 0u;
+      const int k2 = ok ? next_needed(m2) : K;
       ring_wait<8>();  // slot sl landed; the two younger tiles stay in flight
       if (mc) {  // wave-uniform (0: a speculative tile that is not needed)
         h16x8 hc[KS];
@@ -1071,9 +1077,16 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         if (pass) {  // wave-uniform
           nfull += __popc(pass);
           ntp++;
+          // one list for the workgroup; a wave's first passing tile is marked (bit 31): the wave
+          // itself takes it in the second pass, the others go to the pool
           if (lane == 0) {
-            plk[wave + NW * np] = kc;
-            plm[wave + NW * np] = pass;
+            const int x = atomicAdd(&pcount, 1);
+            plk[x] = kc;
+            plm[x] = pass | (np == 0 ? 0x80000000u : 0u);
+          }
+          if (np == 0) {
+            kown = kc;
+            mown = pass;
           }
           np++;
         }
@@ -1090,57 +1103,67 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     ring_wait<0>();   // the DMAs past the last tile land before the ring area is reused
     unsigned long long pq0 = 0, pq1 = 0, pq2 = 0, pq3 = 0;
     K3P_T(pq0);
-    if (lane == 0) wcnt[wave] = np;
+    // second pass.  A wave with passing tiles starts on its own first one, whose whole tile is
+    // requested now (in flight during the barriers); the list's unmarked entries form a pool
+    // handed out through pctr
+    int kcur = kown;
+    unsigned mcur = mown;
+    if (kcur >= 0) ld_tile<KS>(a, db, tk(kcur), lane);
     __syncthreads();  // every wave's passing tiles are listed, every ring is idle
     K3P_T(pq1);
-    // the passing tiles in list order: entry j = wave w's n-th, w the first with j < sum wcnt[..w]
-    int npass = 0;
-#pragma unroll
-    for (int w = 0; w < NW; w++) npass += wcnt[w];
-    auto pent = [&](int jj) -> int {  // list entry -> index into plk / plm
-      int w = 0;
-      for (; w < NW - 1 && jj >= wcnt[w]; w++) jj -= wcnt[w];
-      return w + NW * jj;
+    const int npass = pcount;
+    auto grab2 = [&]() -> int {  // the next unmarked list entry (>= npass: none)
+      int g;
+      for (;;) {
+        g = 0;
+        if (lane == 0) g = atomicAdd(&pctr, 1);
+        g = __builtin_amdgcn_readfirstlane(g);
+        if (g >= npass || !(plm[g] >> 31)) break;
+      }
+      return g;
     };
-    int j = wave;  // passing tiles: wave w takes list entry w first, then entries from pctr
     // the query lo pieces into the ring area ([QT][KS][64], the hi layout): this launch's sorted
-    // slots, gathered from the unsorted fragments through the sort (PRE: the presorted slice)
+    // slots (gathered into registers before the stream)
     h16x8 *qlo_f = ring;
 #pragma unroll
     for (int i = 0; i < NLO; i++) {
       const int e = tid + WGT * i;
       if (e < QT * KS * IA_WAVE) qlo_f[e] = lo_r[i];
     }
-    // (C) the DB rows of the passing tiles' positions, staged by the second pass behind the lo
-    // pieces (rowmap[32 k + j] = pos2row of the WG's tile k, position j): the records' row
-    // lookups below are then LDS reads instead of dependent global loads
+    // the DB rows of the passing tiles' positions, staged by the second pass behind the lo pieces
+    // (rowmap[32 k + j] = pos2row of the WG's tile k, position j): the records' row lookups below
+    // are then LDS reads instead of dependent global loads
     int *rowmap = reinterpret_cast<int *>(ring + QT * KS * IA_WAVE);
-    if (j < npass) ld_tile<KS>(a, db, tk(plk[pent(j)]), lane);  // in flight during the barrier
+    if (kcur < 0) {  // no passing tile of its own: the first from the pool
+      const int j0 = grab2();
+      if (j0 < npass) {
+        kcur = plk[j0];
+        mcur = plm[j0];
+        ld_tile<KS>(a, db, tk(kcur), lane);
+      }
+    }
     __syncthreads();
     K3P_T(pq2);
-    if (j < npass) {
-      auto grab2 = [&]() -> int {
-        int g = 0;
-        if (lane == 0) g = atomicAdd(&pctr, 1);
-        return __builtin_amdgcn_readfirstlane(g);
-      };
-      auto step4 = [&](const h16x8(&cur)[NP], h16x8(&nxt)[NP]) {
-        const int jn = grab2();
-        const int xj = pent(j);
-        const int kj = plk[xj];
-        const unsigned pj = plm[xj];
-        ld_tile<KS>(nxt, db, tk(jn < npass ? plk[pent(jn)] : kj), lane);  // unconditional (equal vmcnt)
-        const int prow = pos2row[(int64_t)tk(kj) * IA_TILE + (lane & 31)];
-        asm volatile("" ::: "memory");
-        k3p_pairs_hl<KS, QT, 0>(cur, ldsh + lane, qlo_f + lane, pj, kj, b1, b2, i1);  // i1: the WG-local tile
-        if (lane < 32) rowmap[kj * IA_TILE + lane] = prow;
-        j = jn;
-      };
-      while (j < npass) {
-        step4(a, an);
-        if (j >= npass) break;
-        step4(an, a);
+    auto step4 = [&](const h16x8(&cur)[NP], h16x8(&nxt)[NP]) {
+      const int jn = grab2();
+      int kn = -1;
+      unsigned mn = 0u;
+      if (jn < npass) {
+        kn = plk[jn];
+        mn = plm[jn];
       }
+      ld_tile<KS>(nxt, db, tk(kn >= 0 ? kn : kcur), lane);  // unconditional (equal vmcnt)
+      const int prow = pos2row[(int64_t)tk(kcur) * IA_TILE + (lane & 31)];
+      asm volatile("" ::: "memory");
+      k3p_pairs_hl<KS, QT, 0>(cur, ldsh + lane, qlo_f + lane, mcur, kcur, b1, b2, i1);  // i1: the WG-local tile
+      if (lane < 32) rowmap[kcur * IA_TILE + lane] = prow;
+      kcur = kn;
+      mcur = mn;
+    };
+    while (kcur >= 0) {
+      step4(a, an);
+      if (kcur < 0) break;
+      step4(an, a);
     }
     K3P_T(pq3);
 #if IA_PROBE & 16

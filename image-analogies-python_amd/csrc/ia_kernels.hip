@@ -34,9 +34,6 @@
 // waves (= queries) per workgroup of the one-wave-per-query kernels K2h, K2p, K4: one, so a
 // step's few hundred latency-bound waves spread over as many CUs (their L1, TA and LDS) as
 // possible; 3.35 -> 3.44 M px/s against 4 per workgroup on one box (profiles/r02/wpb)
-#ifndef IA_K1_GATHER
-#define IA_K1_GATHER 0  // 1: the round-2 image-gathering DB builds (same-box A/B only)
-#endif
 #ifndef IA_PQ_WPB
 #define IA_PQ_WPB 1
 #endif
@@ -437,33 +434,8 @@ __global__ void __launch_bounds__(IA_WG) k_db_build(LevelGeo g, Imgs A, const do
 // K1b: the fp64 feature DB, row-major (row = img*h*w + r*w + c, stride Geo::DS doubles, the
 // tail zero), holding the exact pixel values of create_index's As rows (algorithms.py:63-67).
 // The merge reranks candidates from it with contiguous 16-byte loads instead of re-gathering
-// four symmetric-padded images per row.  One thread per (row, 8 features): coalesced stores.
+// four symmetric-padded images per row.
 // ------------------------------------------------------------------------------------------
-#if IA_K1_GATHER  // round-2 K1b (A/B builds only): one thread per (row, 8 features), 0.89 TB/s at 1024^2
-template <int CH>
-__global__ void __launch_bounds__(IA_WG) k_db64_build(LevelGeo g, Imgs A, double *__restrict__ db64) {
-  using G = Geo<CH>;
-  constexpr int NCH = G::DS / 8;
-  const int64_t gid = (int64_t)blockIdx.x * IA_WG + threadIdx.x;
-  if (gid >= g.NA * NCH) return;
-  const int64_t row = gid / NCH;
-  const int chunk = (int)(gid - row * NCH);
-  const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
-  const int img = (int)((unsigned)row / hw);
-  const unsigned rem = (unsigned)row - (unsigned)img * hw;
-  const int pr = (int)(rem / (unsigned)g.aw), pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
-  const Px P = make_px<CH>(A, pr, pc);
-  double v[8];
-#pragma unroll
-  for (int e = 0; e < 8; e++) {
-    const int f = chunk * 8 + e;
-    v[e] = f < G::D ? featp<CH>(A, P, f, img) : 0.;
-  }
-  double2 *dst = reinterpret_cast<double2 *>(db64 + row * G::DS + chunk * 8);
-#pragma unroll
-  for (int e = 0; e < 4; e++) dst[e] = make_double2(v[2 * e], v[2 * e + 1]);
-}
-#else
 // One wave per 64 consecutive DB rows (= raster pixels of one A' image, so lane-adjacent rows are
 // pixel-adjacent): every feature load of the wave reads 64 consecutive image values (coalesced),
 // the rows are assembled in LDS (odd row stride: conflict-light) and leave as one contiguous
@@ -496,7 +468,6 @@ __global__ void __launch_bounds__(IA_WAVE) k_db64_build(LevelGeo g, Imgs A, doub
     dst[i] = make_double2(t[rr * LS + cc], t[rr * LS + cc + 1]);
   }
 }
-#endif
 
 // ------------------------------------------------------------------------------------------
 // K2: queries of one wavefront step (one wave per query pixel)
@@ -723,63 +694,6 @@ __global__ void __launch_bounds__(IA_WG) k_absmax(AbsArrays arr, unsigned *__res
   if ((threadIdx.x & 63) == 0) atomicMax(out, __float_as_uint(m));
 }
 
-#if IA_K1_GATHER  // round-2 K1 (A/B builds only): one thread per row gathering from the images
-template <int CH, int KS>
-__global__ void __launch_bounds__(IA_WG) k_db_build_h(LevelGeo g, Imgs A, const double *__restrict__ mu_part,
-                                                       h16x8 *__restrict__ db, unsigned *__restrict__ Rbits) {
-  constexpr int D = 55 * CH;
-  static_assert(16 * KS >= D + 1, "k-steps must hold D features + the norm column");
-  const int64_t pos = (int64_t)g.tile0 * IA_TILE + (int64_t)blockIdx.x * IA_WG + threadIdx.x;
-  const bool inr = pos < (int64_t)g.tile1 * IA_TILE;
-  const int64_t ltile = pos / IA_TILE - g.tile0;
-  const int j = (int)(pos % IA_TILE);
-  const int64_t row = inr ? ia_pos_row_t(pos, g.n_tiles, g.pos2row) : g.NA;
-  const bool real = inr && row < g.NA;
-  int img = 0, pr = 0, pc = 0;
-  if (real) {
-    const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
-    img = (int)((unsigned)row / hw);
-    const unsigned rem = (unsigned)row - (unsigned)img * hw;
-    pr = (int)(rem / (unsigned)g.aw);
-    pc = (int)(rem - (unsigned)pr * (unsigned)g.aw);
-  }
-  const Px P = make_px<CH>(A, pr, pc);
-  double norm = 0.;
-#pragma unroll
-  for (int s = 0; s < KS; s++) {
-#pragma unroll
-    for (int h = 0; h < 2; h++) {
-      h16x8 vh, vl;
-#pragma unroll
-      for (int e = 0; e < 8; e++) {
-        const int f = 16 * s + 8 * h + e;
-        double a = 0.;
-        if (f < D) {
-          if (real) {
-            a = featp<CH>(A, P, f, img) - mu_part[feat_part<CH>(f) * CH + feat_ch<CH>(f)];
-            norm += a * a;
-          }
-        } else if (f == D) {
-          a = real ? norm * (1.0 / IA_NORM_SCALE) : 60000.0;  // padding rows: never a candidate
-        }
-        _Float16 hi, lo;
-        split_h(a, hi, lo);
-        vh[e] = hi;
-        vl[e] = lo;
-      }
-      if (inr && !(TileFmt<KS>::CMP && s == KS - 1 && h == 1)) {  // (compact: padding half not stored)
-        db[ltile * TileFmt<KS>::STRIDE + TileFmt<KS>::off(2 * s, h * IA_TILE + j)] = vh;
-        db[ltile * TileFmt<KS>::STRIDE + TileFmt<KS>::off(2 * s + 1, h * IA_TILE + j)] = vl;
-      }
-    }
-  }
-  // R = max |a'| (certification bound): wave max first, one atomic per wave
-  float R = real ? (float)(sqrt(norm) * (1.0 + 1e-6)) : 0.f;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) R = fmaxf(R, __shfl_xor(R, o, 64));
-  if ((threadIdx.x & 63) == 0 && R > 0.f) atomicMax(Rbits, __float_as_uint(R));
-}
-#else
 // One wave per DB tile (32 rows x 64 columns in v_mfma_f32_32x32x16_f16 operand order): lane L
 // (row j = L & 31, column half h = L >> 5) holds columns 16s + 8h .. + 7 of every k-step s, i.e.
 // 64 contiguous bytes of its row in the fp64 row DB (K1b, written just before: rows are whole
@@ -871,7 +785,6 @@ __global__ void __launch_bounds__(IA_WG) k_db_build_h(LevelGeo g, const double *
     if (m > 0.f) atomicMax(Rbits, __float_as_uint(m));
   }
 }
-#endif
 
 template <int KS>
 __device__ __forceinline__ void put_qh(_Float16 *qf, int m, int f, double v) {
@@ -2730,12 +2643,7 @@ void ia_launch_merge_xchg(const LevelGeo &g, const StepDesc &sd, const Imgs &A, 
 
 template <int CH>
 static void launch_db64_t(const LevelGeo &g, const Imgs &A, double *db64, hipStream_t st) {
-#if IA_K1_GATHER
-  const int64_t n = g.NA * (Geo<CH>::DS / 8);
-  hipLaunchKernelGGL(k_db64_build<CH>, dim3(cdiv(n, IA_WG)), dim3(IA_WG), 0, st, g, A, db64);
-#else
   hipLaunchKernelGGL(k_db64_build<CH>, dim3(cdiv(g.NA, IA_WAVE)), dim3(IA_WAVE), 0, st, g, A, db64);
-#endif
 }
 void ia_launch_db64_build(const LevelGeo &g, const Imgs &A, double *db64, hipStream_t st) {
   if (g.ch == 1) launch_db64_t<1>(g, A, db64, st);
@@ -2817,16 +2725,10 @@ void ia_launch_absmax(const double *const *p, const int64_t *n, unsigned *out, h
 template <int CH, int KS>
 static void launch_db_h_t(const LevelGeo &g, const Imgs &A, const double *db64, const double *mu, void *db, unsigned *Rbits,
                           hipStream_t st) {
-#if IA_K1_GATHER
-  (void)db64;
-  const int64_t rows = (int64_t)(g.tile1 - g.tile0) * IA_TILE;
-  hipLaunchKernelGGL((k_db_build_h<CH, KS>), dim3(cdiv(rows, IA_WG)), dim3(IA_WG), 0, st, g, A, mu, (h16x8 *)db, Rbits);
-#else
   (void)A;
   const int64_t tiles = (int64_t)g.tile1 - g.tile0;  // one wave per tile, <= 4 tiles per wave
   const int64_t nwg = std::max<int64_t>(1, std::min<int64_t>(cdiv(tiles, IA_WG / IA_WAVE), 2048));
   hipLaunchKernelGGL((k_db_build_h<CH, KS>), dim3((unsigned)nwg), dim3(IA_WG), 0, st, g, db64, mu, (h16x8 *)db, Rbits);
-#endif
 }
 void ia_launch_db_build_h(const LevelGeo &g, const Imgs &A, const double *db64, const double *mu, void *db, unsigned *Rbits,
                           hipStream_t st) {
@@ -2918,7 +2820,7 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   // the in-kernel sort (20, 22, 24) holds <= 512 queries (wider: the host ran K2s, the presorted
   // form 21 / 25); every variant walks any number of tiles (the host keeps kmax <= IA_K3P_MAXK_LDS)
   const bool in_kernel_sort = variant == 20 || variant == 22 || variant == 24;
-  if (in_kernel_sort && Mpad > 512) variant = variant == 24 ? 25 : 21;
+  if (in_kernel_sort && Mpad > 512) variant = 21;
   const size_t NQ = (size_t)qt * IA_TILE;
   const int nthr = IA_WGH;
   auto dyn_lds = [&](int v) {

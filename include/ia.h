@@ -156,15 +156,15 @@ int ia_version(void);
  * "prune" = 1 (default) / 0: certified pruned scan on 1-channel split-f16 levels with at least
  * "prune_min_rows" DB rows (default 2^19): (DB tile, query tile) pairs a
  * projection bound proves farther than the query's best coherence candidate are skipped.
- * "k3p_variant" / "k3_variant": kernel versions of DESIGN.md §4b; the product build accepts
- * k3p_variant 22 (default: the pruned scan sorts a step's queries itself up to 512 of them and
- * streams only the hi halves of the DB tiles; every box-needed block runs the hi x hi product
- * first, and a tile with a block whose value can lie within its query's bound loads its lo
- * halves for the full products + top-2 one tile later; a step wider than 512 queries is sorted
- * once by k_query_sort and runs 21), 20 (the same on whole tiles; 21 presorted), 23 (22
- * presorted), 14 / 15 (filter, then full chains), 18 / 19 (fused corrections, single chains),
- * 7 / 11 (no block filter) and k3_variant 1.  The other versions of DESIGN.md §4b / §4f are in
- * git history.
+ * "k3p_variant" / "k3_variant": kernel versions of DESIGN.md §4b / §4h / §4i; the product build
+ * accepts k3p_variant 24 (default: the pruned scan sorts a step's queries itself up to 512 of
+ * them, then runs two passes: every wave streams the hi halves of its DB tiles into LDS by
+ * LDS-DMA, two tiles in flight, and runs the hi x hi block filter on the box-needed blocks;
+ * then the tiles with a block that can lie within its query's bound get their full products +
+ * top-2, handed out over the workgroup's waves; a step wider than 512 queries is sorted once by
+ * k_query_sort and runs 21), 25 (24 presorted), 22 (one pass: the hi stream in registers, the
+ * passing tiles' lo halves one tile later), 20 (whole tiles; 21 presorted) and k3_variant 1.
+ * The other versions of DESIGN.md §4b / §4f are in git history.
  * "k3p_blocks" = 1 (default) / 0: a presorted pruned scan wider than one launch's 11 query tiles
  * runs as ONE launch of (query block x DB chunk) workgroups instead of one launch per block.
  * "fuse_gather" = 1 (default) / 0: on one-job unsharded pruned levels the merge of step t and the
@@ -178,7 +178,7 @@ int ia_version(void);
  * interleaved (sort neighbours in different tiles and scan chunks: fewer certification rescans,
  * looser tile boxes).
  * "row_source" = 0 (exact rows of the rerank / coherence / pruning bound from the fp64 row DB);
- * 1 (gathered from the A-side pyramid images, 1 channel) is in DIAG=1 builds only (slower).
+ * 1 (gathered from the A-side pyramid images; measured slower) is in git history only.
  * "shard_emulate" = W (1 = off): on a single-rank context, every level with >= 64 W DB tiles
  * runs as a W-way DB shard on this device (per-shard scans and certified winners, then the
  * multi-rank finish; no RCCL): the sharded code path, testable on one GPU.
@@ -186,7 +186,8 @@ int ia_version(void);
  * level with >= 64 W tiles.  "exchange" = 0 (RCCL all-gather + finish) / 1 (peer-write merge)
  * / 2 (owner computes: each rank brings its own job, every rank scans its shard for all of them,
  * queries and scan records exchanged by peer writes; emulated: one job per shard).
- * "nn_bound" = 1 (default) / 0: on pruned one-rank levels the merge also keeps each pixel's certified
+ * "nn_bound" = 1 (default) / 0: on all pruned levels (every merge form: one-rank, sharded,
+ * peer-write, owner-computes) the merge also keeps each pixel's certified
  * exact NN row, and the gathers bound U' (the pruned scan's radius) by the causal neighbours' NN
  * rows shifted by the neighbour's offset as well as by the coherence candidates (exact either way:
  * any DB row's exact distance bounds the NN distance).

@@ -76,11 +76,11 @@ def test_batched_levels_match_separate_and_reference(ctx, name, mode):
         assert stb.pruned_levels == len(jb) * (z['L'] - 1)
 
 
-@pytest.mark.parametrize('variant', [20, 22, 24])
+@pytest.mark.parametrize('variant', [20, 22, 24, 25])
 def test_batched_512_pruned_wide_step(ctx, variant):
     """3 jobs on a 512^2 level with the pruned scan forced: 513 queries per step in one scan (the
     separate runs sort 171 per step) - a different kernel path, the same decisions.  The wide
-    steps run the presorted forms (20 and 22: 21; 24: 25)."""
+    steps run the presorted form 21 (under 20, 22 and 24) or 25 (forced)."""
     from ia_amd import synth
     job = synth.make_job(512, n_levels=3)
     ctx.set_option('prune_min_rows', 1)
@@ -94,7 +94,7 @@ def test_batched_512_pruned_wide_step(ctx, variant):
         Ss, IMs, sts = _run(ctx, z, js, False)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 22)
+        ctx.set_option('k3p_variant', 24)
     for j in range(len(jb)):
         for level in range(1, job.L):
             assert np.array_equal(Sb[j][level], Ss[j][level]) and np.array_equal(IMb[j][level], IMs[j][level])
@@ -156,7 +156,7 @@ def test_device_sweep_two_streams_equals_one(ctx):
     assert st2.pixels == st1.pixels and st2.coherence_wins == st1.coherence_wins and st2.bound_violations == 0
 
 
-@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_seq', 'pruned_v20', 'pruned_v24'])
+@pytest.mark.parametrize('mode', ['unpruned', 'pruned', 'pruned_seq', 'pruned_v20', 'pruned_v25'])
 def test_batched_g256_wide_steps_match_reference(ctx, mode):
     """8 jobs on the golden g256 run's A side: job 0 is the reference's own
     run, jobs 1..7 other kappas and B' seeds.  On the 256^2 level a step holds 8 x 86 = 688
@@ -166,13 +166,13 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
         2 query blocks x 128 DB chunks (k3p_blocks = 1, the default);
       pruned_seq: the same as one launch per query block (k3p_blocks = 0);
       pruned_v20: the same kernels under option k3p_variant 20;
-      pruned_v24: the two-pass scan's presorted form v25.
+      pruned_v25: the two-pass scan's presorted form.
     Job 0 must reproduce the reference's s, im and B' on every level; every job must equal its
     own separate run (86-query steps: a single launch, the in-kernel sort)."""
     z = load_e2e('g256')
     if mode != 'unpruned':
         ctx.set_option('prune_min_rows', 1)
-    if mode in ('pruned_v20', 'pruned_v24'):
+    if mode in ('pruned_v20', 'pruned_v25'):
         ctx.set_option('k3p_variant', int(mode[-2:]))
     if mode == 'pruned_seq':
         ctx.set_option('k3p_blocks', 0)
@@ -183,7 +183,7 @@ def test_batched_g256_wide_steps_match_reference(ctx, mode):
         Ss, IMs, sts = _run(ctx, z, js, False)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 22)
+        ctx.set_option('k3p_variant', 24)
         ctx.set_option('k3p_blocks', 1)
     h, w = z['B_pyr'][-1].shape
     assert 8 * min(h, (w + 2) // 3) > 512

@@ -19,10 +19,10 @@ from golden_util import BIG_CASES, E2E_CASES, load_e2e
 pytestmark = pytest.mark.gpu
 
 
-def _run_debug(ctx, z, prune_all=False, variant=22):
+def _run_debug(ctx, z, prune_all=False, variant=24):
     """prune_all: option prune_min_rows = 1, so every 1-channel level goes through the certified
     pruned scan (K2p -> K3p) instead of only DB levels of >= 2^19 rows; variant:
-    the pruned-scan kernel (option k3p_variant; 22 = the library default)."""
+    the pruned-scan kernel (option k3p_variant; 24 = the library default)."""
     from ia_amd import _native
     L, k = z['L'], float(z['k'])
     Bp = [x.copy() for x in z['Bp_init']]
@@ -42,11 +42,11 @@ def _run_debug(ctx, z, prune_all=False, variant=22):
             out[level] = (s, im, dbg)
     finally:
         ctx.set_option('prune_min_rows', 524288)
-        ctx.set_option('k3p_variant', 22)
+        ctx.set_option('k3p_variant', 24)
     return out, Bp, st
 
 
-@pytest.mark.parametrize('prune_all,variant', [(False, 22), (True, 20), (True, 21), (True, 22), (True, 24), (True, 25)],
+@pytest.mark.parametrize('prune_all,variant', [(False, 24), (True, 20), (True, 21), (True, 22), (True, 24), (True, 25)],
                          ids=['default', 'pruned_v20', 'pruned_presorted_v21', 'pruned_v22', 'pruned_v24',
                               'pruned_presorted_v25'])
 @pytest.mark.parametrize('name', E2E_CASES + BIG_CASES)

@@ -27,7 +27,7 @@ def _run(ctx, job, prune, variant=22, group=1):
                 Bp[level], job.weights, job.kappa_factor(level), st)
     finally:
         ctx.set_option('prune', 1)
-        ctx.set_option('k3p_variant', 22)
+        ctx.set_option('k3p_variant', 24)
         ctx.set_option('prune_min_rows', 524288)
         ctx.set_option('prune_group', 1)
     return Bp, S, IM, st
@@ -155,7 +155,7 @@ def test_pruned_scan_over_512_tiles_per_workgroup(ctx, variant):
         finally:
             ctx.set_option('prune', 1)
             ctx.set_option('prune_min_rows', 524288)
-            ctx.set_option('k3p_variant', 22)
+            ctx.set_option('k3p_variant', 24)
         out.append((s, im, Bp, st))
     (s0, im0, Bp0, st0), (s1, im1, Bp1, st1) = out
     assert st0.pruned_levels == 0 and st1.pruned_levels == 1

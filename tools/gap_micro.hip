@@ -52,6 +52,36 @@ __global__ void __launch_bounds__(512, 1) k_scan_dirty(unsigned long long *st, i
     st[2 * blockIdx.x + 1] = rt();
   }
 }
+// the scan's DB stream: every workgroup reads its 1/256 of `nbytes` (16 B per lane per load,
+// 4 loads in flight), so the L2s end the launch full of clean DB lines, as the real scan leaves
+// them; NT = the loads carry the non-temporal hint
+typedef float f4v __attribute__((ext_vector_type(4)));
+template <bool NT>
+__global__ void __launch_bounds__(512, 1) k_scan_stream(unsigned long long *st, const f4v *db, long long n4, float *sink) {
+  extern __shared__ float lds[];
+  const unsigned long long t0 = rt();
+  lds[threadIdx.x] = (float)threadIdx.x;
+  __syncthreads();
+  const long long per = n4 / gridDim.x, b = per * blockIdx.x;
+  float acc = 0.f;
+  for (long long i = threadIdx.x; i < per; i += 4 * 512) {
+    f4v v[4];
+#pragma unroll
+    for (int u = 0; u < 4; u++) {
+      const long long j = i + u * 512;
+      if (j < per) v[u] = NT ? __builtin_nontemporal_load(db + b + j) : db[b + j];
+      else v[u] = f4v{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int u = 0; u < 4; u++) acc += v[u].x + v[u].y + v[u].z + v[u].w;
+  }
+  if (acc == 12345.f) sink[threadIdx.x] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    st[2 * blockIdx.x] = t0;
+    st[2 * blockIdx.x + 1] = rt() + (unsigned long long)lds[5] * 0;
+  }
+}
 __global__ void __launch_bounds__(64) k_merge_big(BigArgs a) {
   const unsigned long long t0 = rt();
   while ((long long)(rt() - t0) < a.ticks) __builtin_amdgcn_s_sleep(2);
@@ -64,11 +94,22 @@ __global__ void __launch_bounds__(64) k_merge_big(BigArgs a) {
 
 int main(int argc, char **argv) {
   const int steps = argc > 1 ? atoi(argv[1]) : 2000;
-  const int mode = argc > 2 ? atoi(argv[2]) : 0;  // 1: the real kernels' argument size and written bytes
+  // mode 1: the real kernels' argument size and written bytes; 2: the scan streams 120 MB
+  // (L2s full of clean lines at each boundary); 6: the same with non-temporal loads
+  const int mode = argc > 2 ? atoi(argv[2]) : 0;
   const int nA = 256, nB = 342, ldsA = 150 * 1024;
   const int tA = 3000, tB = 1500;  // 30 / 15 us of work
   CK(hipFuncSetAttribute((const void *)k_scan_like, hipFuncAttributeMaxDynamicSharedMemorySize, ldsA));
   CK(hipFuncSetAttribute((const void *)k_scan_dirty, hipFuncAttributeMaxDynamicSharedMemorySize, ldsA));
+  CK(hipFuncSetAttribute((const void *)k_scan_stream<false>, hipFuncAttributeMaxDynamicSharedMemorySize, ldsA));
+  CK(hipFuncSetAttribute((const void *)k_scan_stream<true>, hipFuncAttributeMaxDynamicSharedMemorySize, ldsA));
+  // mode 2: a 120 MB DB stream per scan launch (the real scan's hi bytes)
+  const long long n4 = (mode & 2) ? 120000000LL / 16 : 0;
+  f4v *dbs = nullptr;
+  if (mode & 2) {
+    CK(hipMalloc(&dbs, (size_t)n4 * 16));
+    CK(hipMemset(dbs, 0, (size_t)n4 * 16));
+  }
   float *dirty;
   CK(hipMalloc(&dirty, (size_t)2 << 20));
   BigArgs ba{};
@@ -82,7 +123,11 @@ int main(int argc, char **argv) {
   CK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   auto enqueue = [&](int i0, int n) {
     for (int i = i0; i < i0 + n; i++) {
-      if (mode & 1) {
+      if (mode & 2) {
+        if (mode & 4) hipLaunchKernelGGL(k_scan_stream<true>, dim3(nA), dim3(512), ldsA, s, st + (size_t)(2 * i) * per, dbs, n4, dirty);
+        else hipLaunchKernelGGL(k_scan_stream<false>, dim3(nA), dim3(512), ldsA, s, st + (size_t)(2 * i) * per, dbs, n4, dirty);
+        hipLaunchKernelGGL(k_merge_like, dim3(nB), dim3(64), 0, s, st + (size_t)(2 * i + 1) * per, tB);
+      } else if (mode & 1) {
         hipLaunchKernelGGL(k_scan_dirty, dim3(nA), dim3(512), ldsA, s, st + (size_t)(2 * i) * per, tA, dirty, 1750000LL / 4);
         ba.st = st + (size_t)(2 * i + 1) * per;
         hipLaunchKernelGGL(k_merge_big, dim3(nB), dim3(64), 0, s, ba);
