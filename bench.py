@@ -842,6 +842,11 @@ def main():
             roofline['merge_launches_timed'] = st_all['merge_stamp_launches']
         if st_all['stamp_gaps'] > 0:
             roofline['chain_gap_us_timed'] = st_all['stamp_gap_ms'] * 1e3 / st_all['stamp_gaps']
+            if st_all.get('stamp_gaps_sm', 0) > 0 and st_all['stamp_gaps'] > st_all['stamp_gaps_sm']:
+                # the two boundaries of a step: scan end -> merge start, merge end -> next scan start
+                roofline['chain_gap_scan_merge_us_timed'] = st_all['stamp_gap_sm_ms'] * 1e3 / st_all['stamp_gaps_sm']
+                roofline['chain_gap_merge_scan_us_timed'] = ((st_all['stamp_gap_ms'] - st_all['stamp_gap_sm_ms']) * 1e3
+                                                             / (st_all['stamp_gaps'] - st_all['stamp_gaps_sm']))
             roofline['chain_window_ms_timed'] = st_all['stamp_window_ms'] / args.steps
         roofline['timing_timed'] = ('frac_timed / *_timed: every pruned-scan (and fused merge) launch of the %d timed '
                                     'steps, device time = max(workgroup end) - min(workgroup start) from s_memrealtime '

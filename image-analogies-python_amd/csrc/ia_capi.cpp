@@ -19,6 +19,9 @@
 #include "../../include/ia.h"
 #include "ia_internal.h"
 #include "ia_launch.h"
+#ifndef IA_REC_CHUNK_MAJOR  // 0: the pruned scan's records query-major too (A/B builds)
+#define IA_REC_CHUNK_MAJOR 1
+#endif
 
 #if IA_PROBE & 16
 void ia_k3p_probe_dump();
@@ -1097,6 +1100,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   ma.img_rows = (c->row_source == 1 && g.ch == 1) ? 1 : 0;
   ma.eps_c = use_h ? ia_eps_c_h(g.KS, prune || c->k3_variant == 1) : ia_eps_c(DP);
   ma.eps_a = use_h ? ia_eps_a_h() : 0.;
+  // the pruned scan writes its records chunk-major (rec[w Mtmax + m]: each workgroup's records one
+  // contiguous run, so the scan leaves a few dirty lines per workgroup for the kernel boundary to
+  // write back instead of one per record); the unpruned scans query-major
+  const int rstride = prune && IA_REC_CHUNK_MAJOR ? (int)Mtmax : 0;
+  ma.rstride = rstride;
   // per shard: its records, decomposition, DB positions (and table / boxes of a pruned level)
   std::vector<MergeArgs> mas(shards.size(), ma);
   std::vector<int64_t> shard_rows(shards.size(), 0);  // real DB rows in each shard (unpruned flops)
@@ -1511,7 +1519,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
             ia_launch_k3p(qtb, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, 0, Mt, sd.Mpad, nch,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t, c->qs_order.as<int>(),
-                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp());
+                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp(), rstride);
             m.nwg = nch;
             pairs_full += (double)n * qtt;
             tiles_full += (double)n * nqb;
@@ -1532,13 +1540,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
             ia_launch_k3p(qt, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t,
-                          c->qs_order.as<int>(), 0, sd.r0, nullptr, tboxp, tn, c->st, 1, 0, nullptr, k3_stamp());
+                          c->qs_order.as<int>(), 0, sd.r0, nullptr, tboxp, tn, c->st, 1, 0, nullptr, k3_stamp(), rstride);
           else if (prune)
             ia_launch_k3p(qt, dbp, c->qf.p, qinfot, m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
                           k3v, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
-                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, nullptr, k3_stamp());
+                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, nullptr, k3_stamp(), rstride);
           else if (use_h)
             ia_launch_k3h(g.KS, qt, dbp, c->qf.p, n, x.tpw, qt0, Mt, x.nwg, m.pos0, g.n_tiles, (float4 *)m.rec,
                           (float *)m.recT, c->k3_variant, c->st);
@@ -1763,7 +1771,8 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         stats->prune_ms_timed = stats->prune_flops_timed = stats->prune_bytes_timed = 0.;
         stats->prune_launches_timed = 0;
         stats->k3p_stamp_ms = stats->k3p_bytes_all = stats->merge_stamp_ms = stats->stamp_gap_ms = stats->stamp_window_ms = 0.;
-        stats->k3p_stamp_start_ms = stats->k3p_stamp_wg_ms = 0.;
+        stats->k3p_stamp_start_ms = stats->k3p_stamp_wg_ms = stats->stamp_gap_sm_ms = 0.;
+        stats->stamp_gaps_sm = 0;
         stats->k3p_stamp_launches = stats->merge_stamp_launches = stats->stamp_gaps = 0;
         stats->prune_rows = g.NA;
       }
@@ -1795,20 +1804,22 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       // chain between its kernels, scan(t) -> merge(t) and merge(t) -> scan(t + 1)
       if (k3_n == mg_n + 1 || k3_n == mg_n) {
         const unsigned long long *m = sp.data() + 2 * k3_n;
-        double gap = 0.;
-        int64_t ng = 0;
+        double gap = 0., gsm = 0.;
+        int64_t ng = 0, nsm = 0;
         for (int64_t i = 0; i < mg_n; i++) {
           if (m[2 * i] && sp[2 * i + 1] && m[2 * i] >= sp[2 * i + 1]) {
-            gap += (double)(m[2 * i] - sp[2 * i + 1]);
-            ng++;
+            gsm += (double)(m[2 * i] - sp[2 * i + 1]);
+            nsm++;
           }
           if (i + 1 < k3_n && sp[2 * (i + 1)] && m[2 * i + 1] && sp[2 * (i + 1)] >= m[2 * i + 1]) {
             gap += (double)(sp[2 * (i + 1)] - m[2 * i + 1]);
             ng++;
           }
         }
-        stats->stamp_gap_ms += gap * 1e-5;
-        stats->stamp_gaps += ng;
+        stats->stamp_gap_ms += (gap + gsm) * 1e-5;
+        stats->stamp_gaps += ng + nsm;
+        stats->stamp_gap_sm_ms += gsm * 1e-5;
+        stats->stamp_gaps_sm += nsm;
         stats->stamp_window_ms += (double)(std::max(sp[2 * k3_n - 1], m[2 * mg_n - 1]) - sp[0]) * 1e-5;
       }
       stats->k3p_bytes_all += tile_stream_bytes((double)(prs[2] + prs[3]), (double)(ext[0] + ext[1])) + bytes_all_fixed;

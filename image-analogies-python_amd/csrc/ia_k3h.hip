@@ -65,7 +65,7 @@ __device__ __forceinline__ void slot_hi(h16x8 (&h)[4], const h16x8 *slot, int la
 #define IA_PROBE 0
 #endif
 #if IA_PROBE & 16  // diagnostic build only: per-wave phase cycle sums of the pruned scan (K3p, V >= 1)
-__device__ unsigned long long k3p_prof[16];
+__device__ unsigned long long k3p_prof[24];
 #define K3P_T(x) do { __builtin_amdgcn_sched_barrier(0); x = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #else
 #define K3P_T(x) do { } while (0)
@@ -591,6 +591,9 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 #ifndef IA_K3P_ROWS_EARLY  // 1: candidate rows looked up before the subset merge (0: after it)
 #define IA_K3P_ROWS_EARLY 1
 #endif
+#ifndef IA_K3P_SUBBOX  // k3p_variant 24 / 25: the stream's need test on 8-query sub-boxes (0: per query)
+#define IA_K3P_SUBBOX 1
+#endif
 #define IA_K3P3_MAXQ 512   // queries per step (one per thread)
 // steps of up to IA_K3P_RANK_MAX queries are sorted by rank counting, wider ones by the bitonic
 // network (at 342 queries the network measured faster: profiles/r02/ab3)
@@ -791,10 +794,42 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       tU[j] = u;
     }
   };
-  if (PRE && !tbox) {
-    tile_boxes();
-    __syncthreads();
-  }
+  // HHX 4 (IA_K3P_SUBBOX): the boxes of every 8 consecutive sorted slots (min lo, max hi, max U'
+  // over the real queries), 4 per query tile: the stream's need test takes them instead of the
+  // per-query bounds - one box test per lane covers the 11 query tiles at once
+  __shared__ float4 sblo[HHX == 4 ? 4 * QT : 1], sbhi[HHX == 4 ? 4 * QT : 1];
+  __shared__ float sbU[HHX == 4 ? 4 * QT : 1];
+  auto sub_boxes = [&]() {
+    if constexpr (HHX == 4 && IA_K3P_SUBBOX) {
+      float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+      float u = -INFINITY;
+      if (tid < NQ && qU[tid] != -INFINITY) {
+        lo = qlo[tid];
+        hi = qhi[tid];
+        u = qU[tid];
+      }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        lo.x = fminf(lo.x, xlane_xor_f(lo.x, o));
+        lo.y = fminf(lo.y, xlane_xor_f(lo.y, o));
+        lo.z = fminf(lo.z, xlane_xor_f(lo.z, o));
+        lo.w = fminf(lo.w, xlane_xor_f(lo.w, o));
+        hi.x = fmaxf(hi.x, xlane_xor_f(hi.x, o));
+        hi.y = fmaxf(hi.y, xlane_xor_f(hi.y, o));
+        hi.z = fmaxf(hi.z, xlane_xor_f(hi.z, o));
+        hi.w = fmaxf(hi.w, xlane_xor_f(hi.w, o));
+        u = fmaxf(u, xlane_xor_f(u, o));
+      }
+      if ((tid & 7) == 0 && tid < NQ) {
+        sblo[tid >> 3] = lo;
+        sbhi[tid >> 3] = hi;
+        sbU[tid >> 3] = u;
+      }
+    }
+  };
+  if (PRE && !tbox) tile_boxes();
+  if (PRE) sub_boxes();
+  if (PRE && (!tbox || (HHX == 4 && IA_K3P_SUBBOX))) __syncthreads();
   if constexpr (!PRE) {
   if (xo.on) {  // owner-computes: wait for each of the block's queries (published by its owner's K2p)
     const unsigned *qs = xo.flag + (int64_t)qblk * Mpad;
@@ -907,7 +942,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       }
     }
   }
+  unsigned long long pa = 0, pb = 0, pc = 0;
+  K3P_T(pa);
   __syncthreads();
+  K3P_T(pb);
 #pragma unroll
   for (int i = 0; i < NE; i++) {
     const int e = tid + WGT * i;
@@ -917,7 +955,16 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       if (x >= 0 && x < NQ) ldsh[((x >> 5) * NPL + p) * IA_WAVE + (L & 32) + (x & 31)] = qe[i];
     }
   }
+  K3P_T(pc);
+#if IA_PROBE & 16
+  if (lane == 0 && M == Mpad - 10 && wg < 8) {  // the sort phase: network / rank, barrier, scatter
+    atomicAdd(&k3p_prof[16], pa - ph[1]);
+    atomicAdd(&k3p_prof[17], pb - pa);
+    atomicAdd(&k3p_prof[18], pc - pb);
+  }
+#endif
   tile_boxes();
+  sub_boxes();
   __syncthreads();
   }  // !PRE
   K3P_T(ph[2]);
@@ -984,10 +1031,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     // (b) after a barrier the query lo pieces are staged into the ring area and the listed tiles
     //     are handed out through an LDS counter: whole tiles (two register buffers) and the full
     //     12-MFMA chains of their passing blocks (k3p_pairs_hl: v14's products and records).
-    // Tiles: wave w walks k = w + NW j (the first two are the speculative DMAs issued before the
-    // query sort).  No LDS atomic in this loop: the compiler puts a vmcnt(0) before any LDS
-    // atomic while an LDS-DMA is pending, so the passing tiles go to per-wave lists (plk / plm
-    // at w + NW n) instead of one counted list.
+    // Tiles: wave w's first two are w and w + NW (the speculative DMAs issued before the query
+    // sort), the others come from the workgroup's LDS counter; the passing tiles go to one list
+    // (plk / plm, LDS atomic).  The DMAs are inline asm, which the compiler does not track, so it
+    // puts no vmcnt(0) before these LDS atomics (it does for the builtin's DMAs).
     // the box need test of a tile with the wave's per-query bounds held in registers (lane L of
     // pair pr: sorted slot (2 pr + L / 32) 32 + L % 32): no LDS round trip per query-tile pair
     float4 pql[NPAIR], pqh[NPAIR];
@@ -1000,10 +1047,23 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       pqh[pr] = ok ? qhi[x] : make_float4(0.f, 0.f, 0.f, 0.f);
       pqu[pr] = ok ? qU[x] : -INFINITY;
     }
+    // IA_K3P_SUBBOX: lane L tests sub-box 4 (L % 16) + L / 16 (query tile L % 16, its slots
+    // 8 (L / 16) .. + 7), so the ballot's bits j, j + 16, j + 32, j + 48 are query tile j's four
+    // sub-boxes: one box test and one ballot per DB tile
+    const bool sv = (lane & 15) < QT;
+    const int sbx = sv ? 4 * (lane & 15) + (lane >> 4) : 0;
+    const float4 sbl = sv ? sblo[sbx] : make_float4(0.f, 0.f, 0.f, 0.f), sbh = sv ? sbhi[sbx] : sbl;
+    const float sbu = sv ? sbU[sbx] : -INFINITY;
     auto need_r = [&](int k) -> unsigned {
       const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
-      const bool cpass = cl && prune_lb(blo, bhi, ctl, cth) <= ctu;
-      const unsigned coarse = (unsigned)__ballot(cpass);
+      unsigned coarse;
+      if constexpr (IA_K3P_SUBBOX) {  // the sub-boxes as the coarse test, then per query
+        const unsigned long long b = __ballot(sv && prune_lb(blo, bhi, sbl, sbh) <= sbu);
+        const unsigned t = (unsigned)b | (unsigned)(b >> 32);
+        coarse = (t | (t >> 16)) & ((1u << QT) - 1u);
+      } else {
+        coarse = (unsigned)__ballot(cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
+      }
       unsigned msk = 0;
 #pragma unroll
       for (int pr = 0; pr < NPAIR; pr++) {
@@ -1337,6 +1397,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         __hip_atomic_store(reinterpret_cast<unsigned long long *>(ar + XOLayout::RTS) + ix,
                            ((unsigned long long)xo.seq << 32) | __float_as_uint(m.T), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+      } else if (xo.rstride) {  // chunk-major: the workgroup's records are one contiguous run
+        rec[(int64_t)wg * xo.rstride + mq] = rv;
+        recT[(int64_t)wg * xo.rstride + mq] = m.T;
       } else {
         rec[(int64_t)mq * nwg + wg] = rv;
         recT[(int64_t)mq * nwg + wg] = m.T;
@@ -1385,8 +1448,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
 
 #if (IA_PROBE & 16) && defined(IA_K3H_KS) && defined(IA_K3H_QT) && IA_K3H_KS == 4 && IA_K3H_QT == 11
 void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau wave, to stderr
-  unsigned long long v[16];
+  unsigned long long v[24];
   if (hipMemcpyFromSymbol(v, HIP_SYMBOL(k3p_prof), sizeof(v)) != hipSuccess || v[4] == 0) return;
+  fprintf(stderr, "K3P_PROBE sort phase: network %.0f, barrier %.0f, fragment scatter %.0f\n", (double)v[16] / v[4],
+          (double)v[17] / v[4], (double)v[18] / v[4]);
   fprintf(stderr, "K3P_PROBE two-pass (v24/25): stream %.0f, barrier %.0f, lo staging %.0f, chains %.0f\n", (double)v[12] / v[4],
           (double)v[13] / v[4], (double)v[14] / v[4], (double)v[15] / v[4]);
   fprintf(stderr, "K3P_PROBE tail split: half merge %.0f, barrier %.0f, subset merge + records %.0f\n", (double)v[9] / v[4],
@@ -1397,7 +1462,7 @@ void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau w
   fprintf(stderr, "K3P_PROBE waves=%llu setup=%.0f need=%.0f loop=%.0f tail=%.0f tiles/wave=%.2f pairs/wave=%.2f (cycles/wave)\n",
           v[4], (double)v[0] / v[4], (double)v[1] / v[4], (double)v[2] / v[4], (double)v[3] / v[4], (double)v[5] / v[4],
           (double)v[6] / v[4]);
-  unsigned long long z[16] = {};
+  unsigned long long z[24] = {};
   (void)hipMemcpyToSymbol(HIP_SYMBOL(k3p_prof), z, sizeof(z));
 }
 #endif

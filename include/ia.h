@@ -109,6 +109,8 @@ typedef struct {
                              * stamp_* (the largest pruned level seen: the bench's finest) */
   double k3p_stamp_start_ms; /* the same K3p launches: last workgroup start - first start, summed */
   double k3p_stamp_wg_ms;    /* ... their mean workgroup duration (end - start), summed */
+  double stamp_gap_sm_ms;   /* the scan end -> merge start part of stamp_gap_ms */
+  int64_t stamp_gaps_sm;
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),

@@ -16,8 +16,14 @@
 __device__ __forceinline__ unsigned long long rt() { return __builtin_amdgcn_s_memrealtime(); }
 
 // busy for `ticks` of the 100 MHz clock, then stamp (first, last) of the workgroup
+// KA: the first stamp is taken only once the kernel arguments have arrived (as in the real
+// kernels, whose first stamp follows code that reads them); otherwise s_memrealtime may issue
+// before the kernel-argument loads return
+#define KA_WAIT(x) do { if (KA) asm volatile("s_waitcnt lgkmcnt(0)" :: "s"(x) : "memory"); } while (0)
+template <bool KA>
 __global__ void __launch_bounds__(512, 1) k_scan_like(unsigned long long *st, int ticks) {
   extern __shared__ float lds[];
+  KA_WAIT(ticks);
   const unsigned long long t0 = rt();
   lds[threadIdx.x] = (float)threadIdx.x;
   __syncthreads();
@@ -28,7 +34,9 @@ __global__ void __launch_bounds__(512, 1) k_scan_like(unsigned long long *st, in
     st[2 * blockIdx.x + 1] = rt() + (unsigned long long)lds[5] * 0;
   }
 }
+template <bool KA>
 __global__ void __launch_bounds__(64) k_merge_like(unsigned long long *st, int ticks) {
+  KA_WAIT(ticks);
   const unsigned long long t0 = rt();
   while ((long long)(rt() - t0) < ticks) __builtin_amdgcn_s_sleep(2);
   if (threadIdx.x == 0) {
@@ -41,6 +49,7 @@ __global__ void __launch_bounds__(64) k_merge_like(unsigned long long *st, int t
 struct BigArgs { unsigned long long pad[190]; int ticks; float *dirty; long long ndirty; unsigned long long *st; };
 __global__ void __launch_bounds__(512, 1) k_scan_dirty(unsigned long long *st, int ticks, float *dirty, long long n) {
   extern __shared__ float lds[];
+  asm volatile("s_waitcnt lgkmcnt(0)" :: "s"(ticks) : "memory");
   const unsigned long long t0 = rt();
   lds[threadIdx.x] = (float)threadIdx.x;
   __syncthreads();
@@ -59,6 +68,7 @@ typedef float f4v __attribute__((ext_vector_type(4)));
 template <bool NT>
 __global__ void __launch_bounds__(512, 1) k_scan_stream(unsigned long long *st, const f4v *db, long long n4, float *sink) {
   extern __shared__ float lds[];
+  asm volatile("s_waitcnt lgkmcnt(0)" :: "s"(n4) : "memory");
   const unsigned long long t0 = rt();
   lds[threadIdx.x] = (float)threadIdx.x;
   __syncthreads();
@@ -82,7 +92,9 @@ __global__ void __launch_bounds__(512, 1) k_scan_stream(unsigned long long *st, 
     st[2 * blockIdx.x + 1] = rt() + (unsigned long long)lds[5] * 0;
   }
 }
+template <bool KA>
 __global__ void __launch_bounds__(64) k_merge_big(BigArgs a) {
+  KA_WAIT(a.ticks);
   const unsigned long long t0 = rt();
   while ((long long)(rt() - t0) < a.ticks) __builtin_amdgcn_s_sleep(2);
   for (long long i = (long long)blockIdx.x * 64 + threadIdx.x; i < a.ndirty; i += (long long)gridDim.x * 64) a.dirty[i] = (float)i;
@@ -95,11 +107,13 @@ __global__ void __launch_bounds__(64) k_merge_big(BigArgs a) {
 int main(int argc, char **argv) {
   const int steps = argc > 1 ? atoi(argv[1]) : 2000;
   // mode 1: the real kernels' argument size and written bytes; 2: the scan streams 120 MB
-  // (L2s full of clean lines at each boundary); 6: the same with non-temporal loads
+  // (L2s full of clean lines at each boundary); 6: the same with non-temporal loads; 8: mode 0
+  // with the first stamps after the kernel arguments arrived (modes 1, 2, 6 always so)
   const int mode = argc > 2 ? atoi(argv[2]) : 0;
   const int nA = 256, nB = 342, ldsA = 150 * 1024;
   const int tA = 3000, tB = 1500;  // 30 / 15 us of work
-  CK(hipFuncSetAttribute((const void *)k_scan_like, hipFuncAttributeMaxDynamicSharedMemorySize, ldsA));
+  CK(hipFuncSetAttribute((const void *)k_scan_like<false>, hipFuncAttributeMaxDynamicSharedMemorySize, ldsA));
+  CK(hipFuncSetAttribute((const void *)k_scan_like<true>, hipFuncAttributeMaxDynamicSharedMemorySize, ldsA));
   CK(hipFuncSetAttribute((const void *)k_scan_dirty, hipFuncAttributeMaxDynamicSharedMemorySize, ldsA));
   CK(hipFuncSetAttribute((const void *)k_scan_stream<false>, hipFuncAttributeMaxDynamicSharedMemorySize, ldsA));
   CK(hipFuncSetAttribute((const void *)k_scan_stream<true>, hipFuncAttributeMaxDynamicSharedMemorySize, ldsA));
@@ -126,14 +140,19 @@ int main(int argc, char **argv) {
       if (mode & 2) {
         if (mode & 4) hipLaunchKernelGGL(k_scan_stream<true>, dim3(nA), dim3(512), ldsA, s, st + (size_t)(2 * i) * per, dbs, n4, dirty);
         else hipLaunchKernelGGL(k_scan_stream<false>, dim3(nA), dim3(512), ldsA, s, st + (size_t)(2 * i) * per, dbs, n4, dirty);
-        hipLaunchKernelGGL(k_merge_like, dim3(nB), dim3(64), 0, s, st + (size_t)(2 * i + 1) * per, tB);
+        hipLaunchKernelGGL(k_merge_like<true>, dim3(nB), dim3(64), 0, s, st + (size_t)(2 * i + 1) * per, tB);
       } else if (mode & 1) {
         hipLaunchKernelGGL(k_scan_dirty, dim3(nA), dim3(512), ldsA, s, st + (size_t)(2 * i) * per, tA, dirty, 1750000LL / 4);
         ba.st = st + (size_t)(2 * i + 1) * per;
-        hipLaunchKernelGGL(k_merge_big, dim3(nB), dim3(64), 0, s, ba);
+        hipLaunchKernelGGL(k_merge_big<true>, dim3(nB), dim3(64), 0, s, ba);
       } else {
-        hipLaunchKernelGGL(k_scan_like, dim3(nA), dim3(512), ldsA, s, st + (size_t)(2 * i) * per, tA);
-        hipLaunchKernelGGL(k_merge_like, dim3(nB), dim3(64), 0, s, st + (size_t)(2 * i + 1) * per, tB);
+        if (mode & 8) {
+          hipLaunchKernelGGL(k_scan_like<true>, dim3(nA), dim3(512), ldsA, s, st + (size_t)(2 * i) * per, tA);
+          hipLaunchKernelGGL(k_merge_like<true>, dim3(nB), dim3(64), 0, s, st + (size_t)(2 * i + 1) * per, tB);
+        } else {
+          hipLaunchKernelGGL(k_scan_like<false>, dim3(nA), dim3(512), ldsA, s, st + (size_t)(2 * i) * per, tA);
+          hipLaunchKernelGGL(k_merge_like<false>, dim3(nB), dim3(64), 0, s, st + (size_t)(2 * i + 1) * per, tB);
+        }
       }
     }
   };
