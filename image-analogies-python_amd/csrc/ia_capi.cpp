@@ -19,9 +19,6 @@
 #include "../../include/ia.h"
 #include "ia_internal.h"
 #include "ia_launch.h"
-#ifndef IA_REC_CHUNK_MAJOR  // 0: the pruned scan's records query-major too (A/B builds)
-#define IA_REC_CHUNK_MAJOR 1
-#endif
 
 #if IA_PROBE & 16
 void ia_k3p_probe_dump();
@@ -1100,11 +1097,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   ma.img_rows = (c->row_source == 1 && g.ch == 1) ? 1 : 0;
   ma.eps_c = use_h ? ia_eps_c_h(g.KS, prune || c->k3_variant == 1) : ia_eps_c(DP);
   ma.eps_a = use_h ? ia_eps_a_h() : 0.;
-  // the pruned scan writes its records chunk-major (rec[w Mtmax + m]: each workgroup's records one
-  // contiguous run, so the scan leaves a few dirty lines per workgroup for the kernel boundary to
-  // write back instead of one per record); the unpruned scans query-major
-  const int rstride = prune && IA_REC_CHUNK_MAJOR ? (int)Mtmax : 0;
-  ma.rstride = rstride;
   // per shard: its records, decomposition, DB positions (and table / boxes of a pruned level)
   std::vector<MergeArgs> mas(shards.size(), ma);
   std::vector<int64_t> shard_rows(shards.size(), 0);  // real DB rows in each shard (unpruned flops)
@@ -1519,7 +1511,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
             ia_launch_k3p(qtb, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, 0, Mt, sd.Mpad, nch,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t, c->qs_order.as<int>(),
-                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp(), rstride);
+                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp());
             m.nwg = nch;
             pairs_full += (double)n * qtt;
             tiles_full += (double)n * nqb;
@@ -1540,13 +1532,13 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
             ia_launch_k3p(qt, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t,
-                          c->qs_order.as<int>(), 0, sd.r0, nullptr, tboxp, tn, c->st, 1, 0, nullptr, k3_stamp(), rstride);
+                          c->qs_order.as<int>(), 0, sd.r0, nullptr, tboxp, tn, c->st, 1, 0, nullptr, k3_stamp());
           else if (prune)
             ia_launch_k3p(qt, dbp, c->qf.p, qinfot, m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
                           k3v, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
-                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, nullptr, k3_stamp(), rstride);
+                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, nullptr, k3_stamp());
           else if (use_h)
             ia_launch_k3h(g.KS, qt, dbp, c->qf.p, n, x.tpw, qt0, Mt, x.nwg, m.pos0, g.n_tiles, (float4 *)m.rec,
                           (float *)m.recT, c->k3_variant, c->st);

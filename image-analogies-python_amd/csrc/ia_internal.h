@@ -106,10 +106,6 @@ struct MergeArgs {
   unsigned *xo_err = nullptr;         // bit 3: a record did not arrive in time
   long long xo_timeout = 0;
   unsigned long long *stamp = nullptr;  // option "stamps": this launch's per-workgroup (start, end)
-  // record layout (the scans' writes, the merges' reads): 0 = query-major rec[m nwg + w] (K3h /
-  // K3 / the unpruned levels); > 0 = chunk-major rec[w rstride + m] (the pruned scan: each
-  // workgroup's records are one contiguous run, a few dirty lines instead of one per query)
-  int rstride = 0;
 };
 
 // Per-launch device timing without HIP events (option "stamps"): every workgroup of a stamped
@@ -320,7 +316,6 @@ struct XOScan {
   int *inv;                       // in-kernel sort: the owner's table (written by the owner's shard)
   int on, s, bpj;                 // owner of block b = b / bpj; this launch scans shard s
   int Mrec;                       // record rows per chunk (slots of the step layout)
-  int rstride;                    // not owner-computes: 0 = records rec[m nwg + w]; > 0 = rec[w rstride + m]
   unsigned seq;
   unsigned *err;                  // bit 2: a tile flag did not arrive in time
   long long timeout_ticks;

@@ -591,9 +591,6 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 #ifndef IA_K3P_ROWS_EARLY  // 1: candidate rows looked up before the subset merge (0: after it)
 #define IA_K3P_ROWS_EARLY 1
 #endif
-#ifndef IA_K3P_SUBBOX  // k3p_variant 24 / 25: the stream's need test on 8-query sub-boxes (0: per query)
-#define IA_K3P_SUBBOX 1
-#endif
 #define IA_K3P3_MAXQ 512   // queries per step (one per thread)
 // steps of up to IA_K3P_RANK_MAX queries are sorted by rank counting, wider ones by the bitonic
 // network (at 342 queries the network measured faster: profiles/r02/ab3)
@@ -794,42 +791,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       tU[j] = u;
     }
   };
-  // HHX 4 (IA_K3P_SUBBOX): the boxes of every 8 consecutive sorted slots (min lo, max hi, max U'
-  // over the real queries), 4 per query tile: the stream's need test takes them instead of the
-  // per-query bounds - one box test per lane covers the 11 query tiles at once
-  __shared__ float4 sblo[HHX == 4 ? 4 * QT : 1], sbhi[HHX == 4 ? 4 * QT : 1];
-  __shared__ float sbU[HHX == 4 ? 4 * QT : 1];
-  auto sub_boxes = [&]() {
-    if constexpr (HHX == 4 && IA_K3P_SUBBOX) {
-      float4 lo = make_float4(INFINITY, INFINITY, INFINITY, INFINITY), hi = make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
-      float u = -INFINITY;
-      if (tid < NQ && qU[tid] != -INFINITY) {
-        lo = qlo[tid];
-        hi = qhi[tid];
-        u = qU[tid];
-      }
-#pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        lo.x = fminf(lo.x, xlane_xor_f(lo.x, o));
-        lo.y = fminf(lo.y, xlane_xor_f(lo.y, o));
-        lo.z = fminf(lo.z, xlane_xor_f(lo.z, o));
-        lo.w = fminf(lo.w, xlane_xor_f(lo.w, o));
-        hi.x = fmaxf(hi.x, xlane_xor_f(hi.x, o));
-        hi.y = fmaxf(hi.y, xlane_xor_f(hi.y, o));
-        hi.z = fmaxf(hi.z, xlane_xor_f(hi.z, o));
-        hi.w = fmaxf(hi.w, xlane_xor_f(hi.w, o));
-        u = fmaxf(u, xlane_xor_f(u, o));
-      }
-      if ((tid & 7) == 0 && tid < NQ) {
-        sblo[tid >> 3] = lo;
-        sbhi[tid >> 3] = hi;
-        sbU[tid >> 3] = u;
-      }
-    }
-  };
-  if (PRE && !tbox) tile_boxes();
-  if (PRE) sub_boxes();
-  if (PRE && (!tbox || (HHX == 4 && IA_K3P_SUBBOX))) __syncthreads();
+  if (PRE && !tbox) {
+    tile_boxes();
+    __syncthreads();
+  }
   if constexpr (!PRE) {
   if (xo.on) {  // owner-computes: wait for each of the block's queries (published by its owner's K2p)
     const unsigned *qs = xo.flag + (int64_t)qblk * Mpad;
@@ -964,7 +929,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   }
 #endif
   tile_boxes();
-  sub_boxes();
   __syncthreads();
   }  // !PRE
   K3P_T(ph[2]);
@@ -1047,23 +1011,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       pqh[pr] = ok ? qhi[x] : make_float4(0.f, 0.f, 0.f, 0.f);
       pqu[pr] = ok ? qU[x] : -INFINITY;
     }
-    // IA_K3P_SUBBOX: lane L tests sub-box 4 (L % 16) + L / 16 (query tile L % 16, its slots
-    // 8 (L / 16) .. + 7), so the ballot's bits j, j + 16, j + 32, j + 48 are query tile j's four
-    // sub-boxes: one box test and one ballot per DB tile
-    const bool sv = (lane & 15) < QT;
-    const int sbx = sv ? 4 * (lane & 15) + (lane >> 4) : 0;
-    const float4 sbl = sv ? sblo[sbx] : make_float4(0.f, 0.f, 0.f, 0.f), sbh = sv ? sbhi[sbx] : sbl;
-    const float sbu = sv ? sbU[sbx] : -INFINITY;
     auto need_r = [&](int k) -> unsigned {
       const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
-      unsigned coarse;
-      if constexpr (IA_K3P_SUBBOX) {  // the sub-boxes as the coarse test, then per query
-        const unsigned long long b = __ballot(sv && prune_lb(blo, bhi, sbl, sbh) <= sbu);
-        const unsigned t = (unsigned)b | (unsigned)(b >> 32);
-        coarse = (t | (t >> 16)) & ((1u << QT) - 1u);
-      } else {
-        coarse = (unsigned)__ballot(cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
-      }
+      const unsigned coarse = (unsigned)__ballot(cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
       unsigned msk = 0;
 #pragma unroll
       for (int pr = 0; pr < NPAIR; pr++) {
@@ -1397,9 +1347,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         __hip_atomic_store(reinterpret_cast<unsigned long long *>(ar + XOLayout::RTS) + ix,
                            ((unsigned long long)xo.seq << 32) | __float_as_uint(m.T), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
-      } else if (xo.rstride) {  // chunk-major: the workgroup's records are one contiguous run
-        rec[(int64_t)wg * xo.rstride + mq] = rv;
-        recT[(int64_t)wg * xo.rstride + mq] = m.T;
       } else {
         rec[(int64_t)mq * nwg + wg] = rv;
         recT[(int64_t)mq * nwg + wg] = m.T;

@@ -888,16 +888,15 @@ __device__ __forceinline__ double cert_theta(const MergeArgs &a, double R, doubl
 template <int RPL = IA_WG_TARGET / IA_WAVE, class DistFn>
 __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, unsigned *stat_out) {
   const int lane = threadIdx.x & 63;
-  const int64_t rs = a.rstride ? a.rstride : 1;  // record w of query m: rr[w rs]
-  const float4 *rr = a.rec + (a.rstride ? (int64_t)m : (int64_t)m * a.nwg);
-  const float *rT = a.recT + (a.rstride ? (int64_t)m : (int64_t)m * a.nwg);
+  const float4 *rr = a.rec + (int64_t)m * a.nwg;
+  const float *rT = a.recT + (int64_t)m * a.nwg;
   // issue every record load at once (clamped index, no per-load branch), mask afterwards
   float v1[RPL], v2[RPL], tt[RPL];
 #pragma unroll
   for (int j = 0; j < RPL; j++) {
     const int w = min(lane + IA_WAVE * j, a.nwg - 1);
-    const float4 x = rr[w * rs];
-    const float t = rT[w * rs];
+    const float4 x = rr[w];
+    const float t = rT[w];
     const bool ok = lane + IA_WAVE * j < a.nwg;
     v1[j] = ok ? x.x : FLT_MAX;
     v2[j] = ok ? x.z : FLT_MAX;
@@ -926,7 +925,7 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
   while (cmask) {
     const int b = __ffs(cmask) - 1;
     cmask &= cmask - 1;
-    const float4 x = rr[lane + IA_WAVE * (b >> 1)];  // L2-hot re-read of the record
+    const float4 x = rr[min(lane + IA_WAVE * (b >> 1), a.nwg - 1)];  // L2-hot re-read of the record
     const int64_t i = __float_as_int((b & 1) ? x.w : x.y);
     if (i >= 0 && i < a.NA) {
       const double d = dist(i);
@@ -1543,9 +1542,8 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   const double *__restrict__ weights = jp.weights;
   const double kf = jp.kf;
   const double *q = a.q64 + (int64_t)m * Geo<CH>::D;
-  const int64_t rs = a.rstride ? a.rstride : 1;  // record w of query m: rr[w rs]
-  const float4 *rr = a.rec + (a.rstride ? (int64_t)m : (int64_t)m * a.nwg);
-  const float *rT = a.recT + (a.rstride ? (int64_t)m : (int64_t)m * a.nwg);
+  const float4 *rr = a.rec + (int64_t)m * a.nwg;
+  const float *rT = a.recT + (int64_t)m * a.nwg;
   const unsigned hw = (unsigned)g.ah * (unsigned)g.aw;
 
   // ---- round 1: records (clamped, unconditional loads), coherence neighbours, query/weights
@@ -1580,8 +1578,8 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
       x = a.rec[ix];
       t = __uint_as_float((unsigned)ts);
     } else {
-      x = rr[w * rs];
-      t = rT[w * rs];
+      x = rr[w];
+      t = rT[w];
     }
     const bool ok = lane + IA_WAVE * j < a.nwg;
     v1[j] = ok ? x.x : FLT_MAX;
@@ -1885,7 +1883,7 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_level(LevelGeo g, StepDesc s
 #endif
   const double *q = ma.q64 + (int64_t)m * Geo<CH>::D;
 #if IA_PROBE & 1  // diagnostic build only: take the first record's candidate, no rerank
-  const Winner wn{0., (int64_t)__float_as_int(ma.rec[ma.rstride ? (int64_t)m : (int64_t)m * ma.nwg].y)};
+  const Winner wn{0., (int64_t)__float_as_int(ma.rec[(int64_t)m * ma.nwg].y)};
 #else
   unsigned stat = 0;
   const Winner wn = certified_winner(ma, m, [&](int64_t row) {
@@ -2813,7 +2811,7 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
                    const float4 *tbox, const float *tnorm, hipStream_t st, int nqb, int qt_end, const XOScan *xo,
-                   unsigned long long *stamp, int rstride) {
+                   unsigned long long *stamp) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
@@ -2856,7 +2854,6 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   XOScan x{};  // off unless an owner-computes step passes its exchange
   if (xo) x = *xo;
   x.stamp = stamp;
-  x.rstride = rstride;
   allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nqb * nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row,
                      NT, qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm, nqb, qt_end, x);

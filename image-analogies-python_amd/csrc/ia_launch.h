@@ -70,7 +70,7 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
                    const float4 *tbox, const float *tnorm, hipStream_t st, int nqb = 1, int qt_end = 0,
-                   const XOScan *xo = nullptr, unsigned long long *stamp = nullptr, int rstride = 0);
+                   const XOScan *xo = nullptr, unsigned long long *stamp = nullptr);
 // GPU preprocessing (ia_pyramid.hip)
 void ia_launch_pyramid_reduce(const double *in, double *out, double *tmp, double *sm, double *mm, int h, int w, int ch,
                               const double *w7, hipStream_t st);
