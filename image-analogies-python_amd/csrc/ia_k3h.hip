@@ -374,6 +374,9 @@ __device__ __forceinline__ f32x16 k3p_hh(const h16x8 (&a)[2 * KS], const h16x8 *
   for (int s = 0; s < KS; s++) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], qb[(2 * s) * IA_WAVE], c, 0, 0, 0);
   return c;
 }
+// (this file is built with -fno-honor-nans - no value here is ever NaN - so fminf / fmaxf are
+// single v_min3 / v_max3 instructions instead of a canonicalizing v_max_f32 x, x per operand
+// first; the MFMA read hazards stay the compiler's)
 __device__ __forceinline__ float k3p_min16(const f32x16 &c) {
   const float m0 = fminf(fminf(c[0], c[1]), c[2]), m1 = fminf(fminf(c[3], c[4]), c[5]);
   const float m2 = fminf(fminf(c[6], c[7]), c[8]), m3 = fminf(fminf(c[9], c[10]), c[11]);
@@ -392,8 +395,13 @@ __device__ __forceinline__ void k3p_hhpipe_h(const h16x8 (&h)[KS], const h16x8 *
       if ((msk >> Q) & 1u) {
         const h16x8 *qb = lq + Q * QS * IA_WAVE;
         f32x16 c = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        h16x8 qv[KS];  // the block's query pieces, all requested before the first product
 #pragma unroll
-        for (int s = 0; s < KS; s++) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(h[s], qb[(PS * s) * IA_WAVE], c, 0, 0, 0);
+        for (int s = 0; s < KS; s++) qv[s] = qb[(PS * s) * IA_WAVE];
+#pragma unroll
+        for (int s = 0; s < KS; s++) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(h[s], qv[s], c, 0, 0, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, KS, 0);  // the KS LDS reads first (one wait),
+        __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);  // then the KS products
         acc[Q & 1] = c;
       }
     }
@@ -1013,13 +1021,19 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
     auto need_r = [&](int k) -> unsigned {
       const float4 blo = wbox[2 * k], bhi = wbox[2 * k + 1];
-      const unsigned coarse = (unsigned)__ballot(cl && prune_lb(blo, bhi, ctl, cth) <= ctu);
+      // (lanes >= QT: ctu = -inf, never passing; no branch around the test)
+      const unsigned coarse = (unsigned)__ballot(prune_lb(blo, bhi, ctl, cth) <= ctu);
       unsigned msk = 0;
 #pragma unroll
       for (int pr = 0; pr < NPAIR; pr++) {
         if ((coarse >> (2 * pr)) & 3u) {
           const unsigned long long b = __ballot(prune_lb(blo, bhi, pql[pr], pqh[pr]) <= pqu[pr]);
-          msk |= (((unsigned)b != 0u ? 1u : 0u) | ((unsigned)(b >> 32) != 0u ? 2u : 0u)) << (2 * pr);
+          // (the two 32-lane halves' bits by scalar compares in asm: the compiler turns the C
+          // form into a 64-bit VALU compare and a VALU select + readfirstlane)
+          unsigned x0, x1;
+          asm("s_cmp_lg_u32 %1, 0\n\ts_cselect_b32 %0, 1, 0" : "=s"(x0) : "s"((unsigned)b) : "scc");
+          asm("s_cmp_lg_u32 %1, 0\n\ts_cselect_b32 %0, 2, 0" : "=s"(x1) : "s"((unsigned)(b >> 32)) : "scc");
+          msk |= (x0 | x1) << (2 * pr);
         }
       }
       return msk & coarse;
