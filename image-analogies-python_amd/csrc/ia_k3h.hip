@@ -414,6 +414,51 @@ __device__ __forceinline__ void k3p_hhpipe_h(const h16x8 (&h)[KS], const h16x8 *
     k3p_hhpipe_h<KS, QT, Q + 1, HO>(h, lq, msk, rt, qzt, qzw, acc, pass);
   }
 }
+// k3p_variant 24 / 25: the same filter walking only the set bits of the need mask (a tile has
+// ≈ 2.7 of 11 blocks needed: the unrolled form spends its scalar instructions testing the other
+// bits).  Blocks in bit order, two accumulators: a block's products are issued before the
+// previous block's bound test, as in k3p_hhpipe_h; the query hi pieces at lq ([QT][KS][64]).
+template <int KS>
+__device__ __forceinline__ unsigned k3p_filter_bits(const h16x8 (&h)[KS], const h16x8 *lq, unsigned msk, float rt,
+                                                    const float *qzt, const float *qzw) {
+  const float rr = fmaf(rt, 0x1p-9f, 0x1p-20f);
+  auto prod = [&](int q) {
+    const h16x8 *qb = lq + q * KS * IA_WAVE;
+    f32x16 c = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    h16x8 qv[KS];
+#pragma unroll
+    for (int s = 0; s < KS; s++) qv[s] = qb[s * IA_WAVE];
+#pragma unroll
+    for (int s = 0; s < KS; s++) c = __builtin_amdgcn_mfma_f32_32x32x16_f16(h[s], qv[s], c, 0, 0, 0);
+    __builtin_amdgcn_sched_group_barrier(0x100, KS, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, KS, 0);
+    return c;
+  };
+  auto test = [&](const f32x16 &c, int q) -> unsigned {
+    const float lim = fmaf(rt, qzw[q * IA_TILE] + rr, qzt[q * IA_TILE]);
+    return __ballot(k3p_min16(c) <= lim) != 0ull ? 1u << q : 0u;
+  };
+  unsigned pass = 0;
+  f32x16 a0, a1;
+  int qa = -1, qb = -1;  // the block whose products sit in a0 / a1, its test still due
+  for (;;) {
+    if (!msk) break;
+    qa = __builtin_ctz(msk);
+    msk &= msk - 1;
+    a0 = prod(qa);
+    if (qb >= 0) pass |= test(a1, qb);
+    qb = -1;
+    if (!msk) break;
+    qb = __builtin_ctz(msk);
+    msk &= msk - 1;
+    a1 = prod(qb);
+    pass |= test(a0, qa);
+    qa = -1;
+  }
+  if (qa >= 0) pass |= test(a0, qa);
+  if (qb >= 0) pass |= test(a1, qb);
+  return pass;
+}
 
 // k3p_variant 24 / 25, second pass: the full 12-MFMA chains of a tile's filter-passing blocks
 // with the query hi pieces at qh ([QT][KS][64], LDS) and the lo pieces at ql (same layout, LDS):
@@ -598,6 +643,9 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // ------------------------------------------------------------------------------------------
 #ifndef IA_K3P_ROWS_EARLY  // 1: candidate rows looked up before the subset merge (0: after it)
 #define IA_K3P_ROWS_EARLY 1
+#endif
+#ifndef IA_K3P_FBITS  // k3p_variant 24 / 25: the stream's filter walks the need mask's set bits (0: unrolled)
+#define IA_K3P_FBITS 1
 #endif
 #define IA_K3P3_MAXQ 512   // queries per step (one per thread)
 // steps of up to IA_K3P_RANK_MAX queries are sorted by rank counting, wider ones by the bitonic
@@ -1094,9 +1142,13 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       if (mc) {  // wave-uniform (0: a speculative tile that is not needed)
         h16x8 hc[KS];
         slot_hi(hc, wring + sl * IA_HSLOT, lane);
+#if IA_K3P_FBITS
+        const unsigned pass = k3p_filter_bits<KS>(hc, ldsh + lane, mc, wR[kc], qzt + (lane & 31), qzw + (lane & 31));
+#else
         f32x16 acc[2];
         unsigned pass = 0;
         k3p_hhpipe_h<KS, QT, 0, true>(hc, ldsh + lane, mc, wR[kc], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
+#endif
         cnt += __popc(mc);
         if (pass) {  // wave-uniform
           nfull += __popc(pass);
