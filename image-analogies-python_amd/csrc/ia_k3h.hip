@@ -644,6 +644,9 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 #ifndef IA_K3P_ROWS_EARLY  // 1: candidate rows looked up before the subset merge (0: after it)
 #define IA_K3P_ROWS_EARLY 1
 #endif
+#ifndef IA_K3P_TAIL16  // k3p_variant 24 / 25: the subset merge takes every lane's subset (no half-wave merge)
+#define IA_K3P_TAIL16 1
+#endif
 #ifndef IA_K3P_FBITS  // k3p_variant 24 / 25: the stream's filter walks the need mask's set bits (0: unrolled)
 #define IA_K3P_FBITS 1
 #endif
@@ -915,10 +918,12 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       for (int jb = kb >> 1; jb > 0; jb >>= 1) {
         unsigned o;
         if (jb >= IA_WAVE) {
-          sx[tid] = v;
+          // two buffers used in turn: a buffer is rewritten two LDS stages later, after every
+          // thread passed the barrier that follows its reads, so one barrier per stage
+          unsigned *sb = sx + (((kb == 256 && jb == 128) || (kb == 512 && jb != 128)) ? WGT : 0);
+          sb[tid] = v;
           __syncthreads();
-          o = sx[tid ^ jb];
-          __syncthreads();
+          o = sb[tid ^ jb];
         } else {
           o = xlane_xor(v, jb);
         }
@@ -977,15 +982,20 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
   }
   K3P_T(pc);
+  tile_boxes();
+  unsigned long long pd = 0, pe = 0;
+  K3P_T(pd);
+  __syncthreads();
+  K3P_T(pe);
 #if IA_PROBE & 16
-  if (lane == 0 && M == Mpad - 10 && wg < 8) {  // the sort phase: network / rank, barrier, scatter
-    atomicAdd(&k3p_prof[16], pa - ph[1]);
+  if (lane == 0 && M == Mpad - 10 && wg < 8) {  // the sort phase: network / rank, barrier, scatter,
+    atomicAdd(&k3p_prof[16], pa - ph[1]);        // query-tile boxes, barrier
     atomicAdd(&k3p_prof[17], pb - pa);
     atomicAdd(&k3p_prof[18], pc - pb);
+    atomicAdd(&k3p_prof[19], pd - pc);
+    atomicAdd(&k3p_prof[20], pe - pd);
   }
 #endif
-  tile_boxes();
-  __syncthreads();
   }  // !PRE
   K3P_T(ph[2]);
 
@@ -1373,6 +1383,20 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     wtp[wave] = ntp;
   }
   Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32], inside the query-fragment area
+  // IA_K3P_TAIL16 (HHX 4): every lane's subset (b1, b2 as T, tile) goes to LDS as it stands
+  // ([NW][QT][64] per field) and the per-query merge takes 16 subsets: no half-wave merge
+  float *rv1 = reinterpret_cast<float *>(ldsh), *rvT = rv1 + NW * QT * IA_WAVE;
+  int *ri1 = reinterpret_cast<int *>(rvT + NW * QT * IA_WAVE);
+  constexpr bool T16 = HHX == 4 && IA_K3P_TAIL16;
+  if constexpr (T16) {
+#pragma unroll
+    for (int q = 0; q < QT; q++) {
+      const int ix = (wave * QT + q) * IA_WAVE + lane;
+      rv1[ix] = b1[q];
+      rvT[ix] = b2[q];
+      ri1[ix] = i1[q];
+    }
+  } else {
 #pragma unroll
   for (int q = 0; q < QT; q++) {
     // the two halves of the wave hold the same query's subsets: (b1, row) + runner-up value each;
@@ -1385,13 +1409,25 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
                         (int)(half ? si[0] : si[1]), 0x7fffffff};
     if (half == 0) red[(wave * QT + q) * IA_TILE + lane] = top2_merge_sel(mine, other);
   }
+  }  // !T16
   K3P_T(ph[7]);
   __syncthreads();
   K3P_T(ph[8]);
   for (int x = tid; x < NQ; x += WGT) {
-    Top2 m = red[x];
+    Top2 m;
+    if constexpr (T16) {
+      const int b0 = (x >> 5) * IA_WAVE + (x & 31);  // wave 0, lane x % 32 of query tile x / 32
+      m = Top2{rv1[b0], FLT_MAX, rvT[b0], ri1[b0], 0x7fffffff};
 #pragma unroll
-    for (int w = 1; w < NW; w++) m = top2_merge_sel(m, red[(w * QT) * IA_TILE + x]);
+      for (int e = 1; e < 2 * NW; e++) {
+        const int ix = b0 + (e >> 1) * QT * IA_WAVE + (e & 1) * 32;
+        m = top2_merge_sel(m, Top2{rv1[ix], FLT_MAX, rvT[ix], ri1[ix], 0x7fffffff});
+      }
+    } else {
+      m = red[x];
+#pragma unroll
+      for (int w = 1; w < NW; w++) m = top2_merge_sel(m, red[(w * QT) * IA_TILE + x]);
+    }
     const int mq = WGT >= NQ ? mq_pre : (PRE ? (int)skey[x] : order[s0 + x]);
     if (mq < M) {
 #if IA_K3P_ROWS_EARLY
@@ -1463,8 +1499,8 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
 void ia_k3p_probe_dump() {  // diagnostic build only: phase cycles per plateau wave, to stderr
   unsigned long long v[24];
   if (hipMemcpyFromSymbol(v, HIP_SYMBOL(k3p_prof), sizeof(v)) != hipSuccess || v[4] == 0) return;
-  fprintf(stderr, "K3P_PROBE sort phase: network %.0f, barrier %.0f, fragment scatter %.0f\n", (double)v[16] / v[4],
-          (double)v[17] / v[4], (double)v[18] / v[4]);
+  fprintf(stderr, "K3P_PROBE sort phase: network %.0f, barrier %.0f, fragment scatter %.0f, tile boxes %.0f, barrier %.0f\n",
+          (double)v[16] / v[4], (double)v[17] / v[4], (double)v[18] / v[4], (double)v[19] / v[4], (double)v[20] / v[4]);
   fprintf(stderr, "K3P_PROBE two-pass (v24/25): stream %.0f, barrier %.0f, lo staging %.0f, chains %.0f\n", (double)v[12] / v[4],
           (double)v[13] / v[4], (double)v[14] / v[4], (double)v[15] / v[4]);
   fprintf(stderr, "K3P_PROBE tail split: half merge %.0f, barrier %.0f, subset merge + records %.0f\n", (double)v[9] / v[4],

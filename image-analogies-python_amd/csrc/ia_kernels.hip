@@ -2830,7 +2830,8 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
                    : ia_k3p_lds(qt, Mpad) - (size_t)qt * 8 * IA_WAVE * 16 + qfrag + (size_t)Mpad * 4 + (size_t)kmax * 40;
     l += NQ * 8 + (size_t)kmax * 4;            // (z, w) per sorted query slot, R_t per tile
     if (v >= 24) l += (size_t)kmax * 8;        // the filter-passing tiles and their blocks
-    const size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
+    size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
+    if (v >= 24) red = std::max(red, (size_t)(nthr / IA_WAVE) * qt * IA_WAVE * 12);  // (every lane's subset)
     return l > red ? l : red;
   };
   size_t lds = dyn_lds(variant);
