@@ -4,7 +4,7 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
-O=gpurun_out/r5final; mkdir -p $O
+O=gpurun_out/${1:-r5final}; mkdir -p $O
 pass() {  # name counters...
   local name=$1; shift
   timeout -s KILL 150 rocprofv3 --pmc "$@" --kernel-include-regex k3h_prune3 --output-format csv \
