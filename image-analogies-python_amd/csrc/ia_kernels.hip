@@ -1236,6 +1236,12 @@ __device__ __forceinline__ double feat_q1(const Imgs &B, int f, int r, int c, co
 // owner-computes sharded step (XOPub): query m's fragments (16 h16x8 pieces from LDS, one store
 // instruction per area), its pruning record, then - once those stores completed - its seq, into
 // every rank's area
+// lane k < 3 picks record k, component by component (a float4 chosen by a lane-dependent
+// ternary becomes a dynamically indexed private array: scratch, and a scratch-using kernel)
+__device__ __forceinline__ float4 sel3(int k, const float4 &a, const float4 &b, const float4 &c) {
+  return make_float4(k == 0 ? a.x : k == 1 ? b.x : c.x, k == 0 ? a.y : k == 1 ? b.y : c.y,
+                     k == 0 ? a.z : k == 1 ? b.z : c.z, k == 0 ? a.w : k == 1 ? b.w : c.w);
+}
 template <int KS>
 __device__ __forceinline__ void xo_publish(const XOPub &xp, int m, int lane, const _Float16 *xh0, const _Float16 *xh1,
                                            float4 i0, float4 i1, float4 i2) {
@@ -1248,7 +1254,7 @@ __device__ __forceinline__ void xo_publish(const XOPub &xp, int m, int lane, con
   for (int o = 0; o < xp.W; o++) {
     if (c < 4 * KS)
       reinterpret_cast<h16x8 *>(xp.area[o] + XOLayout::FRAG)[((t0 + qt) * 2 * KS + 2 * sp + part) * IA_WAVE + h * IA_TILE + j] = v;
-    if (lane < 3) reinterpret_cast<float4 *>(xp.area[o] + XOLayout::INFO)[3 * (xp.slot0 + m) + lane] = lane == 0 ? i0 : lane == 1 ? i1 : i2;
+    if (lane < 3) reinterpret_cast<float4 *>(xp.area[o] + XOLayout::INFO)[3 * (xp.slot0 + m) + lane] = sel3(lane, i0, i1, i2);
   }
   ia_stores_done();
   if (lane < xp.W)
@@ -1293,7 +1299,7 @@ __device__ __forceinline__ void sorted_publish(const NextStep &nx, int m, int la
   const int x = __builtin_amdgcn_readfirstlane(below);
   const int qt = x / IA_TILE, j = x % IA_TILE;
   if (c < 4 * KS) reinterpret_cast<h16x8 *>(nx.sfrag)[((int64_t)qt * 2 * KS + 2 * sp + part) * IA_WAVE + h * IA_TILE + j] = v;
-  if (lane < 3) nx.sinfo[3 * x + lane] = lane == 0 ? i0 : lane == 1 ? i1 : i2;
+  if (lane < 3) nx.sinfo[3 * x + lane] = sel3(lane, i0, i1, i2);
   if (lane == 3) nx.sorder[x] = m;
 }
 
