@@ -645,7 +645,7 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 #define IA_K3P_ROWS_EARLY 1
 #endif
 #ifndef IA_K3P_BUCKETS  // the in-kernel query sort as a counting sort on the key's leading bits (0: bitonic)
-#define IA_K3P_BUCKETS 1
+#define IA_K3P_BUCKETS 0
 #endif
 #ifndef IA_K3P_TAIL16  // k3p_variant 24 / 25: the subset merge takes every lane's subset (no half-wave merge)
 #define IA_K3P_TAIL16 1
@@ -916,8 +916,9 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
 #if IA_K3P_BUCKETS
     // (IA_K3P_BUCKETS) a counting sort on the key's leading 10 bits (the Morton code's top: ≈ 3
     // buckets per query, so the query tiles hold what the full sort gives them up to swaps inside
-    // a bucket; any order is exact, only the tiles' compactness depends on it): LDS counters, a
-    // block scan, one rank per query - four barriers and no exchange network
+    // a bucket; any order that every workgroup derives alike is exact, only the tiles'
+    // compactness depends on it): LDS counters, a block scan, one rank per query - five barriers
+    // and no exchange network
     static_assert(2 * WGT == 1024, "two buckets per thread");
     unsigned *hist = reinterpret_cast<unsigned *>(ldsh);  // [1024] counts, then bases
     unsigned *wsum = hist + 2 * WGT;                       // [NW] per-wave totals
@@ -944,8 +945,20 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     hist[2 * tid] = ex;
     hist[2 * tid + 1] = ex + h0;
     __syncthreads();
+    // the atomics' order inside a bucket varies from workgroup to workgroup, and the order must
+    // not (a wide step's query blocks, other launches and other workgroups take their slots from
+    // the same order): inside each bucket the queries are ordered by index instead
+    int *tmp = reinterpret_cast<int *>(wsum + NW);  // [Mpad] provisional slot -> query
+    int b0 = 0, b1 = 0;
     if (tid < Mpad) {
-      const int rank = (int)hist[bk] + inb;
+      b0 = (int)hist[bk];
+      b1 = bk + 1 < 2u * WGT ? (int)hist[bk + 1] : Mpad;
+      tmp[b0 + inb] = tid;
+    }
+    __syncthreads();
+    if (tid < Mpad) {
+      int rank = b0;
+      for (int j = b0; j < b1; j++) rank += tmp[j] < tid ? 1 : 0;
       order[rank] = tid;
       rankof[tid] = rank;
     }
