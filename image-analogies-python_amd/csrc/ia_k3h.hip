@@ -644,9 +644,6 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 #ifndef IA_K3P_ROWS_EARLY  // 1: candidate rows looked up before the subset merge (0: after it)
 #define IA_K3P_ROWS_EARLY 1
 #endif
-#ifndef IA_K3P_BUCKETS  // the in-kernel query sort as a counting sort on the key's leading bits (0: bitonic)
-#define IA_K3P_BUCKETS 0
-#endif
 #ifndef IA_K3P_TAIL16  // k3p_variant 24 / 25: the subset merge takes every lane's subset (no half-wave merge)
 #define IA_K3P_TAIL16 1
 #endif
@@ -913,56 +910,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     // bitonic network over the first 512 threads' unique keys (padding: 0xFFFFFFFF, last):
     // exchanges at distance < 64 are lane swaps, the 6 at distance >= 64 go through LDS (the
     // query-fragment area, free until the scatter below)
-#if IA_K3P_BUCKETS
-    // (IA_K3P_BUCKETS) a counting sort on the key's leading 10 bits (the Morton code's top: ≈ 3
-    // buckets per query, so the query tiles hold what the full sort gives them up to swaps inside
-    // a bucket; any order that every workgroup derives alike is exact, only the tiles'
-    // compactness depends on it): LDS counters, a block scan, one rank per query - five barriers
-    // and no exchange network
-    static_assert(2 * WGT == 1024, "two buckets per thread");
-    unsigned *hist = reinterpret_cast<unsigned *>(ldsh);  // [1024] counts, then bases
-    unsigned *wsum = hist + 2 * WGT;                       // [NW] per-wave totals
-    hist[2 * tid] = 0u;
-    hist[2 * tid + 1] = 0u;
-    __syncthreads();
-    const unsigned bk = mkey >> 22;
-    int inb = 0;
-    if (tid < Mpad) inb = (int)atomicAdd(&hist[bk], 1u);
-    __syncthreads();
-    const unsigned h0 = hist[2 * tid], h1 = hist[2 * tid + 1];
-    unsigned incl = h0 + h1;
-#pragma unroll
-    for (int o = 1; o < IA_WAVE; o <<= 1) {
-      const unsigned y = __shfl_up(incl, o, IA_WAVE);
-      incl += lane >= o ? y : 0u;
-    }
-    if (lane == IA_WAVE - 1) wsum[wave] = incl;
-    __syncthreads();
-    unsigned wb = 0u;
-#pragma unroll
-    for (int w = 0; w < NW; w++) wb += w < wave ? wsum[w] : 0u;
-    const unsigned ex = wb + incl - h0 - h1;
-    hist[2 * tid] = ex;
-    hist[2 * tid + 1] = ex + h0;
-    __syncthreads();
-    // the atomics' order inside a bucket varies from workgroup to workgroup, and the order must
-    // not (a wide step's query blocks, other launches and other workgroups take their slots from
-    // the same order): inside each bucket the queries are ordered by index instead
-    int *tmp = reinterpret_cast<int *>(wsum + NW);  // [Mpad] provisional slot -> query
-    int b0 = 0, b1 = 0;
-    if (tid < Mpad) {
-      b0 = (int)hist[bk];
-      b1 = bk + 1 < 2u * WGT ? (int)hist[bk + 1] : Mpad;
-      tmp[b0 + inb] = tid;
-    }
-    __syncthreads();
-    if (tid < Mpad) {
-      int rank = b0;
-      for (int j = b0; j < b1; j++) rank += tmp[j] < tid ? 1 : 0;
-      order[rank] = tid;
-      rankof[tid] = rank;
-    }
-#else
     unsigned *sx = reinterpret_cast<unsigned *>(ldsh);
     unsigned v = mkey;
 #pragma unroll
@@ -989,7 +936,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       order[tid] = q;
       rankof[q] = tid;
     }
-#endif
     __syncthreads();
     if (tid < Mpad) {
       const int x = rankof[tid] - s0;
