@@ -414,6 +414,9 @@ __device__ __forceinline__ void k3p_hhpipe_h(const h16x8 (&h)[KS], const h16x8 *
     k3p_hhpipe_h<KS, QT, Q + 1, HO>(h, lq, msk, rt, qzt, qzw, acc, pass);
   }
 }
+#ifndef IA_K3P_A1DEF  // k3p_variant 24 / 25: the filter's second accumulator defined by an empty asm
+#define IA_K3P_A1DEF 1 // (0: the compiler zeroes its 16 registers per tile)
+#endif
 // k3p_variant 24 / 25: the same filter walking only the set bits of the need mask (a tile has
 // ≈ 2.7 of 11 blocks needed: the unrolled form spends its scalar instructions testing the other
 // bits).  Blocks in bit order, two accumulators: a block's products are issued before the
@@ -440,6 +443,10 @@ __device__ __forceinline__ unsigned k3p_filter_bits(const h16x8 (&h)[KS], const 
   };
   unsigned pass = 0;
   f32x16 a0, a1;
+#if IA_K3P_A1DEF
+  // a1 is read only after a product wrote it; without a definition here the compiler zeroes it
+  asm volatile("" : "=v"(a1));
+#endif
   int qa = -1, qb = -1;  // the block whose products sit in a0 / a1, its test still due
   for (;;) {
     if (!msk) break;
