@@ -261,8 +261,8 @@ def make_context(args, local):
     ALL_CTX.append(cx)
     cx.set_option('matcher', _native.IA_MATCH_F16X3 if args.matcher == 'f16x3' else _native.IA_MATCH_F32)
     cx.set_option('prune', args.prune)
-    if args.k3p_variant != 22:
-        cx.set_option('k3p_variant', args.k3p_variant)     # 20, 21, 22, 24, 25
+    # always explicit (the library default is 24, so a skipped set_option for 22 ran v24)
+    cx.set_option('k3p_variant', args.k3p_variant)     # 20, 21, 22, 24, 25
     cx.set_option('prune_min_rows', args.prune_min_rows)
     if args.k3p_blocks != 1:
         cx.set_option('k3p_blocks', args.k3p_blocks)
@@ -276,6 +276,8 @@ def make_context(args, local):
         cx.set_option('fuse_sort', args.fuse_sort)
     if not args.prefetch_next:
         cx.set_option('prefetch_next', 0)
+    if args.rec_wt:
+        cx.set_option('rec_wt', 1)
     if not args.nn_bound:
         cx.set_option('nn_bound', 0)
     if args.shard_unpruned:
@@ -397,6 +399,9 @@ def main():
     ap.add_argument('--nn-bound', type=int, default=1, choices=[0, 1],
                     help='1 (default): the pruned levels\' gathers also bound U\' by the causal neighbours\' exact NN rows '
                          '(include/ia.h option nn_bound)')
+    ap.add_argument('--rec-wt', type=int, default=0, choices=[0, 1],
+                    help='1: the pruned scan stores its records write-through (sc1), so the scan -> merge kernel '
+                         'boundary finds no dirty record lines in L2 (include/ia.h option rec_wt, DESIGN.md §6e)')
     ap.add_argument('--prefetch-next', type=int, default=1, choices=[0, 1],
                     help='1 (default): fused merge + gather waves load the next query\'s step-independent inputs during '
                          'the merge (include/ia.h option prefetch_next)')
@@ -828,11 +833,21 @@ def main():
         # pruned-scan launch of every timed step, in the configuration that is timed (pipelined
         # levels, concurrent streams)
         k3t = st_all['k3p_stamp_ms'] * 1e-3
-        roofline['frac_timed'] = st_all['k3p_bytes_all'] / k3t / HBM_PEAK
-        roofline['achieved_timed'] = st_all['k3p_bytes_all'] / k3t / 1e9
+        # algorithmic bytes count each DB tile of a launch at most once: a
+        # launch of several query blocks (cfg4's wide steps) streams its tiles once per block, and
+        # those repeats are priced as waste, not as work (streamed_bytes_per_launch_timed)
+        ub = st_all.get('k3p_bytes_unique_all') or st_all['k3p_bytes_all']
+        roofline['frac_timed'] = ub / k3t / HBM_PEAK
+        roofline['achieved_timed'] = ub / k3t / 1e9
         roofline['k3_us_per_launch_timed'] = st_all['k3p_stamp_ms'] * 1e3 / st_all['k3p_stamp_launches']
         roofline['k3_launches_timed'] = st_all['k3p_stamp_launches']
-        roofline['algorithmic_bytes_per_launch_timed'] = st_all['k3p_bytes_all'] / st_all['k3p_stamp_launches']
+        roofline['algorithmic_bytes_per_launch_timed'] = ub / st_all['k3p_stamp_launches']
+        roofline['streamed_bytes_per_launch_timed'] = st_all['k3p_bytes_all'] / st_all['k3p_stamp_launches']
+        if ub < st_all['k3p_bytes_all']:  # the sampled reading on the same basis
+            for k in ('achieved', 'frac', 'algorithmic_bytes_per_launch'):
+                roofline[k] *= ub / st_all['k3p_bytes_all']
+        if roofline.get('traffic'):
+            roofline['traffic_over_algorithmic'] = roofline['traffic'] / roofline['algorithmic_bytes_per_launch_timed']
         # the launch = its workgroups' start spread (dispatch, CUs held by concurrent kernels)
         # + their mean duration + the imbalance tail
         roofline['k3_wg_us_timed'] = st_all['k3p_stamp_wg_ms'] * 1e3 / st_all['k3p_stamp_launches']
@@ -878,6 +893,7 @@ def main():
                                                            'dbshard%d_jobs%d' % (max(world, args.shard_emulate),
                                                                                  args.shard_jobs)),
                                            'jobs_per_step': jobs,
+                                           'k3p_variant': args.k3p_variant,
                                            'level_pipeline': (('%d contexts%s' % (args.pipe_ctx, ', finest level high priority'
                                                                                   if args.pipe_priority else ''))
                                                               if args.pipeline and sw is None and (not owner or pipe_owner)

@@ -55,14 +55,15 @@ class Stats(ctypes.Structure):
                 ('merge_stamp_launches', ctypes.c_int64), ('stamp_gap_ms', ctypes.c_double),
                 ('stamp_gaps', ctypes.c_int64), ('stamp_window_ms', ctypes.c_double), ('prune_rows', ctypes.c_int64),
                 ('k3p_stamp_start_ms', ctypes.c_double), ('k3p_stamp_wg_ms', ctypes.c_double),
-                ('stamp_gap_sm_ms', ctypes.c_double), ('stamp_gaps_sm', ctypes.c_int64)]
+                ('stamp_gap_sm_ms', ctypes.c_double), ('stamp_gaps_sm', ctypes.c_int64),
+                ('k3p_bytes_unique_all', ctypes.c_double)]
 
     # fields that describe only the levels with the largest DB seen (build_rows / prune_rows)
     _BUILD = ('k1b_ms', 'k1b_bytes', 'k1_ms', 'k1_bytes', 'build_levels')
     _PRUNE = ('prune_ms_timed', 'prune_launches_timed', 'prune_flops_timed', 'prune_bytes_timed', 'k3p_stamp_ms',
               'k3p_stamp_launches', 'k3p_bytes_all', 'merge_stamp_ms', 'merge_stamp_launches', 'stamp_gap_ms',
               'stamp_gaps', 'stamp_window_ms', 'k3p_stamp_start_ms', 'k3p_stamp_wg_ms', 'stamp_gap_sm_ms',
-              'stamp_gaps_sm')
+              'stamp_gaps_sm', 'k3p_bytes_unique_all')
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

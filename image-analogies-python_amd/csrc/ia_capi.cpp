@@ -156,6 +156,7 @@ struct ia_ctx {
   // per-step K3 timing (optional)
   int time_dist = 0;
   int stamps = 0;                 // option "stamps": per-launch device time from kernel stamps
+  int rec_wt = 0;                 // option "rec_wt": K3p records stored write-through
   DevBuf stamp_k3, stamp_mg, stamp_dur;
   std::vector<hipEvent_t> evs, evg, evm;  // sampled steps: K3, K2 and K4 brackets
   hipEvent_t lv0 = nullptr, lv1 = nullptr, lv2 = nullptr;
@@ -392,6 +393,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!c || !name) return fail(IA_EINVAL, "ia_set_option: NULL argument");
   if (!std::strcmp(name, "time_dist")) {
     c->time_dist = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "rec_wt")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: rec_wt must be 0 or 1");
+    c->rec_wt = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "stamps")) {
@@ -1049,7 +1055,20 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   auto mg_stamp = [&]() -> unsigned long long * {
     return stamped && mg_n < mg_cap ? c->stamp_mg.as<unsigned long long>() + (size_t)2 * mg_stride * mg_n++ : nullptr;
   };
+  // the slots this level wrote are cleared on EVERY exit (an early error return after
+  // some stamped launches left non-zero slots that a later, smaller launch would have read)
+  struct StampClear {
+    ia_ctx *c;
+    const int64_t &k3_n, &mg_n;
+    int mg_stride;
+    ~StampClear() {
+      if (k3_n) (void)hipMemsetAsync(c->stamp_k3.p, 0, (size_t)k3_n * IA_NWG_H * 16, c->st);
+      if (mg_n) (void)hipMemsetAsync(c->stamp_mg.p, 0, (size_t)mg_n * mg_stride * 16, c->st);
+    }
+  } stamp_clear{c, k3_n, mg_n, mg_stride};
   double bytes_all_fixed = 0.;  // algorithmic bytes of every pruned launch besides its DB tiles
+  double db_cap_all = 0.;       // the whole tiles of every pruned launch's DB range, each counted once
+                                // (a launch of nqb query blocks streams a tile once per block)
   // per-workgroup counters of the pruned scan: [pairs | pairs (timed steps) | tiles | tiles (timed) |
   // extra half-tiles | extra half-tiles (timed)][wg]
   HIP_TRY(hipMemsetAsync(c->pairs.p, 0, 6 * IA_NWG_H * 8, c->st));
@@ -1358,17 +1377,20 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         const int kv = c->k3p_variant;
         // the in-kernel-sort variant (ink: 20 / 22 / 24) or its presorted form (21 / 25)
         const int k3x = ink ? (kv == 21 ? 20 : kv == 25 ? 24 : kv) : (kv == 25 ? 25 : 21);
-        ia_launch_k3p(ink ? QTs : xo_QTx, dbp, loc + XOLayout::FRAG, reinterpret_cast<const float4 *>(loc + XOLayout::INFO),
+        {
+            if (ia_launch_k3p(ink ? QTs : xo_QTx, dbp, loc + XOLayout::FRAG, reinterpret_cast<const float4 *>(loc + XOLayout::INFO),
                       mas[i].boxes, mas[i].pos2row, n, 0, sd.M, ink ? Mpj : Mrec, nch, nullptr, nullptr,
                       c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                       c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3x, sd.t,
                       reinterpret_cast<const int *>(loc + XOLayout::ORD), 0, sd.r0, nullptr,
                       reinterpret_cast<const float4 *>(loc + XOLayout::TBOX), c->tnorm.as<float>() + x.t0, c->st, nqb,
-                      Wsh * QTs, &xs, k3_stamp());
+                      Wsh * QTs, &xs, k3_stamp(), c->rec_wt)) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
+          }
         pairs_full += (double)n * Wsh * QTs;
         tiles_full += (double)n * nqb;
         dist_launches++;
         bytes_all_fixed += (double)n * nqb * 32 + (double)Mrec * (16.0 * 16 * g.KS + 48) + (double)Mrec * nch * 24;
+        db_cap_all += (double)n * tile_bytes;
         if (timed) {
           launches_timed++;
           bytes_timed_fixed += (double)n * nqb * 32 + (double)Mrec * (16.0 * 16 * g.KS + 48) + (double)Mrec * nch * 24;
@@ -1508,15 +1530,18 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           if ((n + nch - 1) / nch <= IA_K3P_MAXK_LDS) {
             const int qtb = (qtt + nqb - 1) / nqb;
             const float *tn = c->tnorm.as<float>() + x.t0;
-            ia_launch_k3p(qtb, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, 0, Mt, sd.Mpad, nch,
+            {
+            if (ia_launch_k3p(qtb, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, 0, Mt, sd.Mpad, nch,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t, c->qs_order.as<int>(),
-                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp());
+                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp(), c->rec_wt)) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
+          }
             m.nwg = nch;
             pairs_full += (double)n * qtt;
             tiles_full += (double)n * nqb;
             dist_launches++;
             bytes_all_fixed += (double)n * nqb * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) + (double)Mt * nch * 20;
+            db_cap_all += (double)n * tile_bytes;
             if (timed) {
               launches_timed++;
               bytes_timed_fixed += (double)n * nqb * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) + (double)Mt * nch * 20;
@@ -1529,16 +1554,20 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           const int qt = qtt / nqb + (b < qtt % nqb ? 1 : 0);
           const float *tn = prune ? c->tnorm.as<float>() + x.t0 : nullptr;
           if (prune && presorted)
-            ia_launch_k3p(qt, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
+            {
+            if (ia_launch_k3p(qt, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t,
-                          c->qs_order.as<int>(), 0, sd.r0, nullptr, tboxp, tn, c->st, 1, 0, nullptr, k3_stamp());
+                          c->qs_order.as<int>(), 0, sd.r0, nullptr, tboxp, tn, c->st, 1, 0, nullptr, k3_stamp(), c->rec_wt)) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
+          }
           else if (prune)
-            ia_launch_k3p(qt, dbp, c->qf.p, qinfot, m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
+            {
+            if (ia_launch_k3p(qt, dbp, c->qf.p, qinfot, m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
                           k3v, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
-                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, nullptr, k3_stamp());
+                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, nullptr, k3_stamp(), c->rec_wt)) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
+          }
           else if (use_h)
             ia_launch_k3h(g.KS, qt, dbp, c->qf.p, n, x.tpw, qt0, Mt, x.nwg, m.pos0, g.n_tiles, (float4 *)m.rec,
                           (float *)m.recT, c->k3_variant, c->st);
@@ -1551,7 +1580,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           pairs_full += (double)n * qt;
           tiles_full += (double)n;
           dist_launches++;
-          if (prune) bytes_all_fixed += (double)n * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) + (double)mq * x.nwg * 20;
+          if (prune) {
+            bytes_all_fixed += (double)n * 32 + (double)sd.Mpad * (16.0 * 16 * g.KS + 48) + (double)mq * x.nwg * 20;
+            db_cap_all += (double)n * tile_bytes;
+          }
           if (timed) {
             flops_timed += fl;
             launches_timed++;
@@ -1637,9 +1669,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                               c->st, c->stamp_dur.as<unsigned long long>() + 2 * (k3_n + mg_n));
     ia_launch_stamp_durations(c->stamp_mg.as<unsigned long long>(), (int)mg_n, mg_stride,
                               c->stamp_dur.as<unsigned long long>() + 2 * k3_n, c->st);
-    // clear only the slots this level wrote (the whole buffer was cleared per level)
-    if (k3_n) HIP_TRY(hipMemsetAsync(c->stamp_k3.p, 0, (size_t)k3_n * IA_NWG_H * 16, c->st));
-    if (mg_n) HIP_TRY(hipMemsetAsync(c->stamp_mg.p, 0, (size_t)mg_n * mg_stride * 16, c->st));
+    // (the slots this level wrote are cleared by stamp_clear when the call returns)
   }
   if (stats)
     for (int j = 0; j < J; j++) ia_launch_reduce_stats(jp[j].pstat, NB, c->counters.as<unsigned long long>(), c->st);
@@ -1766,6 +1796,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         stats->k3p_stamp_start_ms = stats->k3p_stamp_wg_ms = stats->stamp_gap_sm_ms = 0.;
         stats->stamp_gaps_sm = 0;
         stats->k3p_stamp_launches = stats->merge_stamp_launches = stats->stamp_gaps = 0;
+        stats->k3p_bytes_unique_all = 0.;
         stats->prune_rows = g.NA;
       }
       prune_acc = true;
@@ -1814,7 +1845,11 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         stats->stamp_gaps_sm += nsm;
         stats->stamp_window_ms += (double)(std::max(sp[2 * k3_n - 1], m[2 * mg_n - 1]) - sp[0]) * 1e-5;
       }
-      stats->k3p_bytes_all += tile_stream_bytes((double)(prs[2] + prs[3]), (double)(ext[0] + ext[1])) + bytes_all_fixed;
+      const double db_stream = tile_stream_bytes((double)(prs[2] + prs[3]), (double)(ext[0] + ext[1]));
+      stats->k3p_bytes_all += db_stream + bytes_all_fixed;
+      // unique DB bytes: a launch reads each tile of its range at most once as
+      // far as the roofline is concerned, however many query blocks stream it
+      stats->k3p_bytes_unique_all += std::min(db_stream, db_cap_all) + bytes_all_fixed;
     }
     if (stride && ns > 0) {
       double tot = 0.;

@@ -320,6 +320,7 @@ struct XOScan {
   unsigned *err;                  // bit 2: a tile flag did not arrive in time
   long long timeout_ticks;
   unsigned long long *stamp;      // option "stamps" (any K3p launch, owner-computes or not): per-WG ticks
+  int rec_wt;                     // option "rec_wt": records stored write-through (sc1), nothing left dirty in L2
 };
 
 // fused K4(t) + K2p(t + 1) (k_merge_gather, option "fuse_gather"): the next step's gather

@@ -36,7 +36,21 @@ __device__ __forceinline__ void ld_hi(h16x8 (&h)[KS], const h16x8 *__restrict__ 
 // consumer waits with an explicit s_waitcnt vmcnt before it reads a slot (ring_wait, which
 // clobbers "memory", so no LDS read is scheduled above it).  The DMAs write LDS only, never a
 // register, so nothing the register allocator does can observe them early.
+//
+// Two rules this asm must keep (both broke once in round 5):
+//  * M0-offset rule: an LDS-DMA's immediate offset is added to the LDS destination (M0) as well
+//    as to the global address.  dma16 therefore takes no offset at all: the piece steps are in
+//    the per-lane global pointer and in lds_addr, and the instruction's offset field is 0 ("off",
+//    no offset:) - a saddr form with the piece steps in the immediate made the slots overlap and
+//    run past the ring (a memory-aperture fault, profiles/r05/saddr/pytest_first_form_fault.log).
+//  * MFMA -> VALU hazard rule: hipcc pads no wait states inside an asm statement, so no asm in this
+//    file reads an MFMA result (a v_min3_f32 in asm on the filter's accumulators read stale values;
+//    the filter's minimum is compiler code, k3p_min16).  The asm v_min / v_med3 of the epilogue
+//    read only packed values built by VALU code from the accumulators (k3h_pack), whose MFMA hazard
+//    the compiler already padded.
+typedef unsigned v4u32 __attribute__((ext_vector_type(4)));  // 16-B buffer store payload
 #define IA_HSLOT 224  // h16x8 per ring slot (3.5 KiB)
+static_assert(3 * 1024 + 512 == IA_HSLOT * 16, "a slot holds pieces 0, 2, 4 (1 KiB each) and the compact piece 6");
 __device__ __forceinline__ void dma16(const void *g, unsigned lds_addr) {
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr), "v"(g) : "memory", "m0");
 }
@@ -278,11 +292,8 @@ __device__ __forceinline__ f32x16 k3p_chain(const h16x8 (&a)[2 * KS], const h16x
 #pragma unroll
   for (int s = 0; s < KS; s++) {
     const h16x8 xh = qb[(2 * s) * IA_WAVE], xl = qb[(2 * s + 1) * IA_WAVE];
-#if !(IA_PROBE & 32)  // PROBE=32 (timing only, results invalid): one f16 product per 16 k, the
-                      // cost of a single-pass f16/bf16 prefilter
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], xh, c, 0, 0, 0);
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], xl, c, 0, 0, 0);
-#endif
     c = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], xh, c, 0, 0, 0);
   }
   return c;
@@ -297,12 +308,10 @@ __device__ __forceinline__ void k3p_chain2(const h16x8 (&a)[2 * KS], const h16x8
   for (int s = 0; s < KS; s++) {
     const h16x8 x0h = qb0[(2 * s) * IA_WAVE], x0l = qb0[(2 * s + 1) * IA_WAVE];
     const h16x8 x1h = qb1[(2 * s) * IA_WAVE], x1l = qb1[(2 * s + 1) * IA_WAVE];
-#if !(IA_PROBE & 32)
     c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x0h, c0, 0, 0, 0);
     c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s + 1], x1h, c1, 0, 0, 0);
     c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0l, c0, 0, 0, 0);
     c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1l, c1, 0, 0, 0);
-#endif
     c0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x0h, c0, 0, 0, 0);
     c1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(a[2 * s], x1h, c1, 0, 0, 0);
   }
@@ -385,12 +394,11 @@ __device__ __forceinline__ float k3p_min16(const f32x16 &c) {
 }
 // HHX = 3 (k3p_variant 22 / 23): the same filter on a hi-only tile buffer (ld_hi); the blocks
 // that pass run their full chains one tile later, from the whole tile loaded only then
-// HO (k3p_variant 24 / 25): the query fragments in LDS are the hi pieces only ([QT][KS][64])
-template <int KS, int QT, int Q, bool HO = false>
+template <int KS, int QT, int Q>
 __device__ __forceinline__ void k3p_hhpipe_h(const h16x8 (&h)[KS], const h16x8 *lq, unsigned msk, float rt,
                                              const float *qzt, const float *qzw, f32x16 (&acc)[2], unsigned &pass) {
   if constexpr (Q <= QT) {
-    constexpr int NP = 2 * KS, QS = HO ? KS : NP, PS = HO ? 1 : 2;
+    constexpr int NP = 2 * KS, QS = NP, PS = 2;
     if constexpr (Q < QT) {
       if ((msk >> Q) & 1u) {
         const h16x8 *qb = lq + Q * QS * IA_WAVE;
@@ -411,12 +419,9 @@ __device__ __forceinline__ void k3p_hhpipe_h(const h16x8 (&h)[KS], const h16x8 *
         pass |= __ballot(k3p_min16(acc[(Q - 1) & 1]) <= lim) != 0ull ? 1u << (Q - 1) : 0u;
       }
     }
-    k3p_hhpipe_h<KS, QT, Q + 1, HO>(h, lq, msk, rt, qzt, qzw, acc, pass);
+    k3p_hhpipe_h<KS, QT, Q + 1>(h, lq, msk, rt, qzt, qzw, acc, pass);
   }
 }
-#ifndef IA_K3P_A1DEF  // k3p_variant 24 / 25: the filter's second accumulator defined by an empty asm
-#define IA_K3P_A1DEF 1 // (0: the compiler zeroes its 16 registers per tile)
-#endif
 // k3p_variant 24 / 25: the same filter walking only the set bits of the need mask (a tile has
 // ≈ 2.7 of 11 blocks needed: the unrolled form spends its scalar instructions testing the other
 // bits).  Blocks in bit order, two accumulators: a block's products are issued before the
@@ -443,10 +448,10 @@ __device__ __forceinline__ unsigned k3p_filter_bits(const h16x8 (&h)[KS], const 
   };
   unsigned pass = 0;
   f32x16 a0, a1;
-#if IA_K3P_A1DEF
-  // a1 is read only after a product wrote it; without a definition here the compiler zeroes it
+  // a1 is read only after a product wrote it; without a definition here the compiler zeroes its
+  // 16 registers at every tile (an empty asm output: no instruction, no hazard - it is never an
+  // MFMA result that an asm statement reads)
   asm volatile("" : "=v"(a1));
-#endif
   int qa = -1, qb = -1;  // the block whose products sit in a0 / a1, its test still due
   for (;;) {
     if (!msk) break;
@@ -648,21 +653,11 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // buffers, software-pipelined single chains, the previous step's order, the rotated-DB head
 // filter - are in the history of this file up to round 3.)
 // ------------------------------------------------------------------------------------------
-#ifndef IA_K3P_ROWS_EARLY  // 1: candidate rows looked up before the subset merge (0: after it)
-#define IA_K3P_ROWS_EARLY 1
-#endif
-#ifndef IA_K3P_TAIL16  // k3p_variant 24 / 25: the subset merge takes every lane's subset (no half-wave merge)
-#define IA_K3P_TAIL16 1
-#endif
-#ifndef IA_K3P_FBITS  // k3p_variant 24 / 25: the stream's filter walks the need mask's set bits (0: unrolled)
-#define IA_K3P_FBITS 1
-#endif
 #define IA_K3P3_MAXQ 512   // queries per step (one per thread)
 // steps of up to IA_K3P_RANK_MAX queries are sorted by rank counting, wider ones by the bitonic
-// network (at 342 queries the network measured faster: profiles/r02/ab3)
-#ifndef IA_K3P_RANK_MAX
+// network (at 342 queries the network measured faster: profiles/r02/ab3, again in round 5:
+// profiles/r05/rank_sort)
 #define IA_K3P_RANK_MAX 256
-#endif
 // PRE (k3p_variant 11, any Mpad <= 4096): the step's queries were sorted once by k_query_sort
 // (ia_prune.hip): qf / qinfo hold them in sorted order (fragments; lo, hi, (U', key) per slot),
 // ord_in maps a sorted slot to its query and tbox holds the sorted query tiles' boxes, so phase
@@ -740,7 +735,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   unsigned *plm = reinterpret_cast<unsigned *>(plk + K);                // HHX 4: [K] their passing blocks
   __shared__ unsigned wpairs[NW], wtiles[NW], wfull[NW], wtp[NW];
   __shared__ int pcount, pctr;  // HHX 4: passing tiles listed / handed out
-  __shared__ int wcnt[NW];
   const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = qt0 * IA_TILE;
@@ -975,7 +969,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       }
     }
   }
-  unsigned long long pa = 0, pb = 0, pc = 0;
+  [[maybe_unused]] unsigned long long pa = 0, pb = 0, pc = 0;  // (phase probe stamps)
   K3P_T(pa);
   __syncthreads();
   K3P_T(pb);
@@ -990,7 +984,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   }
   K3P_T(pc);
   tile_boxes();
-  unsigned long long pd = 0, pe = 0;
+  [[maybe_unused]] unsigned long long pd = 0, pe = 0;
   K3P_T(pd);
   __syncthreads();
   K3P_T(pe);
@@ -1159,13 +1153,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       if (mc) {  // wave-uniform (0: a speculative tile that is not needed)
         h16x8 hc[KS];
         slot_hi(hc, wring + sl * IA_HSLOT, lane);
-#if IA_K3P_FBITS
         const unsigned pass = k3p_filter_bits<KS>(hc, ldsh + lane, mc, wR[kc], qzt + (lane & 31), qzw + (lane & 31));
-#else
-        f32x16 acc[2];
-        unsigned pass = 0;
-        k3p_hhpipe_h<KS, QT, 0, true>(hc, ldsh + lane, mc, wR[kc], qzt + (lane & 31), qzw + (lane & 31), acc, pass);
-#endif
         cnt += __popc(mc);
         if (pass) {  // wave-uniform
           nfull += __popc(pass);
@@ -1194,7 +1182,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       sl = sl == 2 ? 0 : sl + 1;
     }
     ring_wait<0>();   // the DMAs past the last tile land before the ring area is reused
-    unsigned long long pq0 = 0, pq1 = 0, pq2 = 0, pq3 = 0;
+    [[maybe_unused]] unsigned long long pq0 = 0, pq1 = 0, pq2 = 0, pq3 = 0;
     K3P_T(pq0);
     // second pass.  A wave with passing tiles starts on its own first one, whose whole tile is
     // requested now (in flight during the barriers); the list's unmarked entries form a pool
@@ -1366,14 +1354,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   for (int q = 0; q < QT; q++) {  // tile + packed in-tile index -> DB position (-> DB row)
     const int r = (int)(__float_as_uint(b1[q]) & 15u);
     const int pos = i1[q] * IA_TILE + 4 * half + (r & 3) + 8 * (r >> 2);
-#if IA_K3P_ROWS_EARLY
     // the lane's candidate rows are looked up here, their loads in flight while the workgroup
     // waits for its slowest wave and merges; the merge then orders ties by row instead of
     // position (any order is exact: K4 reranks the listed rows and T bounds every other one)
     i1[q] = b1[q] == FLT_MAX ? 0x7fffffff : pos2row[pos];
-#else
-    i1[q] = b1[q] == FLT_MAX ? 0x7fffffff : pos;
-#endif
   }
   }  // HHX != 4
 
@@ -1390,11 +1374,11 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     wtp[wave] = ntp;
   }
   Top2 *red = reinterpret_cast<Top2 *>(ldsh);  // [NW][QT][32], inside the query-fragment area
-  // IA_K3P_TAIL16 (HHX 4): every lane's subset (b1, b2 as T, tile) goes to LDS as it stands
+  // HHX 4: every lane's subset (b1, b2 as T, row) goes to LDS as it stands
   // ([NW][QT][64] per field) and the per-query merge takes 16 subsets: no half-wave merge
   float *rv1 = reinterpret_cast<float *>(ldsh), *rvT = rv1 + NW * QT * IA_WAVE;
   int *ri1 = reinterpret_cast<int *>(rvT + NW * QT * IA_WAVE);
-  constexpr bool T16 = HHX == 4 && IA_K3P_TAIL16;
+  constexpr bool T16 = HHX == 4;
   if constexpr (T16) {
 #pragma unroll
     for (int q = 0; q < QT; q++) {
@@ -1420,6 +1404,10 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   K3P_T(ph[7]);
   __syncthreads();
   K3P_T(ph[8]);
+  // (option "rec_wt") buffer descriptors of the record arrays, from kernel arguments only
+  const int nrec = M * nwg;
+  const __amdgpu_buffer_rsrc_t rrs = __builtin_amdgcn_make_buffer_rsrc(rec, 0, nrec * 16, 0x00020000);
+  const __amdgpu_buffer_rsrc_t trs = __builtin_amdgcn_make_buffer_rsrc(recT, 0, nrec * 4, 0x00020000);
   for (int x = tid; x < NQ; x += WGT) {
     Top2 m;
     if constexpr (T16) {
@@ -1437,12 +1425,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
     const int mq = WGT >= NQ ? mq_pre : (PRE ? (int)skey[x] : order[s0 + x]);
     if (mq < M) {
-#if IA_K3P_ROWS_EARLY
-      const int r1 = m.i1, r2 = m.i2;
-#else
-      const int r1 = m.i1 == 0x7fffffff ? m.i1 : pos2row[m.i1];
-      const int r2 = m.i2 == 0x7fffffff ? m.i2 : pos2row[m.i2];
-#endif
+      const int r1 = m.i1, r2 = m.i2;  // DB rows (looked up before the merge, above)
       const float4 rv = make_float4(m.v1, __int_as_float(r1), m.v2, __int_as_float(r2));
       if (xo.on) {
         // owner-computes sharded step: into the block's owner's area, record w = s nch + wg of
@@ -1456,6 +1439,13 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         __hip_atomic_store(reinterpret_cast<unsigned long long *>(ar + XOLayout::RTS) + ix,
                            ((unsigned long long)xo.seq << 32) | __float_as_uint(m.T), __ATOMIC_RELAXED,
                            __HIP_MEMORY_SCOPE_SYSTEM);
+      } else if (xo.rec_wt) {
+        // option "rec_wt": write-through (sc1) stores, so the kernel boundary finds no partially
+        // dirty record lines in this XCD's L2 to write back; the merge reads them
+        // after the boundary either way
+        const int64_t ix = (int64_t)mq * nwg + wg;
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u32, rv), rrs, (int)(ix * 16), 0, 16);
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(m.T), trs, (int)(ix * 4), 0, 16);
       } else {
         rec[(int64_t)mq * nwg + wg] = rv;
         recT[(int64_t)mq * nwg + wg] = m.T;

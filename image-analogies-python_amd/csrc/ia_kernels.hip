@@ -29,7 +29,7 @@
 #include "ia_prune.h"
 
 #ifndef IA_PROBE
-#define IA_PROBE 0  // diagnostic phase-skipping builds (never set in the product build)
+#define IA_PROBE 0  // diagnostic phase-stamp builds (8: merge, 16: K3p, 256: K2r; never the product build)
 #endif
 // waves (= queries) per workgroup of the one-wave-per-query kernels K2h, K2p, K4: one, so a
 // step's few hundred latency-bound waves spread over as many CUs (their L1, TA and LDS) as
@@ -1875,7 +1875,6 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_level(LevelGeo g, StepDesc s
   if (m >= sd.J * sd.M) return;
   const QPix px = ia_qpix(sd, g.bw, m);
   const JobPtrs jp = jobs.get(px.job);
-#if (IA_PROBE & 3) == 0
   if constexpr (FUSED) {
     __shared__ double qsh[IA_PQ_WPB][Geo<CH>::DS], wsh[IA_PQ_WPB][Geo<CH>::DS];
     __shared__ int crsh[IA_PQ_WPB][IA_WAVE];
@@ -1886,24 +1885,11 @@ __global__ void __launch_bounds__(IA_PQ_WG) k_merge_level(LevelGeo g, StepDesc s
     if (ma.stamp && (threadIdx.x & 63) == 0) ia_stamp_wg(ma.stamp, t0);
     return;
   }
-#endif
   const double *q = ma.q64 + (int64_t)m * Geo<CH>::D;
-#if IA_PROBE & 1  // diagnostic build only: take the first record's candidate, no rerank
-  const Winner wn{0., (int64_t)__float_as_int(ma.rec[(int64_t)m * ma.nwg].y)};
-#else
   unsigned stat = 0;
   const Winner wn = certified_winner(ma, m, [&](int64_t row) {
     return exact_dist_level<CH>(ma.db64, row, q, IMG ? &A : nullptr);
   }, &stat);
-#endif
-#if IA_PROBE & 2  // diagnostic build only: no coherence / kappa
-  if ((threadIdx.x & 63) == 0) {
-    jp.s[2 * px.qi] = (int)(wn.idx / g.aw) % g.ah;
-    jp.s[2 * px.qi + 1] = (int)(wn.idx % g.aw);
-    jp.im[px.qi] = 0;
-  }
-  return;
-#endif
   if constexpr (FUSED) {
     finish_pixel<CH>(g, A, ma.db64, px.r, px.c, wn.idx, q, jp.s, jp.im, jp.Bp, jp.weights, jp.kf, jp.pstat, stat, jp.nn);
   } else {
@@ -2813,11 +2799,11 @@ size_t ia_k3p_lds(int qt, int Mpad) {
   const size_t qfrag = (size_t)qt * 8 * IA_WAVE * 16;  // KS = 4: NP = 8 h16x8 per lane
   return qfrag + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + (size_t)Mpad * 8;
 }
-void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
+int ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
                    const float4 *tbox, const float *tnorm, hipStream_t st, int nqb, int qt_end, const XOScan *xo,
-                   unsigned long long *stamp) {
+                   unsigned long long *stamp, int rec_wt) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
@@ -2853,7 +2839,9 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
     }
   }
   const k3p_fn fn = g4[qt - 1](variant);
-  if (!fn) return;  // (the host accepts only the built variants: ia_set_option)
+  // (the host accepts only the built variants, ia_set_option; a missing instance is an error the
+  // level reports, never a silently skipped scan whose stale records the merge would consume)
+  if (!fn) return -1;  // IA_EINVAL (include/ia.h)
   const bool pre = variant == 21 || variant == 25;
   // nqb > 1 (presorted variants only): one launch of nqb query blocks x nwg DB chunks
   if (!pre && !(xo && xo->on)) nqb = 1;
@@ -2861,7 +2849,9 @@ void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, 
   XOScan x{};  // off unless an owner-computes step passes its exchange
   if (xo) x = *xo;
   x.stamp = stamp;
+  x.rec_wt = rec_wt;
   allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nqb * nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row,
                      NT, qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm, nqb, qt_end, x);
+  return 0;
 }

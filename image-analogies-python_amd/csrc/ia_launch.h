@@ -66,11 +66,12 @@ void ia_launch_query_sort(const float4 *qinfo, const void *qf, int Mpad, int KS,
 void ia_launch_query_sort_xo(const float4 *qinfo, const void *qf, const XOSort &xs, hipStream_t st);
 size_t ia_k3p_lds(int qt, int Mpad);
 void ia_merge_gather_occupancy(int *vgprs, int *blocks_per_cu, int *wg_threads);
-void ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
+// returns IA_EINVAL (nothing launched) when no kernel instance exists for the variant
+int ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, const float4 *boxes, const int *pos2row,
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
                    const float4 *tbox, const float *tnorm, hipStream_t st, int nqb = 1, int qt_end = 0,
-                   const XOScan *xo = nullptr, unsigned long long *stamp = nullptr);
+                   const XOScan *xo = nullptr, unsigned long long *stamp = nullptr, int rec_wt = 0);
 // GPU preprocessing (ia_pyramid.hip)
 void ia_launch_pyramid_reduce(const double *in, double *out, double *tmp, double *sm, double *mm, int h, int w, int ch,
                               const double *w7, hipStream_t st);

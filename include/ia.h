@@ -111,6 +111,9 @@ typedef struct {
   double k3p_stamp_wg_ms;    /* ... their mean workgroup duration (end - start), summed */
   double stamp_gap_sm_ms;   /* the scan end -> merge start part of stamp_gap_ms */
   int64_t stamp_gaps_sm;
+  double k3p_bytes_unique_all; /* k3p_bytes_all with each launch's DB tiles counted at most once
+                                * (<= the launch's whole tiles): launches of several query blocks
+                                * stream a tile once per block (cfg4's wide steps) */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
@@ -203,6 +206,10 @@ int ia_version(void);
  * Fused merge + gather launches (option "fuse_gather") wait row to row; a level uses them only
  * while the chained waves of all levels in flight in the process stay under twice the GPU's
  * resident k_merge_gather waves (else it runs separate launches; ia_capi.cpp g_chain_waves).
+ * "rec_wt" = 0 (default) / 1: the pruned scan stores its per-(query, chunk) records write-through
+ * (sc1 buffer stores), so the scan -> merge kernel boundary has no dirty record lines to write
+ * back (one-rank steps; the owner-computes exchange has its own uncached stores).  Exact either
+ * way: the merge reads the records after the boundary.
  * "stamps" = 1: every pruned-scan and fused-merge launch of a pruned level stamps its
  * workgroups' first / last s_memrealtime tick; ia_stats.k3p_stamp_ms / merge_stamp_ms sum the
  * per-launch device times (bench.py roofline.frac_timed: the timed, pipelined steps' own kernels).

@@ -60,14 +60,37 @@ def _check_blas_order():
 
 # ----------------------------------------------------------------------------- shims
 class _ExactFlann(object):
-    """Stand-in for pyflann.FLANN: exact linear scan, fp64, first-argmin (lowest index)."""
+    """Stand-in for pyflann.FLANN: exact linear scan, fp64, first-argmin (lowest index).
+
+    Large indexes (the g512 case) split the rows over threads: every row's distance is the
+    same numpy expression on the same row ((p - q)**2 summed along the row), and the argmin runs
+    on the concatenation, so the result is the single-threaded one bit for bit."""
+    THREADS = int(os.environ.get('GEN_GOLDEN_THREADS', '1'))
+    _pool = None
 
     def build_index(self, pts, algorithm='kdtree', **kw):
         self.pts = np.ascontiguousarray(pts, dtype=np.float64)
+        n = len(self.pts)
+        t = self.THREADS if n >= 65536 else 1
+        self.cuts = [n * i // t for i in range(t + 1)]
+        self.d = np.empty(n)
+        if t > 1 and _ExactFlann._pool is None:
+            from concurrent.futures import ThreadPoolExecutor
+            _ExactFlann._pool = ThreadPoolExecutor(self.THREADS)
         return {'checks': 32, 'algorithm': algorithm}
 
+    def _part(self, q, a, b):
+        self.d[a:b] = ((self.pts[a:b] - q) ** 2).sum(axis=1)
+
     def nn_index(self, q, num_neighbors=1, checks=32, **kw):
-        d = ((self.pts - np.asarray(q, dtype=np.float64)) ** 2).sum(axis=1)
+        q = np.asarray(q, dtype=np.float64)
+        if len(self.cuts) == 2:
+            d = ((self.pts - q) ** 2).sum(axis=1)
+        else:
+            fs = [self._pool.submit(self._part, q, a, b) for a, b in zip(self.cuts[:-1], self.cuts[1:])]
+            for f in fs:
+                f.result()
+            d = self.d
         i = int(np.argmin(d))
         return np.array([i]), np.array([d[i]])
 
@@ -144,12 +167,29 @@ def blocky(h, w, seed, ch=None):
 
 
 # ----------------------------------------------------------------------------- end to end
+def _sha1(x):
+    import hashlib
+    return hashlib.sha1(np.ascontiguousarray(x, dtype=np.float64).tobytes()).hexdigest()
+
+
 def run_case(mods, name, A, Ap_list, B, convert=False, remap=False, init_rand=True,
-             AB_weight=1, k=0.5, seed=3, lean=False):
+             AB_weight=1, k=0.5, seed=3, lean=False, slim=False, n_levels=None):
     """lean: larger cases keep the fixture small: int32 index arrays, no colour pyramid when it
-    equals the A' pyramid (convert=False), colour output of the finest level only."""
+    equals the A' pyramid (convert=False), colour output of the finest level only.
+    slim (g512): the reference's A / A' / B pyramids, the per-level outputs s (int16) / im
+    (uint8), and the sha1 of every B' initialisation and final B' level - the test rebuilds the
+    seeded B' initialisation with the product's host code (proved equal by the hashes), and
+    compares its own s / im exactly and its B' by hash.  (The pyramids are stored because
+    skimage's least-squares resize transform differs from the product's restatement in the last
+    ulp, test_host_preprocess.py; the B' arrays are A' values at s, so their hashes suffice.)  n_levels: keep the finest n_levels images of every pyramid
+    (the bench's cfg2 shape: 512^2 with 5 levels) by wrapping the reference's
+    compute_gaussian_pyramid (img_preprocess.py:50-65: pyramid_gaussian builds each image from
+    the previous one, so the finest five are the same arrays as in the full pyramid)."""
     config, img_preprocess, algorithms, ia = mods
     import matplotlib.pyplot as plt
+    orig_cgp = ia.compute_gaussian_pyramid
+    if n_levels is not None:
+        ia.compute_gaussian_pyramid = lambda img, m: orig_cgp(img, m)[-n_levels:]
     imgs = {'A': A, 'B': B}
     for j, Ap in enumerate(Ap_list):
         imgs['Ap%d' % j] = Ap
@@ -207,8 +247,33 @@ def run_case(mods, name, A, Ap_list, B, convert=False, remap=False, init_rand=Tr
     shutil.rmtree(tmp)
     ia.img_setup, ia.best_approximate_match = orig_setup, orig_bam
     ia.best_coherence_match, ia.compute_distance = orig_bcm, orig_cd
+    ia.compute_gaussian_pyramid = orig_cgp
 
     L = config.max_levels
+    if slim:
+        out = {'L': L, 'k': k, 'seed': seed, 'weights': config.weights, 'n_ap': len(Ap_list),
+               'n_levels': -1 if n_levels is None else n_levels, 'slim': True,
+               'n_app': len(cap['app'])}
+        sh = {}
+        for l in range(L):
+            out['A_%d' % l] = cap['A_pyr'][l]
+            out['B_%d' % l] = cap['B_pyr'][l]
+            for j, p in enumerate(cap['Ap_pyr']):
+                out['Ap%d_%d' % (j, l)] = p[l]
+            sh['A_%d' % l] = _sha1(cap['A_pyr'][l])
+            sh['B_%d' % l] = _sha1(cap['B_pyr'][l])
+            sh['Bp0_%d' % l] = _sha1(cap['Bp_init'][l])
+            sh['Bp_%d' % l] = _sha1(cap['Bp_live'][l])
+            for j, p in enumerate(cap['Ap_pyr']):
+                sh['Ap%d_%d' % (j, l)] = _sha1(p[l])
+        out['sha1_keys'] = np.array(sorted(sh))
+        out['sha1_vals'] = np.array([sh[x] for x in sorted(sh)])
+        for l, (s, im) in zip(range(1, L), cap['s'].values()):
+            out['s_%d' % l] = np.array([np.asarray(p, dtype=np.int64) for p in s]).reshape(-1, 2).astype(np.int16)
+            out['im_%d' % l] = np.array(im, dtype=np.uint8)
+        np.savez_compressed(os.path.join(OUT, 'e2e_%s.npz' % name), **out)
+        print('case %-10s L=%d levels, %d px synthesised (slim)' % (name, L, len(cap['app'])))
+        return
     ity = np.int32 if lean else np.int64
     out = {'A': A, 'B': B, 'Ap': np.stack(Ap_list), 'L': L, 'convert': convert, 'remap': remap,
            'init_rand': init_rand, 'AB_weight': AB_weight, 'k': k, 'seed': seed,
@@ -257,6 +322,14 @@ def big_cases(mods, names):
                                 smooth(96, 96, 2, 19), k=25.0, seed=6, lean=True),
         'g256': lambda: run_case(mods, 'g256', smooth(256, 256, 2, 1), [filt(smooth(256, 256, 2, 1))],
                                  smooth(256, 256, 2, 2), seed=3, lean=True),
+        # round 6: BASELINE config 2's shape, the size at which the product's
+        # default path prunes (512^2 DB rows >= prune_min_rows): 512^2, the finest 5 pyramid
+        # levels, slim fixture.  ~1.5-2.5 h of container CPU with GEN_GOLDEN_THREADS=6.
+        'g512': lambda: run_case(mods, 'g512', smooth(512, 512, 2, 1), [filt(smooth(512, 512, 2, 1))],
+                                 smooth(512, 512, 2, 2), seed=3, slim=True, n_levels=5),
+        # check of the slim writer and the level cap against e2e_g64 (not committed)
+        'g64slim': lambda: run_case(mods, 'g64slim', smooth(64, 64, 2, 1), [filt(smooth(64, 64, 2, 1))],
+                                    smooth(64, 64, 2, 2), seed=3, slim=True, n_levels=4),
     }
     for n in names:
         todo[n]()
