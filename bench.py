@@ -150,12 +150,20 @@ class HostCopy(object):
         return sum(t.numel() * t.element_size() for t in self.dev)
 
     def digest(self):
+        return self.digest_groups([len(self.host)])[0]
+
+    def digest_groups(self, sizes):
+        """one sha1 per group of consecutive buffers (cfg5: one per job)"""
         import hashlib
         self.torch.cuda.synchronize()
-        hs = hashlib.sha1()
-        for h in self.host:
-            hs.update(h.numpy().tobytes())
-        return hs.hexdigest()
+        out, i = [], 0
+        for n in sizes:
+            hs = hashlib.sha1()
+            for h in self.host[i:i + n]:
+                hs.update(h.numpy().tobytes())
+            out.append(hs.hexdigest())
+            i += n
+        return out
 
 
 EXCHANGE = {'rccl': 0, 'peer': 1, 'owner': 2}   # include/ia.h option "exchange"
@@ -668,7 +676,19 @@ def main():
     # must equal, bit for bit, a one-stream sequential run of the same job - the roofline pass
     # below when the timed steps ran concurrently (pipelined levels, several cfg5 streams), else
     # one extra run
-    h_timed = hc.digest() if world == 1 else None
+    # (cfg5 at any N: the rank's own jobs, also one sha1 per job - job_digests in the line, gathered
+    # over the ranks, so a 2-rank sweep can be compared job by job with a one-GPU run)
+    self_check = world == 1 or sw is not None
+    h_timed = hc.digest() if self_check else None
+    job_digests = None
+    if sw is not None:
+        dg = dict(zip(mine, hc.digest_groups([3 * (sw.L[j] - 1) for j in mine])))
+        if dist:
+            allg = [None] * world
+            dist.all_gather_object(allg, dg)   # host objects only: no collective on the data path
+            for x in allg:
+                dg.update(x)
+        job_digests = {str(j): dg[j] for j in sorted(dg)}
     dj1 = h_shard = None
     if world > 1 and args.mode == 'shard':
         # this rank's own job (owner mode: job `rank`; every rank holds every job otherwise: job
@@ -681,12 +701,16 @@ def main():
         _, stats_rl = timed(1, lambda st: run(st, [ctx]), True)
     else:
         stats_rl = stats
-        if world == 1:
+        if self_check:
             run(_native.Stats(), [ctx])
     parity = None
-    if world == 1:
+    if self_check:
         hc.fetch()
         parity = hc.digest() == h_timed
+        if dist:
+            pp = [None] * world
+            dist.all_gather_object(pp, parity)
+            parity = all(pp)
         log('[bench] timed run %s the one-stream sequential run (sha1 of B\', s, im of every level)'
             % ('equals' if parity else 'DIFFERS FROM'))
     value_replicas = value_strong = shard_parity = strong_parity = None
@@ -951,6 +975,8 @@ def main():
         out['value_replicas'] = value_replicas
         out['config']['replicas'] = ('value_replicas = %d independent cfg jobs, one per GPU, no collective '
                                      '(B\' px/s aggregate)' % world)
+    if job_digests is not None:
+        out['job_digests'] = job_digests
     if parity is not None:
         out['parity'] = parity
         out['config']['parity'] = ("sha1 of the last timed step's fetched B', s, im (every level) == a one-stream "

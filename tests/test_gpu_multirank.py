@@ -57,3 +57,35 @@ def test_two_ranks_bit_exact_to_single_gpu(config, exchange, tmp_path):
     assert line['config']['jobs_per_step'] == 1 and line['config']['parallelism'].endswith('_jobs1')
     assert line['value_weak'] > 0 and line['config']['weak']['scaling'] == 'weak'
     assert line['stats']['bound_violations'] == 0 and line['stats']['kappa_ambiguous'] == 0
+
+
+def _bench(args, env, port=None, nproc=1, timeout=600):
+    if nproc > 1:
+        cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', '--nproc-per-node', str(nproc),
+               '--master-addr', '127.0.0.1', '--master-port', str(port), os.path.join(ROOT, 'bench.py')]
+    else:
+        cmd = [sys.executable, os.path.join(ROOT, 'bench.py')]
+    r = subprocess.run(cmd + args, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, timeout=timeout)
+    assert r.returncode == 0, r.stderr.decode()[-3000:]
+    return json.loads(r.stdout.decode().strip().splitlines()[-1])
+
+
+def test_cfg5_sweep_two_ranks_equal_one_gpu(tmp_path):
+    """BASELINE config 5 on two ranks: the 64-job sweep split job j -> rank
+    j mod 2 with no collective on the data path.  Every job's B', s, im (every level; bench.py
+    job_digests, one sha1 per job, gathered over the ranks as host objects) must equal the same
+    job of a one-GPU run of the whole sweep, and each rank's timed run must equal its own one-stream
+    rerun (parity)."""
+    mode = _ranks_available()
+    if mode is None:
+        pytest.skip('needs 2 GPUs (or IA_TEST_SHARE_GPU=1 for the one-GPU rehearsal)')
+    env = dict(os.environ)
+    common = ['--steps', '1', '--warmup', '1', '--no-cpu-baseline', '--no-replicas-extra', '--config', 'cfg5']
+    one = _bench(['--gpus', '1'] + common, env)
+    if mode == 'share':
+        env.update(IA_BENCH_SHARE_GPU='1', IA_BENCH_BACKEND='gloo')
+    two = _bench(['--gpus', '2'] + common, env, port=29641, nproc=2)
+    assert one['parity'] is True and two['parity'] is True
+    assert len(one['job_digests']) == 64 and two['job_digests'] == one['job_digests']
+    assert two['n_gpus'] == 2 and two['config']['parallelism'] == 'jobs2'
+    assert two['stats']['bound_violations'] == 0 and two['stats']['kappa_ambiguous'] == 0

@@ -11,7 +11,7 @@ bit-identical, and the kappa test's weighted distances follow the golden host's 
 import numpy as np
 import pytest
 
-from golden_util import BIG_CASES, E2E_CASES, load_e2e
+from golden_util import BIG_CASES, E2E_CASES, SLIM_CASES, load_e2e
 
 pytestmark = pytest.mark.gpu
 
@@ -112,3 +112,31 @@ def test_exact_index_ties_lowest_index(ctx):
     for j in range(len(q)):
         dd = ((pts - q[j]) ** 2).sum(axis=1)
         assert i_gpu[j] == int(np.argmin(dd))
+
+
+@pytest.mark.parametrize('name', SLIM_CASES)
+def test_slim_reference_runs_with_product_defaults(ctx, name):
+    """Reference runs in 'slim' fixtures (oracle/gen_golden.py run_case slim=True): g512 is
+    BASELINE config 2's shape (512^2, the finest 5 pyramid levels), where the product's default
+    path runs the certified pruned scan on the 512^2 level (262,144 DB rows >= the bench's
+    prune_min_rows) -
+    the bench's dominant kernel pinned end to end to the reference; g64slim
+    checks the slim writer and the level cap on a 4-level 64^2 run.  Every level's s and im must
+    equal the reference's exactly, and every B' level its sha1."""
+    from golden_util import load_slim, sha1_f64
+    z = load_slim(name)
+    Bp = [x.copy() for x in z['Bp_init']]
+    # the bench's setting for every configuration whose 512^2 levels it runs (cfg3 pipelined, cfg4,
+    # cfg5: bench.py --prune-min-rows 262144), so the 512^2 level runs the pruned scan K3p
+    ctx.set_option('prune_min_rows', 262144)
+    try:
+        out, st = _run_levels(ctx, z, Bp)
+    finally:
+        ctx.set_option('prune_min_rows', 524288)
+    for level, (s, im) in out.items():
+        assert np.array_equal(s, z['s'][level]), 'level %d source map differs' % level
+        assert np.array_equal(im, z['im'][level]), 'level %d image map differs' % level
+        assert sha1_f64(Bp[level]) == z['sha1']['Bp_%d' % level], 'level %d B\' differs' % level
+    assert st.bound_violations == 0 and st.kappa_ambiguous == 0
+    if name == 'g512':
+        assert st.pruned_levels >= 1, 'the 512^2 level must run the pruned scan under the product defaults'

@@ -112,3 +112,18 @@ def test_libm_pow_square_differs_from_product_only_near_midpoints():
         n_diff += p != h
     assert n_diff > 0   # the effect is real (about 1 in 1000) ...
     assert n_diff < 1000
+
+
+def test_oracle_reproduces_slim_reference_run():
+    """The slim fixture format (oracle/gen_golden.py run_case slim=True, the g512 case's format)
+    on its 64^2 / 4-level check case: the reference's pyramids, the product's seeded B' init
+    (hash-checked by load_slim), and the oracle's s / im / B' equal to the reference's."""
+    from golden_util import load_slim, sha1_f64
+    from oracle import ia_oracle as O
+    z = load_slim('g64slim')
+    Bp = [x.copy() for x in z['Bp_init']]
+    S, IM = O.run_all_levels(z['A_pyr'], z['Ap_pyr'], z['B_pyr'], Bp, z['k'], z['weights'])
+    for level in range(1, z['L']):
+        assert np.array_equal(S[level], z['s'][level])
+        assert np.array_equal(IM[level], z['im'][level])
+        assert sha1_f64(Bp[level]) == z['sha1']['Bp_%d' % level]
