@@ -284,8 +284,8 @@ def make_context(args, local):
         cx.set_option('fuse_sort', args.fuse_sort)
     if not args.prefetch_next:
         cx.set_option('prefetch_next', 0)
-    if args.rec_wt:
-        cx.set_option('rec_wt', 1)
+    cx.set_option('rec_wt', args.rec_wt)
+    cx.set_option('early_gather', args.early_gather)
     if not args.nn_bound:
         cx.set_option('nn_bound', 0)
     if args.shard_unpruned:
@@ -407,9 +407,12 @@ def main():
     ap.add_argument('--nn-bound', type=int, default=1, choices=[0, 1],
                     help='1 (default): the pruned levels\' gathers also bound U\' by the causal neighbours\' exact NN rows '
                          '(include/ia.h option nn_bound)')
-    ap.add_argument('--rec-wt', type=int, default=0, choices=[0, 1],
-                    help='1: the pruned scan stores its records write-through (sc1), so the scan -> merge kernel '
+    ap.add_argument('--rec-wt', type=int, default=1, choices=[0, 1],
+                    help='1 (default): the pruned scan stores its records write-through (sc1), so the scan -> merge kernel '
                          'boundary finds no dirty record lines in L2 (include/ia.h option rec_wt, DESIGN.md §6e)')
+    ap.add_argument('--early-gather', type=int, default=1, choices=[0, 1],
+                    help='1 (default): a fused merge wave runs its next query\'s gather up to the row above\'s feature before '
+                         'waiting for that handoff (include/ia.h option early_gather, DESIGN.md §6f)')
     ap.add_argument('--prefetch-next', type=int, default=1, choices=[0, 1],
                     help='1 (default): fused merge + gather waves load the next query\'s step-independent inputs during '
                          'the merge (include/ia.h option prefetch_next)')

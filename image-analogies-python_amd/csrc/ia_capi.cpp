@@ -143,6 +143,7 @@ struct ia_ctx {
   HandSlot *hand = nullptr;      // its per-row handoff slots (uncached)
   int hand_rows = 0;
   int prefetch_next = 1;         // option "prefetch_next" (NextStep::prefetch)
+  int early_gather = 1;          // option "early_gather" (NextStep::early)
   int nn_bound = 1;              // option "nn_bound" (JobPtrs::nn): the pruned one-rank levels' gathers also
                                  // bound U' by the causal neighbours' exact NN rows, shifted
   int fuse_sort = 0;             // option "fuse_sort": the fused gathers of step t + 1 also sort it (NextStep::kslot);
@@ -156,7 +157,7 @@ struct ia_ctx {
   // per-step K3 timing (optional)
   int time_dist = 0;
   int stamps = 0;                 // option "stamps": per-launch device time from kernel stamps
-  int rec_wt = 0;                 // option "rec_wt": K3p records stored write-through
+  int rec_wt = 1;                 // option "rec_wt": K3p records stored write-through
   DevBuf stamp_k3, stamp_mg, stamp_dur;
   std::vector<hipEvent_t> evs, evg, evm;  // sampled steps: K3, K2 and K4 brackets
   hipEvent_t lv0 = nullptr, lv1 = nullptr, lv2 = nullptr;
@@ -464,6 +465,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!std::strcmp(name, "nn_bound")) {
     if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: nn_bound must be 0 or 1");
     c->nn_bound = value;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "early_gather")) {
+    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: early_gather must be 0 or 1");
+    c->early_gather = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "prefetch_next")) {
@@ -1459,6 +1465,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         nx.err = c->xerr.as<unsigned>();
         nx.timeout_ticks = 2000000000LL;
         nx.prefetch = c->prefetch_next;
+        nx.early = c->early_gather;
         if (ink_n) {  // the next step's queries go straight to every rank's area (else its K2s sorts them)
           nx.xp.W = sharded ? Wsh : 1;
           for (int p = 0; p < nx.xp.W; p++) nx.xp.area[p] = area_s(p, seq + 1);
@@ -1616,6 +1623,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       nx.err = c->xerr.as<unsigned>();
       nx.timeout_ticks = 2000000000LL;  // 20 s of the 100 MHz s_memrealtime clock
       nx.prefetch = c->prefetch_next;
+      nx.early = c->early_gather;
       // the gathers also sort step t + 1 into k_query_sort's outputs when every wave of the launch
       // can be resident at once (each gather waits for all of the step's keys): k_merge_gather
       // holds one wave per SIMD (264 VGPRs), 1,024 on the chip; 768 leaves room for the kernels of
@@ -1802,6 +1810,20 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       prune_acc = true;
     }
     if (stamped && prune_acc && k3_n + mg_n > 0) {
+      if (const char *dp = std::getenv("IA_STAMP_DUMP")) {
+        // diagnostic: the raw per-workgroup stamps of this level's launches (K3p: IA_NWG_H slots
+        // per launch, merges: mg_stride slots; (start | 1, end) ticks of 100 MHz) appended to a file
+        std::vector<unsigned long long> r3((size_t)k3_n * IA_NWG_H * 2), rm((size_t)mg_n * mg_stride * 2);
+        HIP_TRY(hipMemcpy(r3.data(), c->stamp_k3.p, r3.size() * 8, hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(rm.data(), c->stamp_mg.p, rm.size() * 8, hipMemcpyDeviceToHost));
+        if (FILE *f = std::fopen(dp, "ab")) {
+          const int64_t hdr[4] = {k3_n, IA_NWG_H, mg_n, mg_stride};
+          std::fwrite(hdr, 8, 4, f);
+          std::fwrite(r3.data(), 8, r3.size(), f);
+          std::fwrite(rm.data(), 8, rm.size(), f);
+          std::fclose(f);
+        }
+      }
       std::vector<unsigned long long> sp((size_t)2 * (k3_n + mg_n));  // (start, end) per launch: K3p, then merges
       HIP_TRY(hipMemcpy(sp.data(), c->stamp_dur.p, sp.size() * 8, hipMemcpyDeviceToHost));
       double tk = 0., tm = 0.;

@@ -355,6 +355,8 @@ struct NextStep {
   // per-workgroup sort (kslot = nullptr: off)
   unsigned long long *kslot;
   int prefetch;              // option "prefetch_next": the gathers' step-independent inputs load during the merge
+  int early;                 // option "early_gather": the merge waves' gathers run everything but the row
+                             // above's feature before its handoff (ia_kernels.hip gather_p_early)
   int *sorder;
   float4 *sinfo;
   void *sfrag;

@@ -52,7 +52,11 @@ typedef unsigned v4u32 __attribute__((ext_vector_type(4)));  // 16-B buffer stor
 #define IA_HSLOT 224  // h16x8 per ring slot (3.5 KiB)
 static_assert(3 * 1024 + 512 == IA_HSLOT * 16, "a slot holds pieces 0, 2, 4 (1 KiB each) and the compact piece 6");
 __device__ __forceinline__ void dma16(const void *g, unsigned lds_addr) {
+#ifdef IA_EXP_DMA_NT  // experiment: the hi stream's DMAs with the non-temporal policy
+  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(lds_addr), "v"(g) : "memory", "m0");
+#else
   asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(lds_addr), "v"(g) : "memory", "m0");
+#endif
 }
 template <int KS>
 __device__ __forceinline__ void dma_hi(const h16x8 *__restrict__ db, int64_t tile, h16x8 *slot, int lane) {
@@ -738,7 +742,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int s0 = qt0 * IA_TILE;
-  unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
+  [[maybe_unused]] unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   K3P_T(ph[0]);
   const unsigned long long stamp0 = xo.stamp ? ia_clock() : 0ull;
 

@@ -1197,6 +1197,10 @@ __device__ __forceinline__ float wave_min_f_x(float v) {
   if constexpr (STEP < 6) return wave_min_f_x<STEP + 1>(fminf(v, lane_xchg_f<STEP>(v)));
   else return v;
 }
+// v of lane l (wave-uniform l): two v_readlane, no LDS crossbar (a __shfl is a ds_bpermute)
+__device__ __forceinline__ double readlane_d(double v, int l) {
+  return __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(v), l), __builtin_amdgcn_readlane(__double2loint(v), l));
+}
 __device__ __forceinline__ int lane_prefix(unsigned long long bal) {  // set bits of bal below this lane
   return __builtin_amdgcn_mbcnt_hi((unsigned)(bal >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)bal, 0u));
 }
@@ -1379,8 +1383,15 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
                                                const double *__restrict__ db64, const double *__restrict__ basis, double ufac,
                                                float4 *__restrict__ qinfo, const Imgs &A, double *qsh, _Float16 *xh0,
                                                _Float16 *xh1, const QHand &h, float4 &o0, float4 &o1, float4 &o2,
-                                               const QPre &pf = QPre{}) {
+                                               const QPre &pf = QPre{}, unsigned long long *gst = nullptr) {
   constexpr int D = 55, KD = 16 * KS;
+#if IA_PROBE & 8
+#define IA_GST(k) do { if (gst) { __builtin_amdgcn_s_waitcnt(0); __builtin_amdgcn_sched_barrier(0); \
+                       gst[k] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } } while (0)
+#else
+#define IA_GST(k) do { (void)gst; } while (0)
+#endif
+  IA_GST(0);
   static_assert(KD <= IA_WAVE, "one feature per lane");
   const QPix px = ia_qpix(sd, g.bw, m);
   const int32_t *__restrict__ s = jp.s, *__restrict__ im = jp.im;
@@ -1395,7 +1406,12 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
   if (qi > 0 && (lane < 15 || nnl)) {
     const int k = lane < 15 ? lane : lane - 15;
     const int nr = r - 2 + k / 5, nc = c - 2 + k % 5;
-    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi) {
+#ifdef IA_EXP_NOABOVE  // experiment: U' without the row-above step-t neighbour's candidates
+    const bool skip_above = FUSE && nr == h.r1 && nc == h.c1;
+#else
+    const bool skip_above = false;
+#endif
+    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi && !skip_above) {
       const int nb = nr * g.bw + nc;
       int sr = 0, sc = 0, si = 0, nnrow = -1;
       if (!nnl) {
@@ -1445,13 +1461,16 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
       if (xh0) split_h(f == D ? IA_NORM_SCALE : 0., xh0[f], xh1[f]);
     }
   }
+  IA_GST(1);
   ss = wave_sum_d(ss);
 #pragma unroll
   for (int i = 0; i < IA_NPC; i++) p[i] = wave_sum_d_x(p[i]);
+  IA_GST(2);
   __builtin_amdgcn_wave_barrier();  // qsh written by this wave's lanes, read below
   double u = DBL_MAX;
   if (crow >= 0) u = exact_dist_level<1>(db64, crow, qsh, IMG ? &A : nullptr);
   u = wave_min_d_x(u);
+  IA_GST(3);
   // the pruning record (uniform values): projection interval, U' and the Morton key, and K3p's
   // hi x hi block filter bound (k3p_variant 14/15, ia_k3h.hip k3p_filtered): value bound
   // z >= U' - |q'|^2 with the f32 rounding of z and of the kernel's lim = z + R_t (...)
@@ -1474,6 +1493,8 @@ __device__ __forceinline__ void gather_p_query(const LevelGeo &g, const StepDesc
     qinfo[3 * m + 1] = o1;
     qinfo[3 * m + 2] = o2;
   }
+  IA_GST(4);
+#undef IA_GST
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1695,18 +1716,30 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
     n_over++;
   }
   if (__ballot(n_over > 0)) recompute_app = true;
-  // NN winner (lowest index on ties) and coherence winner (first argmin of the norm) together
-  double dk = (lane < NCOH && my_row >= 0) ? cr_sqrt(unw) : DBL_MAX;
-  int kk = (lane < NCOH && my_row >= 0) ? lane : INT_MAX;
-  double bd = nd;
-  int bi = ni;
-  wave_min2_di(bd, bi, dk, kk);
+  // NN winner (lowest index on ties) and coherence winner (first argmin of the norm): the two
+  // minima by interleaved DPP butterflies, then the lanes that hold them by ballot (a tie in the
+  // NN distance between lanes - exact duplicate rows - takes the lowest row by a third butterfly)
+  const double dkl = (lane < NCOH && my_row >= 0) ? cr_sqrt(unw) : DBL_MAX;
+  const double bd0 = wave_min_d_x(nd), dk = wave_min_d_x(dkl);
+  double bd = bd0;
+  int bi = INT_MAX;
+  if (bd0 < DBL_MAX) {
+    const unsigned long long eqn = __ballot(nd == bd0);
+    bi = __builtin_amdgcn_readlane(ni, __ffsll((long long)eqn) - 1);
+    if (eqn & (eqn - 1)) {  // (wave-uniform, rare) several lanes at the same distance
+      int x = nd == bd0 ? ni : INT_MAX;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) x = min(x, __shfl_xor(x, o, 64));
+      bi = x;
+    }
+  }
+  const int kk = dk < DBL_MAX ? __ffsll((long long)__ballot(dkl == dk)) - 1 : INT_MAX;
   const unsigned long long own = __ballot(lane >= NCOH && my_row >= 0 && my_row == bi && unw == bd);
   double wsq_app = 0.;
   int app_lane = 0;
   if (own) {
     app_lane = __ffsll((long long)own) - 1;
-    wsq_app = __shfl(wsq, app_lane, 64);
+    wsq_app = readlane_d(wsq, app_lane);
   } else {
     recompute_app = true;
   }
@@ -1776,6 +1809,8 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
       double du = DBL_MAX;
       int iu = INT_MAX;
       wave_min2_di(cd, ci, du, iu);
+      (void)du;
+      (void)iu;
       if (cd < bd || (cd == bd && ci < bi)) {
         bd = cd;
         bi = ci;
@@ -1795,12 +1830,13 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   bool coh_won = false;
   int src_lane = recompute_app ? -1 : app_lane;  // lane holding the chosen row's A' value
   if (kk != INT_MAX) {  // a coherence candidate exists (never for the level's first pixel)
+    // (ds_bpermute here: v_readlane at kk measured 0.25 us slower per launch, profiles/r06/trims)
     const int kpr = __shfl(cpr, kk, 64), kpc = __shfl(cpc, kk, 64), kim = __shfl(cim, kk, 64);
     const double wsq_coh = __shfl(wsq, kk, 64);
     if (recompute_app) {
       double u, wq = 0.;
       if (lane == 0) row_dists<CH>(a.db64, bi, qs, ws, u, wq, IMG ? &A : nullptr);
-      wsq_app = __shfl(wq, 0, 64);
+      wsq_app = readlane_d(wq, 0);
     }
     // compute_distance = norm(x)**2 = sqrt(sum x^2)**2 ; kappa rule image_analogies.py:206
     const double y_app = cr_sqrt(wsq_app), y_coh = cr_sqrt(wsq_coh);
@@ -1819,7 +1855,7 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   IA_STAMP(6);
   double val[CH];
 #pragma unroll
-  for (int k = 0; k < CH; k++) val[k] = src_lane >= 0 ? __shfl(av[k], src_lane, 64) : 0.;
+  for (int k = 0; k < CH; k++) val[k] = src_lane >= 0 ? readlane_d(av[k], src_lane) : 0.;
   if (src_lane < 0) {  // winner from an overflow candidate or a rescan: fetch its A' value
 #pragma unroll
     for (int k = 0; k < CH; k++) val[k] = A.p3[img * A.img_stride_f + ((int64_t)pr * g.aw + pc) * CH + k];
@@ -1945,6 +1981,190 @@ __device__ __forceinline__ void gather_h_query_fused(const LevelGeo &g, const St
   if (lane == 0) qn2[m] = ss;
 }
 
+// Per-level constants of the fused gather (lane f < 55: its feature's basis column and part mean;
+// the key scale), loaded at wave start so no dependent load of them sits behind the handoff.
+struct QConst {
+  double bas[IA_NPC] = {0., 0., 0., 0.};
+  double mu = 0.;
+  double sc[IA_NPC] = {0., 0., 0., 0.};
+};
+__device__ __forceinline__ QConst qconst_load(const NextStep &nx, int lane) {
+  constexpr int D = 55;
+  QConst k;
+  if (lane < D) {
+#pragma unroll
+    for (int i = 0; i < IA_NPC; i++) k.bas[i] = nx.basis[i * D + lane];
+    k.mu = nx.mu[feat_part<1>(lane)];
+  }
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) k.sc[i] = nx.basis[IA_NPC * D + i];
+  return k;
+}
+
+// The fused gather of query mn (step t + 1) for a merge wave of a one-rank pruned level (option
+// "prefetch_next"; no publish): everything that does not depend on the row above's step-t result
+// runs BEFORE the wait for its handoff - the query's other 54 features (q64, split-f16 fragments,
+// projections, |q'|^2 as sums over those lanes) and U': the exact distance of each candidate row
+// over those features, the rows requested first so their loads are in flight during the feature
+// work.  After the handoff only the late feature (the row above's pixel (r - 1, c + 2) of the
+// query's window) is added to each sum.  U' skips the row above's own two candidates (its source
+// pixel and NN row, shifted): any DB row's exact distance bounds the NN distance from above, so U'
+// stays a valid bound (the scan's passing tiles 0.144 -> 0.147); the summation
+// orders of U', |q'|^2 and the projections differ from K2p's, which the bounds' margins cover
+// (the NN decisions are the merge's fp64 reranks, unchanged).
+template <int KS>
+__device__ __forceinline__ void gather_p_early(const LevelGeo &g, const NextStep &nx, const Imgs &B, const JobPtrs &jp,
+                                               int job, int mn, int lane, const double *__restrict__ db64, double *qsh,
+                                               const QHand &h0, const QPre &pf, const QConst &qk) {
+  constexpr int D = 55, KD = 16 * KS, DS = Geo<1>::DS;
+  static_assert(KD <= IA_WAVE, "one feature per lane");
+#if IA_PROBE & 8
+  unsigned long long gst[7] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0, 0, 0};
+  const bool gprobe = mn == nx.sn.M / 2 && (nx.sn.t % 256) == 129;
+#define IA_GST2(k) do { if (gprobe) { __builtin_amdgcn_s_waitcnt(0); __builtin_amdgcn_sched_barrier(0); \
+                        gst[k] = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } } while (0)
+#else
+#define IA_GST2(k) do { } while (0)
+#endif
+  const StepDesc &sn = nx.sn;
+  const QPix pn = ia_qpix(sn, g.bw, mn);
+  const int r = pn.r, c = pn.c, qi = pn.qi;
+  // the row above's step-t pixel: its result arrives through the handoff slot of row r - 1
+  const bool above = r >= 1 && c + 2 < g.bw;
+  const int ar = r - 1, ac = c + 2;
+  // ---- features (lane f < 55): the prefetched value, this wave's own result substituted
+  double v = 0.;
+  bool late = false;
+  if (lane < D) {
+    v = pf.v;
+    if (lane >= 43) {
+      const int k = lane - 43, y = ia_reflect(r + k / 5 - 2, B.h), x = ia_reflect(c + k % 5 - 2, B.w);
+      if (y == h0.r0 && x == h0.c0) v = h0.v0;
+      late = above && y == ar && x == ac;
+    }
+  }
+  // (the late pixel can fill several window slots where the window is reflected at the image's
+  // top or sides: up to four of the twelve B' slots 43..54)
+  const unsigned long long lm = __ballot(late);
+  // ---- U' candidate rows: lanes 0..14 the causal neighbours' shifted sources, 15..29 (option
+  // "nn_bound") their shifted NN rows; the row above's pixel skipped (its result is late)
+  int crow = -1;
+  const bool nnl = jp.nn && lane >= 15 && lane < 30;
+  if (qi > 0 && (lane < 15 || nnl)) {
+    const int k = lane < 15 ? lane : lane - 15;
+    const int nr = r - 2 + k / 5, nc = c - 2 + k % 5;
+    if (nr >= 0 && nc >= 0 && nc < g.bw && nr * g.bw + nc < qi && !(above && nr == ar && nc == ac)) {
+      const bool own = nr == h0.r0 && nc == h0.c0;
+      const int sr = own ? h0.s0r : pf.sr, sc = own ? h0.s0c : pf.sc, si = own ? h0.i0 : pf.si;
+      const int nnrow = own ? h0.n0 : pf.nn;
+      crow = ucand_row(g, r, c, nr, nc, nnl, sr, sc, si, nnrow);
+    }
+  }
+  // the candidate row, requested now (in flight during the feature work below)
+  double2 rowv[DS / 2];
+  {
+    const double2 *src = reinterpret_cast<const double2 *>(db64 + (int64_t)(crow >= 0 ? crow : 0) * DS);
+#pragma unroll
+    for (int i = 0; i < DS / 2; i++) rowv[i] = src[i];
+  }
+  if (lane < D) qsh[lane] = late ? 0. : v;
+  // ---- the non-late features: q64, fragments, projections, |q'|^2 (late lanes hold 0)
+  double ss = 0., p[IA_NPC] = {0., 0., 0., 0.}, qc = 0.;
+  if (lane < KD) {
+    if (lane < D) {
+      if (!late) {
+        nx.q64[(int64_t)mn * D + lane] = v;
+        qc = v - qk.mu;
+        ss = qc * qc;
+        put_qh<KS>((_Float16 *)nx.qf, mn, lane, -2.0 * qc);
+#pragma unroll
+        for (int i = 0; i < IA_NPC; i++) p[i] = qk.bas[i] * qc;
+      }
+    } else {
+      put_qh<KS>((_Float16 *)nx.qf, mn, lane, lane == D ? IA_NORM_SCALE : 0.);
+    }
+  }
+  ss = wave_sum_d_x(ss);
+#pragma unroll
+  for (int i = 0; i < IA_NPC; i++) p[i] = wave_sum_d_x(p[i]);
+  IA_GST2(1);
+  __builtin_amdgcn_wave_barrier();  // qsh written by this wave's lanes, read below
+  // ---- U' partial distances over the non-late features (pairwise order; a late feature adds 0)
+  const double *rv = reinterpret_cast<const double *>(rowv);
+  double part = pw_sum<D>([&](int f) {
+    const double d = rv[f] - qsh[f];
+    return ((lm >> f) & 1ull) ? 0. : d * d;
+  });
+  double al[12];  // the row's values at the B' slots (read after the handoff for the late ones)
+#pragma unroll
+  for (int k = 0; k < 12; k++) al[k] = rv[43 + k];
+  IA_GST2(2);
+  // ---- the row above's result (handoff)
+  QHand h = h0;
+  if (above) {
+    const HandSlot *hs = nx.hand + (int64_t)job * g.bh + ar;
+    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(&hs->seq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != nx.seq) {
+      if ((long long)__builtin_amdgcn_s_memrealtime() - t0 > nx.timeout_ticks) {
+        atomicOr(nx.err, 16u);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    h.v1 = hs->v;
+  }
+  IA_GST2(3);
+  // ---- the late slots: their value, fragments and terms, in slot order
+  if (lm) {
+    if (late) {
+      nx.q64[(int64_t)mn * D + lane] = h.v1;
+      qc = h.v1 - qk.mu;
+      put_qh<KS>((_Float16 *)nx.qf, mn, lane, -2.0 * qc);
+    }
+#pragma unroll
+    for (int k = 0; k < 12; k++) {
+      if ((lm >> (43 + k)) & 1ull) {  // wave-uniform
+        const double qcl = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(qc), 43 + k),
+                                            __builtin_amdgcn_readlane(__double2loint(qc), 43 + k));
+        ss += qcl * qcl;
+#pragma unroll
+        for (int i = 0; i < IA_NPC; i++) {
+          const double bl = __hiloint2double(__builtin_amdgcn_readlane(__double2hiint(qk.bas[i]), 43 + k),
+                                             __builtin_amdgcn_readlane(__double2loint(qk.bas[i]), 43 + k));
+          p[i] += bl * qcl;
+        }
+        const double d = al[k] - h.v1;
+        part += d * d;
+      }
+    }
+  }
+  double u = crow >= 0 ? part : DBL_MAX;
+  u = wave_min_d_x(u);
+  IA_GST2(4);
+  // ---- the pruning record (gather_p_query's, from these sums)
+  const double qn = sqrt(ss);
+  const bool fin = u < DBL_MAX;
+  const unsigned key = fin ? prune_key(p, qk.sc) : IA_PRUNE_KEY_INF;
+  const float up = fin ? round_up_f(u * nx.ufac) : INFINITY;
+  const float z = fin ? round_up_f((double)up - ss + 0x1p-22 * (ss + (double)up) + 0x1p-24 * (16.0 * qn + 300.0)) : INFINITY;
+  const float w = round_up_f(0x1p-8 * qn * (1.0 + 0x1p-40));
+  if (lane == 0) {
+    nx.qn2[mn] = ss;
+    nx.qinfo[3 * mn] = make_float4(round_down_f(p[0] - IA_PRUNE_MABS), round_down_f(p[1] - IA_PRUNE_MABS),
+                                   round_down_f(p[2] - IA_PRUNE_MABS), round_down_f(p[3] - IA_PRUNE_MABS));
+    nx.qinfo[3 * mn + 1] = make_float4(round_up_f(p[0] + IA_PRUNE_MABS), round_up_f(p[1] + IA_PRUNE_MABS),
+                                       round_up_f(p[2] + IA_PRUNE_MABS), round_up_f(p[3] + IA_PRUNE_MABS));
+    nx.qinfo[3 * mn + 2] = make_float4(up, __uint_as_float(key), z, w);
+  }
+  IA_GST2(5);
+#if IA_PROBE & 8
+  if (gprobe && lane == 0)
+    printf("ESTAMP bw=%d t=%d M=%d pre=%llu part=%llu handoff=%llu late=%llu rec=%llu\n", g.bw, sn.t, sn.M, gst[1] - gst[0],
+           gst[2] - gst[1], gst[3] - gst[2], gst[4] - gst[3], gst[5] - gst[4]);
+#endif
+#undef IA_GST2
+}
+
 // ------------------------------------------------------------------------------------------
 // K4 + K2 fused (option "fuse_gather"): K4 of step t, then the gather (K2p on pruned levels,
 // K2h on the others) of step t + 1, one launch.  Pixel (r, c + 1) of step t + 1 reads two
@@ -1988,8 +2208,12 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
   int mn = -1;   // this wave's query of step t + 1
   int job = 0;
   QPre pf;       // its step-independent inputs, prefetched during the merge (pruned levels)
+  // the early gather path (gather_p_early): merge waves of one-rank pruned levels, no publish
+  const bool early = PR && !XO && !nx.kslot && nx.prefetch && nx.early;
+  QConst qk;
+  if (early) qk = qconst_load(nx, lane);
 #if IA_PROBE & 8  // diagnostic build only: fused merge + gather phase stamps of one sampled wave
-  unsigned long long gs[5] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0};
+  unsigned long long gs[5] = {__builtin_amdgcn_s_memtime(), 0, 0, 0, 0}, gst[5] = {0, 0, 0, 0, 0};
   const bool gprobe = w == sd.M / 2 && (sd.t % 256) == 128 && JM == sd.M;
 #endif
   if (w < JM) {
@@ -2050,6 +2274,13 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
   }
   const JobPtrs jp = jobs.get(job);
   if constexpr (!JS::single) B = job_imgs(B, jp);  // single job: B already holds its images
+  if constexpr (PR) {
+    if (early && pf.on) {
+      __builtin_amdgcn_wave_barrier();  // the merge's LDS rows are done with
+      gather_p_early<KS>(g, nx, B, jp, job, mn, lane, ma.db64, qsh[wv], h, pf, qk);
+      return;
+    }
+  }
   const QPix pn = ia_qpix(nx.sn, g.bw, mn);
   if (pn.r >= 1 && pn.c + 2 < g.bw) {  // (r - 1, c + 2) of step t: the row above's handoff
     const HandSlot *hs = nx.hand + (int64_t)job * g.bh + (pn.r - 1);
@@ -2079,7 +2310,11 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
   if constexpr (PR) {
     const bool pub = (XO && nx.xp.W) || (!XO && nx.kslot);
     gather_p_query<KS, false, true>(g, nx.sn, B, jp, mn, lane, nx.mu, nx.q64, nx.qn2, qf, ma.db64, nx.basis, nx.ufac,
-                                    nx.qinfo, A, qsh[wv], pub ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2, pf);
+                                    nx.qinfo, A, qsh[wv], pub ? xh[wv][0] : nullptr, xh[wv][1], h, o0, o1, o2, pf
+#if IA_PROBE & 8
+                                    , gprobe ? gst : nullptr
+#endif
+                                    );
     if (XO && nx.xp.W) xo_publish<KS>(nx.xp, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
     if (!XO && nx.kslot) sorted_publish<KS>(nx, mn, lane, xh[wv][0], xh[wv][1], o0, o1, o2);
   } else {
@@ -2089,8 +2324,9 @@ __device__ __forceinline__ void merge_gather_body(const LevelGeo &g, const StepD
   __builtin_amdgcn_s_waitcnt(0);
   gs[3] = __builtin_amdgcn_s_memtime();
   if (gprobe && lane == 0)
-    printf("GSTAMP bw=%d t=%d M=%d merge=%llu handoff_wait=%llu gather=%llu\n", g.bw, sd.t, sd.M, gs[1] - gs[0],
-           gs[2] - gs[1], gs[3] - gs[2]);
+    printf("GSTAMP bw=%d t=%d M=%d merge=%llu handoff_wait=%llu gather=%llu [feat+frag=%llu sums=%llu urow=%llu rec=%llu]\n",
+           g.bw, sd.t, sd.M, gs[1] - gs[0], gs[2] - gs[1], gs[3] - gs[2], gst[1] - gst[0], gst[2] - gst[1], gst[3] - gst[2],
+           gst[4] - gst[3]);
 #endif
 }
 template <int RPL, bool PR, bool XO, class JS>

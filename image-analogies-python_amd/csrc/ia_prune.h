@@ -47,12 +47,14 @@ __device__ __forceinline__ unsigned prune_key(const double (&p)[IA_NPC], const d
     const double t = (p[i] * scale[i] + 1.0) * 128.0;
     qv[i] = t <= 0. ? 0u : t >= 255. ? 255u : (unsigned)t;
   }
-  unsigned key = 0;
-#pragma unroll
-  for (int b = 7; b >= 0; b--) {
-#pragma unroll
-    for (int i = 0; i < IA_NPC; i++) key = (key << 1) | ((qv[i] >> b) & 1u);
-  }
+  // bit b of qv[i] goes to bit 4 b + 3 - i (Morton order, axis 0 most significant): each 8-bit
+  // coordinate spread to every fourth bit by three shift-and-mask steps
+  auto spread = [](unsigned x) {
+    x = (x | (x << 12)) & 0x000F000Fu;
+    x = (x | (x << 6)) & 0x03030303u;
+    return (x | (x << 3)) & 0x11111111u;
+  };
+  const unsigned key = (spread(qv[0]) << 3) | (spread(qv[1]) << 2) | (spread(qv[2]) << 1) | spread(qv[3]);
   return key < IA_PRUNE_KEY_MAX ? key : IA_PRUNE_KEY_MAX;
 }
 

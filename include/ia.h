@@ -206,10 +206,15 @@ int ia_version(void);
  * Fused merge + gather launches (option "fuse_gather") wait row to row; a level uses them only
  * while the chained waves of all levels in flight in the process stay under twice the GPU's
  * resident k_merge_gather waves (else it runs separate launches; ia_capi.cpp g_chain_waves).
- * "rec_wt" = 0 (default) / 1: the pruned scan stores its per-(query, chunk) records write-through
+ * "rec_wt" = 1 (default) / 0: the pruned scan stores its per-(query, chunk) records write-through
  * (sc1 buffer stores), so the scan -> merge kernel boundary has no dirty record lines to write
  * back (one-rank steps; the owner-computes exchange has its own uncached stores).  Exact either
  * way: the merge reads the records after the boundary.
+ * "early_gather" = 1 (default) / 0: a fused merge + gather wave of a one-rank pruned level (option
+ * prefetch_next on, no publish) runs its next query's gather up to the row above's late feature
+ * before waiting for that handoff: the other 54 features, fragments, projection and |q'|^2 sums,
+ * and U' over the candidate rows requested first; U' then leaves out the row above's own two
+ * candidates (a valid bound either way).
  * "stamps" = 1: every pruned-scan and fused-merge launch of a pruned level stamps its
  * workgroups' first / last s_memrealtime tick; ia_stats.k3p_stamp_ms / merge_stamp_ms sum the
  * per-launch device times (bench.py roofline.frac_timed: the timed, pipelined steps' own kernels).
