@@ -882,6 +882,32 @@ def main():
         if st_all['merge_stamp_launches'] > 0:
             roofline['merge_us_per_launch_timed'] = st_all['merge_stamp_ms'] * 1e3 / st_all['merge_stamp_launches']
             roofline['merge_launches_timed'] = st_all['merge_stamp_launches']
+        # the fused merge + gather (k_merge_gather) of the same level: a latency-bound chain of
+        # dependent memory rounds per query (one wave each), priced against HBM for scale only.
+        # Bytes per query: the scan's records (20 B per chunk), the query row and
+        # its pruning record, the coherence neighbours' s / im, the fp64 rows of the 15 coherence
+        # candidates and the reranked MFMA candidates (+ their A' values), then the next query's
+        # 55 features, its 30 U' candidates' s / im / NN rows and <= 28 fp64 U' rows, and the
+        # writes (B', s, im, NN row, stats word, q64, fragments, pruning record, handoff slot)
+        if st_all['merge_stamp_launches'] > 0 and sw is None:
+            lvl_px = float(np.prod(job.B_pyr[job.L - 1].shape[:2]))
+            q_per_launch = lvl_px * args.steps * jobs / st_all['merge_stamp_launches']
+            rr = st_all['reranked'] / max(st_all['pixels'], 1)
+            nwg = 256
+            bq = nwg * 20 + 496 + 15 * 12 + (15 + rr) * 456 + 440 + 30 * 12 + 28 * 448 + 780
+            mus = roofline['merge_us_per_launch_timed']
+            roofline['merge'] = {
+                'kernel': 'k_merge_gather (fused K4 merge of step t + K2p gather of step t + 1, one wave per query)',
+                'bound': 'latency', 'queries_per_launch': q_per_launch, 'reranked_per_query': rr,
+                'algorithmic_bytes_per_launch': bq * q_per_launch,
+                'achieved_gbs': bq * q_per_launch / (mus * 1e-6) / 1e9,
+                'frac_of_hbm': bq * q_per_launch / (mus * 1e-6) / HBM_PEAK,
+                'dependent_memory_rounds': 3,
+                'rounds': ('(1) the scan records + query row + neighbours\' s / im, (2) the candidates\' fp64 rows '
+                           '(the next query\'s features, neighbours and U\' rows load beside it and during the '
+                           'merge\'s compute: option early_gather), (3) the row above\'s handoff slot; then the '
+                           'late feature and the pruning record from registers'),
+                'us_per_launch_timed': mus}
         if st_all['stamp_gaps'] > 0:
             roofline['chain_gap_us_timed'] = st_all['stamp_gap_ms'] * 1e3 / st_all['stamp_gaps']
             if st_all.get('stamp_gaps_sm', 0) > 0 and st_all['stamp_gaps'] > st_all['stamp_gaps_sm']:
