@@ -945,11 +945,12 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
   // certification: every unlisted row of chunk w has MFMA value >= T_w, hence true distance
   // >= T_w + |q'|^2 - eps.  Chunks with T_w <= theta may hide a row that beats or ties bd.
   const double theta = cert_theta(a, R, qn, qn2, bd);
+  const float thetaf = round_down_f(theta);  // (t <= theta  <=>  t <= theta rounded down, t a float)
   unsigned long long nfb = 0;
 #pragma unroll
   for (int jb = 0; jb < RPL; jb++) {
     const int base = jb * IA_WAVE;
-    unsigned long long mask = __ballot((double)tt[jb] <= theta);
+    unsigned long long mask = __ballot(tt[jb] <= thetaf);
     while (mask) {
       const int j = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
@@ -1650,10 +1651,13 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
   const double eps = merge_eps(a, R, qn);
   const double thr = (double)a1 + 2.0 * eps;
   unsigned cmask = 0;
+  // a float v satisfies v <= thr exactly when v <= thr rounded down to float: one conversion
+  // instead of one per compared value
+  const float thf = round_down_f(thr);
 #pragma unroll
   for (int j = 0; j < RPL; j++) {
-    if ((double)v1[j] <= thr && i1[j] >= 0 && i1[j] < a.NA) cmask |= 1u << (2 * j);
-    if ((double)v2[j] <= thr && i2[j] >= 0 && i2[j] < a.NA) cmask |= 1u << (2 * j + 1);
+    if (v1[j] <= thf && i1[j] >= 0 && i1[j] < a.NA) cmask |= 1u << (2 * j);
+    if (v2[j] <= thf && i2[j] >= 0 && i2[j] < a.NA) cmask |= 1u << (2 * j + 1);
   }
   int placed = 0;  // candidates given a rerank lane so far (wave-uniform)
   unsigned long long bal = __ballot(cmask != 0);
@@ -1747,10 +1751,11 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
 
   // certification (see certified_winner): rescan chunks whose threshold does not clear bd
   const double theta = cert_theta(a, R, qn, qn2, bd);
+  const float thetaf = round_down_f(theta);  // (t <= theta  <=>  t <= theta rounded down, t a float)
   unsigned long long nfb = 0;
 #pragma unroll
   for (int jb = 0; jb < RPL; jb++) {
-    unsigned long long mask = __ballot((double)tt[jb] <= theta);
+    unsigned long long mask = __ballot(tt[jb] <= thetaf);
     while (mask) {
       const int j = __ffsll((long long)mask) - 1;
       mask &= mask - 1;
