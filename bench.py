@@ -305,6 +305,11 @@ def pipe_contexts(args, local, ctx):
         ctx.set_option('stream_priority', hi)
         for cx in extra:
             cx.set_option('stream_priority', lo)
+    if args.scan_wgs:
+        ctx.set_option('scan_wgs', args.scan_wgs)
+    if args.coarse_scan_wgs:
+        for cx in extra:
+            cx.set_option('scan_wgs', args.coarse_scan_wgs)
     if not args.coarse_fuse_gather:   # the coarser levels' merge and gather as separate launches
         for cx in extra:
             cx.set_option('fuse_gather', 0)
@@ -426,6 +431,12 @@ def main():
                          'DESIGN.md §6b)')
     ap.add_argument('--pipe-priority', type=int, default=1, choices=[0, 1, 2],
                     help='1: the finest level\'s stream at high priority, the coarser levels\' at low; 2: reversed')
+    ap.add_argument('--coarse-scan-wgs', type=int, default=128,
+                    help='pipelined levels: workgroups of the coarser levels\' pruned scans (0: one per CU, 256; '
+                         'default 128: half the CUs, so the finest level\'s launches are not queued behind a '
+                         'whole-GPU scan, DESIGN.md §6g)')
+    ap.add_argument('--scan-wgs', type=int, default=0,
+                    help='workgroups of the finest level\'s pruned scans (0: one per CU, 256)')
     ap.add_argument('--k3p-blocks', type=int, default=1, choices=[0, 1],
                     help='pruned scan of a step wider than 11 query tiles: 1 = one launch of (query block x DB '
                          'chunk) workgroups, 0 = one launch per query block')

@@ -150,6 +150,7 @@ struct ia_ctx {
                                  // 2 = on levels whose widest step has >= IA_FUSE_SORT_MINQ queries; off by
                                  // default: no gain left with nn_bound
   int chain_budget = 0;          // waves of handoff-chained launches this context's CUs hold deadlock-free
+  int scan_wgs = IA_NWG_H;       // option "scan_wgs": workgroups of a pruned scan launch (<= one per CU)
                                  // (ia_init: 2 x the resident merge-gather waves - a margin; see g_chain_waves)
   unsigned long long *kslot = nullptr;  // their per-query key slots (uncached)
   int kslot_n = 0;
@@ -511,6 +512,11 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
     HIP_TRY(hipStreamCreateWithPriority(&ns, hipStreamNonBlocking, value == 0 ? 0 : value == 1 ? greatest : least));
     hipStreamDestroy(c->st);
     c->st = ns;
+    return IA_OK;
+  }
+  if (!std::strcmp(name, "scan_wgs")) {
+    if (value < 8 || value > IA_NWG_H || value % 8) return fail(IA_EINVAL, "ia_set_option: scan_wgs must be a multiple of 8 in [8, 256]");
+    c->scan_wgs = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "xo_wait")) {
@@ -951,7 +957,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   const int64_t Mpad_max = std::max((Mtmax + IA_TILE - 1) / IA_TILE * IA_TILE,
                                     xo ? J * ((Mmax + IA_TILE - 1) / IA_TILE * IA_TILE) : 0);
   const bool prune = c->prune && use_h && g.ch == 1 && g.NA >= c->prune_min_rows && Mpad_max <= 4096 &&
-                     (g.n_tiles + IA_NWG_H - 1) / IA_NWG_H <= IA_K3P_MAXK_LDS;
+                     (g.n_tiles + c->scan_wgs - 1) / c->scan_wgs <= IA_K3P_MAXK_LDS;
   // option "nn_bound": per-pixel exact NN rows of a pruned one-rank level (-1 until merged)
   for (int j = 0; j < J; j++) {
     jp[j].nn = nullptr;
@@ -993,7 +999,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   auto decomp = [&](int t0, int t1) {
     Shard d{t0, t1, 0, 0};
     const int n = t1 - t0;
-    if (prune) d.nwg = std::min(IA_NWG_H, n);  // round-robin chunks: WG w owns tiles w + nwg*k
+    if (prune) d.nwg = std::min(c->scan_wgs, n);  // round-robin chunks: WG w owns tiles w + nwg*k
     else {
       d.tpw = use_h ? std::max(IA_WGH / IA_WAVE, (n + IA_NWG_H - 1) / IA_NWG_H) : std::max(4, (n + IA_WG_TARGET - 1) / IA_WG_TARGET);
       d.nwg = (n + d.tpw - 1) / d.tpw;
