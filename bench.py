@@ -285,11 +285,6 @@ def make_context(args, local):
     if not args.prefetch_next:
         cx.set_option('prefetch_next', 0)
     cx.set_option('rec_wt', args.rec_wt)
-    try:
-        cx.set_option('steal', args.steal)
-    except Exception:
-        if args.steal:   # (an older diagnostic library without the option runs its only form)
-            raise
     cx.set_option('early_gather', args.early_gather)
     if not args.nn_bound:
         cx.set_option('nn_bound', 0)
@@ -436,9 +431,6 @@ def main():
                          'DESIGN.md §6b)')
     ap.add_argument('--pipe-priority', type=int, default=1, choices=[0, 1, 2],
                     help='1: the finest level\'s stream at high priority, the coarser levels\' at low; 2: reversed')
-    ap.add_argument('--steal', type=int, default=0, choices=[0, 1],
-                    help='1: pruned-scan workgroups take tiles from the back of their partner\'s walk once '
-                         'their own are done (DESIGN.md §6g)')
     ap.add_argument('--coarse-scan-wgs', type=int, default=128,
                     help='pipelined levels: workgroups of the coarser levels\' pruned scans (0: one per CU, 256; '
                          'default 128: half the CUs, so the finest level\'s launches are not queued behind a '
@@ -986,7 +978,7 @@ def main():
            'stats': {k: st_all[k] for k in ('pixels', 'steps', 'coherence_wins', 'reranked', 'fallbacks', 'db_ms',
                                         'synth_ms', 'bound_violations', 'kappa_ambiguous', 'f16_levels', 'pruned_levels',
                                         'dist_pairs', 'dist_pairs_full', 'dist_tiles', 'dist_tiles_full',
-                                        'dist_pairs_corrected', 'stolen_tiles')}}
+                                        'dist_pairs_corrected')}}
     if sw is not None:
         out['config']['sweep'] = {'jobs': len(sw.jobs), 'batched': not args.sequential, 'max_batch': args.max_batch,
                                   'streams': args.streams,

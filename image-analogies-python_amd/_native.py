@@ -56,7 +56,7 @@ class Stats(ctypes.Structure):
                 ('stamp_gaps', ctypes.c_int64), ('stamp_window_ms', ctypes.c_double), ('prune_rows', ctypes.c_int64),
                 ('k3p_stamp_start_ms', ctypes.c_double), ('k3p_stamp_wg_ms', ctypes.c_double),
                 ('stamp_gap_sm_ms', ctypes.c_double), ('stamp_gaps_sm', ctypes.c_int64),
-                ('k3p_bytes_unique_all', ctypes.c_double), ('stolen_tiles', ctypes.c_double)]
+                ('k3p_bytes_unique_all', ctypes.c_double)]
 
     # fields that describe only the levels with the largest DB seen (build_rows / prune_rows)
     _BUILD = ('k1b_ms', 'k1b_bytes', 'k1_ms', 'k1_bytes', 'build_levels')

@@ -159,9 +159,6 @@ struct ia_ctx {
   int time_dist = 0;
   int stamps = 0;                 // option "stamps": per-launch device time from kernel stamps
   int rec_wt = 1;                 // option "rec_wt": K3p records stored write-through
-  int steal = 0;                  // option "steal": K3p workgroups take tiles from their partner's back (§6g)
-  int steal_delay = 0;            // option "steal_delay" (tests): us the upper half of the scan's workgroups waits
-  DevBuf steal_front, steal_cnt;  // its frontier words (2 x IA_NWG_H, one per 128-B line) and stolen counts
   DevBuf stamp_k3, stamp_mg, stamp_dur;
   std::vector<hipEvent_t> evs, evg, evm;  // sampled steps: K3, K2 and K4 brackets
   hipEvent_t lv0 = nullptr, lv1 = nullptr, lv2 = nullptr;
@@ -373,7 +370,7 @@ void ia_destroy(ia_ctx *c) {
                     &c->mu, &c->Rbits, &c->q64, &c->qn2, &c->qf, &c->rec, &c->recT, &c->win, &c->allwin, &c->counters, &c->absmax,
                     &c->pr_part, &c->pr_cov, &c->pr_basis, &c->pr_proj, &c->pr_keys, &c->pr_rows, &c->pr_tmp, &c->pos2row,
                     &c->boxes, &c->qinfo, &c->pairs, &c->ord, &c->qs_order, &c->qs_info, &c->qs_frag, &c->qs_tbox, &c->tnorm,
-                    &c->stamp_k3, &c->stamp_mg, &c->stamp_dur, &c->steal_front, &c->steal_cnt,
+                    &c->stamp_k3, &c->stamp_mg, &c->stamp_dur,
                     &c->py_in, &c->py_tmp, &c->py_sm, &c->py_mm, &c->py_out})
     b->release();
   for (auto *v : {&c->evs, &c->evg, &c->evm, &c->p_ev[0], &c->p_ev[1], &c->p_ev[2]})
@@ -398,16 +395,6 @@ int ia_set_option(ia_ctx *c, const char *name, int value) {
   if (!c || !name) return fail(IA_EINVAL, "ia_set_option: NULL argument");
   if (!std::strcmp(name, "time_dist")) {
     c->time_dist = value;
-    return IA_OK;
-  }
-  if (!std::strcmp(name, "steal")) {
-    if (value != 0 && value != 1) return fail(IA_EINVAL, "ia_set_option: steal must be 0 or 1");
-    c->steal = value;
-    return IA_OK;
-  }
-  if (!std::strcmp(name, "steal_delay")) {
-    if (value < 0 || value > 1000) return fail(IA_EINVAL, "ia_set_option: steal_delay must be 0..1000 (us)");
-    c->steal_delay = value;
     return IA_OK;
   }
   if (!std::strcmp(name, "rec_wt")) {
@@ -1053,14 +1040,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
       (rc = c->pairs.ensure(6 * IA_NWG_H * 8)) || (rc = c->ord.ensure(2 * 4096 * 4)) ||
       (rc = c->qinfo.ensure(prune ? (size_t)Mpad_max * 3 * 16 * 2 : 16)))
     return rc;
-  // option "steal": one-rank pruned levels; the frontier words start every level at 0 (no tag
-  // of this level's launches, whose sseq is the step index + 1)
-  const bool steal = prune && c->steal && !multi && !xo;
-  if (steal) {
-    // (one frontier word per 128-B line: 2 x IA_NWG_H lines)
-    if ((rc = c->steal_front.ensure(2 * IA_NWG_H * 128)) || (rc = c->steal_cnt.ensure(IA_NWG_H * 4))) return rc;
-    HIP_TRY(hipMemsetAsync(c->steal_front.p, 0, 2 * IA_NWG_H * 128, c->st));
-  }
   if (prune && ((rc = c->qs_order.ensure((size_t)Mpad_max * 4)) || (rc = c->qs_info.ensure((size_t)Mpad_max * 3 * 16)) ||
                 (rc = c->qs_frag.ensure((size_t)Mpad_max * db_row_bytes)) ||
                 (rc = c->qs_tbox.ensure((size_t)Mpad_max / IA_TILE * 3 * 16))))
@@ -1417,7 +1396,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
                       c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3x, sd.t,
                       reinterpret_cast<const int *>(loc + XOLayout::ORD), 0, sd.r0, nullptr,
                       reinterpret_cast<const float4 *>(loc + XOLayout::TBOX), c->tnorm.as<float>() + x.t0, c->st, nqb,
-                      Wsh * QTs, &xs, k3_stamp(), c->rec_wt) < 0) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
+                      Wsh * QTs, &xs, k3_stamp(), c->rec_wt)) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
           }
         pairs_full += (double)n * Wsh * QTs;
         tiles_full += (double)n * nqb;
@@ -1555,7 +1534,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
         const int n = x.t1 - x.t0;
         const char *dbp = (const char *)c->db.p + (size_t)(x.t0 - g.tile0) * tile_bytes;
         m.nwg = x.nwg;
-        m.steal = nullptr;  // (set below by a stealing launch)
         if (prune && presorted && nqb > 1 && c->k3p_blocks) {
           // one launch for all query blocks (option "k3p_blocks"): nqb blocks x nch DB chunks of
           // the shard, nch a multiple of 8 (the blocks of a chunk on one XCD) when that loses
@@ -1569,7 +1547,7 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
             if (ia_launch_k3p(qtb, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, 0, Mt, sd.Mpad, nch,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t, c->qs_order.as<int>(),
-                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp(), c->rec_wt) < 0) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
+                          0, sd.r0, nullptr, tboxp, tn, c->st, nqb, qtt, nullptr, k3_stamp(), c->rec_wt)) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
           }
             m.nwg = nch;
             pairs_full += (double)n * qtt;
@@ -1593,21 +1571,15 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
             if (ia_launch_k3p(qt, dbp, c->qs_frag.p, c->qs_info.as<float4>(), m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H, k3v, sd.t,
-                          c->qs_order.as<int>(), 0, sd.r0, nullptr, tboxp, tn, c->st, 1, 0, nullptr, k3_stamp(), c->rec_wt) < 0) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
+                          c->qs_order.as<int>(), 0, sd.r0, nullptr, tboxp, tn, c->st, 1, 0, nullptr, k3_stamp(), c->rec_wt)) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
           }
           else if (prune)
             {
-            const int lr = ia_launch_k3p(qt, dbp, c->qf.p, qinfot, m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
+            if (ia_launch_k3p(qt, dbp, c->qf.p, qinfot, m.boxes, m.pos2row, n, qt0, Mt, sd.Mpad, x.nwg,
                           (float4 *)m.rec, (float *)m.recT, c->pairs.as<unsigned long long>() + (timed ? IA_NWG_H : 0),
                           c->pairs.as<unsigned long long>() + (timed ? 3 : 2) * IA_NWG_H,
                           k3v, sd.t, c->ord.as<int>() + (sd.t & 1 ? 0 : 4096), ord_n, sd.r0,
-                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, nullptr, k3_stamp(), c->rec_wt,
-                          steal && nqb == 1 ? c->steal_front.as<unsigned>() : nullptr, c->steal_cnt.as<int>(),
-                          (unsigned)(sd.t + 1), c->steal_delay * 100);
-            if (lr < 0) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
-            // (a stealing launch's merge rescans the stolen tiles too, in this step's walk direction)
-            m.steal = lr == 1 ? c->steal_cnt.as<int>() : nullptr;
-            m.srev = sd.t & 1;
+                          c->ord.as<int>() + (sd.t & 1 ? 4096 : 0), nullptr, tn, c->st, 1, 0, nullptr, k3_stamp(), c->rec_wt)) return fail(IA_EINVAL, "pruned scan: no kernel instance for k3p_variant");
           }
           else if (use_h)
             ia_launch_k3h(g.KS, qt, dbp, c->qf.p, n, x.tpw, qt0, Mt, x.nwg, m.pos0, g.n_tiles, (float4 *)m.rec,
@@ -1745,7 +1717,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
   }
   if (stats) {
     unsigned long long ctr[5], prs[4], pfull = 0, ptp = 0, ext[2] = {0, 0};
-    double stolen = 0.;  // option "steal": tiles taken from partners (the scan's slots, bits 40+)
     HIP_TRY(hipMemcpy(ctr, c->counters.p, sizeof(ctr), hipMemcpyDeviceToHost));
     {  // per-workgroup counter slots (no same-address atomics in the distance kernel)
       std::vector<unsigned long long> slots(6 * IA_NWG_H);
@@ -1763,10 +1734,9 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
           }
         }
       }
-      for (int w = 0; w < IA_NWG_H; w++) {  // DB half-tiles loaded besides one per loaded tile (<< 40: stolen tiles)
-        ext[0] += slots[4 * IA_NWG_H + w] & ((1ull << 40) - 1);
-        ext[1] += slots[5 * IA_NWG_H + w] & ((1ull << 40) - 1);
-        stolen += (double)(slots[4 * IA_NWG_H + w] >> 40);
+      for (int w = 0; w < IA_NWG_H; w++) {  // DB half-tiles loaded besides one per loaded tile
+        ext[0] += slots[4 * IA_NWG_H + w];
+        ext[1] += slots[5 * IA_NWG_H + w];
       }
     }
     const double pair_flops = 2.0 * g.D * IA_TILE * IA_TILE;  // one (DB tile, query tile) pair
@@ -1786,7 +1756,6 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     stats->dist_tiles_full += tiles_full;
     stats->dist_pairs_corrected += (double)pfull;
     stats->dist_tiles_rows += (double)ptp;
-    stats->stolen_tiles += stolen;
     float ms_db = 0.f, ms_syn = 0.f, ms_k1b = 0.f, ms_k1 = 0.f;
     hipEventElapsedTime(&ms_db, c->lv0, c->lv1);
     hipEventElapsedTime(&ms_syn, c->lv1, c->lv2);

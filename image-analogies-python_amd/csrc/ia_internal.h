@@ -106,10 +106,6 @@ struct MergeArgs {
   unsigned *xo_err = nullptr;         // bit 3: a record did not arrive in time
   long long xo_timeout = 0;
   unsigned long long *stamp = nullptr;  // option "stamps": this launch's per-workgroup (start, end)
-  // option "steal": per workgroup the tiles it took from the back of workgroup (w + nwg / 2) % nwg's
-  // walk (XOScan::steal; nullptr: no stealing), and the scan's walk direction (step parity)
-  const int *steal = nullptr;
-  int srev = 0;
 };
 
 // Per-launch device timing without HIP events (option "stamps"): every workgroup of a stamped
@@ -325,15 +321,6 @@ struct XOScan {
   long long timeout_ticks;
   unsigned long long *stamp;      // option "stamps" (any K3p launch, owner-computes or not): per-WG ticks
   int rec_wt;                     // option "rec_wt": records stored write-through (sc1), nothing left dirty in L2
-  // option "steal" (k3p_variant 24, one-rank steps): workgroup w also takes tiles from the back of
-  // workgroup (w + nwg / 2) % nwg's walk once its own are done.  front: per workgroup
-  // its own progress [32 w] and its thief's lowest taken index [32 (nwg + w)] (one word per
-  // 128-B line, one writer each), each (sseq << 12) | index; steal: per workgroup the number of
-  // tiles it took from its victim
-  unsigned *front;
-  int *steal;
-  unsigned sseq;
-  int sdelay;  // option "steal_delay" (tests): workgroups >= nwg / 2 start this many 100 MHz ticks late
 };
 
 // fused K4(t) + K2p(t + 1) (k_merge_gather, option "fuse_gather"): the next step's gather

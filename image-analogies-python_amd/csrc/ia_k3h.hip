@@ -67,16 +67,6 @@ __device__ __forceinline__ void dma_hi(const h16x8 *__restrict__ db, int64_t til
   for (int s = 0; s < 3; s++) dma16(src + TileFmt<KS>::off(2 * s, lane), base + s * 1024u);
   if (lane < 32) dma16(src + TileFmt<KS>::off(6, lane), base + 3072u);
 }
-// option "steal": one frontier word (lane 0's address) into LDS by an LDS-DMA of device scope (sc1:
-// read from the L2, not a stale vector-cache line); issued with the ring's DMAs and counted with
-// them, so the word lands without any wave waiting for it (no offset: the M0-offset rule above)
-__device__ __forceinline__ void dma_word(const void *g, unsigned lds_addr) {
-#ifdef IA_EXP_SC0
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc0" ::"s"(lds_addr), "v"(g) : "memory", "m0");
-#else
-  asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off sc1" ::"s"(lds_addr), "v"(g) : "memory", "m0");
-#endif
-}
 template <int N>
 __device__ __forceinline__ void ring_wait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -680,7 +670,7 @@ k3h_fn IA_K3H_CAT(ia_k3h_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
 // counter slot then holds (pairs with corrections << 32) + box-needed pairs.  HHX: how the
 // correction products follow the filter (0: full chains, 1: fused single chains, 2: fused on
 // query-tile pairs, k3p_hhpairs).
-template <int KS, int QT, int NW, bool PRE = false, bool HHF = false, int HHX = 0, bool STEAL = false>
+template <int KS, int QT, int NW, bool PRE = false, bool HHF = false, int HHX = 0>
 __global__ void __launch_bounds__(NW * IA_WAVE, 1)
 k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const float4 *__restrict__ qinfo,
            const float4 *__restrict__ boxes, const int *__restrict__ pos2row, int NT, int qt0, int M, int Mpad, int nwg,
@@ -703,9 +693,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   // a vmcnt(0) before any LDS access it cannot prove disjoint from one)
   constexpr int QFP = HHX == 4 ? KS : NP;
   __shared__ h16x8 ring[HHX == 4 ? NW * 3 * IA_HSLOT : 1];
-  // option "steal": per wave and ring slot the two frontier words loaded with that slot's tile
-  // (the thief's lowest taken index of this workgroup's walk, the victim's progress)
-  __shared__ unsigned fring[STEAL ? NW * 3 * 2 : 1];
   float4 *qlo = reinterpret_cast<float4 *>(ldsh + QT * QFP * IA_WAVE);  // [NQ]
   float4 *qhi = qlo + NQ;                                               // [NQ]
   float *qU = reinterpret_cast<float *>(qhi + NQ);                     // [NQ]
@@ -742,32 +729,14 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   // rev: this step walks the workgroup's tiles in reverse (alternate steps: the tiles read last
   // by one step are read first by the next, while they are still in the memory-side cache)
   auto tk = [&](int k) { return wg + nwg * (rev ? K - 1 - k : k); };
-  // option "steal" (HHX 4, in-kernel sort, one rank): after its own K tiles the
-  // workgroup takes tiles from the back of its victim's walk (workgroup vic, same XCD when nwg / 2
-  // is a multiple of 8), local indices K + j = the victim's walk index Kv - 1 - j, j < Ks.  Each side
-  // publishes how far it got (xo.front, tagged with the launch's sseq) and stops where the other
-  // already was; a stale read only makes both take a tile (its rows then sit in two records), never
-  // leaves one to nobody.
-  // (a kernel instance of its own, k3p_variant 24's stealing form: the plain form's code is untouched)
-  constexpr bool STL = STEAL && HHX == 4 && !PRE;
-  const int vic = STL ? (wg + (nwg >> 1)) % nwg : 0;
-  const int Kv = STL ? (NT - vic + nwg - 1) / nwg : 0;
-#if defined(IA_EXP_NODEC) || defined(IA_EXP_NOMEM)
-  const int Ks = 0;
-#else
-  const int Ks = STL ? Kv >> 1 : 0;
-#endif
-  const int KL = K + Ks;  // local tile indices [0, K) own, [K, KL) stolen
-  auto tile_of = [&](int k) {
-    if constexpr (STL) return k < K ? tk(k) : vic + nwg * (rev ? k - K : Kv - 1 - (k - K));
-    else return tk(k);
-  };
-  float4 *wbox = reinterpret_cast<float4 *>(rankof + (PRE ? 0 : Mpad));  // [2 KL] the WG's tile boxes
-  float *qzt = reinterpret_cast<float *>(wbox + 2 * KL);                // HHF: [NQ] z per sorted slot
+  float4 *wbox = reinterpret_cast<float4 *>(rankof + (PRE ? 0 : Mpad));  // [2K] the WG's tile boxes
+  unsigned *kmask = reinterpret_cast<unsigned *>(wbox + 2 * K);        // [K] need mask per tile
+  int *items = reinterpret_cast<int *>(kmask + K);                     // [K] needed tiles, in order
+  float *qzt = reinterpret_cast<float *>(items + K);                    // HHF: [NQ] z per sorted slot
   float *qzw = qzt + NQ;                                                // HHF: [NQ] w per sorted slot
-  float *wR = qzw + NQ;                                                 // HHF: [KL] R_t of the WG's tiles
-  int *plk = reinterpret_cast<int *>(wR + KL);                          // HHX 4: [KL] filter-passing tiles
-  unsigned *plm = reinterpret_cast<unsigned *>(plk + KL);               // HHX 4: [KL] their passing blocks
+  float *wR = qzw + NQ;                                                 // HHF: [K] R_t of the WG's tiles
+  int *plk = reinterpret_cast<int *>(wR + K);                           // HHX 4: [K] filter-passing tiles
+  unsigned *plm = reinterpret_cast<unsigned *>(plk + K);                // HHX 4: [K] their passing blocks
   __shared__ unsigned wpairs[NW], wtiles[NW], wfull[NW], wtp[NW];
   __shared__ int pcount, pctr;  // HHX 4: passing tiles listed / handed out
   const int tid = threadIdx.x, lane = tid & 63, half = lane >> 5;
@@ -776,10 +745,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
   [[maybe_unused]] unsigned long long ph[10] = {0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
   K3P_T(ph[0]);
   const unsigned long long stamp0 = xo.stamp ? ia_clock() : 0ull;
-  if (STL && xo.sdelay > 0 && wg >= (nwg >> 1)) {  // option "steal_delay" (tests): a late half, whose tiles get stolen
-    const long long t0 = (long long)__builtin_amdgcn_s_memrealtime();
-    while ((long long)__builtin_amdgcn_s_memrealtime() - t0 < xo.sdelay) __builtin_amdgcn_s_sleep(8);
-  }
 
   // ---- 1. one global round
   h16x8 a[NP], an[NP];
@@ -844,58 +809,17 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       if constexpr (HHF) wR[x] = tnorm[t];
     }
   }
-  // option "steal": one frontier word per pass-(a) tile (publish), so every tile of the hi stream
-  // costs exactly five vector-memory operations (four DMAs, one store) and the ring's vmcnt count
-  // stays a constant (ring_wait<11> instead of <8>)
-  const unsigned stag = xo.sseq << 12;
-  // (frontier word i at front[32 i]: one 128-B line per word, each written by one workgroup)
-  auto publish = [&](int ix, unsigned val) {
-    if (lane == 0) {
-      unsigned *pa = xo.front + 32 * ix;
-      asm volatile("global_store_dword %0, %1, off" ::"v"(pa), "v"(val) : "memory");
-    }
-  };
-  // the two frontier words into the wave's slot fs (lane 0; two of the tile's seven operations)
-  auto load_front = [&](int fs) {
-#ifdef IA_EXP_NOMEM
-    if constexpr (false) {
-#else
-    if constexpr (STL) {
-#endif
-      if (lane == 0) {
-        const unsigned base = (unsigned)(uintptr_t)(__attribute__((address_space(3))) unsigned *)(fring + (wave * 3 + fs) * 2);
-        dma_word(xo.front + 32 * (nwg + wg), base);
-        dma_word(xo.front + 32 * vic, base + 4u);
-      }
-    }
-  };
   auto spec_hi = [&]() {
     if constexpr (HHX == 4) {
-      load_front(0);
       dma_hi<KS>(db, tk(min(wave, K - 1)), wring, lane);
-#ifndef IA_EXP_NOMEM
-      if constexpr (STL) publish(wg, stag | (unsigned)(2 * NW));  // tiles 0 .. 2 NW - 1: static, never stolen
-#endif
-      load_front(1);
       dma_hi<KS>(db, tk(min(wave + NW, K - 1)), wring + IA_HSLOT, lane);
-#ifndef IA_EXP_NOMEM
-      if constexpr (STL) publish(wg, stag | (unsigned)(2 * NW));
-#endif
     }
   };
   __shared__ int kctr;  // next tile index to hand out
-  // option "steal": the next local index to decide (own indices below K - K / 2 are never stolen
-  // and need no decision) and the workgroup's stolen count
-  __shared__ int s_dec, s_smax;
-  __shared__ int s_ftl, s_fvn;  // the frontiers last read: the thief's lowest taken index, the victim's progress
   if (tid == 0) {
     kctr = HHX == 4 ? 2 * NW : NW;  // HHX 4: each wave's first two tiles are static (the speculative DMAs)
     pcount = 0;
     pctr = 0;
-    s_dec = K - (K >> 1);
-    s_smax = 0;
-    s_ftl = K;
-    s_fvn = 0;
   }
   if constexpr (PRE) {
     __syncthreads();
@@ -972,8 +896,8 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     if constexpr (HHX == 4) e = ((e >> 6) / KS * NP + 2 * ((e >> 6) % KS)) * IA_WAVE + (e & 63);
     qe[i] = qf[e];  // unconditional: equal vmcnt on every path
   }
-  for (int x = tid; x < KL; x += WGT) {
-    const int t = tile_of(x);
+  for (int x = tid; x < K; x += WGT) {
+    const int t = tk(x);
     wbox[2 * x] = boxes[2 * t];
     wbox[2 * x + 1] = boxes[2 * t + 1];
     if constexpr (HHF) wR[x] = tnorm[t];
@@ -1209,64 +1133,13 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     int np = 0;  // this wave's passing tiles
     int kown = -1;       // its first one (tile, passing blocks)
     unsigned mown = 0u;
-    int kc = wave, kq = wave + NW;                     // tiles in slots sl, sl + 1 (>= KL: none)
+    int kc = wave, kq = wave + NW;                     // tiles in slots sl, sl + 1 (>= K: none)
     const int klast = min(wave, K - 1);                 // the dummy DMA's source (L2-hot)
     unsigned mc = kc < K ? need_r(kc) : 0u, mq = kq < K ? need_r(kq) : 0u;
-    // option "steal": who takes a tile of the contested ranges (own indices >= K - K / 2, stolen
-    // indices) is decided in index order (s_dec), so each side's accepted indices form a prefix of
-    // its walk: the victim rejects own index k only if k >= a frontier its thief published (the
-    // thief accepted every index from there on), the thief rejects victim index kv only if kv < a
-    // progress its victim published (the victim accepted every index below it).  A rejection closes
-    // that side's range (the counter and s_dec jump past it).  Frontiers are read with scalar loads
-    // that bypass the scalar cache (the thief and victim share an XCD's L2 when nwg / 2 is a multiple
-    // of 8; a stale value only makes both take a tile).
-    int own_last = 2 * NW - 1, st_last = -1;  // this wave's latest own / stolen tile (published)
-    // both frontiers as they were when slot fs's tile was requested (two iterations ago), into
-    // s_ftl / s_fvn (min / max: any value once published is a valid bound; the newest the tightest)
-    auto take_front = [&](int fs) __attribute__((always_inline)) {
-      if (lane == 0) {
-        const unsigned a = fring[(wave * 3 + fs) * 2], b = fring[(wave * 3 + fs) * 2 + 1];
-        if ((a & 0xFFFFF000u) == stag) atomicMin(&s_ftl, (int)(a & 0xFFFu));
-        if ((b & 0xFFFFF000u) == stag) atomicMax(&s_fvn, (int)(b & 0xFFFu));
-      }
-    };
-    auto decide = [&](int k) __attribute__((always_inline)) -> bool {  // k contested; true: this workgroup takes it
-      // the other side's frontier as last read (s_ftl: the thief's lowest taken index; s_fvn: the
-      // victim's progress)
-      // (relaxed workgroup-scope atomics on the LDS words: a volatile access would make the
-      // compiler wait for every outstanding vector-memory operation, i.e. drain the DMA ring)
-      int d;
-      while ((d = __builtin_amdgcn_readfirstlane(__hip_atomic_load(&s_dec, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP))) < k)
-        __builtin_amdgcn_s_sleep(1);
-      if (d > k) return false;  // the range was closed below this index
-      const int fr = __builtin_amdgcn_readfirstlane(
-          __hip_atomic_load(k < K ? &s_ftl : &s_fvn, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP));
-      // (the thief keeps 2 NW tiles off its victim's published progress: that word lags the
-      // victim's grabs by up to a store + load round trip, and a victim that close to its end
-      // finishes the rest about as soon; any thief rule is exact, its taken set stays a suffix)
-      const bool take = k < K ? k < fr : Kv - 1 - (k - K) >= fr + 2 * NW;
-      if (lane == 0) {
-        if (take) {
-          __hip_atomic_store(&s_dec, k + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-          if (k >= K) atomicMax(&s_smax, k - K + 1);
-        } else {
-          const int nx = k < K ? K : KL;  // close the range
-          atomicMax(&kctr, nx);
-          __hip_atomic_store(&s_dec, nx, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        }
-      }
-      return take;
-    };
-    // (the next tile this wave takes: every index below it was decided, so its own index + 1 or
-    // its victim index is what the wave publishes)
-    auto next_needed = [&](unsigned &m) __attribute__((always_inline)) -> int {  // the next needed tile (>= KL: none)
+    auto next_needed = [&](unsigned &m) -> int {  // the next needed tile from the counter (>= K: none)
       m = 0u;
       int k = grab();
-      for (; k < KL; k = grab()) {
-#ifndef IA_EXP_NODEC
-        if constexpr (STL)
-          if (k >= K - (K >> 1) && !decide(k)) continue;
-#endif
+      for (; k < K; k = grab()) {
         m = need_r(k);
         if (m) break;
       }
@@ -1274,32 +1147,13 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     };
     unsigned mn;
     int kn = next_needed(mn);
-    if (kn < K) own_last = kn;
-    else if (kn < KL) st_last = kn;
     int sl = 0;  // ring slot of tile kc
-    while (kc < KL) {
-      const bool ok = kn < KL;
-      load_front(sl == 0 ? 2 : sl - 1);
-      dma_hi<KS>(db, tile_of(ok ? kn : klast), wring + (sl == 0 ? 2 : sl - 1) * IA_HSLOT, lane);
+    while (kc < K) {
+      const bool ok = kn < K;
+      dma_hi<KS>(db, tk(ok ? kn : klast), wring + (sl == 0 ? 2 : sl - 1) * IA_HSLOT, lane);
       unsigned m2 = 0u;
-      const int k2 = ok ? next_needed(m2) : KL;
-      if (k2 < K) own_last = k2;
-      else if (k2 < KL) st_last = k2;
-      if constexpr (STL) {
-        // seven operations per tile: the two frontier loads, the four DMAs, and this store of the
-        // wave's latest frontier (stolen: the victim index, own: the progress); the slot's wait
-        // then allows the store after its tile and the two younger tiles' fourteen
-#ifdef IA_EXP_NOMEM
-        ring_wait<8>();
-#else
-        if (st_last >= 0) publish(nwg + vic, stag | (unsigned)(Kv - 1 - (st_last - K)));
-        else publish(wg, stag | (unsigned)(own_last + 1));
-        ring_wait<15>();
-        take_front(sl);
-#endif
-      } else {
-        ring_wait<8>();  // slot sl landed; the two younger tiles stay in flight
-      }
+      const int k2 = ok ? next_needed(m2) : K;
+      ring_wait<8>();  // slot sl landed; the two younger tiles stay in flight
       if (mc) {  // wave-uniform (0: a speculative tile that is not needed)
         h16x8 hc[KS];
         slot_hi(hc, wring + sl * IA_HSLOT, lane);
@@ -1339,7 +1193,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     // handed out through pctr
     int kcur = kown;
     unsigned mcur = mown;
-    if (kcur >= 0) ld_tile<KS>(a, db, tile_of(kcur), lane);
+    if (kcur >= 0) ld_tile<KS>(a, db, tk(kcur), lane);
     __syncthreads();  // every wave's passing tiles are listed, every ring is idle
     K3P_T(pq1);
     const int npass = pcount;
@@ -1370,7 +1224,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
       if (j0 < npass) {
         kcur = plk[j0];
         mcur = plm[j0];
-        ld_tile<KS>(a, db, tile_of(kcur), lane);
+        ld_tile<KS>(a, db, tk(kcur), lane);
       }
     }
     __syncthreads();
@@ -1383,8 +1237,8 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
         kn = plk[jn];
         mn = plm[jn];
       }
-      ld_tile<KS>(nxt, db, tile_of(kn >= 0 ? kn : kcur), lane);  // unconditional (equal vmcnt)
-      const int prow = pos2row[(int64_t)tile_of(kcur) * IA_TILE + (lane & 31)];
+      ld_tile<KS>(nxt, db, tk(kn >= 0 ? kn : kcur), lane);  // unconditional (equal vmcnt)
+      const int prow = pos2row[(int64_t)tk(kcur) * IA_TILE + (lane & 31)];
       asm volatile("" ::: "memory");
       k3p_pairs_hl<KS, QT, 0>(cur, ldsh + lane, qlo_f + lane, mcur, kcur, b1, b2, i1);  // i1: the WG-local tile
       if (lane < 32) rowmap[kcur * IA_TILE + lane] = prow;
@@ -1603,8 +1457,6 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     }
   }
   K3P_T(ph[9]);
-  if constexpr (STL)
-    if (tid == 0) xo.steal[wg] = s_smax;  // option "steal": the merge's rescans (MergeArgs::steal)
   if (tid == 0) {  // the workgroup's own counter slots (stream-ordered launches: no atomics)
     unsigned long long sp = 0, st = 0, sf = 0, stp = 0;
 #pragma unroll
@@ -1619,8 +1471,7 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     // DB half-tiles loaded besides one per loaded tile (the algorithmic bytes):
     // whole tiles (HHX <= 2): the lo half of each; hi-only stream (3): the lo halves of the
     // passing tiles; two passes (4): the passing tiles again, whole
-    // (option "steal": the tiles this workgroup took from its victim, << 40)
-    tiles[blockIdx.x + 2 * IA_NWG_H] += (HHX == 4 ? 2 * stp : HHX == 3 ? stp : st) + (STL ? (unsigned long long)s_smax << 40 : 0ull);
+    tiles[blockIdx.x + 2 * IA_NWG_H] += HHX == 4 ? 2 * stp : HHX == 3 ? stp : st;
   }
   if (xo.stamp) {  // (uniform) option "stamps": the workgroup's first and last tick
     __syncthreads();
@@ -1682,8 +1533,6 @@ k3p_fn IA_K3H_CAT(ia_k3p_get_, IA_K3H_KS, IA_K3H_QT)(int variant) {
     // 24 / 25: a hi stream three tiles deep, then the passing tiles' full chains (two passes)
     if (variant == 24) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true, 4>;
     if (variant == 25) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, true, true, 4>;
-    // 24's stealing form (option "steal"; the launcher's internal id 26)
-    if (variant == 26) return k3h_prune3<IA_K3H_KS, IA_K3H_QT, NW, false, true, 4, true>;
     return nullptr;
   } else {
     return nullptr;

@@ -885,24 +885,6 @@ __device__ __forceinline__ double cert_theta(const MergeArgs &a, double R, doubl
 
 // the certified single-rank winner of query m (exact NN over this rank's shard); RPL records per
 // lane (nwg <= 64 RPL)
-// The tiles behind workgroup w's records on a pruned level, as runs f(t0, p0, p1) of tiles t0 + nwg p,
-// p0 <= p < p1: its chunk {w + nwg k} and, when the scan stole (option "steal", MergeArgs::steal),
-// the s tiles it took from the back of workgroup (w + nwg / 2) % nwg's walk (ia_k3h.hip k3h_prune3:
-// walk index k is chunk position k, or K - 1 - k on odd steps).  A superset of the tiles w scanned:
-// the victim's own chunk stays whole.
-template <class F>
-__device__ __forceinline__ void record_tiles(const MergeArgs &a, int w, F &&f) {
-  f(w, 0, (a.NT - w + a.nwg - 1) / a.nwg);
-  if (a.steal) {
-    const int s = a.steal[w];
-    if (s > 0) {
-      const int v = (w + (a.nwg >> 1)) % a.nwg, Kv = (a.NT - v + a.nwg - 1) / a.nwg;
-      if (a.srev) f(v, 0, s);
-      else f(v, Kv - s, Kv);
-    }
-  }
-}
-
 template <int RPL = IA_WG_TARGET / IA_WAVE, class DistFn>
 __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, unsigned *stat_out) {
   const int lane = threadIdx.x & 63;
@@ -983,24 +965,22 @@ __device__ Winner certified_winner(const MergeArgs &a, int m, DistFn &&dist, uns
         // no such row: nothing is rescanned and it reports no winner (d = DBL_MAX).
         const float4 ql = a.qinfo[3 * m], qh = a.qinfo[3 * m + 1];
         const float ub = fminf(round_up_f(bd * a.ufac), a.qinfo[3 * m + 2].x);
-        record_tiles(a, wgid, [&](int t0, int p0, int p1) {
-          for (int pb = p0; pb < p1; pb += IA_WAVE) {
-            const int64_t t = t0 + (int64_t)a.nwg * (pb + lane);
-            const bool nd = pb + lane < p1 && prune_lb(a.boxes[2 * t], a.boxes[2 * t + 1], ql, qh) <= ub;
-            unsigned long long nm = __ballot(nd);
-            while (nm) {
-              const int jt = __ffsll((long long)nm) - 1;
-              nm &= nm - 1;
-              if (lane < IA_TILE) {
-                const int64_t i = a.pos2row[(t0 + (int64_t)a.nwg * (pb + jt)) * IA_TILE + lane];
-                if (i < a.NA) {
-                  const double d = dist(i);
-                  if (d < cd || (d == cd && i < ci)) { cd = d; ci = i; }
-                }
+        for (int64_t tb = 0; wgid + (int64_t)a.nwg * tb < a.NT; tb += IA_WAVE) {
+          const int64_t t = wgid + (int64_t)a.nwg * (tb + lane);
+          const bool nd = t < a.NT && prune_lb(a.boxes[2 * t], a.boxes[2 * t + 1], ql, qh) <= ub;
+          unsigned long long nm = __ballot(nd);
+          while (nm) {
+            const int jt = __ffsll((long long)nm) - 1;
+            nm &= nm - 1;
+            if (lane < IA_TILE) {
+              const int64_t i = a.pos2row[(wgid + (int64_t)a.nwg * (tb + jt)) * IA_TILE + lane];
+              if (i < a.NA) {
+                const double d = dist(i);
+                if (d < cd || (d == cd && i < ci)) { cd = d; ci = i; }
               }
             }
           }
-        });
+        }
       } else {
         const int64_t p0 = (int64_t)a.pos0 + (int64_t)wgid * a.tpw * IA_TILE;
         const int64_t p1 = min((int64_t)a.pos_end, p0 + (int64_t)a.tpw * IA_TILE);
@@ -1791,39 +1771,35 @@ __device__ __forceinline__ void merge_fused(const LevelGeo &g, const StepDesc &s
         const float ub = round_up_f(bd * a.ufac);
         // the chunk's tiles t0 + tst k < tend (owner-computes step: chunk wgid mod nch of shard
         // wgid / nch, in that shard's storage range of the whole level's table)
-        // (one-rank steps with option "steal": the tiles of record_tiles)
-        auto run = [&](int64_t t0, int64_t tst, int64_t p0, int64_t p1) {
-          for (int64_t pb = p0; pb < p1; pb += IA_WAVE) {
-            const int64_t t = t0 + tst * (pb + lane);
-            bool nd = false;
-            if (pb + lane < p1) nd = prune_lb(a.boxes[2 * t], a.boxes[2 * t + 1], ql, qh) <= ub;
-            unsigned long long nm = __ballot(nd);
-            while (nm) {
-              const int j0 = __ffsll((long long)nm) - 1;
+        int64_t t0 = wgid, tst = a.nwg, tend = a.NT;
+        if (a.xo_W) {
+          const int sh = wgid / a.xo_nch;
+          t0 = ia_shard_off(a.NT, a.xo_W, sh) + (wgid - sh * a.xo_nch);
+          tst = a.xo_nch;
+          tend = ia_shard_off(a.NT, a.xo_W, sh + 1);
+        }
+        for (int64_t tb = 0; t0 + tst * tb < tend; tb += IA_WAVE) {
+          const int64_t t = t0 + tst * (tb + lane);
+          bool nd = false;
+          if (t < tend) nd = prune_lb(a.boxes[2 * t], a.boxes[2 * t + 1], ql, qh) <= ub;
+          unsigned long long nm = __ballot(nd);
+          while (nm) {
+            const int j0 = __ffsll((long long)nm) - 1;
+            nm &= nm - 1;
+            int j1 = -1;
+            if (nm) {
+              j1 = __ffsll((long long)nm) - 1;
               nm &= nm - 1;
-              int j1 = -1;
-              if (nm) {
-                j1 = __ffsll((long long)nm) - 1;
-                nm &= nm - 1;
-              }
-              const int j = lane < 32 ? j0 : j1;
-              if (j >= 0) {
-                const int64_t i = a.pos2row[(t0 + tst * (pb + j)) * IA_TILE + (lane & 31)];
-                if (i < a.NA) {
-                  const double d = exact_dist_level<CH>(a.db64, i, qs, IMG ? &A : nullptr);
-                  if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
-                }
+            }
+            const int j = lane < 32 ? j0 : j1;
+            if (j >= 0) {
+              const int64_t i = a.pos2row[(t0 + tst * (tb + j)) * IA_TILE + (lane & 31)];
+              if (i < a.NA) {
+                const double d = exact_dist_level<CH>(a.db64, i, qs, IMG ? &A : nullptr);
+                if (d < cd || (d == cd && (int)i < ci)) { cd = d; ci = (int)i; }
               }
             }
           }
-        };
-        if (a.xo_W) {
-          const int sh = wgid / a.xo_nch;
-          const int64_t t0 = ia_shard_off(a.NT, a.xo_W, sh) + (wgid - sh * a.xo_nch), tst = a.xo_nch;
-          const int64_t tend = ia_shard_off(a.NT, a.xo_W, sh + 1);
-          run(t0, tst, 0, (tend - t0 + tst - 1) / tst);
-        } else {
-          record_tiles(a, wgid, [&](int t0, int p0, int p1) { run(t0, a.nwg, p0, p1); });
         }
       } else {
         const int64_t p0 = (int64_t)a.pos0 + (int64_t)wgid * a.tpw * IA_TILE;
@@ -3068,8 +3044,7 @@ int ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, c
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
                    const float4 *tbox, const float *tnorm, hipStream_t st, int nqb, int qt_end, const XOScan *xo,
-                   unsigned long long *stamp, int rec_wt, unsigned *steal_front, int *steal_cnt, unsigned steal_seq,
-                   int steal_delay) {
+                   unsigned long long *stamp, int rec_wt) {
   typedef k3p_fn (*getter)(int);
   static const getter g4[] = {ia_k3p_get_4_1, ia_k3p_get_4_2, ia_k3p_get_4_3, ia_k3p_get_4_4,  ia_k3p_get_4_5, ia_k3p_get_4_6,
                               ia_k3p_get_4_7, ia_k3p_get_4_8, ia_k3p_get_4_9, ia_k3p_get_4_10, ia_k3p_get_4_11};
@@ -3081,19 +3056,13 @@ int ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, c
   if (in_kernel_sort && Mpad > 512) variant = 21;
   const size_t NQ = (size_t)qt * IA_TILE;
   const int nthr = IA_WGH;
-  // option "steal" (v24, one query block, not owner-computes): up to kmax / 2 more local tiles (the
-  // back half of the victim's walk, ia_k3h.hip k3h_prune3); every workgroup walks >= 32 tiles and
-  // thief and victim (w + nwg / 2) share an XCD (nwg a multiple of 16)
-  bool steal = steal_front && steal_cnt && variant == 24 && nqb == 1 && !(xo && xo->on) && NT / nwg >= 32 &&
-               nwg % 16 == 0;
   auto dyn_lds = [&](int v) {
     const bool pre = v == 21 || v == 25;
-    const size_t kl = (size_t)kmax + (steal && v == 24 ? kmax / 2 : 0);  // local tiles (own + stolen)
     const size_t qfrag = (size_t)qt * (v >= 24 ? 4 : 8) * IA_WAVE * 16;  // v24 / 25: hi pieces only
-    size_t l = pre ? qfrag + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 + kl * 32
-                   : ia_k3p_lds(qt, Mpad) - (size_t)qt * 8 * IA_WAVE * 16 + qfrag + (size_t)Mpad * 4 + kl * 32;
-    l += NQ * 8 + kl * 4;                      // (z, w) per sorted query slot, R_t per tile
-    if (v >= 24) l += kl * 8;                  // the filter-passing tiles and their blocks
+    size_t l = pre ? qfrag + NQ * 36 + (size_t)qt * 32 + (size_t)((qt + 3) & ~3) * 4 + NQ * 4 + (size_t)kmax * 40
+                   : ia_k3p_lds(qt, Mpad) - (size_t)qt * 8 * IA_WAVE * 16 + qfrag + (size_t)Mpad * 4 + (size_t)kmax * 40;
+    l += NQ * 8 + (size_t)kmax * 4;            // (z, w) per sorted query slot, R_t per tile
+    if (v >= 24) l += (size_t)kmax * 8;        // the filter-passing tiles and their blocks
     size_t red = (size_t)(nthr / IA_WAVE) * qt * IA_TILE * 20;  // the subset merge's Top2 area
     if (v >= 24) red = std::max(red, (size_t)(nthr / IA_WAVE) * qt * IA_WAVE * 12);  // (every lane's subset)
     return l > red ? l : red;
@@ -3101,21 +3070,16 @@ int ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, c
   size_t lds = dyn_lds(variant);
   if (variant >= 24) {  // the static LDS-DMA rings (86 KiB) + this launch's dynamic part must fit 160 KiB
     hipFuncAttributes fa;
-    const k3p_fn f24 = g4[qt - 1](steal && variant == 24 ? 26 : variant);
+    const k3p_fn f24 = g4[qt - 1](variant);
     const size_t stat = f24 && hipFuncGetAttributes(&fa, (const void *)f24) == hipSuccess ? fa.sharedSizeBytes : 0;
     // (and the second pass stages the lo pieces + a row map of the WG's tiles in the rings' 84 KiB)
-    auto ring_fits = [&](size_t kl) { return (size_t)qt * 4 * IA_WAVE * 16 + kl * IA_TILE * 4 <= (size_t)8 * 3 * 3584; };
-    if (steal && (!ring_fits((size_t)kmax + kmax / 2) || stat + lds > 160 * 1024)) {  // no room for the stolen tiles
-      steal = false;
-      lds = dyn_lds(variant);
-    }
-    if (!f24 || !ring_fits((size_t)kmax) || stat + lds > 160 * 1024) {  // (many tiles per workgroup or wide steps): the one-pass forms
+    const bool ring_fits = (size_t)qt * 4 * IA_WAVE * 16 + (size_t)kmax * IA_TILE * 4 <= (size_t)8 * 3 * 3584;
+    if (!f24 || !ring_fits || stat + lds > 160 * 1024) {  // (many tiles per workgroup or wide steps): the one-pass forms
       variant = variant == 25 ? 21 : 22;
       lds = dyn_lds(variant);
     }
   }
-  steal = steal && variant == 24;
-  const k3p_fn fn = g4[qt - 1](steal ? 26 : variant);  // 26: 24's stealing form (ia_k3h.hip)
+  const k3p_fn fn = g4[qt - 1](variant);
   // (the host accepts only the built variants, ia_set_option; a missing instance is an error the
   // level reports, never a silently skipped scan whose stale records the merge would consume)
   if (!fn) return -1;  // IA_EINVAL (include/ia.h)
@@ -3127,12 +3091,8 @@ int ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, c
   if (xo) x = *xo;
   x.stamp = stamp;
   x.rec_wt = rec_wt;
-  x.front = steal ? steal_front : nullptr;
-  x.steal = steal ? steal_cnt : nullptr;
-  x.sseq = steal_seq & 0xFFFFFu;
-  x.sdelay = steal ? steal_delay : 0;
   allow_full_lds((const void *)fn);
   hipLaunchKernelGGL(fn, dim3(nqb * nwg), dim3(nthr), lds, st, (const h16x8 *)db, (const h16x8 *)qf, qinfo, boxes, pos2row,
                      NT, qt0, M, Mpad, nwg, rec, recT, pairs, tiles, rev, ord_in, n_in, r0, ord_out, tbox, tnorm, nqb, qt_end, x);
-  return steal ? 1 : 0;
+  return 0;
 }

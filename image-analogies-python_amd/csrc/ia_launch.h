@@ -71,11 +71,7 @@ int ia_launch_k3p(int qt, const void *db, const void *qf, const float4 *qinfo, c
                    int NT, int qt0, int M, int Mpad, int nwg, float4 *rec, float *recT, unsigned long long *pairs,
                    unsigned long long *tiles, int variant, int step, const int *ord_in, int n_in, int r0, int *ord_out,
                    const float4 *tbox, const float *tnorm, hipStream_t st, int nqb = 1, int qt_end = 0,
-                   const XOScan *xo = nullptr, unsigned long long *stamp = nullptr, int rec_wt = 0,
-                   unsigned *steal_front = nullptr, int *steal_cnt = nullptr, unsigned steal_seq = 0,
-                   int steal_delay = 0);
-// (returns -1: no kernel instance for the variant; 1: the launch steals tiles (option "steal", the
-// merge's rescans then read steal_cnt); 0 otherwise)
+                   const XOScan *xo = nullptr, unsigned long long *stamp = nullptr, int rec_wt = 0);
 // GPU preprocessing (ia_pyramid.hip)
 void ia_launch_pyramid_reduce(const double *in, double *out, double *tmp, double *sm, double *mm, int h, int w, int ch,
                               const double *w7, hipStream_t st);

@@ -114,8 +114,6 @@ typedef struct {
   double k3p_bytes_unique_all; /* k3p_bytes_all with each launch's DB tiles counted at most once
                                 * (<= the launch's whole tiles): launches of several query blocks
                                 * stream a tile once per block (cfg4's wide steps) */
-  double stolen_tiles;      /* option "steal": DB tiles pruned-scan workgroups took from the back of
-                             * their partner's walk (summed over the launches) */
 } ia_stats;
 
 /* One pyramid level (image_analogies.py:130-239).  Shapes: A/A' level l is (a_h, a_w[, ch]),
@@ -217,14 +215,10 @@ int ia_version(void);
  * before waiting for that handoff: the other 54 features, fragments, projection and |q'|^2 sums,
  * and U' over the candidate rows requested first; U' then leaves out the row above's own two
  * candidates (a valid bound either way).
- * "steal" = 1 / 0 (default): in a one-rank pruned step's scan (in-kernel sort, >= 32 DB tiles per
- * workgroup) each workgroup, once its own tiles are done, takes tiles from the back of workgroup
- * (w + nwg / 2) % nwg's walk; the two publish how far they got and decide the contested tiles in
- * order, so a workgroup that started late (its CU held by another level's kernel) finishes with
- * fewer tiles; the merge's rescans visit the taken tiles too.  "steal_delay" = us
- * (tests; default 0): the upper half of those workgroups start that late, so stealing happens.
- * "scan_wgs" = 8..256 (multiple of 8; default 256): workgroups of the context's split-f16 scans
- * (bench.py gives the coarser pipelined levels 128).
+ * "scan_wgs" = 8..256 (a multiple of 8; default 256, one per CU): workgroups of the context's
+ * split-f16 scans (pruned: one chunk of DB tiles each; unpruned: contiguous tile ranges).  bench.py
+ * gives the coarser pipelined levels' contexts 128, so their scans never queue for the whole GPU
+ * while the finest level's kernels are dispatched.
  * "stamps" = 1: every pruned-scan and fused-merge launch of a pruned level stamps its
  * workgroups' first / last s_memrealtime tick; ia_stats.k3p_stamp_ms / merge_stamp_ms sum the
  * per-launch device times (bench.py roofline.frac_timed: the timed, pipelined steps' own kernels).

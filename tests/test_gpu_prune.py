@@ -93,42 +93,6 @@ def test_fused_gather_equals_separate_launches(ctx, variant):
         assert abs(st.fallbacks - runs[0][3].fallbacks) <= 0.05 * runs[0][3].fallbacks + 10
 
 
-@pytest.mark.parametrize('size', [512, 1024])
-def test_work_stealing_is_exact(ctx, size):
-    """option steal (ia_k3h.hip k3h_prune3): a scan workgroup done with its own DB
-    tiles takes tiles from the back of its partner's walk, the contested ones decided in index
-    order against the frontiers both publish.  With the upper half of the workgroups started
-    late (steal_delay) their partners take many of their tiles; every run is bit-identical to the
-    run without stealing, in the fused merge and in the separate merge of sampled steps (time_dist),
-    whose certification rescans visit the taken tiles."""
-    from ia_amd import synth
-    job = synth.make_job(size)
-    runs = []
-    for steal, delay, stride in ((0, 0, 0), (1, 0, 0), (1, 20, 0), (1, 20, 3)):
-        ctx.set_option('steal', steal)
-        ctx.set_option('steal_delay', delay)
-        ctx.set_option('time_dist', stride)
-        try:
-            runs.append(_run(ctx, job, 1, 24))
-        finally:
-            ctx.set_option('steal', 1)
-            ctx.set_option('steal_delay', 0)
-            ctx.set_option('time_dist', 0)
-    Bp0, S0, IM0, st0 = runs[0]
-    assert st0.stolen_tiles == 0
-    for Bp, S, IM, st in runs[1:]:
-        for level in range(1, job.L):
-            assert np.array_equal(S[level], S0[level]), level
-            assert np.array_equal(IM[level], IM0[level]), level
-            assert np.array_equal(Bp[level], Bp0[level]), level
-        assert st.bound_violations == 0 and st.pruned_levels == (1 if size == 512 else 2)
-    # a late half: its partners take a good share of its tiles (each at most the back half)
-    for _, _, _, st in runs[2:]:
-        assert st.stolen_tiles > 0.05 * st.dist_tiles_full / 2, (st.stolen_tiles, st.dist_tiles_full)
-    print('size %d: stolen tiles %d (natural), %d / %d (late half), of %d' % (
-        size, runs[1][3].stolen_tiles, runs[2][3].stolen_tiles, runs[3][3].stolen_tiles, st0.dist_tiles_full))
-
-
 @pytest.mark.parametrize('size,group', [(512, 2), (1024, 4), (1024, 8)])
 def test_pruned_groups_equal_unpruned(ctx, size, group):
     """option prune_group: Morton tiles interleaved in groups of G (sort neighbours in different
