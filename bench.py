@@ -883,7 +883,8 @@ def main():
         roofline['streamed_bytes_per_launch_timed'] = st_all['k3p_bytes_all'] / st_all['k3p_stamp_launches']
         if ub < st_all['k3p_bytes_all']:  # the sampled reading on the same basis
             for k in ('achieved', 'frac', 'algorithmic_bytes_per_launch'):
-                roofline[k] *= ub / st_all['k3p_bytes_all']
+                if k in roofline:   # (absent without sampled timing, --time-stride 0)
+                    roofline[k] *= ub / st_all['k3p_bytes_all']
         if roofline.get('traffic'):
             roofline['traffic_over_algorithmic'] = roofline['traffic'] / roofline['algorithmic_bytes_per_launch_timed']
         # the launch = its workgroups' start spread (dispatch, CUs held by concurrent kernels)
