@@ -1516,9 +1516,10 @@ int ia_synthesize_levels(ia_ctx *c, const ia_level_args *args, int n_jobs, ia_st
     const bool wide = sd.Mpad > 512 || (c->k3p_blocks && sd.Mpad > qtmax * IA_TILE);
     // sorted by the previous launch's gathers: the presorted form of the variant, no K2s
     const bool gsorted = fsort && gathered == t && gsort;
-    // wide steps: the presorted form; under 24 that is 21 (cfg4's two-block steps measured faster
-    // with whole tiles than with the two-pass form 25: 6.20 vs 6.03 M px/s)
-    const int k3v = (kv == 21 || kv == 25) ? kv : (prune && (wide || gsorted) ? 21 : kv);
+    // wide steps: the presorted form of the variant - under 24 that is 25, the two-pass form
+    // (round 6, on the trimmed stream: cfg4 6.66 -> 6.91 M px/s against 21's whole tiles; round 4's
+    // kernels had it the other way), under 20 / 22 it is 21
+    const int k3v = (kv == 21 || kv == 25) ? kv : (prune && (wide || gsorted) ? (kv == 24 ? 25 : 21) : kv);
     const bool presorted = k3v == 21 || k3v == 25;
     const float4 *tboxp = gsorted ? nullptr : c->qs_tbox.as<float4>();  // nullptr: boxes from the slice
     if (prune && presorted && !gsorted)
