@@ -93,6 +93,33 @@ def test_fused_gather_equals_separate_launches(ctx, variant):
         assert abs(st.fallbacks - runs[0][3].fallbacks) <= 0.05 * runs[0][3].fallbacks + 10
 
 
+@pytest.mark.parametrize('wgs', [128, 64])
+def test_scan_workgroups_equal_default(ctx, wgs):
+    """option scan_wgs (bench.py gives the coarser pipelined levels' contexts 128):
+    the pruned and unpruned split-f16 scans on fewer workgroups (more DB tiles each, fewer records
+    per query for the merge) give the same decisions on every level as one workgroup per CU"""
+    from ia_amd import synth
+    job = synth.make_job(512)
+    Bp0, S0, IM0, st0 = _run(ctx, job, 1, 24)
+    ctx.set_option('scan_wgs', wgs)
+    try:
+        Bp1, S1, IM1, st1 = _run(ctx, job, 1, 24)
+    finally:
+        ctx.set_option('scan_wgs', 256)
+    for level in range(1, job.L):
+        assert np.array_equal(S0[level], S1[level]), level
+        assert np.array_equal(IM0[level], IM1[level]), level
+        assert np.array_equal(Bp0[level], Bp1[level]), level
+    assert st1.bound_violations == 0 and st1.pruned_levels == st0.pruned_levels == 1
+
+
+def test_scan_workgroups_option_rejects_bad_values(ctx):
+    from ia_amd import _native
+    for bad in (0, 4, 12, 264):
+        with pytest.raises(_native.IAError):
+            ctx.set_option('scan_wgs', bad)
+
+
 @pytest.mark.parametrize('size,group', [(512, 2), (1024, 4), (1024, 8)])
 def test_pruned_groups_equal_unpruned(ctx, size, group):
     """option prune_group: Morton tiles interleaved in groups of G (sort neighbours in different
