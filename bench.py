@@ -272,6 +272,8 @@ def make_context(args, local):
     # always explicit (the library default is 24, so a skipped set_option for 22 ran v24)
     cx.set_option('k3p_variant', args.k3p_variant)     # 20, 21, 22, 24, 25
     cx.set_option('prune_min_rows', args.prune_min_rows)
+    if args.scan_wgs:   # (every context; pipelined runs then size the coarser levels' with --coarse-scan-wgs)
+        cx.set_option('scan_wgs', args.scan_wgs)
     if args.k3p_blocks != 1:
         cx.set_option('k3p_blocks', args.k3p_blocks)
     if args.prune_group != 1:
@@ -305,8 +307,6 @@ def pipe_contexts(args, local, ctx):
         ctx.set_option('stream_priority', hi)
         for cx in extra:
             cx.set_option('stream_priority', lo)
-    if args.scan_wgs:
-        ctx.set_option('scan_wgs', args.scan_wgs)
     if args.coarse_scan_wgs:
         for cx in extra:
             cx.set_option('scan_wgs', args.coarse_scan_wgs)
@@ -436,7 +436,8 @@ def main():
                          'default 128: half the CUs, so the finest level\'s launches are not queued behind a '
                          'whole-GPU scan, DESIGN.md §6g)')
     ap.add_argument('--scan-wgs', type=int, default=0,
-                    help='workgroups of the finest level\'s pruned scans (0: one per CU, 256)')
+                    help='workgroups of every context\'s split-f16 scans (0: one per CU, 256; pipelined runs: '
+                         'the finest level\'s, the coarser levels\' follow --coarse-scan-wgs)')
     ap.add_argument('--k3p-blocks', type=int, default=1, choices=[0, 1],
                     help='pruned scan of a step wider than 11 query tiles: 1 = one launch of (query block x DB '
                          'chunk) workgroups, 0 = one launch per query block')
