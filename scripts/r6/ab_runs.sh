@@ -1,5 +1,6 @@
 #!/bin/bash
-# same-box A/B of (library, bench flags) pairs: ab_runs.sh OUT "name|lib.so|flags" ... (two passes, cfg3, 10 steps)
+# same-box A/B of (library, bench flags) pairs: ab_runs.sh OUT "name|lib.so|flags" ... (two passes, 10 steps;
+# cfg3 unless the flags name another --config)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-.}"
 export TMPDIR=/tmp
