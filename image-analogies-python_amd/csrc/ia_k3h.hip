@@ -1416,12 +1416,21 @@ k3h_prune3(const h16x8 *__restrict__ db, const h16x8 *__restrict__ qf, const flo
     Top2 m;
     if constexpr (T16) {
       const int b0 = (x >> 5) * IA_WAVE + (x & 31);  // wave 0, lane x % 32 of query tile x / 32
-      m = Top2{rv1[b0], FLT_MAX, rvT[b0], ri1[b0], 0x7fffffff};
+      // the 2 NW subsets merged as a tree (depth log2(2 NW) instead of a chain of 2 NW - 1; round 6:
+      // K3p workgroups 29.4 -> 29.0 us, profiles/r06/tree/): the merge keeps the two
+      // lexicographically smallest (value, row) pairs and the smallest other value, which no merge
+      // order changes (bit-identical records)
+      Top2 t[2 * NW];
 #pragma unroll
-      for (int e = 1; e < 2 * NW; e++) {
+      for (int e = 0; e < 2 * NW; e++) {
         const int ix = b0 + (e >> 1) * QT * IA_WAVE + (e & 1) * 32;
-        m = top2_merge_sel(m, Top2{rv1[ix], FLT_MAX, rvT[ix], ri1[ix], 0x7fffffff});
+        t[e] = Top2{rv1[ix], FLT_MAX, rvT[ix], ri1[ix], 0x7fffffff};
       }
+#pragma unroll
+      for (int st = 1; st < 2 * NW; st <<= 1)
+#pragma unroll
+        for (int e = 0; e < 2 * NW; e += 2 * st) t[e] = top2_merge_sel(t[e], t[e + st]);
+      m = t[0];
     } else {
       m = red[x];
 #pragma unroll
